@@ -1,0 +1,678 @@
+/*
+ * hg_oracle.c -- CPU restatement of the reference hashgraph consensus path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see hg_oracle.h).  Used by tests/ as the parity
+ * checker and by bench.py as the "CPU restatement of reference Go path,
+ * 1 thread" baseline.  Never linked into libbabble_hip.
+ *
+ * Every function cites the Go code it restates (paths under
+ * /root/reference/src).  Hash-string keys of the Go code become dense event
+ * ids (insertion order == topologicalIndex, hashgraph.go:731-732); the LRU
+ * memo caches become plain memo arrays (the reference runs batch consensus
+ * with cacheSize >= #events, so nothing is ever evicted).
+ */
+#include "hg_oracle.h"
+
+#include <limits.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define UNSET INT32_MIN
+#define FD_NONE INT32_MAX /* math.MaxInt32, hashgraph.go:447 */
+
+enum { TRI_UNDEFINED = 0, TRI_TRUE = 1, TRI_FALSE = 2 }; /* roundInfo.go:10-16 */
+
+typedef struct {
+  int32_t id;
+  uint8_t witness;
+  uint8_t famous; /* Trilean */
+  uint8_t consensus;
+} round_event; /* roundInfo.go:29-33 */
+
+typedef struct {
+  int exists;
+  int queued; /* roundInfo.go:35 */
+  round_event *ev;
+  int32_t len, cap;
+} round_info; /* roundInfo.go:33-42 */
+
+typedef struct {
+  int32_t index;
+  int8_t decided;
+} pending_round; /* roundInfo.go:22-25 */
+
+struct hgo {
+  int32_t n, sm;
+  int64_t *pids;
+  int64_t cap, N;
+  /* event bodies */
+  int32_t *creator, *index, *sp, *op, *ntx;
+  uint8_t *hash, *sigr;
+  /* coordinates: lastAncestors / firstDescendants indexes, [N][n] */
+  int32_t *la, *fd;
+  /* memo caches (hashgraph.go:36-40) */
+  int32_t *round_memo, *lt_memo;
+  /* Event private fields (event.go:107-116): nil == UNSET */
+  int32_t *ev_round, *ev_lt, *ev_rr;
+  /* RoundInfo.Events is a Go map keyed by event hash: an event has at most two
+   * entries (its own round, and its round-received), indexed here for O(1)
+   * lookup like the map */
+  int32_t *ent_round[2], *ent_slot[2];
+  /* participant event chains (ParticipantEventsCache) */
+  int32_t **chain;
+  int32_t *chain_len, *chain_cap;
+  /* hashgraph state (hashgraph.go:19-34) */
+  int32_t *und;
+  int64_t und_len;
+  pending_round *pend;
+  int32_t pend_len, pend_cap;
+  int has_lcr;
+  int32_t lcr;
+  int64_t consensus_txs, pending_loaded;
+  /* InmemStore rounds / consensus / blocks (inmem_store.go) */
+  round_info *rounds;
+  int32_t rounds_cap;
+  int32_t last_round;
+  int32_t *cons;
+  int64_t ncons;
+  int64_t *cons_pos;
+  int32_t *blk_rr;
+  int64_t *blk_first, *blk_count, *blk_ntx;
+  int64_t nblocks, blk_cap;
+  /* frames cache (InmemStore.GetFrame/SetFrame, inmem_store.go:254-270) */
+  int8_t *frame_done;
+  int64_t *frame_first, *frame_len;
+  int32_t *frame_ev;
+  int64_t frame_ev_len;
+};
+
+static void *xcalloc(size_t n, size_t s) {
+  void *p = calloc(n ? n : 1, s);
+  if (!p) abort();
+  return p;
+}
+static void *xrealloc(void *p, size_t s) {
+  void *q = realloc(p, s ? s : 1);
+  if (!q) abort();
+  return q;
+}
+
+hgo *hgo_create(int32_t n, const int64_t *participant_ids, int64_t capacity) {
+  hgo *h = (hgo *)xcalloc(1, sizeof(hgo));
+  h->n = n;
+  h->sm = 2 * n / 3 + 1; /* hashgraph.go:54 */
+  h->pids = (int64_t *)xcalloc(n, 8);
+  memcpy(h->pids, participant_ids, (size_t)n * 8);
+  h->cap = capacity;
+  size_t C = (size_t)capacity;
+  h->creator = (int32_t *)xcalloc(C, 4);
+  h->index = (int32_t *)xcalloc(C, 4);
+  h->sp = (int32_t *)xcalloc(C, 4);
+  h->op = (int32_t *)xcalloc(C, 4);
+  h->ntx = (int32_t *)xcalloc(C, 4);
+  h->hash = (uint8_t *)xcalloc(C, 32);
+  h->sigr = (uint8_t *)xcalloc(C, 32);
+  h->la = (int32_t *)xcalloc(C * (size_t)n, 4);
+  h->fd = (int32_t *)xcalloc(C * (size_t)n, 4);
+  h->round_memo = (int32_t *)xcalloc(C, 4);
+  h->lt_memo = (int32_t *)xcalloc(C, 4);
+  h->ev_round = (int32_t *)xcalloc(C, 4);
+  h->ev_lt = (int32_t *)xcalloc(C, 4);
+  h->ev_rr = (int32_t *)xcalloc(C, 4);
+  h->cons_pos = (int64_t *)xcalloc(C, 8);
+  for (int k = 0; k < 2; k++) {
+    h->ent_round[k] = (int32_t *)xcalloc(C, 4);
+    h->ent_slot[k] = (int32_t *)xcalloc(C, 4);
+  }
+  h->und = (int32_t *)xcalloc(C, 4);
+  h->cons = (int32_t *)xcalloc(C, 4);
+  h->frame_ev = (int32_t *)xcalloc(C, 4);
+  h->chain = (int32_t **)xcalloc(n, sizeof(int32_t *));
+  h->chain_len = (int32_t *)xcalloc(n, 4);
+  h->chain_cap = (int32_t *)xcalloc(n, 4);
+  h->last_round = -1; /* inmem_store.go:45 */
+  h->lcr = -1;
+  return h;
+}
+
+void hgo_destroy(hgo *h) {
+  if (!h) return;
+  free(h->pids);
+  free(h->creator); free(h->index); free(h->sp); free(h->op); free(h->ntx);
+  free(h->hash); free(h->sigr); free(h->la); free(h->fd);
+  free(h->round_memo); free(h->lt_memo);
+  free(h->ev_round); free(h->ev_lt); free(h->ev_rr); free(h->cons_pos);
+  for (int k = 0; k < 2; k++) { free(h->ent_round[k]); free(h->ent_slot[k]); }
+  free(h->und); free(h->cons); free(h->frame_ev);
+  for (int i = 0; i < h->n; i++) free(h->chain[i]);
+  free(h->chain); free(h->chain_len); free(h->chain_cap);
+  free(h->pend);
+  for (int32_t r = 0; r < h->rounds_cap; r++) free(h->rounds[r].ev);
+  free(h->rounds);
+  free(h->blk_rr); free(h->blk_first); free(h->blk_count); free(h->blk_ntx);
+  free(h->frame_done); free(h->frame_first); free(h->frame_len);
+  free(h);
+}
+
+/* ------------------------------------------------------------------------ */
+/* InmemStore rounds (inmem_store.go:185-211)                               */
+
+static void ensure_round_cap(hgo *h, int32_t r) {
+  if (r < h->rounds_cap) return;
+  int32_t nc = h->rounds_cap ? h->rounds_cap : 64;
+  while (nc <= r) nc *= 2;
+  h->rounds = (round_info *)xrealloc(h->rounds, (size_t)nc * sizeof(round_info));
+  memset(h->rounds + h->rounds_cap, 0, (size_t)(nc - h->rounds_cap) * sizeof(round_info));
+  h->frame_done = (int8_t *)xrealloc(h->frame_done, (size_t)nc);
+  memset(h->frame_done + h->rounds_cap, 0, (size_t)(nc - h->rounds_cap));
+  h->frame_first = (int64_t *)xrealloc(h->frame_first, (size_t)nc * 8);
+  h->frame_len = (int64_t *)xrealloc(h->frame_len, (size_t)nc * 8);
+  h->rounds_cap = nc;
+}
+
+/* GetRound: KeyNotFound for missing rounds (inmem_store.go:185-191) */
+static round_info *get_round(hgo *h, int32_t r) {
+  if (r < 0 || r >= h->rounds_cap || !h->rounds[r].exists) return NULL;
+  return &h->rounds[r];
+}
+
+/* SetRound tracks LastRound (inmem_store.go:193-199) */
+static round_info *set_round(hgo *h, int32_t r) {
+  ensure_round_cap(h, r);
+  h->rounds[r].exists = 1;
+  if (r > h->last_round) h->last_round = r;
+  return &h->rounds[r];
+}
+
+static round_event *ri_find(hgo *h, int32_t r, int32_t x) {
+  for (int k = 0; k < 2; k++)
+    if (h->ent_round[k][x] == r) return &h->rounds[r].ev[h->ent_slot[k][x]];
+  return NULL;
+}
+
+static round_event *ri_append(hgo *h, int32_t r, int32_t x) {
+  round_info *ri = &h->rounds[r];
+  if (ri->len == ri->cap) {
+    ri->cap = ri->cap ? 2 * ri->cap : 8;
+    ri->ev = (round_event *)xrealloc(ri->ev, (size_t)ri->cap * sizeof(round_event));
+  }
+  int k = h->ent_round[0][x] == INT32_MIN ? 0 : 1;
+  h->ent_round[k][x] = r;
+  h->ent_slot[k][x] = ri->len;
+  round_event *e = &ri->ev[ri->len++];
+  e->id = x; e->witness = 0; e->famous = TRI_UNDEFINED; e->consensus = 0;
+  return e;
+}
+
+/* RoundInfo.AddEvent (roundInfo.go:44-51) */
+static void ri_add_event(hgo *h, int32_t r, int32_t x, int witness) {
+  if (!ri_find(h, r, x)) ri_append(h, r, x)->witness = (uint8_t)witness;
+}
+
+/* RoundInfo.Witnesses (roundInfo.go:88-96) into buf; returns count */
+static int32_t ri_witnesses(const round_info *ri, int32_t **buf, int32_t *bcap) {
+  int32_t k = 0;
+  if (!ri) return 0;
+  for (int32_t i = 0; i < ri->len; i++) {
+    if (!ri->ev[i].witness) continue;
+    if (k == *bcap) {
+      *bcap = *bcap ? 2 * *bcap : 64;
+      *buf = (int32_t *)xrealloc(*buf, (size_t)*bcap * 4);
+    }
+    (*buf)[k++] = ri->ev[i].id;
+  }
+  return k;
+}
+
+/* RoundInfo.WitnessesDecided (roundInfo.go:78-85) */
+static int ri_witnesses_decided(const round_info *ri) {
+  for (int32_t i = 0; i < ri->len; i++)
+    if (ri->ev[i].witness && ri->ev[i].famous == TRI_UNDEFINED) return 0;
+  return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ancestry primitives                                                       */
+
+static inline int32_t *LA(const hgo *h, int32_t e) { return h->la + (size_t)e * h->n; }
+static inline int32_t *FD(const hgo *h, int32_t e) { return h->fd + (size_t)e * h->n; }
+
+/* _ancestor / see (hashgraph.go:92-117, 152-157) */
+static int see(const hgo *h, int32_t x, int32_t y) {
+  if (x == y) return 1;
+  return LA(h, x)[h->creator[y]] >= h->index[y];
+}
+
+/* _stronglySee (hashgraph.go:172-191) */
+static int strongly_see(const hgo *h, int32_t x, int32_t y) {
+  const int32_t *lx = LA(h, x), *fy = FD(h, y);
+  int c = 0;
+  for (int32_t i = 0; i < h->n; i++) c += lx[i] >= fy[i];
+  return c >= h->sm;
+}
+
+/* round / _round (hashgraph.go:193-278) for base roots (root.go:75-106):
+ * the Root's SelfParent has Round -1 and NextRound is 0, Others is empty. */
+static int32_t round_of(hgo *h, int32_t x);
+
+static int32_t *g_wbuf;
+static int32_t g_wcap;
+
+static int32_t round_impl(hgo *h, int32_t x) {
+  int32_t sp = h->sp[x], op = h->op[x];
+  if (sp < 0 && op < 0) return 0; /* directly attached to the Root: NextRound */
+  int32_t pr = sp < 0 ? -1 : round_of(h, sp);
+  if (op >= 0) {
+    int32_t opr = round_of(h, op);
+    if (opr > pr) pr = opr;
+  }
+  /* count the parentRound witnesses that x strongly sees */
+  int32_t nw = ri_witnesses(get_round(h, pr), &g_wbuf, &g_wcap);
+  int c = 0;
+  for (int32_t i = 0; i < nw; i++) c += strongly_see(h, x, g_wbuf[i]);
+  if (c >= h->sm) pr++;
+  return pr;
+}
+
+static int32_t round_of(hgo *h, int32_t x) {
+  if (x < 0) return -1; /* x is the Root: Root.SelfParent.Round */
+  if (h->round_memo[x] != UNSET) return h->round_memo[x];
+  int32_t r = round_impl(h, x);
+  h->round_memo[x] = r;
+  return r;
+}
+
+/* witness (hashgraph.go:281-296) */
+static int witness_of(hgo *h, int32_t x) { return round_of(h, x) > round_of(h, h->sp[x]); }
+
+/* lamportTimestamp / _lamportTimestamp (hashgraph.go:313-379) */
+static int32_t lamport_of(hgo *h, int32_t x) {
+  if (x < 0) return -1; /* Root.SelfParent.LamportTimestamp */
+  if (h->lt_memo[x] != UNSET) return h->lt_memo[x];
+  int32_t plt = lamport_of(h, h->sp[x]);
+  if (h->op[x] >= 0) {
+    int32_t o = lamport_of(h, h->op[x]);
+    if (o > plt) plt = o;
+  }
+  h->lt_memo[x] = plt + 1;
+  return plt + 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* InsertEvent (hashgraph.go:714-761)                                        */
+
+static void chain_push(hgo *h, int32_t c, int32_t id) {
+  if (h->chain_len[c] == h->chain_cap[c]) {
+    h->chain_cap[c] = h->chain_cap[c] ? 2 * h->chain_cap[c] : 64;
+    h->chain[c] = (int32_t *)xrealloc(h->chain[c], (size_t)h->chain_cap[c] * 4);
+  }
+  h->chain[c][h->chain_len[c]++] = id;
+}
+
+int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
+               const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx) {
+  if (creator < 0 || creator >= h->n) return HGO_ERR_BAD_CREATOR;
+  if (h->N >= h->cap) return HGO_ERR_CAPACITY;
+  /* checkSelfParent: self-parent must be the creator's last known event,
+   * or its Root when it has none (hashgraph.go:398-414, inmem_store.go:118-134) */
+  int32_t clen = h->chain_len[creator];
+  int32_t last = clen ? h->chain[creator][clen - 1] : -1;
+  if (sp != last) return HGO_ERR_SELF_PARENT;
+  /* checkOtherParent (hashgraph.go:417-436) */
+  if (op >= h->N || op < -1) return HGO_ERR_OTHER_PARENT;
+  /* Index continuity: ParticipantEventsCache.Set rejects skipped/passed
+   * indexes (caches.go / common/rolling_index.go:58-96) */
+  if (index != clen) return HGO_ERR_SELF_PARENT;
+
+  int32_t x = (int32_t)h->N++;
+  h->creator[x] = creator; h->index[x] = index; h->sp[x] = sp; h->op[x] = op;
+  h->ntx[x] = ntx;
+  memcpy(h->hash + (size_t)x * 32, hash32, 32);
+  memcpy(h->sigr + (size_t)x * 32, sig_r32, 32);
+  h->round_memo[x] = UNSET; h->lt_memo[x] = UNSET;
+  h->ev_round[x] = UNSET; h->ev_lt[x] = UNSET; h->ev_rr[x] = UNSET;
+  h->cons_pos[x] = -1;
+  h->ent_round[0][x] = h->ent_round[1][x] = INT32_MIN;
+
+  /* initEventCoordinates (hashgraph.go:439-507) */
+  int32_t n = h->n;
+  int32_t *la = LA(h, x), *fd = FD(h, x);
+  for (int32_t i = 0; i < n; i++) fd[i] = FD_NONE;
+  if (sp < 0 && op < 0) {
+    for (int32_t i = 0; i < n; i++) la[i] = -1;
+  } else if (sp < 0) {
+    memcpy(la, LA(h, op), (size_t)n * 4);
+  } else if (op < 0) {
+    memcpy(la, LA(h, sp), (size_t)n * 4);
+  } else {
+    const int32_t *a = LA(h, sp), *b = LA(h, op);
+    for (int32_t i = 0; i < n; i++) la[i] = a[i] < b[i] ? b[i] : a[i];
+  }
+  fd[creator] = index;
+  la[creator] = index;
+  chain_push(h, creator, x); /* Store.SetEvent -> addParticipantEvent */
+
+  /* updateAncestorFirstDescendant (hashgraph.go:510-544): walk each last
+   * ancestor's self-parent chain while its firstDescendant is unset */
+  for (int32_t i = 0; i < n; i++) {
+    int32_t k = la[i];
+    while (k >= 0) {
+      int32_t a = h->chain[i][k];
+      int32_t *fa = FD(h, a);
+      if (fa[creator] != FD_NONE) break;
+      fa[creator] = index;
+      k--; /* a.SelfParent(); the Root is not an event -> GetEvent fails -> break */
+    }
+  }
+
+  h->und[h->und_len++] = x; /* UndeterminedEvents */
+  if (index == 0 || ntx > 0) h->pending_loaded++; /* IsLoaded, event.go:169-178 */
+  return HGO_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* DivideRounds (hashgraph.go:767-849)                                       */
+
+int hgo_divide_rounds(hgo *h) {
+  for (int64_t u = 0; u < h->und_len; u++) {
+    int32_t x = h->und[u];
+    if (h->ev_round[x] == UNSET) {
+      int32_t r = round_of(h, x);
+      h->ev_round[x] = r;
+      round_info *ri = get_round(h, r);
+      int fresh = ri == NULL; /* GetRound KeyNotFound -> NewRoundInfo */
+      if (fresh) { ensure_round_cap(h, r); ri = &h->rounds[r]; }
+      if (!ri->queued && (!h->has_lcr || r >= h->lcr)) {
+        if (h->pend_len == h->pend_cap) {
+          h->pend_cap = h->pend_cap ? 2 * h->pend_cap : 64;
+          h->pend = (pending_round *)xrealloc(h->pend, (size_t)h->pend_cap * sizeof(pending_round));
+        }
+        h->pend[h->pend_len].index = r;
+        h->pend[h->pend_len].decided = 0;
+        h->pend_len++;
+        ri->queued = 1;
+      }
+      int w = witness_of(h, x);
+      ri_add_event(h, r, x, w);
+      set_round(h, r);
+    }
+    if (h->ev_lt[x] == UNSET) h->ev_lt[x] = lamport_of(h, x);
+  }
+  return HGO_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* DecideFame (hashgraph.go:852-947)                                         */
+
+static int middle_bit(const hgo *h, int32_t y) { /* hashgraph.go:1526-1535 */
+  return h->hash[(size_t)y * 32 + 16] != 0;
+}
+
+int hgo_decide_fame(hgo *h) {
+  int32_t *W = NULL, wcap = 0;      /* Witnesses of round r */
+  int32_t *Wj = NULL, wjcap = 0;    /* RoundWitnesses(j) */
+  int32_t *Wp = NULL, wpcap = 0;    /* RoundWitnesses(j-1) */
+  /* The Go votes map is keyed [y][x]; for a fixed x the j iteration only
+   * reads the votes cast in round j-1, so two arrays indexed by witness
+   * position carry exactly the same data flow. */
+  int8_t *vprev = NULL, *vcur = NULL;
+  int32_t vcap = 0;
+  int8_t *decided = (int8_t *)xcalloc((size_t)h->pend_len, 1);
+
+  for (int32_t pos = 0; pos < h->pend_len; pos++) {
+    int32_t r = h->pend[pos].index;
+    round_info *ri = get_round(h, r);
+    if (!ri) { free(W); free(Wj); free(Wp); free(vprev); free(vcur); free(decided); return HGO_ERR_STATE; }
+    int32_t nw = ri_witnesses(ri, &W, &wcap);
+    for (int32_t xi = 0; xi < nw; xi++) {
+      int32_t x = W[xi];
+      round_event *rex = ri_find(h, r, x);
+      if (rex && rex->witness && rex->famous != TRI_UNDEFINED) continue; /* IsDecided */
+      int32_t nprev = 0;
+      for (int32_t j = r + 1; j <= h->last_round; j++) {
+        int32_t nj = ri_witnesses(get_round(h, j), &Wj, &wjcap);
+        if (nj > vcap) {
+          vcap = nj * 2;
+          vprev = (int8_t *)xrealloc(vprev, (size_t)vcap);
+          vcur = (int8_t *)xrealloc(vcur, (size_t)vcap);
+        }
+        int32_t diff = j - r;
+        int decided_x = 0;
+        for (int32_t yi = 0; yi < nj; yi++) {
+          int32_t y = Wj[yi];
+          if (diff == 1) {
+            vcur[yi] = (int8_t)see(h, y, x);
+          } else {
+            int32_t np = ri_witnesses(get_round(h, j - 1), &Wp, &wpcap);
+            int yays = 0, nays = 0;
+            for (int32_t wi = 0; wi < np; wi++) {
+              if (!strongly_see(h, y, Wp[wi])) continue;
+              if (wi < nprev && vprev[wi]) yays++;
+              else nays++;
+            }
+            int v = 0, t = nays;
+            if (yays >= nays) { v = 1; t = yays; }
+            if (diff % h->n > 0) { /* normal round: math.Mod(diff, n) > 0 */
+              if (t >= h->sm) {
+                rex->famous = v ? TRI_TRUE : TRI_FALSE; /* SetFame */
+                vcur[yi] = (int8_t)v;
+                decided_x = 1;
+                break; /* break VOTE_LOOP */
+              }
+              vcur[yi] = (int8_t)v;
+            } else { /* coin round */
+              vcur[yi] = (int8_t)(t >= h->sm ? v : middle_bit(h, y));
+            }
+          }
+        }
+        if (decided_x) break;
+        int8_t *tmp = vprev; vprev = vcur; vcur = tmp;
+        nprev = nj;
+      }
+    }
+    set_round(h, r);
+    if (ri_witnesses_decided(ri)) decided[pos] = 1;
+  }
+  /* updatePendingRounds (hashgraph.go:689-695) */
+  for (int32_t pos = 0; pos < h->pend_len; pos++)
+    if (decided[pos]) h->pend[pos].decided = 1;
+  free(W); free(Wj); free(Wp); free(vprev); free(vcur); free(decided);
+  return HGO_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* DecideRoundReceived (hashgraph.go:951-1036)                               */
+
+int hgo_decide_round_received(hgo *h) {
+  int32_t *FW = NULL;
+  int32_t fcap = 0;
+  int64_t keep = 0;
+  for (int64_t u = 0; u < h->und_len; u++) {
+    int32_t x = h->und[u];
+    int received = 0;
+    int32_t r = round_of(h, x);
+    for (int32_t i = r + 1; i <= h->last_round; i++) {
+      round_info *tr = get_round(h, i);
+      if (!tr) {
+        if (h->has_lcr && r < h->lcr) { received = 1; break; }
+        free(FW);
+        return HGO_ERR_STATE;
+      }
+      if (!ri_witnesses_decided(tr)) break;
+      /* FamousWitnesses (roundInfo.go:120-128) */
+      int32_t nf = 0;
+      for (int32_t k = 0; k < tr->len; k++) {
+        if (!(tr->ev[k].witness && tr->ev[k].famous == TRI_TRUE)) continue;
+        if (nf == fcap) { fcap = fcap ? 2 * fcap : 64; FW = (int32_t *)xrealloc(FW, (size_t)fcap * 4); }
+        FW[nf++] = tr->ev[k].id;
+      }
+      int32_t s = 0;
+      for (int32_t k = 0; k < nf; k++) s += see(h, FW[k], x);
+      if (s == nf && s > 0) {
+        received = 1;
+        h->ev_rr[x] = i;
+        /* RoundInfo.SetConsensusEvent (roundInfo.go:53-60) */
+        round_event *e = ri_find(h, i, x);
+        if (!e) e = ri_append(h, i, x);
+        e->consensus = 1;
+        set_round(h, i);
+        break;
+      }
+    }
+    if (!received) h->und[keep++] = x;
+  }
+  h->und_len = keep;
+  free(FW);
+  return HGO_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* GetFrame + ProcessDecidedRounds (hashgraph.go:1041-1231)                  */
+
+static const hgo *g_sort_h;
+/* ByLamportTimestamp.Less (event.go:332-347): LT, then the ECDSA r parsed
+ * as a big.Int.  r is held as 32 big-endian bytes, so memcmp == Cmp. */
+static int cmp_lamport(const void *a, const void *b) {
+  int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+  int32_t tx = g_sort_h->ev_lt[x] == UNSET ? -1 : g_sort_h->ev_lt[x];
+  int32_t ty = g_sort_h->ev_lt[y] == UNSET ? -1 : g_sort_h->ev_lt[y];
+  if (tx != ty) return tx < ty ? -1 : 1;
+  return memcmp(g_sort_h->sigr + (size_t)x * 32, g_sort_h->sigr + (size_t)y * 32, 32);
+}
+
+static int get_frame(hgo *h, int32_t rr, int64_t *first, int64_t *len) {
+  ensure_round_cap(h, rr);
+  if (h->frame_done[rr]) { *first = h->frame_first[rr]; *len = h->frame_len[rr]; return HGO_OK; }
+  round_info *ri = get_round(h, rr);
+  if (!ri) return HGO_ERR_STATE;
+  int64_t f = h->frame_ev_len;
+  for (int32_t k = 0; k < ri->len; k++)
+    if (ri->ev[k].consensus) h->frame_ev[h->frame_ev_len++] = ri->ev[k].id;
+  int64_t l = h->frame_ev_len - f;
+  g_sort_h = h;
+  qsort(h->frame_ev + f, (size_t)l, 4, cmp_lamport); /* sort.Sort(ByLamportTimestamp) */
+  h->frame_done[rr] = 1; h->frame_first[rr] = f; h->frame_len[rr] = l;
+  *first = f; *len = l;
+  return HGO_OK;
+}
+
+int hgo_process_decided_rounds(hgo *h) {
+  int32_t processed = 0;
+  for (int32_t p = 0; p < h->pend_len; p++) {
+    pending_round *pr = &h->pend[p];
+    if (!pr->decided) break;
+    if (h->has_lcr && pr->index == h->lcr) continue;
+    int64_t f, l;
+    if (get_frame(h, pr->index, &f, &l) != HGO_OK) return HGO_ERR_STATE;
+    if (l > 0) {
+      int64_t first = h->ncons, txs = 0;
+      for (int64_t k = 0; k < l; k++) {
+        int32_t e = h->frame_ev[f + k];
+        h->cons_pos[e] = h->ncons;
+        h->cons[h->ncons++] = e; /* Store.AddConsensusEvent */
+        h->consensus_txs += h->ntx[e];
+        txs += h->ntx[e];
+        if (h->index[e] == 0 || h->ntx[e] > 0) h->pending_loaded--;
+      }
+      /* NewBlockFromFrame(LastBlockIndex()+1, frame) (block.go:100-110) */
+      if (h->nblocks == h->blk_cap) {
+        h->blk_cap = h->blk_cap ? 2 * h->blk_cap : 64;
+        h->blk_rr = (int32_t *)xrealloc(h->blk_rr, (size_t)h->blk_cap * 4);
+        h->blk_first = (int64_t *)xrealloc(h->blk_first, (size_t)h->blk_cap * 8);
+        h->blk_count = (int64_t *)xrealloc(h->blk_count, (size_t)h->blk_cap * 8);
+        h->blk_ntx = (int64_t *)xrealloc(h->blk_ntx, (size_t)h->blk_cap * 8);
+      }
+      h->blk_rr[h->nblocks] = pr->index;
+      h->blk_first[h->nblocks] = first;
+      h->blk_count[h->nblocks] = l;
+      h->blk_ntx[h->nblocks] = txs;
+      h->nblocks++;
+    }
+    processed++;
+    if (!h->has_lcr || pr->index > h->lcr) { h->has_lcr = 1; h->lcr = pr->index; }
+  }
+  /* defer: h.PendingRounds = h.PendingRounds[processedIndex:] */
+  memmove(h->pend, h->pend + processed, (size_t)(h->pend_len - processed) * sizeof(pending_round));
+  h->pend_len -= processed;
+  return HGO_OK;
+}
+
+int hgo_run_consensus(hgo *h) {
+  int rc;
+  if ((rc = hgo_divide_rounds(h))) return rc;
+  if ((rc = hgo_decide_fame(h))) return rc;
+  if ((rc = hgo_decide_round_received(h))) return rc;
+  return hgo_process_decided_rounds(h);
+}
+
+/* ------------------------------------------------------------------------ */
+/* queries                                                                   */
+
+int64_t hgo_num_events(const hgo *h) { return h->N; }
+int32_t hgo_last_round(const hgo *h) { return h->last_round; }
+int32_t hgo_last_consensus_round(const hgo *h) { return h->has_lcr ? h->lcr : -1; }
+int64_t hgo_consensus_transactions(const hgo *h) { return h->consensus_txs; }
+int64_t hgo_pending_loaded_events(const hgo *h) { return h->pending_loaded; }
+int64_t hgo_num_consensus_events(const hgo *h) { return h->ncons; }
+int64_t hgo_num_undetermined(const hgo *h) { return h->und_len; }
+int64_t hgo_num_blocks(const hgo *h) { return h->nblocks; }
+
+void hgo_event_results(const hgo *h, int32_t *round, int8_t *witness, int32_t *lt,
+                       int32_t *rr, int8_t *fame, int64_t *cons_pos) {
+  for (int64_t x = 0; x < h->N; x++) {
+    int32_t r = h->ev_round[x];
+    if (round) round[x] = r;
+    if (lt) lt[x] = h->ev_lt[x];
+    if (rr) rr[x] = h->ev_rr[x];
+    if (cons_pos) cons_pos[x] = h->cons_pos[x];
+    int8_t w = 0, f = -1;
+    if (r != UNSET && r >= 0 && r < h->rounds_cap && h->rounds[r].exists) {
+      const round_event *e = ri_find((hgo *)h, r, (int32_t)x);
+      if (e) {
+        w = (int8_t)e->witness;
+        if (w) f = (int8_t)e->famous;
+      }
+    }
+    if (witness) witness[x] = w;
+    if (fame) fame[x] = f;
+  }
+}
+
+void hgo_consensus_order(const hgo *h, int32_t *ids) {
+  memcpy(ids, h->cons, (size_t)h->ncons * 4);
+}
+
+void hgo_blocks(const hgo *h, int32_t *round_received, int64_t *first, int64_t *count,
+                int64_t *ntx) {
+  for (int64_t b = 0; b < h->nblocks; b++) {
+    if (round_received) round_received[b] = h->blk_rr[b];
+    if (first) first[b] = h->blk_first[b];
+    if (count) count[b] = h->blk_count[b];
+    if (ntx) ntx[b] = h->blk_ntx[b];
+  }
+}
+
+int32_t hgo_pending_rounds(const hgo *h, int32_t *index, int8_t *decided, int32_t cap) {
+  for (int32_t p = 0; p < h->pend_len && p < cap; p++) {
+    if (index) index[p] = h->pend[p].index;
+    if (decided) decided[p] = h->pend[p].decided;
+  }
+  return h->pend_len;
+}
+
+void hgo_coordinates(const hgo *h, int32_t id, int32_t *la, int32_t *fd) {
+  if (la) memcpy(la, LA(h, id), (size_t)h->n * 4);
+  if (fd) memcpy(fd, FD(h, id), (size_t)h->n * 4);
+}
+
+int64_t hgo_undetermined(const hgo *h, int32_t *ids, int64_t cap) {
+  int64_t k = h->und_len < cap ? h->und_len : cap;
+  if (ids) memcpy(ids, h->und, (size_t)k * 4);
+  return h->und_len;
+}
+
+int hgo_see(hgo *h, int32_t x, int32_t y) { return see(h, x, y); }
+int hgo_strongly_see(hgo *h, int32_t x, int32_t y) { return strongly_see(h, x, y); }
+int32_t hgo_round_of(hgo *h, int32_t x) { return round_of(h, x); }
+int32_t hgo_lamport_of(hgo *h, int32_t x) { return lamport_of(h, x); }
+int hgo_witness_of(hgo *h, int32_t x) { return witness_of(h, x); }

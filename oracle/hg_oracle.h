@@ -1,0 +1,97 @@
+/*
+ * hg_oracle.h -- CPU restatement of Babble v0.4.0's hashgraph consensus passes.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This oracle is the parity checker for the
+ * MI355X engine (libbabble_hip).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product path never calls it.
+ *
+ * It follows the reference Go code control flow literally (recursion with
+ * memoisation, the UndeterminedEvents / PendingRounds state machine, the
+ * RoundInfo bookkeeping, the DecideFame vote loop), single threaded, because
+ * the reference consensus is single threaded (no goroutines in
+ * src/hashgraph).  Citations are reference paths (/root/reference/src/...).
+ *
+ * Parity pin: the Go toolchain is absent, so the reference cannot run here.
+ * The restatement is pinned by the known-answer DAG tests of
+ * src/hashgraph/hashgraph_test.go transcribed as tests/golden/kat_*.json and
+ * checked by tests/test_oracle_kat.py.
+ *
+ * Scope: fresh hashgraphs (base roots, hashgraph/root.go:75-106); Reset
+ * roots (root.Others) are a later row.
+ */
+#ifndef HG_ORACLE_H
+#define HG_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hgo hgo;
+
+/* status codes mirror the Go error kinds (common/errors.go:7-15) */
+enum {
+  HGO_OK = 0,
+  HGO_ERR_SELF_PARENT = 1,   /* "Self-parent not last known event by creator" hashgraph.go:409 */
+  HGO_ERR_OTHER_PARENT = 2,  /* "Other-parent not known" hashgraph.go:432 */
+  HGO_ERR_BAD_CREATOR = 3,   /* unknown participant */
+  HGO_ERR_CAPACITY = 4,
+  HGO_ERR_STATE = 5
+};
+
+/* participant_ids: peer IDs (FNV-1a-32 of pubkey) sorted ascending
+ * (peers/peers.go:63-73).  Slot i of every coordinate vector is participant i. */
+hgo *hgo_create(int32_t n, const int64_t *participant_ids, int64_t capacity);
+void hgo_destroy(hgo *h);
+
+/* InsertEvent (hashgraph.go:714-761), minus signature verification (the
+ * inputs are pre-verified).  sp = global id of the self-parent or
+ * -1 for the creator's Root; op = global id of the other-parent or -1 for "".
+ * hash: 32-byte SHA-256 of the Go-JSON body; sig_r: 32-byte big-endian ECDSA r.
+ * Returns HGO_OK (the event gets the next global id) or an error (rejected). */
+int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
+               const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx);
+
+int hgo_divide_rounds(hgo *h);            /* hashgraph.go:767-849 */
+int hgo_decide_fame(hgo *h);              /* hashgraph.go:852-947 */
+int hgo_decide_round_received(hgo *h);    /* hashgraph.go:951-1036 */
+int hgo_process_decided_rounds(hgo *h);   /* hashgraph.go:1041-1122 */
+int hgo_run_consensus(hgo *h);            /* the four, node/core.go:335-377 */
+
+/* ---- queries (test/bench harness) ---- */
+int64_t hgo_num_events(const hgo *h);
+int32_t hgo_last_round(const hgo *h);                 /* InmemStore.LastRound */
+int32_t hgo_last_consensus_round(const hgo *h);       /* -1 == nil */
+int64_t hgo_consensus_transactions(const hgo *h);
+int64_t hgo_pending_loaded_events(const hgo *h);
+int64_t hgo_num_consensus_events(const hgo *h);
+int64_t hgo_num_undetermined(const hgo *h);
+int64_t hgo_num_blocks(const hgo *h);
+
+/* per-event results; round/lt/rr = INT32_MIN when unset (Go nil pointer);
+ * fame: 0 Undefined, 1 True, 2 False (roundInfo.go:10-16) or -1 not a witness;
+ * cons_pos = position in the consensus order or -1 */
+void hgo_event_results(const hgo *h, int32_t *round, int8_t *witness, int32_t *lt,
+                       int32_t *rr, int8_t *fame, int64_t *cons_pos);
+/* consensus order (event ids), length hgo_num_consensus_events */
+void hgo_consensus_order(const hgo *h, int32_t *ids);
+/* blocks: index, round_received, first consensus position, #events, #txs */
+void hgo_blocks(const hgo *h, int32_t *round_received, int64_t *first, int64_t *count,
+                int64_t *ntx);
+/* pending rounds queue */
+int32_t hgo_pending_rounds(const hgo *h, int32_t *index, int8_t *decided, int32_t cap);
+/* coordinates (lastAncestors / firstDescendants indexes) of one event */
+void hgo_coordinates(const hgo *h, int32_t id, int32_t *la, int32_t *fd);
+/* UndeterminedEvents queue, in order */
+int64_t hgo_undetermined(const hgo *h, int32_t *ids, int64_t cap);
+/* primitives, exposed for the ancestry known-answer tests */
+int hgo_see(hgo *h, int32_t x, int32_t y);
+int hgo_strongly_see(hgo *h, int32_t x, int32_t y);
+int32_t hgo_round_of(hgo *h, int32_t x);
+int32_t hgo_lamport_of(hgo *h, int32_t x);
+int hgo_witness_of(hgo *h, int32_t x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
