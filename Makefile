@@ -1,0 +1,24 @@
+# Top-level build: the HIP engine (gfx950), the DAG generator, the CPU oracle.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
+CC ?= gcc
+
+ENGINE_SRC := $(wildcard babble_amd/csrc/engine/*.hip) $(wildcard babble_amd/csrc/engine/*.cpp)
+ENGINE_HDR := $(wildcard babble_amd/csrc/engine/*.h) include/babble_hip.h
+
+all: babble_amd/libbabble_gen.so babble_amd/libbabble_hip.so oracle/liboracle.so
+
+babble_amd/libbabble_gen.so: babble_amd/csrc/dag_gen.c babble_amd/csrc/dag_gen.h
+	$(CC) -O2 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
+
+babble_amd/libbabble_hip.so: $(ENGINE_SRC) $(ENGINE_HDR)
+	$(HIPCC) $(HIPFLAGS) -Iinclude -shared -o $@ $(ENGINE_SRC)
+
+oracle/liboracle.so: oracle/hg_oracle.c oracle/hg_oracle.h
+	$(MAKE) -C oracle
+
+clean:
+	rm -f babble_amd/*.so oracle/*.so
+
+.PHONY: all clean

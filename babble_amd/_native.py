@@ -1,0 +1,83 @@
+"""ctypes binding of libbabble_hip.so (include/babble_hip.h).
+
+The product path: every call below runs HIP kernels on the MI355X.  There is
+no CPU fallback -- if the library or a device is missing this raises.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbabble_hip.so")
+
+BH_OK = 0
+ERRORS = {
+    1: "SelfParent", 2: "OtherParent", 3: "UnknownParticipant", 4: "SkippedIndex",
+    5: "Capacity", 6: "State", 7: "Invalid", 8: "Device",
+}
+
+# exported symbols, in include/babble_hip.h order (checked by tests)
+SYMBOLS = (
+    "bh_create", "bh_destroy", "bh_last_error", "bh_insert_events", "bh_divide_rounds",
+    "bh_decide_fame", "bh_decide_round_received", "bh_process_decided_rounds",
+    "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
+    "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
+    "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile",
+)
+
+
+class Config(C.Structure):
+    _fields_ = [("n_participants", C.c_int32), ("participant_ids", C.POINTER(C.c_int64)),
+                ("max_events", C.c_int64), ("device", C.c_int32)]
+
+
+class Events(C.Structure):
+    _fields_ = [("count", C.c_int64), ("creator_id", C.c_void_p), ("index", C.c_void_p),
+                ("self_parent_index", C.c_void_p), ("other_parent_creator_id", C.c_void_p),
+                ("other_parent_index", C.c_void_p), ("hash", C.c_void_p), ("sig_r", C.c_void_p),
+                ("n_transactions", C.c_void_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("n_events", C.c_int64), ("last_round", C.c_int32),
+                ("last_consensus_round", C.c_int32), ("consensus_events", C.c_int64),
+                ("consensus_transactions", C.c_int64), ("pending_loaded_events", C.c_int64),
+                ("undetermined_events", C.c_int64), ("blocks", C.c_int64),
+                ("pending_rounds", C.c_int32)]
+
+
+_LIB = None
+
+
+def load():
+    """Load libbabble_hip.so; raises if it was not built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `make` or __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    P, VP, I32, I64 = C.c_void_p, C.c_void_p, C.c_int32, C.c_int64
+    L.bh_create.argtypes = [C.POINTER(Config), C.POINTER(P)]
+    L.bh_create.restype = C.c_int
+    L.bh_destroy.argtypes = [P]
+    L.bh_last_error.argtypes = [P]
+    L.bh_last_error.restype = C.c_char_p
+    L.bh_insert_events.argtypes = [P, C.POINTER(Events), VP, C.POINTER(I64)]
+    for f in ("bh_divide_rounds", "bh_decide_fame", "bh_decide_round_received",
+              "bh_process_decided_rounds", "bh_run_consensus", "bh_synchronize"):
+        getattr(L, f).argtypes = [P]
+        getattr(L, f).restype = C.c_int
+    L.bh_get_stats.argtypes = [P, C.POINTER(Stats)]
+    L.bh_get_event_meta.argtypes = [P, I64, I64, VP, VP, VP, VP, VP, VP]
+    L.bh_get_consensus_order.argtypes = [P, I64, I64, VP]
+    L.bh_get_blocks.argtypes = [P, I64, I64, VP, VP, VP, VP]
+    L.bh_get_pending_rounds.argtypes = [P, VP, VP, I32]
+    L.bh_get_pending_rounds.restype = I32
+    L.bh_get_undetermined.argtypes = [P, VP, I64]
+    L.bh_get_undetermined.restype = I64
+    L.bh_get_coordinates.argtypes = [P, I64, VP, VP]
+    L.bh_get_stage_ms.argtypes = [P, C.POINTER(C.c_float), I32]
+    L.bh_get_stage_ms.restype = I32
+    L.bh_get_profile.argtypes = [P, C.POINTER(I64), C.POINTER(C.c_float)]
+    _LIB = L
+    return L

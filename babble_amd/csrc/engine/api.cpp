@@ -1,0 +1,631 @@
+// api.cpp -- C ABI of libbabble_hip (include/babble_hip.h): host state of the
+// drop-in Hashgraph, insert validation, stage orchestration on one HIP
+// stream, result queries.  No CPU fallback: every consensus stage runs as
+// HIP kernels on the device; without a device bh_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "babble_hip.h"
+#include "engine.h"
+
+using bh::Dev;
+
+namespace {
+
+constexpr int ITER_BATCH = 32;  // round-loop iterations per graph replay
+constexpr int NSTAGE = 5;
+
+struct Block {
+  int32_t rr;
+  int64_t first, count, ntx;
+};
+
+}  // namespace
+
+struct bh_handle {
+  Dev d{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int64_t cap = 0;
+  // host mirrors (insert bookkeeping: ParticipantEventsCache + checks)
+  std::vector<int64_t> pids;
+  std::unordered_map<int64_t, int32_t> slot_of;
+  std::vector<std::vector<int32_t>> chain;  // ids by creator, by index
+  std::vector<int32_t> h_creator, h_index, h_sp, h_op, h_ntx;
+  std::vector<uint8_t> h_coin;
+  std::vector<uint32_t> h_sigw;
+  int64_t uploaded = 0;  // events already on the device
+  int64_t loaded_total = 0;
+  // stage bookkeeping: 0 none, 1 rounds, 2 fame, 3 rr, 4 processed
+  int stage = 0;
+  int coords_for = -1;  // N the device coordinates were computed for
+  int32_t R = 0, P = 0;
+  int64_t ncons = 0, cons_txs = 0, cons_loaded = 0, nreceived = 0;
+  std::vector<Block> blocks;
+  std::vector<int8_t> decided_h;
+  // round-loop graph
+  hipGraphExec_t graph = nullptr;
+  Dev graph_dev{};
+  int32_t *pinned_state = nullptr;
+  hipEvent_t ev[NSTAGE + 1]{};
+  hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)
+  float sweep_ms = 0;
+  float stage_ms[NSTAGE]{};
+  int64_t iters = 0;
+  int64_t *d_counters_host = nullptr;
+
+  int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+};
+
+#define HIPCHK(h, call)                                                              \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return (h)->fail(BH_ERR_DEVICE, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                       __FILE__, __LINE__);                                          \
+  } while (0)
+
+namespace {
+
+template <class T>
+int dalloc(bh_handle *h, T **p, size_t count) {
+  HIPCHK(h, hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T)));
+  return BH_OK;
+}
+
+void free_all(bh_handle *h) {
+  Dev &d = h->d;
+  void *ptrs[] = {d.creator, d.index, d.sp, d.op, d.ntx, d.coin, d.sigw, d.chain_start,
+                  d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.B,
+                  d.wofs, d.wcnt, d.wids, d.fdw, d.state, d.round, d.witness, d.fame,
+                  d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (h->pinned_state) (void)hipHostFree(h->pinned_state);
+  if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  for (auto &e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &e : h->ev_sweep)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+}
+
+// upload events inserted since the last upload
+int upload(bh_handle *h) {
+  const int64_t a = h->uploaded, b = (int64_t)h->h_creator.size();
+  if (b == a) return BH_OK;
+  const size_t k = (size_t)(b - a);
+  Dev &d = h->d;
+  hipStream_t s = h->stream;
+  HIPCHK(h, hipMemcpyAsync(d.creator + a, h->h_creator.data() + a, k * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d.index + a, h->h_index.data() + a, k * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d.sp + a, h->h_sp.data() + a, k * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d.op + a, h->h_op.data() + a, k * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d.ntx + a, h->h_ntx.data() + a, k * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d.coin + a, h->h_coin.data() + a, k, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(d.sigw + a * 8, h->h_sigw.data() + a * 8, k * 32, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  h->uploaded = b;
+  return BH_OK;
+}
+
+int set_chain_tables(bh_handle *h) {
+  const int n = h->d.n;
+  std::vector<int32_t> start(n), len(n);
+  int32_t acc = 0;
+  for (int c = 0; c < n; ++c) {
+    start[c] = acc;
+    len[c] = (int32_t)h->chain[c].size();
+    acc += len[c];
+  }
+  HIPCHK(h, hipMemcpyAsync(h->d.chain_start, start.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->d.chain_len, len.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
+
+int build_graph(bh_handle *h) {
+  if (h->graph && memcmp(&h->graph_dev, &h->d, sizeof(Dev)) == 0) return BH_OK;
+  if (h->graph) {
+    (void)hipGraphExecDestroy(h->graph);
+    h->graph = nullptr;
+  }
+  hipGraph_t g;
+  HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(h->d, h->stream);
+  HIPCHK(h, hipStreamEndCapture(h->stream, &g));
+  HIPCHK(h, hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0));
+  (void)hipGraphDestroy(g);
+  h->graph_dev = h->d;
+  return BH_OK;
+}
+
+// stage 1: coordinates, Lamport timestamps, rounds, witnesses
+int stage_rounds(bh_handle *h) {
+  int rc;
+  if ((rc = upload(h))) return rc;
+  Dev &d = h->d;
+  d.N = (int64_t)h->h_creator.size();
+  if ((rc = set_chain_tables(h))) return rc;
+  hipStream_t s = h->stream;
+  HIPCHK(h, hipEventRecord(h->ev[0], s));
+  bh::launch_prep(d, s);
+  bh::launch_chunk_depth(d, s);
+  HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
+  bh::launch_la_sweep(d, s);
+  HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev[1], s));
+  h->coords_for = (int)d.N;
+  if (d.N == 0) {
+    h->R = 0;
+    h->stage = 1;
+    return BH_OK;
+  }
+  if ((rc = build_graph(h))) return rc;
+  // replay batches of iterations; check completion one batch behind so the
+  // device never idles on the host round trip
+  hipEvent_t done_ev[2];
+  HIPCHK(h, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
+  HIPCHK(h, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
+  int32_t *pin = h->pinned_state;
+  bool done = false;
+  int64_t launched = 0;
+  const int64_t max_batches = (int64_t)d.R_cap / ITER_BATCH + 2;
+  for (int64_t b = 0; b < max_batches && !done; ++b) {
+    HIPCHK(h, hipGraphLaunch(h->graph, s));
+    HIPCHK(h, hipMemcpyAsync(pin + (b & 1) * bh::ST_COUNT, d.state, bh::ST_COUNT * 4,
+                             hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
+    ++launched;
+    if (b > 0) {
+      HIPCHK(h, hipEventSynchronize(done_ev[(b - 1) & 1]));
+      if (pin[((b - 1) & 1) * bh::ST_COUNT + bh::ST_DONE]) done = true;
+    }
+  }
+  HIPCHK(h, hipStreamSynchronize(s));
+  (void)hipEventDestroy(done_ev[0]);
+  (void)hipEventDestroy(done_ev[1]);
+  int32_t st[bh::ST_COUNT];
+  HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
+  if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
+  if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
+  h->R = st[bh::ST_ROUNDS];
+  h->iters = st[bh::ST_ITERS];
+  bh::launch_assign_rounds(d, s);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev[2], s));
+  h->stage = 1;
+  h->decided_h.assign((size_t)h->R, 0);
+  h->P = 0;
+  h->blocks.clear();
+  h->ncons = h->cons_txs = h->cons_loaded = h->nreceived = 0;
+  return BH_OK;
+}
+
+int stage_fame(bh_handle *h) {
+  if (h->stage < 1) return h->fail(BH_ERR_STATE, "DecideFame before DivideRounds");
+  bh::launch_fame(h->d, h->R, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
+  if (h->R > 0)
+    HIPCHK(h, hipMemcpyAsync(h->decided_h.data(), h->d.decided, (size_t)h->R, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost));
+  if (err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
+  h->stage = 2;
+  return BH_OK;
+}
+
+int stage_rr(bh_handle *h) {
+  if (h->stage < 2) return h->fail(BH_ERR_STATE, "DecideRoundReceived before DecideFame");
+  bh::launch_round_received(h->d, h->R, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev[4], h->stream));
+  h->stage = 3;
+  return BH_OK;
+}
+
+int stage_order(bh_handle *h) {
+  if (h->stage < 3) return h->fail(BH_ERR_STATE, "ProcessDecidedRounds before DecideRoundReceived");
+  Dev &d = h->d;
+  hipStream_t s = h->stream;
+  bh::launch_order(d, h->R, s);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev[5], s));
+  HIPCHK(h, hipStreamSynchronize(s));
+  int32_t st[bh::ST_COUNT];
+  int64_t ctr[4];
+  HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(ctr, d.counters, sizeof ctr, hipMemcpyDeviceToHost));
+  h->P = st[bh::ST_P];
+  h->ncons = st[bh::ST_NCONS];
+  h->cons_txs = ctr[0];
+  h->cons_loaded = ctr[1];
+  h->nreceived = ctr[2];
+  h->blocks.clear();
+  if (h->P > 0) {
+    std::vector<int32_t> cnt(h->P), ofs(h->P);
+    std::vector<int64_t> ntx(h->P);
+    HIPCHK(h, hipMemcpy(cnt.data(), d.frame_cnt, h->P * 4, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(ofs.data(), d.frame_ofs, h->P * 4, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(ntx.data(), d.frame_ntx, h->P * 8, hipMemcpyDeviceToHost));
+    for (int32_t r = 0; r < h->P; ++r)
+      if (cnt[r] > 0) h->blocks.push_back(Block{r, ofs[r], cnt[r], ntx[r]});
+  }
+  h->stage = 4;
+  for (int i = 0; i < NSTAGE; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]) == hipSuccess) h->stage_ms[i] = ms;
+  }
+  float sms = 0;
+  if (hipEventElapsedTime(&sms, h->ev_sweep[0], h->ev_sweep[1]) == hipSuccess) h->sweep_ms = sms;
+  return BH_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+extern "C" {
+
+int bh_create(const bh_config *cfg, bh_handle **out) {
+  if (!cfg || !out || cfg->n_participants < 1 || cfg->max_events < 0 || !cfg->participant_ids)
+    return BH_ERR_INVALID;
+  *out = nullptr;
+  bh_handle *h = new bh_handle();
+  const int n = cfg->n_participants;
+  for (int i = 1; i < n; ++i)
+    if (cfg->participant_ids[i] <= cfg->participant_ids[i - 1]) {
+      delete h;
+      return BH_ERR_INVALID;  // peers must be ID-sorted (peers.go:63-73)
+    }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) {
+    delete h;
+    return BH_ERR_DEVICE;
+  }
+  if (hipSetDevice(cfg->device) != hipSuccess) {
+    delete h;
+    return BH_ERR_DEVICE;
+  }
+  h->device = cfg->device;
+  h->pids.assign(cfg->participant_ids, cfg->participant_ids + n);
+  for (int i = 0; i < n; ++i) h->slot_of[h->pids[i]] = i;
+  h->chain.resize(n);
+  h->cap = cfg->max_events;
+  Dev &d = h->d;
+  d.n = n;
+  d.npad = (n + 3) & ~3;
+  d.sm = 2 * n / 3 + 1;  // hashgraph.go:54
+  d.N = 0;
+  const int64_t C = std::max<int64_t>(h->cap, 1);
+  d.R_cap = (int32_t)std::min<int64_t>(C / d.sm + 2, INT32_MAX / 2);
+  d.W_cap = C + n;
+  const size_t R1 = (size_t)d.R_cap + 1;
+  int rc = BH_OK;
+  auto A = [&](auto **p, size_t cnt) {
+    if (rc == BH_OK) rc = dalloc(h, p, cnt);
+  };
+  A(&d.creator, C); A(&d.index, C); A(&d.sp, C); A(&d.op, C); A(&d.ntx, C);
+  A(&d.coin, C); A(&d.sigw, (size_t)C * 8);
+  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C);
+  A(&d.la, (size_t)C * d.npad); A(&d.lt, C); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1);
+  A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
+  A(&d.fdw, (size_t)d.W_cap * d.npad); A(&d.state, bh::ST_COUNT);
+  A(&d.round, C); A(&d.witness, C); A(&d.fame, C);
+  A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
+  A(&d.frame_cnt, R1); A(&d.frame_ofs, R1); A(&d.frame_cur, R1); A(&d.blk_of_frame, R1);
+  A(&d.order, C); A(&d.cons_pos, C); A(&d.frame_ntx, R1); A(&d.counters, 4);
+  if (rc == BH_OK) {
+    bh::configure_round_kernels();
+    bh::configure_fame_kernels();
+    bh::configure_order_kernels();
+  }
+  if (rc == BH_OK && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipHostMalloc((void **)&h->pinned_state, 2 * bh::ST_COUNT * 4, 0) != hipSuccess)
+    rc = BH_ERR_DEVICE;
+  for (auto &e : h->ev)
+    if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
+  for (auto &e : h->ev_sweep)
+    if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipMemset(d.state, 0, bh::ST_COUNT * 4) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipMemset(d.counters, 0, 4 * 8) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc != BH_OK) {
+    free_all(h);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return BH_OK;
+}
+
+void bh_destroy(bh_handle *h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  free_all(h);
+  delete h;
+}
+
+const char *bh_last_error(const bh_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted) {
+  if (!h || !ev) return BH_ERR_INVALID;
+  if (!ev->creator_id || !ev->index || !ev->self_parent_index || !ev->other_parent_creator_id ||
+      !ev->other_parent_index || !ev->hash || !ev->sig_r || !ev->n_transactions)
+    return h->fail(BH_ERR_INVALID, "null field in bh_events");
+  int first = BH_OK;
+  int64_t acc = 0;
+  for (int64_t i = 0; i < ev->count; ++i) {
+    int code = BH_OK;
+    int32_t c = -1, op = -1;
+    auto it = h->slot_of.find(ev->creator_id[i]);
+    if (it == h->slot_of.end()) {
+      code = BH_ERR_UNKNOWN_PARTICIPANT;
+    } else {
+      c = it->second;
+      const auto &ch = h->chain[c];
+      const int32_t last = (int32_t)ch.size() - 1;  // base Root index is -1
+      // checkSelfParent (hashgraph.go:398-414): self-parent must be the
+      // creator's last known event (its Root when it has none)
+      if (ev->self_parent_index[i] != last) code = BH_ERR_SELF_PARENT;
+      // ParticipantEventsCache continuity (rolling_index.go: SkippedIndex)
+      else if (ev->index[i] != last + 1) code = BH_ERR_SKIPPED_INDEX;
+      else if (ev->other_parent_index[i] >= 0 || ev->other_parent_creator_id[i] >= 0) {
+        // checkOtherParent (hashgraph.go:417-436) via ReadWireInfo's lookup
+        auto io = h->slot_of.find(ev->other_parent_creator_id[i]);
+        if (io == h->slot_of.end()) code = BH_ERR_OTHER_PARENT;
+        else {
+          const auto &oc = h->chain[io->second];
+          const int32_t k = ev->other_parent_index[i];
+          if (k < 0 || k >= (int32_t)oc.size()) code = BH_ERR_OTHER_PARENT;
+          else op = oc[k];
+        }
+      }
+      if (code == BH_OK && (int64_t)h->h_creator.size() >= h->cap) code = BH_ERR_CAPACITY;
+    }
+    if (status) status[i] = code;
+    if (code != BH_OK) {
+      if (first == BH_OK) {
+        first = code;
+        const char *msg = code == BH_ERR_SELF_PARENT ? "CheckSelfParent: Self-parent not last known event by creator"
+                        : code == BH_ERR_OTHER_PARENT ? "CheckOtherParent: Other-parent not known"
+                        : code == BH_ERR_SKIPPED_INDEX ? "SetEvent: ParticipantEvents, Skipped Index"
+                        : code == BH_ERR_CAPACITY ? "capacity exceeded"
+                        : "ParticipantEvents, Unknown Participant";
+        h->fail(code, "event %lld: %s", (long long)i, msg);
+      }
+      continue;
+    }
+    const int32_t id = (int32_t)h->h_creator.size();
+    auto &ch = h->chain[c];
+    h->h_creator.push_back(c);
+    h->h_index.push_back(ev->index[i]);
+    h->h_sp.push_back(ch.empty() ? -1 : ch.back());
+    h->h_op.push_back(op);
+    h->h_ntx.push_back(ev->n_transactions[i]);
+    h->h_coin.push_back(ev->hash[i * 32 + 16] != 0 ? 1 : 0);
+    const uint8_t *rb = ev->sig_r + i * 32;
+    for (int q = 0; q < 8; ++q)
+      h->h_sigw.push_back((uint32_t)rb[4 * q] << 24 | (uint32_t)rb[4 * q + 1] << 16 |
+                          (uint32_t)rb[4 * q + 2] << 8 | rb[4 * q + 3]);
+    ch.push_back(id);
+    if (ev->index[i] == 0 || ev->n_transactions[i] > 0) h->loaded_total++;
+    ++acc;
+  }
+  if (n_accepted) *n_accepted = acc;
+  if (acc) {
+    h->stage = 0;
+    (void)hipSetDevice(h->device);
+    int rc = upload(h);
+    if (rc) return rc;
+  }
+  return first;
+}
+
+int bh_divide_rounds(bh_handle *h) {
+  if (!h) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  return stage_rounds(h);
+}
+int bh_decide_fame(bh_handle *h) {
+  if (!h) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  return stage_fame(h);
+}
+int bh_decide_round_received(bh_handle *h) {
+  if (!h) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  return stage_rr(h);
+}
+int bh_process_decided_rounds(bh_handle *h) {
+  if (!h) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  return stage_order(h);
+}
+int bh_run_consensus(bh_handle *h) {
+  int rc;
+  if (!h) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  if ((rc = stage_rounds(h))) return rc;
+  if ((rc = stage_fame(h))) return rc;
+  if ((rc = stage_rr(h))) return rc;
+  return stage_order(h);
+}
+int bh_synchronize(bh_handle *h) {
+  if (!h) return BH_ERR_INVALID;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
+
+int bh_get_stats(bh_handle *h, bh_stats *o) {
+  if (!h || !o) return BH_ERR_INVALID;
+  memset(o, 0, sizeof *o);
+  o->n_events = (int64_t)h->h_creator.size();
+  o->last_round = h->stage >= 1 ? h->R - 1 : -1;
+  o->last_consensus_round = h->stage >= 4 && h->P > 0 ? h->P - 1 : -1;
+  o->consensus_events = h->stage >= 4 ? h->ncons : 0;
+  o->consensus_transactions = h->stage >= 4 ? h->cons_txs : 0;
+  o->pending_loaded_events = h->loaded_total - (h->stage >= 4 ? h->cons_loaded : 0);
+  o->undetermined_events = o->n_events - (h->stage >= 4 ? h->nreceived : 0);
+  if (h->stage == 3) {  // received but not yet processed: count on demand
+    int64_t k = bh_get_undetermined(h, nullptr, 0);
+    o->undetermined_events = k;
+  }
+  o->blocks = (int64_t)h->blocks.size();
+  o->pending_rounds = h->stage >= 1 ? h->R - (h->stage >= 4 ? h->P : 0) : 0;
+  return BH_OK;
+}
+
+int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round, int8_t *witness,
+                      int32_t *lamport, int32_t *round_received, int8_t *fame, int64_t *consensus_pos) {
+  if (!h || first < 0 || count < 0 || first + count > (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const Dev &d = h->d;
+  const size_t k = (size_t)count;
+  if (count == 0) return BH_OK;
+  auto fill32 = [&](int32_t *p) { std::fill(p, p + k, INT32_MIN); };
+  if (round) {
+    if (h->stage >= 1) HIPCHK(h, hipMemcpy(round, d.round + first, k * 4, hipMemcpyDeviceToHost));
+    else fill32(round);
+  }
+  if (lamport) {
+    if (h->stage >= 1) HIPCHK(h, hipMemcpy(lamport, d.lt + first, k * 4, hipMemcpyDeviceToHost));
+    else fill32(lamport);
+  }
+  if (witness) {
+    if (h->stage >= 1) HIPCHK(h, hipMemcpy(witness, d.witness + first, k, hipMemcpyDeviceToHost));
+    else std::fill(witness, witness + k, 0);
+  }
+  if (fame) {
+    if (h->stage >= 1) HIPCHK(h, hipMemcpy(fame, d.fame + first, k, hipMemcpyDeviceToHost));
+    else std::fill(fame, fame + k, -1);
+  }
+  if (round_received) {
+    if (h->stage >= 3) HIPCHK(h, hipMemcpy(round_received, d.rr + first, k * 4, hipMemcpyDeviceToHost));
+    else fill32(round_received);
+  }
+  if (consensus_pos) {
+    if (h->stage >= 4) HIPCHK(h, hipMemcpy(consensus_pos, d.cons_pos + first, k * 8, hipMemcpyDeviceToHost));
+    else std::fill(consensus_pos, consensus_pos + k, -1);
+  }
+  return BH_OK;
+}
+
+int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *ids) {
+  if (!h || !ids || first < 0 || count < 0) return BH_ERR_INVALID;
+  if (h->stage < 4 || first + count > h->ncons) return h->fail(BH_ERR_INVALID, "range beyond consensus");
+  (void)hipSetDevice(h->device);
+  if (count) HIPCHK(h, hipMemcpy(ids, h->d.order + first, (size_t)count * 4, hipMemcpyDeviceToHost));
+  return BH_OK;
+}
+
+int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_received,
+                  int64_t *first_event, int64_t *n_events, int64_t *n_transactions) {
+  if (!h || first < 0 || count < 0 || first + count > (int64_t)h->blocks.size()) return BH_ERR_INVALID;
+  for (int64_t i = 0; i < count; ++i) {
+    const Block &b = h->blocks[(size_t)(first + i)];
+    if (round_received) round_received[i] = b.rr;
+    if (first_event) first_event[i] = b.first;
+    if (n_events) n_events[i] = b.count;
+    if (n_transactions) n_transactions[i] = b.ntx;
+  }
+  return BH_OK;
+}
+
+int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap) {
+  if (!h || h->stage < 1) return 0;
+  const int32_t lo = h->stage >= 4 ? h->P : 0;
+  const int32_t cnt = h->R - lo;
+  for (int32_t i = 0; i < cnt && i < cap; ++i) {
+    if (index) index[i] = lo + i;
+    if (decided) decided[i] = h->stage >= 2 ? h->decided_h[(size_t)(lo + i)] : 0;
+  }
+  return cnt;
+}
+
+int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap) {
+  if (!h) return 0;
+  const int64_t N = (int64_t)h->h_creator.size();
+  if (h->stage < 3) {
+    for (int64_t i = 0; i < N && i < cap; ++i) ids[i] = (int32_t)i;
+    return N;
+  }
+  std::vector<int32_t> rr((size_t)N);
+  (void)hipSetDevice(h->device);
+  if (N && hipMemcpy(rr.data(), h->d.rr, (size_t)N * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  int64_t k = 0;
+  for (int64_t i = 0; i < N; ++i)
+    if (rr[(size_t)i] == INT32_MIN) {
+      if (ids && k < cap) ids[k] = (int32_t)i;
+      ++k;
+    }
+  return k;
+}
+
+int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_t *first_descendants) {
+  if (!h || id < 0 || id >= (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  Dev &d = h->d;
+  const int64_t N = (int64_t)h->h_creator.size();
+  if (h->coords_for != N) {  // coordinates are produced lazily by the first pass
+    int rc;
+    if ((rc = upload(h))) return rc;
+    d.N = N;
+    if ((rc = set_chain_tables(h))) return rc;
+    bh::launch_prep(d, h->stream);
+    bh::launch_coordinates(d, h->stream);
+    HIPCHK(h, hipGetLastError());
+    h->coords_for = (int)N;
+    h->stage = 0;
+  }
+  int64_t row = 0;
+  const int32_t c = h->h_creator[(size_t)id];
+  for (int32_t q = 0; q < c; ++q) row += (int64_t)h->chain[q].size();
+  row += h->h_index[(size_t)id];
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (last_ancestors)
+    HIPCHK(h, hipMemcpy(last_ancestors, d.la + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
+  if (first_descendants) {
+    int32_t *tmp = nullptr;
+    HIPCHK(h, hipMalloc((void **)&tmp, (size_t)d.n * 4));
+    bh::launch_fd_row(d, id, tmp, h->stream);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(first_descendants, tmp, (size_t)d.n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(tmp);
+  }
+  return BH_OK;
+}
+
+int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap) {
+  if (!h) return 0;
+  for (int i = 0; i < NSTAGE && i < cap; ++i) ms[i] = h->stage_ms[i];
+  return NSTAGE;
+}
+
+int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {
+  if (!h) return BH_ERR_INVALID;
+  if (rounds_iterated) *rounds_iterated = h->iters;
+  if (sweep_ms) *sweep_ms = h->sweep_ms;
+  return BH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// engine.h -- internal device-state layout and kernel launchers of libbabble_hip.
+//
+// HBM layout (structure of arrays, event id = insertion order):
+//   creator/index/sp/op/ntx  int32[N]       event bodies (sp/op: global ids, -1 = Root/none)
+//   coin                     uint8[N]       hash[16] != 0  (middleBit, hashgraph.go:1526-1535)
+//   sigw                     uint32[N][8]   ECDSA r as 8 big-endian words (tie-break key)
+//   chain_ids                int32[N]       ids grouped by creator, ordered by index
+//   epos                     int32[N]       row of event e = chain_start[creator] + index
+//   la                       int32[N][npad] lastAncestors indexes (-1 = none), chain-major rows
+//   lt                       int32[N]       Lamport timestamp
+//   B                        int32[R_cap+1][n] first index on chain c with round >= r
+//   wids / wofs / wcnt       witnesses of each round (chain order)
+//   fdw                      int32[W_cap][npad] firstDescendants rows of witnesses
+//   round/witness/fame/rr    per-event results
+// See DESIGN.md for the algorithm and the roofline of each kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace bh {
+
+constexpr int32_t UNSET = INT32_MIN;    // Go nil
+constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
+constexpr int RING = 8192;              // events held in the coordinate sweep's LDS ring
+constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
+constexpr int FRAME_LDS_MAX = 2048;     // frames sorted in LDS up to this size
+
+enum StateSlot {
+  ST_NEXT = 0,     // next round to resolve
+  ST_DONE = 1,     // round loop finished
+  ST_ROUNDS = 2,   // number of rounds R (LastRound + 1)
+  ST_CUR = 3,      // round whose witnesses fd/scan work on
+  ST_ERR = 4,      // capacity overflow / inconsistency
+  ST_P = 5,        // processed prefix: rounds [0, P) are decided and ordered
+  ST_NCONS = 6,    // consensus events (int32 ok: < 2^31)
+  ST_ITERS = 7,    // round-loop iterations executed
+  ST_FLAGGED = 8,  // candidates that needed the exact witness resolution
+  ST_NBLOCKS = 9,
+  ST_COUNT = 16
+};
+
+struct Dev {
+  int32_t n, npad, sm;
+  int64_t N;
+  int32_t R_cap;
+  int64_t W_cap;
+  // event bodies
+  int32_t *creator, *index, *sp, *op, *ntx;
+  uint8_t *coin;
+  uint32_t *sigw;
+  // chains
+  int32_t *chain_start, *chain_len, *chain_ids, *epos;
+  // coordinates
+  int32_t *la, *lt;
+  uint8_t *depth, *chunk_maxd;
+  // rounds
+  int32_t *B, *wofs, *wcnt, *wids, *fdw;
+  int32_t *state;
+  int32_t *round;
+  int8_t *witness, *fame;
+  // fame / received
+  int8_t *decided;
+  int32_t *nfam, *minla;
+  int32_t *rr;
+  // frames
+  int32_t *frame_cnt, *frame_ofs, *frame_cur, *blk_of_frame;
+  int32_t *order;
+  int64_t *cons_pos;
+  int64_t *frame_ntx;
+  int64_t *counters;  // [0] consensus txs, [1] loaded consensus events, [2] received
+};
+
+// launchers (kernels_*.hip)
+void configure_round_kernels();
+void configure_fame_kernels();
+void configure_order_kernels();
+void launch_prep(const Dev &d, hipStream_t s);
+void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep
+void launch_chunk_depth(const Dev &d, hipStream_t s);
+void launch_la_sweep(const Dev &d, hipStream_t s);
+void launch_round_iteration(const Dev &d, hipStream_t s);  // resolve + fd + scan
+void launch_assign_rounds(const Dev &d, hipStream_t s);
+void launch_fame(const Dev &d, int32_t R, hipStream_t s);
+void launch_round_received(const Dev &d, int32_t R, hipStream_t s);
+void launch_order(const Dev &d, int32_t R, hipStream_t s);
+void launch_fd_row(const Dev &d, int64_t e, int32_t *out, hipStream_t s);
+
+}  // namespace bh

@@ -1,0 +1,216 @@
+// kernels_fame.hip -- DecideFame (hashgraph.go:852-947) for every round at once.
+//
+// For a witness x of round r the vote of y in W(j) is
+//   j = r+1 : see(y, x)                        (hashgraph.go:879-884)
+//   j > r+1 : majority of the votes of the W(j-1) witnesses y strongly sees
+//             (yays >= nays -> yes, hashgraph.go:886-911); in a normal round
+//             (diff % n != 0) t >= SM decides x's fame and ends x's loop;
+//             in a coin round t >= SM keeps the vote, else y's middle byte
+//             (hashgraph.go:913-928, middleBit :1526-1535).
+// Votes depend only on the DAG, not on the order the Go code visits the map
+// entries, so every round is decided independently: one workgroup per round
+// r keeps the votes of all x in W(r) as bitsets over the voters (n/64 words),
+// and tallies with popcount(S_j[y] & V_{j-1}[x]), where S_j[y] is the bitset
+// of the W(j-1) witnesses y strongly sees.  S_j is an n x n x n integer
+// compare-and-count, register-tiled 8x8 per thread from LDS-staged LA rows
+// (voters) and firstDescendants rows (voted).  The workgroup then publishes
+// the round's decided flag, its famous count and min over famous witnesses
+// of LA (what DecideRoundReceived needs, hashgraph.go:968-1001).
+#include "engine.h"
+
+namespace bh {
+
+constexpr int FAME_MAXN = 128;  // LDS-staged rows up to this many participants
+
+template <bool LDS_ROWS>
+__global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  const int r = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+  const int n = d.n, npad = d.npad, sm = d.sm;
+  const int WW = (n + 63) >> 6;       // words per voter bitset
+  const int rs = npad + 4;            // LDS row stride (ints)
+  // carve
+  unsigned long long *Vp = reinterpret_cast<unsigned long long *>(fsm);
+  unsigned long long *Vc = Vp + n * WW;
+  unsigned long long *S = Vc + n * WW;
+  int32_t *xs = reinterpret_cast<int32_t *>(S + n * WW);
+  int32_t *dec = xs + n;   // 0 undecided, 1 famous, 2 not famous
+  int32_t *nd = dec + n;   // decisions of the current j (bit0 yes, bit1 no)
+  int32_t *misc = nd + n;  // [0] undecided count, [1] error
+  int32_t *ly = misc + 4;               // LDS_ROWS: LA rows of W(j)
+  int32_t *fw = ly + (LDS_ROWS ? n * rs : 0);  // LDS_ROWS: FD rows of W(j-1)
+
+  const int32_t nx = d.wcnt[r], xb = d.wofs[r];
+  for (int i = t; i < nx; i += nt) { xs[i] = d.wids[xb + i]; dec[i] = 0; }
+  if (t == 0) { misc[0] = nx; misc[1] = 0; }
+  __syncthreads();
+
+  if (r + 1 < R) {
+    // ---- j = r+1: vote = see(y, x) ----
+    int32_t ny = d.wcnt[r + 1], yb = d.wofs[r + 1];
+    for (int i = t; i < nx * WW; i += nt) Vp[i] = 0ull;
+    __syncthreads();
+    for (int p = t; p < nx * ny; p += nt) {
+      const int x = p / ny, y = p - x * ny;
+      const int32_t xe = xs[x], ye = d.wids[yb + y];
+      const bool v = d.la[(int64_t)d.epos[ye] * npad + d.creator[xe]] >= d.index[xe];
+      if (v) atomicOr(&Vp[x * WW + (y >> 6)], 1ull << (y & 63));
+    }
+    __syncthreads();
+    // ---- j >= r+2 ----
+    for (int j = r + 2; j < R; ++j) {
+      if (misc[0] == 0) break;
+      const int32_t nw = ny, wb = yb;  // W(j-1)
+      ny = d.wcnt[j];
+      yb = d.wofs[j];
+      for (int i = t; i < ny * WW; i += nt) { S[i] = 0ull; }
+      for (int i = t; i < nx * WW; i += nt) Vc[i] = 0ull;
+      for (int i = t; i < nx; i += nt) nd[i] = 0;
+      if (LDS_ROWS) {
+        const int q4 = npad / 4;
+        for (int q = t; q < ny * q4; q += nt) {
+          const int y = q / q4, c4 = q - y * q4;
+          const int32_t ye = d.wids[yb + y];
+          reinterpret_cast<int4 *>(ly + y * rs)[c4] =
+              reinterpret_cast<const int4 *>(d.la + (int64_t)d.epos[ye] * npad)[c4];
+        }
+        for (int q = t; q < nw * q4; q += nt) {
+          const int w = q / q4, c4 = q - w * q4;
+          reinterpret_cast<int4 *>(fw + w * rs)[c4] =
+              reinterpret_cast<const int4 *>(d.fdw + (int64_t)(wb + w) * npad)[c4];
+        }
+      }
+      __syncthreads();
+      // S_j: 8x8 (y, w) tiles per thread, count columns with LA[y] >= FD[w]
+      const int ty = (ny + 7) >> 3, tw = (nw + 7) >> 3;
+      for (int tile = t; tile < ty * tw; tile += nt) {
+        const int y0 = (tile / tw) * 8, w0 = (tile % tw) * 8;
+        const int32_t *yr[8];
+        const int32_t *wr[8];
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          const int y = min(y0 + a, ny - 1), w = min(w0 + a, nw - 1);
+          if (LDS_ROWS) {
+            yr[a] = ly + y * rs;
+            wr[a] = fw + w * rs;
+          } else {
+            yr[a] = d.la + (int64_t)d.epos[d.wids[yb + y]] * npad;
+            wr[a] = d.fdw + (int64_t)(wb + w) * npad;
+          }
+        }
+        int cnt[8][8];
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < 8; ++b) cnt[a][b] = 0;
+        for (int i = 0; i < npad; i += 4) {
+          int4 yv[8], wv[8];
+#pragma unroll
+          for (int a = 0; a < 8; ++a) {
+            yv[a] = *reinterpret_cast<const int4 *>(yr[a] + i);
+            wv[a] = *reinterpret_cast<const int4 *>(wr[a] + i);
+          }
+#pragma unroll
+          for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+              cnt[a][b] += (yv[a].x >= wv[b].x) + (yv[a].y >= wv[b].y) + (yv[a].z >= wv[b].z) +
+                           (yv[a].w >= wv[b].w);
+        }
+#pragma unroll
+        for (int a = 0; a < 8; ++a) {
+          const int y = y0 + a;
+          if (y >= ny) continue;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            const int w = w0 + b;
+            if (w < nw && cnt[a][b] >= sm) atomicOr(&S[y * WW + (w >> 6)], 1ull << (w & 63));
+          }
+        }
+      }
+      __syncthreads();
+      // tallies and votes
+      const int diff = j - r;
+      const bool normal = (diff % n) != 0;
+      for (int p = t; p < nx * ny; p += nt) {
+        const int x = p / ny, y = p - x * ny;
+        if (dec[x]) continue;
+        int yays = 0, tot = 0;
+        for (int q = 0; q < WW; ++q) {
+          const unsigned long long s = S[y * WW + q];
+          yays += __popcll(s & Vp[x * WW + q]);
+          tot += __popcll(s);
+        }
+        const int nays = tot - yays;
+        const bool v = yays >= nays;
+        const int tt = v ? yays : nays;
+        bool vote;
+        if (normal) {
+          if (tt >= sm) atomicOr(&nd[x], v ? 1 : 2);
+          vote = v;
+        } else {
+          vote = tt >= sm ? v : d.coin[d.wids[yb + y]] != 0;
+        }
+        if (vote) atomicOr(&Vc[x * WW + (y >> 6)], 1ull << (y & 63));
+      }
+      __syncthreads();
+      for (int x = t; x < nx; x += nt) {
+        if (dec[x] == 0 && nd[x]) {
+          if (nd[x] == 3) misc[1] = 1;  // conflicting decisions: impossible without forks
+          dec[x] = nd[x] == 1 ? 1 : 2;
+          atomicSub(&misc[0], 1);
+        }
+      }
+      __syncthreads();
+      unsigned long long *tmp = Vp;
+      Vp = Vc;
+      Vc = tmp;
+    }
+  }
+  // ---- publish ----
+  __syncthreads();
+  for (int x = t; x < nx; x += nt) d.fame[xs[x]] = (int8_t)dec[x];
+  __syncthreads();
+  if (t == 0) {
+    d.decided[r] = misc[0] == 0 ? 1 : 0;
+    if (misc[1]) d.state[ST_ERR] = 2;
+  }
+  // famous count and min LA over famous witnesses (see(w, x) for all w in FW)
+  for (int c = t; c < npad; c += nt) {
+    int32_t m = INT32_MAX;
+    int cntf = 0;
+    for (int x = 0; x < nx; ++x) {
+      if (dec[x] != 1) continue;
+      ++cntf;
+      m = min(m, d.la[(int64_t)d.epos[xs[x]] * npad + c]);
+    }
+    d.minla[(int64_t)r * npad + c] = m;
+    if (c == 0) d.nfam[r] = cntf;
+  }
+}
+
+size_t fame_lds_bytes(int n, int npad, bool lds_rows) {
+  const int WW = (n + 63) >> 6;
+  size_t b = (size_t)3 * n * WW * 8 + (size_t)3 * n * 4 + 16;
+  if (lds_rows) b += (size_t)2 * n * (npad + 4) * 4;
+  return b;
+}
+
+void configure_fame_kernels() {
+  (void)hipFuncSetAttribute((const void *)k_fame<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            150 * 1024);
+  (void)hipFuncSetAttribute((const void *)k_fame<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            150 * 1024);
+}
+
+void launch_fame(const Dev &d, int32_t R, hipStream_t s) {
+  if (R <= 0) return;
+  const bool lds = d.n <= FAME_MAXN;
+  const size_t bytes = fame_lds_bytes(d.n, d.npad, lds);
+  if (lds)
+    k_fame<true><<<R, 256, bytes, s>>>(d, R);
+  else
+    k_fame<false><<<R, 256, bytes, s>>>(d, R);
+}
+
+}  // namespace bh

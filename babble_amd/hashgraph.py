@@ -1,0 +1,208 @@
+"""Hashgraph -- the reference's consensus API, backed by the MI355X engine.
+
+Mirrors the methods node.Core calls on *hashgraph.Hashgraph
+(/root/reference/src/hashgraph/hashgraph.go; node/core.go:51-377):
+
+    NewHashgraph            -> Hashgraph(participant_ids, max_events)
+    InsertEvent             -> insert_event / insert_events (wire form)
+    DivideRounds            -> divide_rounds
+    DecideFame              -> decide_fame
+    DecideRoundReceived     -> decide_round_received
+    ProcessDecidedRounds    -> process_decided_rounds
+    UndeterminedEvents, PendingRounds, LastConsensusRound,
+    ConsensusTransactions, PendingLoadedEvents  -> properties
+
+Go returns `error`; here the same conditions raise HashgraphError carrying
+the Go error kind.  All compute runs in libbabble_hip (HIP kernels); this
+module only marshals arrays.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native
+
+UNSET = -(2 ** 31)
+
+
+class HashgraphError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_native.ERRORS.get(code, code)}: {msg}")
+        self.code = code
+        self.kind = _native.ERRORS.get(code, str(code))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class Hashgraph:
+    def __init__(self, participant_ids, max_events, device=0):
+        self._L = _native.load()
+        ids = np.ascontiguousarray(participant_ids, dtype=np.int64)
+        if np.any(np.diff(ids) <= 0):
+            raise ValueError("participant ids must be sorted ascending (peers.go:63-73)")
+        self.participant_ids = ids
+        self.n = len(ids)
+        cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
+                             int(device))
+        h = C.c_void_p()
+        rc = self._L.bh_create(C.byref(cfg), C.byref(h))
+        if rc != _native.BH_OK:
+            raise HashgraphError(rc, "bh_create failed (no HIP device or out of memory)")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.bh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc):
+        if rc != _native.BH_OK:
+            raise HashgraphError(rc, self._L.bh_last_error(self._h).decode())
+
+    # ---- InsertEvent (hashgraph.go:714-761) ----
+    def insert_events(self, creator_id, index, self_parent_index, other_parent_creator_id,
+                      other_parent_index, hashes, sig_r, n_transactions, raise_on_error=True):
+        """Wire-form batch insert.  Returns the per-event status array (0 = ok)."""
+        arrs = [np.ascontiguousarray(a, dtype=dt) for a, dt in (
+            (creator_id, np.int64), (index, np.int32), (self_parent_index, np.int32),
+            (other_parent_creator_id, np.int64), (other_parent_index, np.int32),
+            (hashes, np.uint8), (sig_r, np.uint8), (n_transactions, np.int32))]
+        cnt = len(arrs[0])
+        if arrs[5].size != cnt * 32 or arrs[6].size != cnt * 32:
+            raise ValueError("hash / sig_r must be [count, 32] bytes")
+        ev = _native.Events(cnt, *[_ptr(a) for a in arrs])
+        status = np.zeros(cnt, np.int32)
+        acc = C.c_int64()
+        rc = self._L.bh_insert_events(self._h, C.byref(ev), _ptr(status), C.byref(acc))
+        if rc != _native.BH_OK and raise_on_error:
+            self._check(rc)
+        return status
+
+    def insert_event(self, creator_id, index, self_parent_index, other_parent_creator_id,
+                     other_parent_index, hash32, sig_r32, n_transactions):
+        st = self.insert_events([creator_id], [index], [self_parent_index],
+                                [other_parent_creator_id], [other_parent_index],
+                                np.frombuffer(bytes(hash32), np.uint8),
+                                np.frombuffer(bytes(sig_r32), np.uint8), [n_transactions],
+                                raise_on_error=True)
+        return int(st[0])
+
+    def insert_dag(self, dag):
+        """Insert a babble_amd.dag.Dag (or any object with its arrays)."""
+        spi, opc, opi = dag.wire()
+        pid = self.participant_ids
+        opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+        return self.insert_events(pid[dag.creator], dag.index, spi, opc_id, opi, dag.hash,
+                                  dag.sig_r, dag.ntx)
+
+    # ---- consensus passes ----
+    def divide_rounds(self):
+        self._check(self._L.bh_divide_rounds(self._h))
+
+    def decide_fame(self):
+        self._check(self._L.bh_decide_fame(self._h))
+
+    def decide_round_received(self):
+        self._check(self._L.bh_decide_round_received(self._h))
+
+    def process_decided_rounds(self):
+        self._check(self._L.bh_process_decided_rounds(self._h))
+
+    def run_consensus(self):
+        self._check(self._L.bh_run_consensus(self._h))
+
+    def synchronize(self):
+        self._check(self._L.bh_synchronize(self._h))
+
+    # ---- state ----
+    def stats(self):
+        s = _native.Stats()
+        self._check(self._L.bh_get_stats(self._h, C.byref(s)))
+        return s
+
+    @property
+    def last_consensus_round(self):
+        r = self.stats().last_consensus_round
+        return None if r < 0 else r
+
+    @property
+    def consensus_transactions(self):
+        return self.stats().consensus_transactions
+
+    @property
+    def pending_loaded_events(self):
+        return self.stats().pending_loaded_events
+
+    def last_round(self):
+        return self.stats().last_round
+
+    @property
+    def pending_rounds(self):
+        k = self._L.bh_get_pending_rounds(self._h, None, None, 0)
+        idx = np.zeros(max(k, 1), np.int32)
+        dec = np.zeros(max(k, 1), np.int8)
+        self._L.bh_get_pending_rounds(self._h, _ptr(idx), _ptr(dec), k)
+        return [(int(idx[i]), bool(dec[i])) for i in range(k)]
+
+    @property
+    def undetermined_events(self):
+        k = self._L.bh_get_undetermined(self._h, None, 0)
+        ids = np.zeros(max(k, 1), np.int32)
+        self._L.bh_get_undetermined(self._h, _ptr(ids), k)
+        return ids[:k]
+
+    def results(self, first=0, count=None):
+        N = self.stats().n_events
+        count = N - first if count is None else count
+        out = dict(round=np.empty(count, np.int32), witness=np.empty(count, np.int8),
+                   lamport=np.empty(count, np.int32), round_received=np.empty(count, np.int32),
+                   fame=np.empty(count, np.int8), cons_pos=np.empty(count, np.int64))
+        self._check(self._L.bh_get_event_meta(
+            self._h, first, count, _ptr(out["round"]), _ptr(out["witness"]), _ptr(out["lamport"]),
+            _ptr(out["round_received"]), _ptr(out["fame"]), _ptr(out["cons_pos"])))
+        return out
+
+    def consensus_order(self):
+        k = self.stats().consensus_events
+        ids = np.empty(k, np.int32)
+        if k:
+            self._check(self._L.bh_get_consensus_order(self._h, 0, k, _ptr(ids)))
+        return ids
+
+    def blocks(self):
+        b = self.stats().blocks
+        out = dict(round_received=np.empty(b, np.int32), first=np.empty(b, np.int64),
+                   count=np.empty(b, np.int64), ntx=np.empty(b, np.int64))
+        if b:
+            self._check(self._L.bh_get_blocks(self._h, 0, b, _ptr(out["round_received"]),
+                                              _ptr(out["first"]), _ptr(out["count"]),
+                                              _ptr(out["ntx"])))
+        return out
+
+    def coordinates(self, event_id):
+        la = np.empty(self.n, np.int32)
+        fd = np.empty(self.n, np.int32)
+        self._check(self._L.bh_get_coordinates(self._h, int(event_id), _ptr(la), _ptr(fd)))
+        return la, fd
+
+    def stage_ms(self):
+        buf = (C.c_float * 8)()
+        k = self._L.bh_get_stage_ms(self._h, buf, 8)
+        return [float(buf[i]) for i in range(k)]
+
+    def profile(self):
+        it = C.c_int64()
+        ms = C.c_float()
+        self._check(self._L.bh_get_profile(self._h, C.byref(it), C.byref(ms)))
+        return int(it.value), float(ms.value)

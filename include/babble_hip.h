@@ -1,0 +1,125 @@
+/*
+ * babble_hip.h -- C ABI of libbabble_hip, the MI355X (gfx950) consensus engine
+ * for Babble's hashgraph virtual-voting path.
+ *
+ * Drop-in boundary: every entry point replaces one method of the reference's
+ * Go `Hashgraph` (/root/reference/src/hashgraph/hashgraph.go) as called by
+ * node.Core (src/node/core.go).  Plain C types only; one owner per handle;
+ * not thread-safe (the reference serialises with Node.coreLock, node.go:27).
+ * The cgo binding a maintainer would add is in INTEGRATION.md.
+ *
+ * Status codes mirror the Go error kinds (common/errors.go:7-15, and the
+ * fmt.Errorf messages of hashgraph.go); bh_last_error() gives the message.
+ */
+#ifndef BABBLE_HIP_H
+#define BABBLE_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  BH_OK = 0,
+  BH_ERR_SELF_PARENT = 1,   /* "Self-parent not last known event by creator" hashgraph.go:409 */
+  BH_ERR_OTHER_PARENT = 2,  /* "Other-parent not known" hashgraph.go:432 */
+  BH_ERR_UNKNOWN_PARTICIPANT = 3, /* StoreErr UnknownParticipant (common/errors.go:13) */
+  BH_ERR_SKIPPED_INDEX = 4, /* StoreErr SkippedIndex / PassedIndex (rolling index) */
+  BH_ERR_CAPACITY = 5,      /* more events than bh_config.max_events */
+  BH_ERR_STATE = 6,         /* pass called before its prerequisites */
+  BH_ERR_INVALID = 7,       /* bad argument */
+  BH_ERR_DEVICE = 8         /* HIP runtime error / no device / kernel fault */
+};
+
+typedef struct bh_handle bh_handle;
+
+/* NewHashgraph(participants, store, commitCh, logger) (hashgraph.go:47-73)
+ * with an InmemStore of capacity max_events (inmem_store.go:27-49). */
+typedef struct {
+  int32_t n_participants;
+  const int64_t *participant_ids; /* peer IDs, ascending (peers.go:63-73, 118-129) */
+  int64_t max_events;             /* capacity; the reference's cacheSize must be >= #events */
+  int32_t device;                 /* HIP device ordinal */
+} bh_config;
+
+/* A batch of events in topological order, in the reference's compact wire
+ * form (WireBody, event.go:353-363): parents are (creator ID, index) pairs,
+ * resolved by the engine exactly like Hashgraph.ReadWireInfo
+ * (hashgraph.go:1414-1479).  Buffers stay owned by the caller. */
+typedef struct {
+  int64_t count;
+  const int64_t *creator_id;              /* WireBody.CreatorID */
+  const int32_t *index;                   /* WireBody.Index */
+  const int32_t *self_parent_index;       /* WireBody.SelfParentIndex, -1 = the Root */
+  const int64_t *other_parent_creator_id; /* WireBody.OtherParentCreatorID, -1 = none */
+  const int32_t *other_parent_index;      /* WireBody.OtherParentIndex, -1 = none */
+  const uint8_t *hash;                    /* [count][32] Event.Hash() = SHA-256(Go-JSON body) */
+  const uint8_t *sig_r;                   /* [count][32] big-endian ECDSA r of Event.Signature */
+  const int32_t *n_transactions;          /* len(Body.Transactions) */
+} bh_events;
+
+int bh_create(const bh_config *cfg, bh_handle **out);
+void bh_destroy(bh_handle *h);
+const char *bh_last_error(const bh_handle *h);
+
+/* InsertEvent(event, setWireInfo) for each event (hashgraph.go:714-761):
+ * checkSelfParent / checkOtherParent / participant-index continuity.  A
+ * rejected event is skipped (like createHashgraph, hashgraph_test.go:134-138)
+ * and its status written to status[i] (nullable).  Accepted events get
+ * consecutive ids (= topologicalIndex).  Signatures are pre-verified inputs.
+ * Returns BH_OK if all were accepted, else the first error code. */
+int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted);
+
+/* The consensus passes (node/core.go:335-377).  Batch schedule: each pass
+ * computes its stage over every inserted event. */
+int bh_divide_rounds(bh_handle *h);           /* hashgraph.go:767-849 (+ coordinates) */
+int bh_decide_fame(bh_handle *h);             /* hashgraph.go:852-947 */
+int bh_decide_round_received(bh_handle *h);   /* hashgraph.go:951-1036 */
+int bh_process_decided_rounds(bh_handle *h);  /* hashgraph.go:1041-1231 */
+int bh_run_consensus(bh_handle *h);           /* all four, queued on one stream */
+int bh_synchronize(bh_handle *h);             /* wait for queued device work */
+
+typedef struct {
+  int64_t n_events;
+  int32_t last_round;             /* Store.LastRound() */
+  int32_t last_consensus_round;   /* Hashgraph.LastConsensusRound, -1 = nil */
+  int64_t consensus_events;       /* Store.ConsensusEventsCount() */
+  int64_t consensus_transactions; /* Hashgraph.ConsensusTransactions */
+  int64_t pending_loaded_events;  /* Hashgraph.PendingLoadedEvents */
+  int64_t undetermined_events;    /* len(Hashgraph.UndeterminedEvents) */
+  int64_t blocks;                 /* Store.LastBlockIndex()+1 */
+  int32_t pending_rounds;         /* len(Hashgraph.PendingRounds) */
+} bh_stats;
+int bh_get_stats(bh_handle *h, bh_stats *out);
+
+/* Per-event private fields (event.go:107-116): round / lamport / rr are
+ * INT32_MIN when unset (Go nil); fame = -1 not a witness, 0 Undefined,
+ * 1 True, 2 False (roundInfo.go:10-16); consensus_pos = -1 if not ordered. */
+int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round,
+                      int8_t *witness, int32_t *lamport, int32_t *round_received,
+                      int8_t *fame, int64_t *consensus_pos);
+/* consensus order (Store.AddConsensusEvent sequence), event ids */
+int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *ids);
+/* Blocks (block.go:100-123): RoundReceived, first consensus position,
+ * #events of its Frame, #transactions (concatenated in consensus order). */
+int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_received,
+                  int64_t *first_event, int64_t *n_events, int64_t *n_transactions);
+/* Hashgraph.PendingRounds: returns the count, fills up to cap entries */
+int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap);
+/* Hashgraph.UndeterminedEvents (insertion order): returns the count */
+int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap);
+/* lastAncestors / firstDescendants indexes of one event (event.go:115-116) */
+int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors,
+                       int32_t *first_descendants);
+/* device milliseconds of the last run, per stage:
+ * [0] coordinates+lamport, [1] rounds+witnesses, [2] fame, [3] round received,
+ * [4] frames/order/blocks; returns the number of stages */
+int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap);
+/* kernel statistics of the last run for the roofline report: number of
+ * round-loop iterations, coordinate sweep launches' average ms */
+int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

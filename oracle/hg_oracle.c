@@ -370,6 +370,16 @@ int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
   return HGO_OK;
 }
 
+int64_t hgo_insert_batch(hgo *h, int64_t count, const int32_t *creator, const int32_t *index,
+                         const int32_t *sp, const int32_t *op, const uint8_t *hash32,
+                         const uint8_t *sig_r32, const int32_t *ntx) {
+  int64_t bad = 0;
+  for (int64_t e = 0; e < count; e++)
+    bad += hgo_insert(h, creator[e], index[e], sp[e], op[e], hash32 + (size_t)e * 32,
+                      sig_r32 + (size_t)e * 32, ntx[e]) != HGO_OK;
+  return bad;
+}
+
 /* ------------------------------------------------------------------------ */
 /* DivideRounds (hashgraph.go:767-849)                                       */
 

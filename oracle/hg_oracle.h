@@ -52,6 +52,12 @@ void hgo_destroy(hgo *h);
 int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
                const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx);
 
+/* hgo_insert over arrays (test/bench harness convenience); returns the
+ * number of rejected events */
+int64_t hgo_insert_batch(hgo *h, int64_t count, const int32_t *creator, const int32_t *index,
+                         const int32_t *sp, const int32_t *op, const uint8_t *hash32,
+                         const uint8_t *sig_r32, const int32_t *ntx);
+
 int hgo_divide_rounds(hgo *h);            /* hashgraph.go:767-849 */
 int hgo_decide_fame(hgo *h);              /* hashgraph.go:852-947 */
 int hgo_decide_round_received(hgo *h);    /* hashgraph.go:951-1036 */

@@ -27,6 +27,8 @@ def lib():
         L.hgo_create.argtypes = [I32, VP, I64]
         L.hgo_destroy.argtypes = [P]
         L.hgo_insert.argtypes = [P, I32, I32, I32, I32, VP, VP, I32]
+        L.hgo_insert_batch.restype = I64
+        L.hgo_insert_batch.argtypes = [P, I64, VP, VP, VP, VP, VP, VP, VP]
         for f in ("hgo_divide_rounds", "hgo_decide_fame", "hgo_decide_round_received",
                   "hgo_process_decided_rounds", "hgo_run_consensus"):
             getattr(L, f).argtypes = [P]
@@ -83,13 +85,13 @@ class Oracle:
         return self.L.hgo_insert(self.h, creator, index, sp, op, _p(h), _p(r), ntx)
 
     def insert_dag(self, creator, index, sp, op, hashes, sig_r, ntx):
+        a = [np.ascontiguousarray(x, dtype=np.int32) for x in (creator, index, sp, op, ntx)]
         hashes = np.ascontiguousarray(hashes, dtype=np.uint8).reshape(-1, 32)
         sig_r = np.ascontiguousarray(sig_r, dtype=np.uint8).reshape(-1, 32)
-        for e in range(len(creator)):
-            rc = self.L.hgo_insert(self.h, int(creator[e]), int(index[e]), int(sp[e]),
-                                   int(op[e]), _p(hashes[e]), _p(sig_r[e]), int(ntx[e]))
-            if rc:
-                raise RuntimeError(f"oracle insert {e} failed rc={rc}")
+        bad = self.L.hgo_insert_batch(self.h, len(a[0]), _p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]),
+                                      _p(hashes), _p(sig_r), _p(a[4]))
+        if bad:
+            raise RuntimeError(f"oracle rejected {bad} events")
 
     def divide_rounds(self):
         return self.L.hgo_divide_rounds(self.h)

