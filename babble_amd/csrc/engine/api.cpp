@@ -175,8 +175,13 @@ int stage_rounds(bh_handle *h) {
   HIPCHK(h, hipEventRecord(h->ev[1], s));
   h->coords_for = (int)d.N;
   if (d.N == 0) {
+    HIPCHK(h, hipEventRecord(h->ev[2], s));
     h->R = 0;
     h->stage = 1;
+    h->decided_h.clear();
+    h->P = 0;
+    h->blocks.clear();
+    h->ncons = h->cons_txs = h->cons_loaded = h->nreceived = 0;
     return BH_OK;
   }
   if ((rc = build_graph(h))) return rc;
@@ -187,14 +192,14 @@ int stage_rounds(bh_handle *h) {
   HIPCHK(h, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
   int32_t *pin = h->pinned_state;
   bool done = false;
-  int64_t launched = 0;
+
   const int64_t max_batches = (int64_t)d.R_cap / ITER_BATCH + 2;
   for (int64_t b = 0; b < max_batches && !done; ++b) {
     HIPCHK(h, hipGraphLaunch(h->graph, s));
     HIPCHK(h, hipMemcpyAsync(pin + (b & 1) * bh::ST_COUNT, d.state, bh::ST_COUNT * 4,
                              hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
-    ++launched;
+
     if (b > 0) {
       HIPCHK(h, hipEventSynchronize(done_ev[(b - 1) & 1]));
       if (pin[((b - 1) & 1) * bh::ST_COUNT + bh::ST_DONE]) done = true;
@@ -278,6 +283,7 @@ int stage_order(bh_handle *h) {
   }
   float sms = 0;
   if (hipEventElapsedTime(&sms, h->ev_sweep[0], h->ev_sweep[1]) == hipSuccess) h->sweep_ms = sms;
+  (void)hipGetLastError();  // an unrecorded stage event (empty DAG) must not stay sticky
   return BH_OK;
 }
 

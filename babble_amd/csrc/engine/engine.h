@@ -27,10 +27,10 @@ constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 2048;     // frames sorted in LDS up to this size
 
 enum StateSlot {
-  ST_NEXT = 0,     // next round to resolve
+  ST_ARRIVE = 0,   // k_scan arrivals (last one advances ST_CUR)
   ST_DONE = 1,     // round loop finished
   ST_ROUNDS = 2,   // number of rounds R (LastRound + 1)
-  ST_CUR = 3,      // round whose witnesses fd/scan work on
+  ST_CUR = 3,      // round r of the current iteration: resolve W(r), scan B[r+1]
   ST_ERR = 4,      // capacity overflow / inconsistency
   ST_P = 5,        // processed prefix: rounds [0, P) are decided and ordered
   ST_NCONS = 6,    // consensus events (int32 ok: < 2^31)

@@ -122,33 +122,65 @@ __global__ __launch_bounds__(64) void k_la_sweep(Dev d) {
     const int64_t ring_lo = base + 64 - RING;
 
     for (int s = 0; s <= maxd; ++s) {
-      if (valid && dep == s) {
+      const bool mine = valid && dep == s;
+      const bool far = mine && ((sp >= 0 && sp < ring_lo) || (op >= 0 && op < ring_lo));
+      if (__builtin_expect(__any(far), 0)) {
+        // rare: a parent left the LDS ring; read its row from HBM (this wave
+        // wrote it >= RING events ago).  Kept on its own wave-uniform path so
+        // the common path below carries no vmcnt wait (which would also
+        // drain this wave's pending LA stores).
+        if (mine) {
+          if (lt_mode) {
+            int a = -1, b = -1;
+            if (sp >= 0) a = sp >= ring_lo ? ring_i[sp & (RING - 1)] : d.lt[sp];
+            if (op >= 0) b = op >= ring_lo ? ring_i[op & (RING - 1)] : d.lt[op];
+            const int v = max(a, b) + 1;
+            ring_i[e & (RING - 1)] = v;
+            d.lt[e] = v;
+          } else {
+            int4 a = none, b = none;
+            if (sp >= 0)
+              a = sp >= ring_lo ? ring[sp & (RING - 1)]
+                                : *reinterpret_cast<const int4 *>(d.la + (int64_t)(pos - 1) * d.npad + col0);
+            if (op >= 0)
+              b = op >= ring_lo ? ring[op & (RING - 1)]
+                                : *reinterpret_cast<const int4 *>(d.la + (int64_t)opos * d.npad + col0);
+            int4 v = max4(a, b);
+            const int own = cr - col0;
+            if (own == 0) v.x = idx;
+            else if (own == 1) v.y = idx;
+            else if (own == 2) v.z = idx;
+            else if (own == 3) v.w = idx;
+            ring[e & (RING - 1)] = v;
+            *reinterpret_cast<int4 *>(d.la + (int64_t)pos * d.npad + col0) = v;
+          }
+        }
+      } else if (mine) {
         if (lt_mode) {
-          int a = -1, b = -1;
-          if (sp >= 0) a = sp >= ring_lo ? ring_i[sp % RING] : d.lt[sp];
-          if (op >= 0) b = op >= ring_lo ? ring_i[op % RING] : d.lt[op];
+          const int a = sp >= 0 ? ring_i[sp & (RING - 1)] : -1;
+          const int b = op >= 0 ? ring_i[op & (RING - 1)] : -1;
           const int v = max(a, b) + 1;
-          ring_i[e % RING] = v;
+          ring_i[e & (RING - 1)] = v;
           d.lt[e] = v;
         } else {
-          int4 a = none, b = none;
-          if (sp >= 0)
-            a = sp >= ring_lo ? ring[sp % RING]
-                              : *reinterpret_cast<const int4 *>(d.la + (int64_t)(pos - 1) * d.npad + col0);
-          if (op >= 0)
-            b = op >= ring_lo ? ring[op % RING]
-                              : *reinterpret_cast<const int4 *>(d.la + (int64_t)opos * d.npad + col0);
+          const int4 a = sp >= 0 ? ring[sp & (RING - 1)] : none;
+          const int4 b = op >= 0 ? ring[op & (RING - 1)] : none;
           int4 v = max4(a, b);
           const int own = cr - col0;
           if (own == 0) v.x = idx;
           else if (own == 1) v.y = idx;
           else if (own == 2) v.z = idx;
           else if (own == 3) v.w = idx;
-          ring[e % RING] = v;
+          ring[e & (RING - 1)] = v;
           *reinterpret_cast<int4 *>(d.la + (int64_t)pos * d.npad + col0) = v;
         }
       }
-      __syncthreads();
+      // The block is ONE wave: its LDS accesses execute in issue order, so
+      // the next sub-step's ds_reads see this sub-step's ds_writes without a
+      // hardware barrier.  Only compiler ordering is needed -- a
+      // __syncthreads() here would also drain the global LA stores
+      // (s_waitcnt vmcnt(0)) on every sub-step.
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
   }
 }

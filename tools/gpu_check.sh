@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench.  Stops at the first step that
+# faults / aborts / times out (exit >= 124 or signal); test failures (exit 1)
+# still let the bench run so one call yields both.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "fatal step $name rc=$rc, stopping"; exit $rc
+  fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench2) step bench_c2 600 python bench.py --cfg 2 --steps 3 --warmup 1 ;;
+    bench3) step bench_c3 900 python bench.py --cfg 3 --steps 3 --warmup 1 ;;
+    bench) step bench 900 python bench.py ;;
+  esac
+done
