@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -92,10 +93,10 @@ int dalloc(bh_handle *h, T **p, size_t count) {
 void free_all(bh_handle *h) {
   Dev &d = h->d;
   void *ptrs[] = {d.creator, d.index, d.sp, d.op, d.ntx, d.coin, d.sigw, d.chain_start,
-                  d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.B,
+                  d.chain_len, d.chain_ids, d.epos, d.opos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.fdw, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters};
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fdc, d.candp};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -149,7 +150,7 @@ int build_graph(bh_handle *h) {
   }
   hipGraph_t g;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-  for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(h->d, h->stream);
+  for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(h->d, i & 1, h->stream);
   HIPCHK(h, hipStreamEndCapture(h->stream, &g));
   HIPCHK(h, hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0));
   (void)hipGraphDestroy(g);
@@ -184,7 +185,10 @@ int stage_rounds(bh_handle *h) {
     h->ncons = h->cons_txs = h->cons_loaded = h->nreceived = 0;
     return BH_OK;
   }
-  if ((rc = build_graph(h))) return rc;
+  // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
+  // captured graph (profiling / A-B; results are identical)
+  static const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
+  if (!no_graph && (rc = build_graph(h))) return rc;
   // replay batches of iterations; check completion one batch behind so the
   // device never idles on the host round trip
   hipEvent_t done_ev[2];
@@ -195,7 +199,12 @@ int stage_rounds(bh_handle *h) {
 
   const int64_t max_batches = (int64_t)d.R_cap / ITER_BATCH + 2;
   for (int64_t b = 0; b < max_batches && !done; ++b) {
-    HIPCHK(h, hipGraphLaunch(h->graph, s));
+    if (no_graph) {
+      for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(d, i & 1, s);
+      HIPCHK(h, hipGetLastError());
+    } else {
+      HIPCHK(h, hipGraphLaunch(h->graph, s));
+    }
     HIPCHK(h, hipMemcpyAsync(pin + (b & 1) * bh::ST_COUNT, d.state, bh::ST_COUNT * 4,
                              hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
@@ -283,6 +292,21 @@ int stage_order(bh_handle *h) {
   }
   float sms = 0;
   if (hipEventElapsedTime(&sms, h->ev_sweep[0], h->ev_sweep[1]) == hipSuccess) h->sweep_ms = sms;
+  if (d.diag) {  // diagnostic run only: phase counters to stderr, then reset
+    unsigned long long g[bh::DG_COUNT];
+    if (hipMemcpy(g, d.diag, sizeof g, hipMemcpyDeviceToHost) == hipSuccess) {
+      fprintf(stderr, "[bh diag] sweep: total %llu cyc, wait_desc %llu, wait_ring %llu, substeps %llu, far %llu, chunks %llu | mem: pref %llu store %llu idle %llu\n",
+              g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]);
+      fprintf(stderr, "[bh diag] scan: calls %llu, avg total %.0f cyc, load %.0f, compute %.0f, windows/call %.3f\n",
+              g[13], g[12] / (double)(g[13] ? g[13] : 1), g[10] / (double)(g[13] ? g[13] : 1),
+              g[11] / (double)(g[13] ? g[13] : 1), g[14] / (double)(g[13] ? g[13] : 1));
+      fprintf(stderr, "[bh diag] cand_fd: calls %llu, avg total %.0f cyc, loads %.0f, compaction %.0f, flag- %.0f, fd %.0f, extra fd windows/call %.3f\n",
+              g[21], g[20] / (double)(g[21] ? g[21] : 1), g[16] / (double)(g[21] ? g[21] : 1),
+              g[17] / (double)(g[21] ? g[21] : 1), g[18] / (double)(g[21] ? g[21] : 1),
+              g[19] / (double)(g[21] ? g[21] : 1), g[22] / (double)(g[21] ? g[21] : 1));
+    }
+    (void)hipMemset(d.diag, 0, bh::DG_COUNT * 8);
+  }
   (void)hipGetLastError();  // an unrecorded stage event (empty DAG) must not stay sticky
   return BH_OK;
 }
@@ -332,10 +356,12 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   };
   A(&d.creator, C); A(&d.index, C); A(&d.sp, C); A(&d.op, C); A(&d.ntx, C);
   A(&d.coin, C); A(&d.sigw, (size_t)C * 8);
-  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C);
-  A(&d.la, (size_t)C * d.npad); A(&d.lt, C); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1);
+  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C); A(&d.opos, C);
+  d.la_rows = C;
+  A(&d.la, (size_t)(C + 64) * d.npad); A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C * 2);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
-  A(&d.fdw, (size_t)d.W_cap * d.npad); A(&d.state, bh::ST_COUNT);
+  A(&d.fdw, (size_t)d.W_cap * d.npad);
+  A(&d.Bp, (size_t)2 * n); A(&d.fdc, (size_t)2 * n * d.npad); A(&d.candp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
   A(&d.frame_cnt, R1); A(&d.frame_ofs, R1); A(&d.frame_cur, R1); A(&d.blk_of_frame, R1);
@@ -354,6 +380,10 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.state, 0, bh::ST_COUNT * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.counters, 0, 4 * 8) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && getenv("BH_DIAG") && atoi(getenv("BH_DIAG"))) {
+    rc = dalloc(h, &d.diag, bh::DG_COUNT);
+    if (rc == BH_OK && hipMemset(d.diag, 0, bh::DG_COUNT * 8) != hipSuccess) rc = BH_ERR_DEVICE;
+  }
   if (rc != BH_OK) {
     free_all(h);
     delete h;

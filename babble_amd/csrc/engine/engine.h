@@ -44,18 +44,23 @@ struct Dev {
   int32_t n, npad, sm;
   int64_t N;
   int32_t R_cap;
+  int64_t la_rows;  // capacity rows of la / lt; 64 scratch rows follow
   int64_t W_cap;
   // event bodies
   int32_t *creator, *index, *sp, *op, *ntx;
   uint8_t *coin;
   uint32_t *sigw;
   // chains
-  int32_t *chain_start, *chain_len, *chain_ids, *epos;
+  int32_t *chain_start, *chain_len, *chain_ids, *epos, *opos;
   // coordinates
   int32_t *la, *lt;
   uint8_t *depth, *chunk_maxd;
+  int4 *desc;  // [N][2] packed sweep descriptors
   // rounds
   int32_t *B, *wofs, *wcnt, *wids, *fdw;
+  int32_t *Bp;     // [2][n] B[r] / B[r+1] by round parity
+  int32_t *fdc;    // [2][n][npad] firstDescendants rows of the candidates
+  int32_t *candp;  // [2][n] candidate event ids
   int32_t *state;
   int32_t *round;
   int8_t *witness, *fame;
@@ -69,7 +74,19 @@ struct Dev {
   int64_t *cons_pos;
   int64_t *frame_ntx;
   int64_t *counters;  // [0] consensus txs, [1] loaded consensus events, [2] received
+  // diagnostic phase counters (BH_DIAG=1 builds the buffer; null otherwise).
+  // Only a separate diagnostic run reads them; no result depends on them.
+  unsigned long long *diag;
 };
+
+enum DiagSlot {
+  DG_SW_TOTAL = 0, DG_SW_WAIT_DESC, DG_SW_WAIT_RING, DG_SW_SUBSTEPS, DG_SW_FAR, DG_SW_CHUNKS,
+  DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,
+  DG_SC_LOAD = 10, DG_SC_COMPUTE, DG_SC_TOTAL, DG_SC_CALLS, DG_SC_WINDOWS,
+  DG_RF_P1 = 16, DG_RF_ROWS, DG_RF_FLAG, DG_RF_FD, DG_RF_TOTAL, DG_RF_CALLS, DG_RF_FDWIN,
+  DG_COUNT = 32
+};
+__device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
 
 // launchers (kernels_*.hip)
 void configure_round_kernels();
@@ -79,7 +96,7 @@ void launch_prep(const Dev &d, hipStream_t s);
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep
 void launch_chunk_depth(const Dev &d, hipStream_t s);
 void launch_la_sweep(const Dev &d, hipStream_t s);
-void launch_round_iteration(const Dev &d, hipStream_t s);  // resolve + fd + scan
+void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // cand_fd + scan
 void launch_assign_rounds(const Dev &d, hipStream_t s);
 void launch_fame(const Dev &d, int32_t R, hipStream_t s);
 void launch_round_received(const Dev &d, int32_t R, hipStream_t s);

@@ -66,9 +66,13 @@ def engine(n, creator, index, sp, op, hashes, sig_r, ntx):
     Bs = [np.zeros(n, np.int64)]
     Ws = [resolve(Bs[0])]
     FDW = [np.stack([fd_row(w) for w in Ws[0]])]
+    ALLC = os.environ.get("ALLC") == "1"
     while True:
         r = len(Bs) - 1
         W, F = Ws[r], FDW[r]
+        if ALLC:  # scan against every candidate of round r
+            cands = [chain[c][Bs[r][c]] for c in range(n) if Bs[r][c] < clen[c]]
+            F = np.stack([fd_row(w) for w in cands])
         Bn = Bs[r].copy()
         for c in range(n):
             k = Bs[r][c]
