@@ -7,7 +7,7 @@ CC ?= gcc
 ENGINE_SRC := $(wildcard babble_amd/csrc/engine/*.hip) $(wildcard babble_amd/csrc/engine/*.cpp)
 ENGINE_HDR := $(wildcard babble_amd/csrc/engine/*.h) include/babble_hip.h
 
-all: babble_amd/libbabble_gen.so babble_amd/libbabble_hip.so oracle/liboracle.so
+all: babble_amd/libbabble_gen.so babble_amd/libbabble_hip.so oracle/liboracle.so tests/cpp/hg_replay
 
 babble_amd/libbabble_gen.so: babble_amd/csrc/dag_gen.c babble_amd/csrc/dag_gen.h
 	$(CC) -O2 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
@@ -18,7 +18,11 @@ babble_amd/libbabble_hip.so: $(ENGINE_SRC) $(ENGINE_HDR)
 oracle/liboracle.so: oracle/hg_oracle.c oracle/hg_oracle.h
 	$(MAKE) -C oracle
 
+# C++ host mirror driver (plain g++; links the engine, rpath to the in-tree .so)
+tests/cpp/hg_replay: tests/cpp/hg_replay.cpp include/babble_hashgraph.hpp include/babble_hip.h babble_amd/libbabble_hip.so
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lbabble_amd -lbabble_hip -Wl,-rpath,'$$ORIGIN/../../babble_amd'
+
 clean:
-	rm -f babble_amd/*.so oracle/*.so
+	rm -f babble_amd/*.so oracle/*.so tests/cpp/hg_replay
 
 .PHONY: all clean

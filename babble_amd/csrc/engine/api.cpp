@@ -94,9 +94,9 @@ void free_all(bh_handle *h) {
   Dev &d = h->d;
   void *ptrs[] = {d.creator, d.index, d.sp, d.op, d.ntx, d.coin, d.sigw, d.chain_start,
                   d.chain_len, d.chain_ids, d.epos, d.opos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
-                  d.wofs, d.wcnt, d.wids, d.fdw, d.state, d.round, d.witness, d.fame,
+                  d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fdc, d.candp};
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fdc};  // la_ev aliases fdc
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -172,6 +172,7 @@ int stage_rounds(bh_handle *h) {
   HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
   bh::launch_la_sweep(d, s);
   HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
+  bh::launch_permute(d, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
   h->coords_for = (int)d.N;
@@ -223,6 +224,7 @@ int stage_rounds(bh_handle *h) {
   if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
   h->R = st[bh::ST_ROUNDS];
   h->iters = st[bh::ST_ITERS];
+  bh::launch_witness_tables(d, h->R, s);
   bh::launch_assign_rounds(d, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[2], s));
@@ -358,10 +360,14 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.coin, C); A(&d.sigw, (size_t)C * 8);
   A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C); A(&d.opos, C);
   d.la_rows = C;
-  A(&d.la, (size_t)(C + 64) * d.npad); A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C * 2);
+  A(&d.la, (size_t)(C + 64) * d.npad);
+  // the sweep's slabs (la_ev) are dead once permuted into la; the round loop's
+  // per-round candidate FD rows (fdc) reuse the same allocation
+  A(&d.fdc, std::max((size_t)(C + 64) * d.npad, (size_t)d.R_cap * n * d.npad));
+  d.la_ev = d.fdc; A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
-  A(&d.fdw, (size_t)d.W_cap * d.npad);
-  A(&d.Bp, (size_t)2 * n); A(&d.fdc, (size_t)2 * n * d.npad); A(&d.candp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
+  A(&d.wrow, (size_t)d.W_cap);
+  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
   A(&d.frame_cnt, R1); A(&d.frame_ofs, R1); A(&d.frame_cur, R1); A(&d.blk_of_frame, R1);

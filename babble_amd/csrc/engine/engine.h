@@ -7,10 +7,12 @@
 //   chain_ids                int32[N]       ids grouped by creator, ordered by index
 //   epos                     int32[N]       row of event e = chain_start[creator] + index
 //   la                       int32[N][npad] lastAncestors indexes (-1 = none), chain-major rows
+//   la_ev                    int4[npad/4][N] the sweep's output (one column group per slab,
+//                                           event order), permuted into `la` afterwards
 //   lt                       int32[N]       Lamport timestamp
 //   B                        int32[R_cap+1][n] first index on chain c with round >= r
 //   wids / wofs / wcnt       witnesses of each round (chain order)
-//   fdw                      int32[W_cap][npad] firstDescendants rows of witnesses
+//   fdc                      int32[R][n][npad] firstDescendants rows of each round's candidates
 //   round/witness/fame/rr    per-event results
 // See DESIGN.md for the algorithm and the roofline of each kernel.
 #pragma once
@@ -54,13 +56,15 @@ struct Dev {
   int32_t *chain_start, *chain_len, *chain_ids, *epos, *opos;
   // coordinates
   int32_t *la, *lt;
+  int32_t *la_ev;  // [npad/4][la_rows+64][4] sweep output: column-group-major, event-major
   uint8_t *depth, *chunk_maxd;
-  int4 *desc;  // [N][2] packed sweep descriptors
+  int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds
-  int32_t *B, *wofs, *wcnt, *wids, *fdw;
+  int32_t *B, *wofs, *wcnt, *wids;
+  int32_t *wrow;   // [W] row of each witness's firstDescendants in fdc (r * n + chain)
   int32_t *Bp;     // [2][n] B[r] / B[r+1] by round parity
-  int32_t *fdc;    // [2][n][npad] firstDescendants rows of the candidates
-  int32_t *candp;  // [2][n] candidate event ids
+  int32_t *fdc;    // [R_cap][n][npad] firstDescendants rows of every round's candidates
+                   // (shares its allocation with la_ev, which is dead by then)
   int32_t *state;
   int32_t *round;
   int8_t *witness, *fame;
@@ -96,7 +100,9 @@ void launch_prep(const Dev &d, hipStream_t s);
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep
 void launch_chunk_depth(const Dev &d, hipStream_t s);
 void launch_la_sweep(const Dev &d, hipStream_t s);
+void launch_permute(const Dev &d, hipStream_t s);  // sweep slabs -> chain-major LA rows
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // cand_fd + scan
+void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wcnt/wrow
 void launch_assign_rounds(const Dev &d, hipStream_t s);
 void launch_fame(const Dev &d, int32_t R, hipStream_t s);
 void launch_round_received(const Dev &d, int32_t R, hipStream_t s);

@@ -91,36 +91,61 @@ __global__ __launch_bounds__(256) void k_chunk_depth(Dev d) {
   if (lane == 0) d.chunk_maxd[chunk] = (uint8_t)m;
 }
 
-// per-event sweep descriptor, 32 B: {sp, op, creator, index}, {depth, row,
-// other-parent row, max depth of the event's chunk}
-__global__ void k_pack_desc(Dev d) {
+// per-event sweep descriptor, 16 B -- everything the compute wave needs,
+// precomputed so that its per-chunk work is one LDS read:
+//   .x = ring slot of sp | ring slot of op << 16
+//   .y = creator | flags << 16
+//   .z = index, .w = LA row (chain-major position, for the write-back)
+// Ring slots are (event & (VRING-1)); an absent parent, or one that is too
+// old to still be in the ring ("far"), maps to the sentinel slot VRING (-1s).
+// flags = maxd (max intra-chunk depth, chunk-uniform) | chunk-has-far << 8 |
+//         sp-far << 9 | op-far << 10.
+constexpr int VRING = 4096;  // value ring (events); parents this recent stay on chip
+constexpr int SW_FAR = 0x100, SW_SPFAR = 0x200, SW_OPFAR = 0x400;
+
+__global__ __launch_bounds__(256) void k_pack_desc(Dev d) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.N) return;
-  d.desc[2 * e] = make_int4(d.sp[e], d.op[e], d.creator[e], d.index[e]);
-  d.desc[2 * e + 1] = make_int4(d.depth[e], d.epos[e], d.opos[e], d.chunk_maxd[e >> 6]);
+  const int64_t base = e & ~(int64_t)63;  // a wave is a chunk
+  const bool valid = e < d.N;
+  const int64_t ring_lo = base + 64 - VRING;
+  int32_t sp = -1, op = -1;
+  if (valid) { sp = d.sp[e]; op = d.op[e]; }
+  const bool spfar = sp >= 0 && sp < ring_lo, opfar = op >= 0 && op < ring_lo;
+  const bool far = __any(spfar || opfar);
+  if (!valid) return;
+  const int sa = (sp < 0 || spfar) ? VRING : (int)(sp & (VRING - 1));
+  const int sb = (op < 0 || opfar) ? VRING : (int)(op & (VRING - 1));
+  const int fl = (int)d.chunk_maxd[e >> 6] | (far ? SW_FAR : 0) | (spfar ? SW_SPFAR : 0) |
+                 (opfar ? SW_OPFAR : 0);
+  d.desc[e] = make_int4(sa | (sb << 16), d.creator[e] | (fl << 16), d.index[e], d.epos[e]);
 }
 
 // ---------------------------------------------------------------------------
 // The coordinate sweep.  blockIdx.x < ngroups: columns [4g, 4g+4);
 // blockIdx.x == ngroups: Lamport timestamps.
 //
-// Wave specialisation inside each two-wave workgroup:
-//   wave 0 (compute) walks the chunks doing LDS-only work: descriptors from
-//          the LDS descriptor ring, parents from the LDS value ring;
-//   wave 1 (memory)  prefetches descriptors of upcoming chunks into the
-//          descriptor ring and writes finished chunks from the value ring to
-//          HBM.
-// vmcnt is one in-order counter per wave covering loads AND stores, so a
-// single wave that both stores rows and prefetches descriptors drains its
-// stores at every descriptor wait (two HBM round trips per chunk, measured
-// 1.9 us/chunk).  Split this way, the compute wave issues no stores and
-// waits only on LDS.  The waves hand off through LDS counters; a wave's LDS
-// operations execute in order, so data written before a counter is visible
-// to a reader that has seen the counter.
-constexpr int VRING = 4096;  // value ring (events)
-constexpr int DRING = 32;    // descriptor ring (chunks)
-constexpr int PBATCH = 16;   // chunks prefetched per memory-wave iteration
+// Three specialised waves per workgroup, handing off through LDS counters:
+//   wave 0 (compute)  walks the chunks touching only LDS: one descriptor
+//                     read per chunk, then maxd+1 sub-steps of
+//                     2 x ds_read_b128, 4 x v_max3, ds_write_b128;
+//   wave 1 (prefetch) streams descriptors into the LDS descriptor ring with
+//                     LDS-DMA (global_load_lds_dwordx4, 1 KiB = one chunk per
+//                     instruction), GROUP chunks per group, two groups in
+//                     flight, retired with counted vmcnt waits;
+//   wave 2 (store)    reads finished chunks out of the value ring and writes
+//                     them to HBM; it frees ring slots as soon as it has READ
+//                     them and publishes HBM visibility separately (needed
+//                     only by the rare chunk whose parent left the ring).
+// vmcnt is one in-order counter per wave covering loads AND stores, so
+// keeping prefetch and stores in different waves means neither ever waits
+// for the other's traffic.  A wave's LDS operations execute in order, and
+// the CU's LDS serves waves through one pipeline, so data written before a
+// counter is visible to a reader that has seen the counter.
+constexpr int DRING = 64;   // descriptor ring (chunks); slot DRING is a sink
+constexpr int GROUP = 8;    // chunks per prefetch group (= vmcnt step)
+static_assert(GROUP == 8, "the prefetch wave's counted wait is vmcnt(8)");
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ int4 nt_load4(const int32_t *p) {  // L1-bypassing 16-B load
   const v4i v = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(p));
@@ -131,188 +156,190 @@ __device__ __forceinline__ int4 max4(int4 a, int4 b) {
   return make_int4(max(a.x, b.x), max(a.y, b.y), max(a.z, b.z), max(a.w, b.w));
 }
 
-__device__ __forceinline__ int4 set_own(int4 v, int own, int idx) {
-  if (own == 0) v.x = idx;
-  else if (own == 1) v.y = idx;
-  else if (own == 2) v.z = idx;
-  else if (own == 3) v.w = idx;
-  return v;
-}
+// progress counters live in LDS; an explicit address space keeps them ds_*
+// ops (through a generic pointer they become flat ops that wait on vmcnt)
+typedef __attribute__((address_space(3))) volatile int lds_flag;
+__device__ __forceinline__ int lds_poll(lds_flag *p) { return *p; }
+#define COMPILER_FENCE() __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront")
 
-__device__ __forceinline__ int lds_poll(volatile int *p) { return *p; }
+enum { F_LANDED = 0, F_COMPUTED = 1, F_READ = 2, F_STORED = 3 };
 
 template <bool LT>
-__device__ __forceinline__ void sweep_body(const Dev &d, int4 *vring, int4 (*dring)[2][64], int *flags) {
+__device__ __forceinline__ void sweep_body(const Dev &d, int4 *vring, int4 (*dring)[64], int *flags) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int ngroups = d.npad / 4;
   const int g = LT ? ngroups : blockIdx.x;
-  const bool lt_mode = LT;
   const int col0 = 4 * g;
   const int64_t N = d.N;
   const int64_t nchunks = (N + 63) / 64;
-  volatile int *vf = flags;
+  lds_flag *vf = (lds_flag *)flags;
+  int4 *const slab = reinterpret_cast<int4 *>(d.la_ev) + (int64_t)g * (d.la_rows + 64);
   const int4 none = make_int4(-1, -1, -1, -1);
   if (threadIdx.x < 4) flags[threadIdx.x] = 0;
-  if (threadIdx.x == 0) vring[VRING] = none;  // sentinel slot for absent parents
+  if (threadIdx.x == 0) vring[VRING] = none;  // sentinel slot for absent / far parents
   __syncthreads();
+  const bool dgw = d.diag != nullptr && g == 0 && lane == 0;
 
   if (wave == 1) {
-    // ---------------- memory wave ----------------
-    int64_t mload = 0, mstore = 0;
-    const bool dgm = d.diag != nullptr && g == 0 && lane == 0;
-    unsigned long long m_pref = 0, m_store = 0, m_idle = 0;
-    while (mstore < nchunks) {
-      bool idle = true;
-      const unsigned long long ta = dgm ? stamp() : 0;
-      // prefetch descriptors into free slots (a slot is free once its chunk
-      // has been written back: the store takes the row index from it).  All
-      // PBATCH chunks' loads are issued unconditionally (clamped) before the
-      // first use, so the wave pays one HBM latency per batch.
-      const int64_t room = min((int64_t)PBATCH, min(nchunks - mload, mstore + DRING - mload));
-      if (room > 0) {
-        int4 pa[PBATCH], pb[PBATCH];
-#pragma unroll
-        for (int q = 0; q < PBATCH; ++q) {
-          const int64_t mq = min(mload + q, nchunks - 1);
-          int64_t e = mq * 64 + lane;
-          e = e < N ? e : N - 1;
-          pa[q] = d.desc[2 * e];
-          pb[q] = d.desc[2 * e + 1];
-        }
-#pragma unroll
-        for (int q = 0; q < PBATCH; ++q) {
-          if (q < room) {
-            int4 b = pb[q];
-            if ((mload + q) * 64 + lane >= N) b.x = 255;  // tail lanes never match a sub-step
-            dring[(mload + q) % DRING][0][lane] = pa[q];
-            dring[(mload + q) % DRING][1][lane] = b;
-          }
-        }
-        mload += room;
-        if (lane == 0) vf[0] = (int)mload;
-        idle = false;
+    // ---------------- prefetch wave ----------------
+    unsigned long long t_busy = 0, n_idle = 0;
+    int64_t issued = 0, freed = DRING;  // chunks issued; slots usable below `freed`
+    int inflight = 0;                   // groups in flight
+    for (;;) {
+      bool can = issued < nchunks;
+      if (can && issued + GROUP > freed) {
+        freed = (int64_t)lds_poll(&vf[F_READ]) + DRING;
+        can = issued + GROUP <= freed;
       }
-      const unsigned long long tb = dgm ? stamp() : 0;
-      if (dgm) m_pref += tb - ta;
-      // write back computed chunks; publish once the stores have drained
-      const int64_t computed = lds_poll(&vf[1]);
-      if (mstore < computed) {
-        for (; mstore < computed; ++mstore) {
-          const int64_t e = mstore * 64 + lane;
-          if (e < N) {
-            const int4 v = vring[e & (VRING - 1)];
-            if (lt_mode) d.lt[e] = v.x;
-            else {
-              const int pos = dring[mstore % DRING][1][lane].y;
-              *reinterpret_cast<int4 *>(d.la + (int64_t)pos * d.npad + col0) = v;
-            }
-          }
+      if (can) {
+        const unsigned long long ta = dgw ? stamp() : 0;
+#pragma unroll
+        for (int q = 0; q < GROUP; ++q) {
+          const int64_t mq = issued + q;
+          const int64_t e = min(mq * 64 + lane, N - 1);
+          int4 *dst = mq < nchunks ? &dring[mq % DRING][0] : &dring[DRING][0];
+          __builtin_amdgcn_global_load_lds((const void *)(d.desc + e), (lds_void *)dst, 16, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) vf[2] = (int)mstore;
-        idle = false;
+        issued += GROUP;
+        ++inflight;
+        if (dgw) t_busy += stamp() - ta;
       }
-      if (dgm) m_store += stamp() - tb;
-      if (idle) {
-        if (dgm) ++m_idle;
+      if (inflight == 2 || (!can && inflight > 0)) {
+        if (inflight == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        --inflight;
+        if (lane == 0) vf[F_LANDED] = (int)min(issued - (int64_t)inflight * GROUP, nchunks);
+      } else if (!can) {
+        if (issued >= nchunks) break;
+        if (dgw) ++n_idle;
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    if (dgm) {
-      d.diag[DG_SW_MEM_PREF] = m_pref;
-      d.diag[DG_SW_MEM_STORE] = m_store;
-      d.diag[DG_SW_MEM_IDLE] = m_idle;
+    if (dgw) { d.diag[DG_SW_MEM_PREF] = t_busy; d.diag[DG_SW_MEM_IDLE] = n_idle; }
+    return;
+  }
+
+  if (wave == 2) {
+    // ---------------- store wave ----------------
+    unsigned long long t_busy = 0;
+    int64_t mstore = 0, computed = 0, published = 0;
+    while (mstore < nchunks) {
+      if (computed <= mstore) {
+        computed = lds_poll(&vf[F_COMPUTED]);
+        if (computed <= mstore) {
+          if (published < mstore) {  // idle: make the stores visible
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) vf[F_STORED] = (int)mstore;
+            published = mstore;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+      }
+      const unsigned long long ta = dgw ? stamp() : 0;
+      const int64_t hi = min(computed, mstore + 8);
+      int4 v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t m = min(mstore + q, hi - 1);
+        v[q] = vring[(m * 64 + lane) & (VRING - 1)];
+      }
+      // one contiguous 1 KiB store per chunk (event-major slab of this
+      // column group); k_permute builds the chain-major rows afterwards
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t e = (mstore + q) * 64 + lane;
+        if (mstore + q < hi && e < N) {
+          if (LT) d.lt[e] = v[q].x;
+          else slab[e] = v[q];
+        }
+      }
+      mstore = hi;
+      COMPILER_FENCE();
+      if (lane == 0) vf[F_READ] = (int)mstore;  // slots read: reusable
+      if (mstore - published >= 64) {           // bound what a far reader may wait for
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) vf[F_STORED] = (int)mstore;
+        published = mstore;
+      }
+      if (dgw) t_busy += stamp() - ta;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) vf[F_STORED] = (int)nchunks;
+    if (dgw) d.diag[DG_SW_MEM_STORE] = t_busy;
     return;
   }
 
   // ---------------- compute wave ----------------
+  // Per chunk: the NEXT chunk's descriptor is read before this chunk's
+  // sub-steps (LDS returns in order, so it costs no extra wait); the other
+  // waves' counters are re-polled only when the cached values run out.
+  // Sub-step s rewrites every lane's slot with max(ring[sa], ring[sb], own)
+  // -- unconditionally: a lane's value is final from sub-step depth(lane) on
+  // (its in-chunk parents are final one sub-step earlier), and nobody needs
+  // it before then.  The slots written alias only events older than the
+  // ring, which no lane reads (far parents map to the sentinel and are
+  // folded into `own` from HBM instead).
   int *vring_i = reinterpret_cast<int *>(vring);
   const bool dg = d.diag != nullptr && g == 0;
   unsigned long long t_start = dg ? stamp() : 0, w_desc = 0, w_ring = 0, nsub = 0, nfar = 0;
-  int4 res4 = none;
+  int64_t have = 0, readc = 0;
+  while ((have = lds_poll(&vf[F_LANDED])) <= 0) __builtin_amdgcn_s_sleep(1);
+  int4 dc = dring[0][lane];
   for (int64_t m = 0; m < nchunks; ++m) {
-    unsigned long long t0 = dg ? stamp() : 0;
-    while (lds_poll(&vf[0]) <= m) __builtin_amdgcn_s_sleep(1);
-    unsigned long long t1 = dg ? stamp() : 0;
-    // chunk m writes value-ring slots last used by chunk m - VRING/64
-    while ((int64_t)lds_poll(&vf[2]) < m - VRING / 64 + 1) __builtin_amdgcn_s_sleep(1);
-    if (dg) { const unsigned long long t2 = stamp(); w_desc += t1 - t0; w_ring += t2 - t1; }
-    const int4 da = dring[m % DRING][0][lane];
-    const int4 db = dring[m % DRING][1][lane];
-    const int32_t sp = da.x, op = da.y, cr = da.z, idx = da.w;
-    const int32_t dep = db.x, pos = db.y, opos = db.z, maxd = db.w;
-    const int64_t base = m * 64;
-    const int64_t e = base + lane;
-    // parents at or after ring_lo are in the value ring; older ones were
-    // written back (stored >= m - VRING/64 + 1 covers their chunks)
-    const int64_t ring_lo = base + 64 - VRING;
-    const bool far = (sp >= 0 && sp < ring_lo) || (op >= 0 && op < ring_lo);
-    const int own = cr - col0;
-    if (__builtin_expect(!__any(far), 1)) {
-      // Common case, branch-free sub-steps: every lane reads its parents'
-      // slots (absent parents -> the sentinel slot of -1s) and rewrites its
-      // own slot each sub-step, the new value once its depth comes up.  Safe:
-      // a lane of depth s only reads parents of depth < s (already final),
-      // and the slots this chunk writes alias only events older than
-      // ring_lo, which no lane of this chunk reads (no far parent).
-      const int sa = sp >= 0 ? (int)(sp & (VRING - 1)) : VRING;
-      const int sb = op >= 0 ? (int)(op & (VRING - 1)) : VRING;
-      const int sw = (int)(e & (VRING - 1));
-      const bool ox = own == 0, oy = own == 1, oz = own == 2, ow = own == 3;
-      if (LT) {
-        int res1 = -1;
-        for (int s = 0; s <= maxd; ++s) {
-          const int v = max(vring_i[4 * sa], vring_i[4 * sb]) + 1;
-          res1 = dep == s ? v : res1;
-          vring_i[4 * sw] = res1;
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        }
-        res4.x = res1;
-      } else {
-        for (int s = 0; s <= maxd; ++s) {
-          int4 v = max4(vring[sa], vring[sb]);
-          v.x = ox ? idx : v.x;
-          v.y = oy ? idx : v.y;
-          v.z = oz ? idx : v.z;
-          v.w = ow ? idx : v.w;
-          const bool mine = dep == s;
-          res4.x = mine ? v.x : res4.x;
-          res4.y = mine ? v.y : res4.y;
-          res4.z = mine ? v.z : res4.z;
-          res4.w = mine ? v.w : res4.w;
-          vring[sw] = res4;
-          // one wave: LDS ops execute in issue order; compiler ordering only
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        }
+    const unsigned long long t0 = dg ? stamp() : 0;
+    const bool nxt = m + 1 < nchunks && (have > m + 1 || (have = lds_poll(&vf[F_LANDED])) > m + 1);
+    int4 dn = dc;
+    if (nxt) dn = dring[(m + 1) % DRING][lane];
+    // chunk m overwrites value-ring slots of chunk m - VRING/64
+    const int64_t need = m - VRING / 64 + 1;
+    if (readc < need)
+      while ((readc = lds_poll(&vf[F_READ])) < need) __builtin_amdgcn_s_sleep(1);
+    if (dg) w_ring += stamp() - t0;
+    const int sa = dc.x & 0xffff, sb = dc.x >> 16;
+    const int own = (dc.y & 0xffff) - col0;
+    const int fl = __builtin_amdgcn_readfirstlane(dc.y >> 16);
+    const int maxd = fl & 0xff;
+    const int sw = (int)((m * 64 + lane) & (VRING - 1));
+    if (__builtin_expect(fl & SW_FAR, 0)) {
+      // parents older than the ring: wait until their chunks are in HBM
+      while (lds_poll(&vf[F_STORED]) < need) __builtin_amdgcn_s_sleep(1);
+    }
+    if (LT) {
+      int farv = -1;
+      if (__builtin_expect(fl & SW_FAR, 0)) {  // L1-bypassing loads of rows written by this CU
+        const int64_t e = min(m * 64 + lane, N - 1);
+        if ((dc.y >> 16) & SW_SPFAR) farv = max(farv, __builtin_nontemporal_load(d.lt + d.sp[e]));
+        if ((dc.y >> 16) & SW_OPFAR) farv = max(farv, __builtin_nontemporal_load(d.lt + d.op[e]));
       }
-      if (dg) nsub += maxd + 1;
-    } else {
-      // rare: some parent left the value ring; read it from HBM with
-      // L1-bypassing loads (the line may hold bytes written after this CU
-      // cached it), predicated per lane
-      if (dg) { nsub += maxd + 1; ++nfar; }
       for (int s = 0; s <= maxd; ++s) {
-        if (dep == s) {
-          if (LT) {
-            int a = -1, b = -1;
-            if (sp >= 0) a = sp >= ring_lo ? vring_i[4 * (sp & (VRING - 1))] : __builtin_nontemporal_load(d.lt + sp);
-            if (op >= 0) b = op >= ring_lo ? vring_i[4 * (op & (VRING - 1))] : __builtin_nontemporal_load(d.lt + op);
-            vring_i[4 * (e & (VRING - 1))] = max(a, b) + 1;
-          } else {
-            int4 a = none, b = none;
-            if (sp >= 0)
-              a = sp >= ring_lo ? vring[sp & (VRING - 1)] : nt_load4(d.la + (int64_t)(pos - 1) * d.npad + col0);
-            if (op >= 0)
-              b = op >= ring_lo ? vring[op & (VRING - 1)] : nt_load4(d.la + (int64_t)opos * d.npad + col0);
-            vring[e & (VRING - 1)] = set_own(max4(a, b), own, idx);
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        vring_i[4 * sw] = max(max(vring_i[4 * sa], vring_i[4 * sb]), farv) + 1;
+        COMPILER_FENCE();  // one wave: LDS ops execute in issue order
+      }
+    } else {
+      const int idx = dc.z;
+      int4 ownv = make_int4(own == 0 ? idx : -1, own == 1 ? idx : -1, own == 2 ? idx : -1,
+                            own == 3 ? idx : -1);
+      if (__builtin_expect(fl & SW_FAR, 0)) {
+        const int64_t e = min(m * 64 + lane, N - 1);
+        if ((dc.y >> 16) & SW_SPFAR) ownv = max4(ownv, nt_load4(reinterpret_cast<const int32_t *>(slab + d.sp[e])));
+        if ((dc.y >> 16) & SW_OPFAR) ownv = max4(ownv, nt_load4(reinterpret_cast<const int32_t *>(slab + d.op[e])));
+      }
+      for (int s = 0; s <= maxd; ++s) {
+        vring[sw] = max4(max4(vring[sa], vring[sb]), ownv);
+        COMPILER_FENCE();
       }
     }
-    if (lane == 0) vf[1] = (int)(m + 1);
+    if (dg) { nsub += maxd + 1; nfar += (fl & SW_FAR) ? 1 : 0; }
+    if (lane == 0) vf[F_COMPUTED] = (int)(m + 1);
+    if (!nxt && m + 1 < nchunks) {
+      const unsigned long long t1 = dg ? stamp() : 0;
+      while ((have = lds_poll(&vf[F_LANDED])) <= m + 1) __builtin_amdgcn_s_sleep(1);
+      if (dg) w_desc += stamp() - t1;
+      dn = dring[(m + 1) % DRING][lane];
+    }
+    dc = dn;
   }
   if (dg && lane == 0) {
     d.diag[DG_SW_TOTAL] = stamp() - t_start;
@@ -333,22 +360,51 @@ void launch_chunk_depth(const Dev &d, hipStream_t s) {
 
 // one launch: column-group workgroups and the Lamport workgroup run
 // concurrently; the branch is uniform per workgroup
-__global__ __launch_bounds__(128) void k_la_sweep(Dev d) {
-  __shared__ int4 vring[VRING + 1];         // 64 KiB results (LT mode: .x); [VRING] = -1s
-  __shared__ int4 dring[DRING][2][64];      // 64 KiB {sp,op,cr,idx},{dep,pos,opos,maxd}
-  __shared__ int flags[4];                  // [0] desc ready, [1] computed, [2] stored
+__global__ __launch_bounds__(192) void k_la_sweep(Dev d) {
+  __shared__ int4 vring[VRING + 1];       // 64 KiB results (LT mode: .x); [VRING] = -1s
+  __shared__ int4 dring[DRING + 1][64];   // 65 KiB descriptors; [DRING] = prefetch sink
+  __shared__ int flags[4];
   if ((int)blockIdx.x == d.npad / 4) sweep_body<true>(d, vring, dring, flags);
   else sweep_body<false>(d, vring, dring, flags);
 }
 
+// the sweep's column-group slabs -> chain-major LA rows (the layout the
+// round loop's per-chain windows read).  One wave per 64 events: every
+// load instruction reads 1 KiB contiguous from a slab; each lane writes its
+// own row's 16-B pieces in column order, so a row's lines are complete by
+// the time they leave L2.  HBM-bound: 2 x 4*npad bytes per event.
+__global__ __launch_bounds__(256) void k_permute(Dev d) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  const int ng = d.npad / 4;
+  const int64_t stride = d.la_rows + 64;
+  const int4 *src = reinterpret_cast<const int4 *>(d.la_ev) + e;
+  int4 *dst = reinterpret_cast<int4 *>(d.la + (int64_t)d.epos[e] * d.npad);
+  int g = 0;
+  for (; g + 8 <= ng; g += 8) {
+    int4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = nt_load4(reinterpret_cast<const int32_t *>(src + (int64_t)(g + u) * stride));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dst[g + u] = v[u];
+  }
+  for (; g < ng; ++g) dst[g] = src[(int64_t)g * stride];
+}
+
 void launch_la_sweep(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
-  k_la_sweep<<<d.npad / 4 + 1, 128, 0, s>>>(d);
+  k_la_sweep<<<d.npad / 4 + 1, 192, 0, s>>>(d);
+}
+
+void launch_permute(const Dev &d, hipStream_t s) {
+  if (d.N == 0) return;
+  k_permute<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
 }
 
 void launch_coordinates(const Dev &d, hipStream_t s) {
   launch_chunk_depth(d, s);
   launch_la_sweep(d, s);
+  launch_permute(d, s);
 }
 
 }  // namespace bh
