@@ -96,7 +96,7 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.opos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fdc};  // la_ev aliases fdc
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -130,12 +130,14 @@ int upload(bh_handle *h) {
 int set_chain_tables(bh_handle *h) {
   const int n = h->d.n;
   std::vector<int32_t> start(n), len(n);
-  int32_t acc = 0;
+  int32_t acc = 0, mx = 0;
   for (int c = 0; c < n; ++c) {
     start[c] = acc;
     len[c] = (int32_t)h->chain[c].size();
     acc += len[c];
+    mx = std::max(mx, len[c]);
   }
+  h->d.max_chain_len = mx;
   HIPCHK(h, hipMemcpyAsync(h->d.chain_start, start.data(), n * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->d.chain_len, len.data(), n * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -173,6 +175,7 @@ int stage_rounds(bh_handle *h) {
   bh::launch_la_sweep(d, s);
   HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
   bh::launch_permute(d, s);
+  bh::launch_first_descendants(d, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
   h->coords_for = (int)d.N;
@@ -299,13 +302,6 @@ int stage_order(bh_handle *h) {
     if (hipMemcpy(g, d.diag, sizeof g, hipMemcpyDeviceToHost) == hipSuccess) {
       fprintf(stderr, "[bh diag] sweep: total %llu cyc, wait_desc %llu, wait_ring %llu, substeps %llu, far %llu, chunks %llu | mem: pref %llu store %llu idle %llu\n",
               g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]);
-      fprintf(stderr, "[bh diag] scan: calls %llu, avg total %.0f cyc, load %.0f, compute %.0f, windows/call %.3f\n",
-              g[13], g[12] / (double)(g[13] ? g[13] : 1), g[10] / (double)(g[13] ? g[13] : 1),
-              g[11] / (double)(g[13] ? g[13] : 1), g[14] / (double)(g[13] ? g[13] : 1));
-      fprintf(stderr, "[bh diag] cand_fd: calls %llu, avg total %.0f cyc, loads %.0f, compaction %.0f, flag- %.0f, fd %.0f, extra fd windows/call %.3f\n",
-              g[21], g[20] / (double)(g[21] ? g[21] : 1), g[16] / (double)(g[21] ? g[21] : 1),
-              g[17] / (double)(g[21] ? g[21] : 1), g[18] / (double)(g[21] ? g[21] : 1),
-              g[19] / (double)(g[21] ? g[21] : 1), g[22] / (double)(g[21] ? g[21] : 1));
     }
     (void)hipMemset(d.diag, 0, bh::DG_COUNT * 8);
   }
@@ -361,10 +357,13 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C); A(&d.opos, C);
   d.la_rows = C;
   A(&d.la, (size_t)(C + 64) * d.npad);
-  // the sweep's slabs (la_ev) are dead once permuted into la; the round loop's
-  // per-round candidate FD rows (fdc) reuse the same allocation
-  A(&d.fdc, std::max((size_t)(C + 64) * d.npad, (size_t)d.R_cap * n * d.npad));
-  d.la_ev = d.fdc; A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
+  // the sweep's slabs (la_ev) are dead once permuted into la; the
+  // firstDescendants walk output (fdt) reuses the same allocation
+  A(&d.fdt, (size_t)(C + 64) * d.npad);
+  d.la_ev = d.fdt;
+  A(&d.fd, (size_t)(C + 64) * d.npad);
+  A(&d.last_la, (size_t)n * d.npad);
+  A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
@@ -374,6 +373,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.order, C); A(&d.cons_pos, C); A(&d.frame_ntx, R1); A(&d.counters, 4);
   if (rc == BH_OK) {
     bh::configure_round_kernels();
+    bh::configure_fd_kernels();
     bh::configure_fame_kernels();
     bh::configure_order_kernels();
   }
@@ -635,6 +635,7 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     if ((rc = set_chain_tables(h))) return rc;
     bh::launch_prep(d, h->stream);
     bh::launch_coordinates(d, h->stream);
+    bh::launch_first_descendants(d, h->stream);
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
     h->stage = 0;
@@ -646,14 +647,8 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (last_ancestors)
     HIPCHK(h, hipMemcpy(last_ancestors, d.la + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
-  if (first_descendants) {
-    int32_t *tmp = nullptr;
-    HIPCHK(h, hipMalloc((void **)&tmp, (size_t)d.n * 4));
-    bh::launch_fd_row(d, id, tmp, h->stream);
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMemcpy(first_descendants, tmp, (size_t)d.n * 4, hipMemcpyDeviceToHost));
-    (void)hipFree(tmp);
-  }
+  if (first_descendants)
+    HIPCHK(h, hipMemcpy(first_descendants, d.fd + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
   return BH_OK;
 }
 

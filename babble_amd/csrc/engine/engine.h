@@ -12,7 +12,8 @@
 //   lt                       int32[N]       Lamport timestamp
 //   B                        int32[R_cap+1][n] first index on chain c with round >= r
 //   wids / wofs / wcnt       witnesses of each round (chain order)
-//   fdc                      int32[R][n][npad] firstDescendants rows of each round's candidates
+//   fd                       int32[N][npad] firstDescendants, chain-major rows (kernels_fd.hip)
+//   fdt                      int32[npad][N] the FD walk's column-major output (aliases la_ev)
 //   round/witness/fame/rr    per-event results
 // See DESIGN.md for the algorithm and the roofline of each kernel.
 #pragma once
@@ -29,10 +30,9 @@ constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 2048;     // frames sorted in LDS up to this size
 
 enum StateSlot {
-  ST_ARRIVE = 0,   // k_scan arrivals (last one advances ST_CUR)
-  ST_DONE = 1,     // round loop finished
-  ST_ROUNDS = 2,   // number of rounds R (LastRound + 1)
-  ST_CUR = 3,      // round r of the current iteration: resolve W(r), scan B[r+1]
+  ST_CUR0 = 0,     // round r of the iteration with parity 0 (ST_CUR0 + 1: parity 1)
+  ST_DONE = 2,     // round loop finished
+  ST_ROUNDS = 3,   // number of rounds R (LastRound + 1)
   ST_ERR = 4,      // capacity overflow / inconsistency
   ST_P = 5,        // processed prefix: rounds [0, P) are decided and ordered
   ST_NCONS = 6,    // consensus events (int32 ok: < 2^31)
@@ -61,10 +61,13 @@ struct Dev {
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds
   int32_t *B, *wofs, *wcnt, *wids;
-  int32_t *wrow;   // [W] row of each witness's firstDescendants in fdc (r * n + chain)
+  int32_t *wrow;   // [W] row of each witness's firstDescendants in fd
   int32_t *Bp;     // [2][n] B[r] / B[r+1] by round parity
-  int32_t *fdc;    // [R_cap][n][npad] firstDescendants rows of every round's candidates
-                   // (shares its allocation with la_ev, which is dead by then)
+  // firstDescendants of every event (updateAncestorFirstDescendant)
+  int32_t *fd;      // [la_rows + 64][npad] chain-major rows
+  int32_t *fdt;     // [npad][la_rows + 64] walk output (shares la_ev's allocation)
+  int32_t *last_la; // [n][npad] LA row of each chain's last event
+  int32_t max_chain_len;
   int32_t *state;
   int32_t *round;
   int8_t *witness, *fame;
@@ -86,8 +89,6 @@ struct Dev {
 enum DiagSlot {
   DG_SW_TOTAL = 0, DG_SW_WAIT_DESC, DG_SW_WAIT_RING, DG_SW_SUBSTEPS, DG_SW_FAR, DG_SW_CHUNKS,
   DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,
-  DG_SC_LOAD = 10, DG_SC_COMPUTE, DG_SC_TOTAL, DG_SC_CALLS, DG_SC_WINDOWS,
-  DG_RF_P1 = 16, DG_RF_ROWS, DG_RF_FLAG, DG_RF_FD, DG_RF_TOTAL, DG_RF_CALLS, DG_RF_FDWIN,
   DG_COUNT = 32
 };
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
@@ -101,12 +102,13 @@ void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_swe
 void launch_chunk_depth(const Dev &d, hipStream_t s);
 void launch_la_sweep(const Dev &d, hipStream_t s);
 void launch_permute(const Dev &d, hipStream_t s);  // sweep slabs -> chain-major LA rows
-void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // cand_fd + scan
+void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
 void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wcnt/wrow
 void launch_assign_rounds(const Dev &d, hipStream_t s);
 void launch_fame(const Dev &d, int32_t R, hipStream_t s);
 void launch_round_received(const Dev &d, int32_t R, hipStream_t s);
 void launch_order(const Dev &d, int32_t R, hipStream_t s);
-void launch_fd_row(const Dev &d, int64_t e, int32_t *out, hipStream_t s);
+void configure_fd_kernels();
+void launch_first_descendants(const Dev &d, hipStream_t s);  // fd from la
 
 }  // namespace bh

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
         for (int q = t; q < nw * q4; q += nt) {
           const int w = q / q4, c4 = q - w * q4;
           reinterpret_cast<int4 *>(fw + w * rs)[c4] =
-              reinterpret_cast<const int4 *>(d.fdc + (int64_t)d.wrow[wb + w] * npad)[c4];
+              reinterpret_cast<const int4 *>(d.fd + (int64_t)d.wrow[wb + w] * npad)[c4];
         }
       }
       __syncthreads();
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
             wr[a] = fw + w * rs;
           } else {
             yr[a] = d.la + (int64_t)d.epos[d.wids[yb + y]] * npad;
-            wr[a] = d.fdc + (int64_t)d.wrow[wb + w] * npad;
+            wr[a] = d.fd + (int64_t)d.wrow[wb + w] * npad;
           }
         }
         int cnt[8][8];

@@ -17,26 +17,19 @@
 //   B[r+1][c] = first k >= B[r][c] whose event strongly sees SM of C(r),
 //   W(r)      = { c in C(r) : B[r+1][c] > B[r][c] }   (round exactly r).
 // The witness resolution therefore never sits on the serial path.  One
-// step per ROUND (not per event or DAG level), two launches, one
-// workgroup per chain c in each:
-//   k_cand_fd  column c of the firstDescendants rows of every candidate:
-//              the first event of chain c seeing it, by binary search in an
-//              LDS window of chain c starting at B[r][c] (descendants of a
-//              round >= r event have round >= r); also compacts W(r-1) and
-//              its FD rows for DecideFame (known now that B[r] exists);
-//   k_scan     FD rows of C(r) and the same window staged in LDS; two lanes
-//              per candidate binary-search T_q, the first window row that
-//              strongly sees it (monotone along the chain); B[r+1][c] = the
-//              SM-th smallest T_q.
-// B[r] and the candidate FD rows are double-buffered by round parity (a
-// launch argument), so a captured graph of iterations replays without host
-// involvement and the critical path starts with one independent load; the
-// round index itself (device state) is only needed for the history writes.
+// step per ROUND (not per event or DAG level), one launch (k_round), one
+// workgroup per chain c: the candidates' firstDescendants rows (precomputed
+// for every event, kernels_fd.hip) are gathered into registers, the window
+// of chain c starting at B[r][c] into LDS; lane groups binary-search T_q,
+// the first window row that strongly sees candidate q (monotone along the
+// chain); B[r+1][c] = the SM-th smallest T_q.
+// B[r] and the round index are double-buffered by round parity (a launch
+// argument), so a captured graph of iterations replays without host
+// involvement and every load of an iteration depends only on B[r].
 #include "engine.h"
 
 namespace bh {
 
-constexpr int MAXN = 1024;   // participants supported by the LDS tables
 constexpr int WROWS = 32;    // window rows per chain
 
 __device__ __forceinline__ int popc64(unsigned long long x) { return __popcll(x); }
@@ -78,237 +71,113 @@ __device__ __forceinline__ void load_window(const Dev &d, int32_t *win, int rs, 
 }
 
 // ---------------------------------------------------------------------------
-// k_cand_fd(r): column c of the firstDescendants rows of every candidate of
-// round r, written to fdc[r] (kept for every round: the fame stage reads the
-// witnesses' rows from there, so nothing is compacted on the serial path).
-__global__ __launch_bounds__(512) void k_cand_fd(Dev d, int p) {
-  extern __shared__ __attribute__((aligned(16))) int32_t rsm[];
-  __shared__ int32_t bcur[MAXN];
-  __shared__ int32_t sh_ncand, sh_open;
-  __shared__ int8_t open[MAXN];
-  if (d.state[ST_DONE]) return;
-  const int t = threadIdx.x;
-  const int n = d.n, npad = d.npad, rs = npad + 4;
-  const int c = blockIdx.x;
-  const int r = d.state[ST_CUR];
-  const int32_t *Bp = d.Bp + (int64_t)p * n;  // B[r]
-  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
-  int32_t k0 = Bp[c];
-  int rows = min(WROWS, max(0, len - k0));
-  int32_t *win = rsm;  // [WROWS][rs]
-  const bool dg = d.diag != nullptr && t == 0;
-  const unsigned long long tr0 = dg ? stamp() : 0;
-  unsigned long long tr1 = 0, nfdw = 0;
-  constexpr int QPT = MAXN / 512;
-  int32_t bq[QPT], lq[QPT];
-#pragma unroll
-  for (int u = 0; u < QPT; ++u) {  // issued before the window, consumed after it
-    const int q = t + u * 512;
-    bq[u] = q < n ? Bp[q] : 0;
-    lq[u] = q < n ? d.chain_len[q] : 0;
-  }
-  load_window<2>(d, win, rs, cs, k0, rows);
-  if (t == 0) sh_ncand = 0;
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < QPT; ++u) {
-    const int q = t + u * 512;
-    if (q < n) {
-      const bool has = bq[u] < lq[u];
-      bcur[q] = bq[u];
-      open[q] = has && q != c;
-      if (has) atomicAdd(&sh_ncand, 1);
-      // a candidate's own column is its own index
-      if (has && q == c) d.fdc[((int64_t)r * n + q) * npad + c] = bq[u];
-    }
-  }
-  __syncthreads();
-  if (sh_ncand == 0) {
-    if (c == 0 && t == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
-    return;
-  }
-  if (r + 1 >= d.R_cap) {
-    if (c == 0 && t == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
-    return;
-  }
-  if (dg) tr1 = stamp();
-  // ---- binary search per candidate, window by window ----
-  int32_t *fcur = d.fdc + (int64_t)r * n * npad;
-  for (;;) {
-    if (t == 0) sh_open = 0;
-    __syncthreads();
-    for (int q = t; q < n; q += blockDim.x) {
-      if (!open[q]) continue;
-      const int32_t kw = bcur[q];
-      int32_t res = -1;
-      if (rows > 0 && win[(rows - 1) * rs + q] >= kw) {
-        int lo = 0, hi = rows - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (win[mid * rs + q] >= kw) hi = mid;
-          else lo = mid + 1;
-        }
-        res = k0 + lo;
-      } else if (k0 + rows >= len) {
-        res = FD_NONE;
-      }
-      if (res != -1) {
-        fcur[(int64_t)q * npad + c] = res;
-        open[q] = 0;
-      } else {
-        atomicAdd(&sh_open, 1);
-      }
-    }
-    __syncthreads();
-    if (sh_open == 0) break;
-    if (dg) ++nfdw;
-    k0 += rows;
-    rows = min(WROWS, len - k0);
-    load_window<2>(d, win, rs, cs, k0, rows);
-    __syncthreads();
-  }
-  if (c == 0)  // padding columns never match
-    for (int q = t; q < n; q += blockDim.x)
-      for (int i = n; i < npad; ++i) fcur[(int64_t)q * npad + i] = FD_NONE;
-  if (dg) {
-    const unsigned long long te = stamp();
-    atomicAdd(&d.diag[DG_RF_P1], tr1 - tr0);
-    atomicAdd(&d.diag[DG_RF_FD], te - tr1);
-    atomicAdd(&d.diag[DG_RF_TOTAL], te - tr0);
-    atomicAdd(&d.diag[DG_RF_CALLS], 1ull);
-    atomicAdd(&d.diag[DG_RF_FDWIN], nfdw);
-  }
+// k_round(p): one round-loop iteration, B[r+1][c] for one chain c per
+// workgroup.  Candidate q = (q, B[r][q]); its firstDescendants row is row
+// chain_start[q] + B[r][q] of FD (kernels_fd.hip), gathered straight into
+// registers: LPC lanes per candidate, each holding every LPC-th 16-B piece
+// (16 pieces = 64 columns per lane).  The window (rows B[r][c] .. +WROWS of
+// chain c) is staged in LDS.  T_q = the first window row strongly seeing q
+// (monotone along the chain) by binary search; B[r+1][c] = the SM-th
+// smallest T_q (a 32-bin histogram and a wave prefix).  All loads of an
+// iteration depend only on B[r] (parity buffer p), so the iteration costs
+// one dependent gather; the round index (for the history row B[r+1] and
+// the termination record) is double-buffered by parity in the state block.
+constexpr int SCAN_PAD = 4;
+constexpr int PIECES = 16;  // 16-B pieces of a candidate row per lane
+
+__device__ __forceinline__ int ge4(int4 a, int4 b) {
+  return (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
 }
 
-// ---------------------------------------------------------------------------
-// k_scan(r): B[r+1][c].  Two lanes per candidate, each taking every other
-// int4 of the columns (adjacent 16-B pieces: with the npad+8 row pitch the
-// 16 lanes of a ds_read_b128 group hit distinct banks), combined with a lane
-// swap; T_q by binary search over the window; B[r+1][c] = SM-th smallest T_q.
-// All staging loads (the chain's window, the candidates' FD rows, B[r]) are
-// issued together, so the workgroup waits for one round trip, not three.
-constexpr int SCAN_PAD = 8;
-
-template <bool FD_LDS>
-__global__ __launch_bounds__(256) void k_scan(Dev d, int p) {
+template <int LPC>
+__global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
   __shared__ int32_t hist[WROWS + 1];
-  __shared__ int32_t clist[MAXN];
-  __shared__ int8_t has[MAXN];
   __shared__ int32_t sh_res, sh_nc;
-  if (d.state[ST_DONE]) return;
-  const int r = d.state[ST_CUR];
-  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int n = d.n, npad = d.npad, sm = d.sm, rs = npad + SCAN_PAD;
-  const int32_t *Bp = d.Bp + (int64_t)p * n;
-  const int32_t *fcur = d.fdc + (int64_t)r * n * npad;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = blockIdx.x;
+  const int n = d.n, npad = d.npad, sm = d.sm, rs = npad + SCAN_PAD, q4 = npad / 4;
+  const int32_t *Bp = d.Bp + (int64_t)p * n;  // B[r]
+  // ---- loads that depend on nothing: state, B[r], chain tables ----
+  const int done = d.state[ST_DONE];
+  const int r = d.state[ST_CUR0 + p];
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
-  int32_t *win = ssm;                  // [WROWS][rs]
-  int32_t *fds = ssm + WROWS * rs;     // [n][rs] when FD_LDS (row q = chain q's candidate)
-  int32_t k0 = Bp[c];
-  const int q4 = npad / 4;
-  const bool dg = d.diag != nullptr && t == 0;
-  const unsigned long long ts0 = dg ? stamp() : 0;
-  unsigned long long ts_load = 0, ts_comp = 0, nwin = 0;
-  constexpr int QPT = MAXN / 256;
-  int32_t bq[QPT], lq[QPT];
-#pragma unroll
-  for (int u = 0; u < QPT; ++u) {
-    const int q = t + u * 256;
-    bq[u] = q < n ? Bp[q] : 0;
-    lq[u] = q < n ? d.chain_len[q] : 0;
-  }
+  const int32_t k0 = Bp[c];
+  const int part = t % LPC;
+  const int q = t / LPC;
+  int32_t bq = 0, lq = 0, sq = 0;
+  if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
+  if (done) return;
+  const bool act = q < n && bq < lq;
+  const int qpl = (q4 + LPC - 1) / LPC;  // pieces per lane (<= PIECES)
+  // ---- the one dependent gather: window rows of chain c and the
+  // candidates' firstDescendants rows, all issued before any is consumed ----
   int rows = min(WROWS, max(0, len - k0));
+  int32_t *win = ssm;  // [WROWS][rs]
+  const int wtot = rows * q4;
+  const int4 *wsrc = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + k0) * npad);
+  int4 wv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) wv[u] = wtot > 0 ? wsrc[min(u * 256 + t, wtot - 1)] : make_int4(0, 0, 0, 0);
+  int4 f[PIECES];
   {
-    // one batch: window rows then (FD_LDS) all n candidate rows
-    const int totA = rows * q4, tot = totA + (FD_LDS ? n * q4 : 0);
-    const int32_t *srcA = d.la + (int64_t)(cs + k0) * npad;
-    constexpr int U = 20;
-    for (int b0 = t; b0 < tot; b0 += U * 256) {
-      int4 v[U];
+    const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = b0 + u * 256;
-        if (i < tot) {
-          const bool a = i < totA;
-          const int j = a ? i : i - totA;
-          const int row = j / q4, c4 = j - row * q4;
-          const int32_t *src = a ? srcA + (int64_t)row * npad : fcur + (int64_t)row * npad;
-          v[u] = reinterpret_cast<const int4 *>(src)[c4];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = b0 + u * 256;
-        if (i < tot) {
-          const bool a = i < totA;
-          const int j = a ? i : i - totA;
-          const int row = j / q4, c4 = j - row * q4;
-          reinterpret_cast<int4 *>((a ? win : fds) + row * rs)[c4] = v[u];
-        }
-      }
+    for (int u = 0; u < PIECES; ++u) {
+      const int pc = u * LPC + part;
+      f[u] = (u < qpl && pc < q4) ? fr[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
     }
   }
+  if (t <= WROWS) hist[t] = 0;
+  if (t == 0) sh_nc = 0;
 #pragma unroll
-  for (int u = 0; u < QPT; ++u) {
-    const int q = t + u * 256;
-    if (q < n) has[q] = bq[u] < lq[u];
-  }
-  for (int q = t; q <= WROWS; q += blockDim.x) hist[q] = 0;
-  __syncthreads();
-  if (wave == 0) {  // candidate list in chain order
-    int nc = 0;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-      const int q = c0 + lane;
-      const bool h = q < n && has[q];
-      const unsigned long long m = __ballot(h);
-      if (h) clist[nc + popc64(m & ((1ull << lane) - 1ull))] = q;
-      nc += popc64(m);
+  for (int u = 0; u < 4; ++u) {
+    const int i = u * 256 + t;
+    if (i < wtot) {
+      const int row = i / q4;
+      reinterpret_cast<int4 *>(win + row * rs)[i - row * q4] = wv[u];
     }
-    if (lane == 0) sh_nc = nc;
+  }
+  for (int i = 4 * 256 + t; i < wtot; i += 256) {  // windows wider than 16 KiB
+    const int row = i / q4;
+    reinterpret_cast<int4 *>(win + row * rs)[i - row * q4] = wsrc[i];
   }
   __syncthreads();
-  const int nC = sh_nc;
-  const int half = t & 1;
-  int32_t result = len;
-  while (k0 < len) {
-    const unsigned long long ts1 = dg ? stamp() : 0;
-    if (dg) { ts_load += ts1 - ts0; ++nwin; }
-    for (int w0 = 0; w0 < nC; w0 += blockDim.x / 2) {
-      const int wi = w0 + (t >> 1);
-      const bool act = wi < nC;
-      const int q = act ? clist[wi] : 0;
-      const int32_t *f = FD_LDS ? fds + q * rs : fcur + (int64_t)q * npad;
-      auto ss = [&](int row) -> bool {
-        const int4 *x4 = reinterpret_cast<const int4 *>(win + row * rs);
-        const int4 *f4 = reinterpret_cast<const int4 *>(f);
-        int cnt = 0;
-        if (act) {
-#pragma unroll 8
-          for (int i = half; i < q4; i += 2) {
-            const int4 a = x4[i], b = f4[i];
-            cnt += (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
-          }
-        }
-        cnt += __shfl_xor(cnt, 1);
-        return cnt >= sm;
-      };
-      int tw = WROWS;  // not within the window
-      if (ss(rows - 1)) {
-        int lo = 0, hi = rows - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (ss(mid)) hi = mid;
-          else lo = mid + 1;
-        }
-        tw = lo;
+  {
+    const unsigned long long m = __ballot(act && part == 0);
+    if (lane == 0 && m) atomicAdd(&sh_nc, __popcll(m));
+  }
+  // strongly-see test of window row `row` against this lane group's candidate
+  auto ss = [&](int row) -> bool {
+    const int4 *x4 = reinterpret_cast<const int4 *>(win + row * rs);
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < PIECES; ++u)
+      if (u < qpl) cnt += ge4(x4[min(u * LPC + part, q4 - 1)], f[u]);
+#pragma unroll
+    for (int o = 1; o < LPC; o <<= 1) cnt += __shfl_xor(cnt, o);
+    return cnt >= sm;
+  };
+  int32_t result = len, wk0 = k0;
+  for (;;) {
+    // T_q within the window: first row strongly seeing q (fixed-depth
+    // binary search; converged groups re-test their row)
+    int tw = WROWS;
+    if (rows > 0 && ss(rows - 1)) {
+      int lo = 0, hi = rows - 1;
+#pragma unroll
+      for (int it = 0; it < 5; ++it) {
+        const int mid = (lo + hi) >> 1;
+        const bool s = ss(mid);
+        hi = s ? mid : hi;
+        lo = s ? lo : mid + 1;
       }
-      if (act && half == 0) atomicAdd(&hist[tw], 1);
+      tw = lo;
     }
+    if (act && part == 0 && tw < WROWS) atomicAdd(&hist[tw], 1);
     __syncthreads();
-    // first window row whose running count of T_q reaches SM: one wave,
-    // inclusive prefix sum over the (<= 32) histogram bins
-    if (wave == 0) {
+    if (sh_nc == 0) break;  // no candidates: the round loop is over
+    if (wave == 0) {  // first row whose running count reaches SM
       int h = lane < rows ? hist[lane] : 0;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
@@ -319,69 +188,190 @@ __global__ __launch_bounds__(256) void k_scan(Dev d, int p) {
       if (lane == 0) sh_res = hit ? (int)__builtin_ctzll(hit) : -1;
     }
     __syncthreads();
-    if (dg) ts_comp = stamp();
-    if (sh_res >= 0) { result = k0 + sh_res; break; }
-    // T not reached in this window (rare): the next one
-    k0 += rows;
-    rows = min(WROWS, len - k0);
+    const int res = sh_res;
+    if (res >= 0) { result = wk0 + res; break; }
+    // SM not reached in this window (rare): the next window of chain c
+    wk0 += rows;
+    rows = min(WROWS, len - wk0);
     if (rows <= 0) break;
-    load_window<4>(d, win, rs, cs, k0, rows);
-    for (int q = t; q <= WROWS; q += blockDim.x) hist[q] = 0;
+    __syncthreads();
+    {
+      const int tot = rows * q4;
+      const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+      for (int i = t; i < tot; i += 256) {
+        const int row = i / q4;
+        reinterpret_cast<int4 *>(win + row * rs)[i - row * q4] = src[i];
+      }
+    }
+    if (t <= WROWS) hist[t] = 0;
     __syncthreads();
   }
-  if (dg) {
-    const unsigned long long te = stamp();
-    atomicAdd(&d.diag[DG_SC_LOAD], ts_load);
-    atomicAdd(&d.diag[DG_SC_COMPUTE], ts_comp ? ts_comp - ts0 - ts_load : 0);
-    atomicAdd(&d.diag[DG_SC_TOTAL], te - ts0);
-    atomicAdd(&d.diag[DG_SC_CALLS], 1ull);
-    atomicAdd(&d.diag[DG_SC_WINDOWS], nwin);
-  }
   if (t == 0) {
+    if (sh_nc == 0) {  // R = r
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      return;
+    }
+    if (r + 1 >= d.R_cap) {
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      return;
+    }
     d.Bp[(int64_t)(p ^ 1) * n + c] = result;
     d.B[(int64_t)(r + 1) * n + c] = result;  // history for the per-event pass
-    // the last workgroup to finish advances the round (every workgroup has
-    // read ST_CUR before it arrives)
-    __threadfence();
-    const int prev = atomicAdd(&d.state[ST_ARRIVE], 1);
-    if (prev == (int)gridDim.x - 1) {
-      d.state[ST_ARRIVE] = 0;
-      d.state[ST_CUR] = r + 1;
-      d.state[ST_ITERS] += 1;
+    if (c == 0) {
+      d.state[ST_CUR0 + (p ^ 1)] = r + 1;
+      d.state[ST_ITERS] = r + 1;
     }
   }
 }
 
-size_t scan_lds_bytes(const Dev &d, bool fd_lds) {
-  size_t b = (size_t)WROWS * (d.npad + SCAN_PAD) * 4;
-  if (fd_lds) b += (size_t)d.n * (d.npad + SCAN_PAD) * 4;
-  return b;
+// n > 256/LPC candidates (wide configurations): T_q per candidate pass
+// accumulated in one histogram over the whole window, windows advanced
+// until SM is reached.  Same arithmetic as k_round, candidate rows reloaded
+// per pass.
+template <int LPC>
+__global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
+  extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
+  __shared__ int32_t hist[WROWS + 1];
+  __shared__ int32_t sh_res, sh_nc;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = blockIdx.x;
+  const int n = d.n, npad = d.npad, sm = d.sm, rs = npad + SCAN_PAD, q4 = npad / 4;
+  const int32_t *Bp = d.Bp + (int64_t)p * n;
+  const int done = d.state[ST_DONE];
+  const int r = d.state[ST_CUR0 + p];
+  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  if (done) return;
+  int32_t *win = ssm;
+  constexpr int CPP = 256 / LPC;
+  const int part = t % LPC;
+  const int npass = (n + CPP - 1) / CPP;
+  const int qpl = (q4 + LPC - 1) / LPC;
+  if (t == 0) sh_nc = 0;
+  __syncthreads();
+  int32_t wk0 = Bp[c];
+  int32_t result = len;
+  for (int w = 0;; ++w) {
+    const int wrows = min(WROWS, len - wk0);
+    if (wrows <= 0) break;
+    __syncthreads();
+    {
+      const int tot = wrows * q4;
+      const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+      for (int i = t; i < tot; i += 256) {
+        const int row = i / q4;
+        reinterpret_cast<int4 *>(win + row * rs)[i - row * q4] = src[i];
+      }
+    }
+    if (t <= WROWS) hist[t] = 0;
+    __syncthreads();
+    for (int pass = 0; pass < npass; ++pass) {
+      const int q = pass * CPP + t / LPC;
+      int32_t bq = 0, lq = 0, sq = 0;
+      if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
+      const bool act = q < n && bq < lq;
+      if (w == 0) {
+        const unsigned long long m = __ballot(act && part == 0);
+        if (lane == 0) atomicAdd(&sh_nc, __popcll(m));
+      }
+      const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad);
+      int4 f[PIECES];
+#pragma unroll
+      for (int u = 0; u < PIECES; ++u) {
+        const int pc = u * LPC + part;
+        f[u] = (u < qpl && pc < q4) ? fr[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+      }
+      auto ss = [&](int row) -> bool {
+        const int4 *x4 = reinterpret_cast<const int4 *>(win + row * rs);
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < PIECES; ++u)
+          if (u < qpl) cnt += ge4(x4[min(u * LPC + part, q4 - 1)], f[u]);
+#pragma unroll
+        for (int o = 1; o < LPC; o <<= 1) cnt += __shfl_xor(cnt, o);
+        return cnt >= sm;
+      };
+      int tw = WROWS;
+      if (ss(wrows - 1)) {
+        int lo = 0, hi = wrows - 1;
+#pragma unroll
+        for (int it = 0; it < 5; ++it) {
+          const int mid = (lo + hi) >> 1;
+          const bool s = ss(mid);
+          hi = s ? mid : hi;
+          lo = s ? lo : mid + 1;
+        }
+        tw = lo;
+      }
+      if (act && part == 0 && tw < WROWS) atomicAdd(&hist[tw], 1);
+    }
+    __syncthreads();
+    if (sh_nc == 0) break;
+    if (wave == 0) {
+      int h = lane < wrows ? hist[lane] : 0;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(h, off);
+        h += lane >= off ? o : 0;
+      }
+      const unsigned long long hit = __ballot(lane < wrows && h >= sm);
+      if (lane == 0) sh_res = hit ? (int)__builtin_ctzll(hit) : -1;
+    }
+    __syncthreads();
+    if (sh_res >= 0) { result = wk0 + sh_res; break; }
+    wk0 += wrows;
+  }
+  if (t == 0) {
+    if (sh_nc == 0) {
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      return;
+    }
+    if (r + 1 >= d.R_cap) {
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      return;
+    }
+    d.Bp[(int64_t)(p ^ 1) * n + c] = result;
+    d.B[(int64_t)(r + 1) * n + c] = result;
+    if (c == 0) {
+      d.state[ST_CUR0 + (p ^ 1)] = r + 1;
+      d.state[ST_ITERS] = r + 1;
+    }
+  }
+}
+
+static int lanes_per_candidate(int npad) {
+  const int q4 = npad / 4;
+  int lpc = 1;
+  while (lpc * PIECES < q4) lpc <<= 1;
+  return lpc;
 }
 
 void configure_round_kernels() {
-  (void)hipFuncSetAttribute((const void *)k_scan<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            140 * 1024);
-  (void)hipFuncSetAttribute((const void *)k_scan<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            140 * 1024);
-  (void)hipFuncSetAttribute((const void *)k_cand_fd, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            140 * 1024);
+#define CFG(K) (void)hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024)
+  CFG(k_round<1>); CFG(k_round<2>); CFG(k_round<4>); CFG(k_round<8>); CFG(k_round<16>);
+  CFG(k_round_wide<1>); CFG(k_round_wide<2>); CFG(k_round_wide<4>); CFG(k_round_wide<8>); CFG(k_round_wide<16>);
+#undef CFG
 }
 
 // iteration parity p = round & 1 (ITER_BATCH is even, rounds start at 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
-  const size_t wbytes = (size_t)WROWS * (d.npad + 4) * 4;
-  k_cand_fd<<<d.n, 512, wbytes, s>>>(d, p);
-  const bool fd_lds = scan_lds_bytes(d, true) <= 128 * 1024;
-  if (fd_lds)
-    k_scan<true><<<d.n, 256, scan_lds_bytes(d, true), s>>>(d, p);
-  else
-    k_scan<false><<<d.n, 256, scan_lds_bytes(d, false), s>>>(d, p);
+  const size_t wbytes = (size_t)WROWS * (d.npad + SCAN_PAD) * 4;
+  const int lpc = lanes_per_candidate(d.npad);
+  const bool wide = d.n > 256 / lpc;
+#define L(K) K<<<d.n, 256, wbytes, s>>>(d, p)
+  switch (lpc) {
+    case 1: if (wide) L(k_round_wide<1>); else L(k_round<1>); break;
+    case 2: if (wide) L(k_round_wide<2>); else L(k_round<2>); break;
+    case 4: if (wide) L(k_round_wide<4>); else L(k_round<4>); break;
+    case 8: if (wide) L(k_round_wide<8>); else L(k_round<8>); break;
+    default: if (wide) L(k_round_wide<16>); else L(k_round<16>); break;
+  }
+#undef L
 }
 
 // ---------------------------------------------------------------------------
 // witness tables for DecideFame, once after the loop: W(r) = the candidates
 // of round r whose round is exactly r (B[r+1][q] > B[r][q]), in chain order;
-// wrow = the row of their firstDescendants in fdc (r * n + q).
+// wrow = the row of their firstDescendants in fd (chain_start[q] + B[r][q]).
 __global__ __launch_bounds__(64) void k_wcount(Dev d) {
   const int r = blockIdx.x, lane = threadIdx.x, n = d.n;
   int cnt = 0;
@@ -431,7 +421,7 @@ __global__ __launch_bounds__(64) void k_wfill(Dev d) {
     if (w) {
       const int32_t k = j + popc64(m & ((1ull << lane) - 1ull));
       d.wids[k] = d.chain_ids[d.chain_start[q] + b0];
-      d.wrow[k] = r * n + q;
+      d.wrow[k] = d.chain_start[q] + b0;  // the witness's FD row
     }
     j += popc64(m);
   }
@@ -470,23 +460,6 @@ __global__ void k_assign(Dev d) {
 void launch_assign_rounds(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   k_assign<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
-}
-
-// firstDescendants row of one event (bh_get_coordinates)
-__global__ void k_fd_row(Dev d, int64_t e, int32_t *out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= d.n) return;
-  const int32_t cw = d.creator[e], kw = d.index[e];
-  if (cw == c) { out[c] = kw; return; }
-  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
-  int32_t res = FD_NONE;
-  for (int32_t k = 0; k < len; ++k)
-    if (d.la[(int64_t)(cs + k) * d.npad + cw] >= kw) { res = k; break; }
-  out[c] = res;
-}
-
-void launch_fd_row(const Dev &d, int64_t e, int32_t *out, hipStream_t s) {
-  k_fd_row<<<(d.n + 63) / 64, 64, 0, s>>>(d, e, out);
 }
 
 }  // namespace bh

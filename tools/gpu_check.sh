@@ -24,5 +24,8 @@ for s in "$@"; do
     bench2) step bench_c2 600 python bench.py --cfg 2 --steps 3 --warmup 1 ;;
     bench3) step bench_c3 900 python bench.py --cfg 3 --steps 3 --warmup 1 ;;
     bench) step bench 900 python bench.py ;;
+    diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_la_sweep|k_scan|k_cand_fd|k_permute" --cfg 3 ;;
+    prof3) step prof_c3 900 bash tools/prof.sh c3 --cfg 3 --steps 3 --warmup 1 ;;
   esac
 done
