@@ -96,7 +96,7 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.opos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la};  // la_ev aliases fdt
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -189,6 +189,7 @@ int stage_rounds(bh_handle *h) {
     h->ncons = h->cons_txs = h->cons_loaded = h->nreceived = 0;
     return BH_OK;
   }
+  bh::launch_round_init(d, s);
   // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
   // captured graph (profiling / A-B; results are identical)
   static const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
@@ -302,6 +303,9 @@ int stage_order(bh_handle *h) {
     if (hipMemcpy(g, d.diag, sizeof g, hipMemcpyDeviceToHost) == hipSuccess) {
       fprintf(stderr, "[bh diag] sweep: total %llu cyc, wait_desc %llu, wait_ring %llu, substeps %llu, far %llu, chunks %llu | mem: pref %llu store %llu idle %llu\n",
               g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]);
+      const double nc = (double)(g[14] ? g[14] : 1);
+      fprintf(stderr, "[bh diag] k_round: calls %llu, avg total %.0f cyc: loads %.0f, (unused) %.0f, search %.0f\n",
+              g[14], g[13] / nc, g[10] / nc, g[11] / nc, g[12] / nc);
     }
     (void)hipMemset(d.diag, 0, bh::DG_COUNT * 8);
   }
@@ -362,7 +366,9 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.fdt, (size_t)(C + 64) * d.npad);
   d.la_ev = d.fdt;
   A(&d.fd, (size_t)(C + 64) * d.npad);
-  A(&d.last_la, (size_t)n * d.npad);
+  A(&d.last_la, (size_t)(n + 1) * d.npad);
+  A(&d.nextwin, (size_t)2 * n * 32 * d.npad);
+  A(&d.candfd, (size_t)2 * n * d.npad);
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);

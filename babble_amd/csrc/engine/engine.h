@@ -68,6 +68,9 @@ struct Dev {
   int32_t *fdt;     // [npad][la_rows + 64] walk output (shares la_ev's allocation)
   int32_t *last_la; // [n][npad] LA row of each chain's last event
   int32_t max_chain_len;
+  // round-loop hand-off (k_round2, npad <= 128), by round parity
+  int32_t *nextwin;  // [2][n][32][npad] LA rows B[r][c] .. +32 of each chain
+  int32_t *candfd;   // [2][n][npad] FD row of each chain's candidate (c, B[r][c])
   int32_t *state;
   int32_t *round;
   int8_t *witness, *fame;
@@ -89,6 +92,7 @@ struct Dev {
 enum DiagSlot {
   DG_SW_TOTAL = 0, DG_SW_WAIT_DESC, DG_SW_WAIT_RING, DG_SW_SUBSTEPS, DG_SW_FAR, DG_SW_CHUNKS,
   DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,
+  DG_RD_B = 10, DG_RD_LOAD, DG_RD_COMP, DG_RD_TOTAL, DG_RD_CALLS,
   DG_COUNT = 32
 };
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
@@ -102,6 +106,7 @@ void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_swe
 void launch_chunk_depth(const Dev &d, hipStream_t s);
 void launch_la_sweep(const Dev &d, hipStream_t s);
 void launch_permute(const Dev &d, hipStream_t s);  // sweep slabs -> chain-major LA rows
+void launch_round_init(const Dev &d, hipStream_t s);  // hand-off buffers for round 0
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
 void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wcnt/wrow
 void launch_assign_rounds(const Dev &d, hipStream_t s);

@@ -239,6 +239,10 @@ __device__ __forceinline__ void sweep_body(const Dev &d, int4 *vring, int4 (*dri
       }
       const unsigned long long ta = dgw ? stamp() : 0;
       const int64_t hi = min(computed, mstore + 8);
+      // all 8 reads first, then 8 unconditional stores: chunks past `hi`
+      // re-store chunk hi-1 to its own place (idempotent), and lanes past N
+      // land in the 64 scratch rows behind the slab, so no store needs a
+      // branch (a branch per store would serialise each LDS read with it)
       int4 v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -249,11 +253,9 @@ __device__ __forceinline__ void sweep_body(const Dev &d, int4 *vring, int4 (*dri
       // column group); k_permute builds the chain-major rows afterwards
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        const int64_t e = (mstore + q) * 64 + lane;
-        if (mstore + q < hi && e < N) {
-          if (LT) d.lt[e] = v[q].x;
-          else slab[e] = v[q];
-        }
+        const int64_t e = min(mstore + q, hi - 1) * 64 + lane;
+        if (LT) d.lt[e] = v[q].x;
+        else slab[e] = v[q];
       }
       mstore = hi;
       COMPILER_FENCE();

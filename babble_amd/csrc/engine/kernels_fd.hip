@@ -10,9 +10,9 @@
 // one pass over chain i yields FD[(c,j)][i] for every j: the rows k at which
 // the column steps from v' to v own the j in (v', v].  That pass is HBM
 // streaming work with no serial dependency between segments of a chain:
-//   k_fd_walk       workgroup = (chain i, segment of rows), thread = column c;
-//                   writes FDT[i][row(c,j)] = k -- each thread appends to its
-//                   own run of chain c, so lines are completed in L2;
+//   k_fd_walk       workgroup = (chain i, 64-row segment) staged in LDS; the
+//                   entries of column c form one contiguous run of
+//                   FDT[i][row(c,j)], written 256 B per wave instruction;
 //   k_fd_transpose  64-row tiles of FDT through LDS into chain-major FD rows
 //                   (the layout the round loop gathers candidates from),
 //                   substituting MaxInt32 where j exceeds what the chain's
@@ -25,42 +25,77 @@
 
 namespace bh {
 
-constexpr int FD_SEG = 256;  // chain rows per walk workgroup
 
-// lastLA[i][c] = LA[(i, len_i - 1)][c] (-1 for an empty chain)
+// lastLA[i][c] = LA[(i, len_i - 1)][c] (-1 for an empty chain); the row
+// [n] below the table holds min_i lastLA[i][c]: rows with j at most that
+// need no substitution at all
 __global__ void k_last_la(Dev d) {
   const int i = blockIdx.x;
   const int32_t len = d.chain_len[i], cs = d.chain_start[i];
-  for (int c = threadIdx.x; c < d.npad; c += blockDim.x)
-    d.last_la[(int64_t)i * d.npad + c] = len > 0 ? d.la[(int64_t)(cs + len - 1) * d.npad + c] : -1;
+  for (int c = threadIdx.x; c < d.npad; c += blockDim.x) {
+    const int32_t v = len > 0 ? d.la[(int64_t)(cs + len - 1) * d.npad + c] : -1;
+    d.last_la[(int64_t)i * d.npad + c] = v;
+    atomicMin(&d.last_la[(int64_t)d.n * d.npad + c], v);
+  }
 }
 
+__global__ void k_last_la_init(Dev d) {
+  for (int c = threadIdx.x; c < d.npad; c += blockDim.x) d.last_la[(int64_t)d.n * d.npad + c] = INT32_MAX;
+}
+
+// One workgroup per (chain i, 64-row segment).  The segment's LA rows (and
+// the row before it) are staged in LDS; column c then owns the FD entries
+// j in (LA[k0-1][c], LA[k0+63][c]], a contiguous run of FDT[i][row(c, j)].
+// A wave writes that run 64 entries per instruction (256 B coalesced), each
+// lane finding its k by binary search down column c in LDS.
+constexpr int WSEG = 64;
+
 __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
+  extern __shared__ int32_t seg[];  // [WSEG + 1][npad]: row 0 = LA[k0 - 1]
   const int i = blockIdx.y;
   const int32_t len = d.chain_len[i];
-  const int32_t k0 = blockIdx.x * FD_SEG;
+  const int32_t k0 = blockIdx.x * WSEG;
   if (k0 >= len) return;
-  const int32_t k1 = min(len, k0 + FD_SEG);
+  const int rows = min(WSEG, len - k0);
   const int32_t cs = d.chain_start[i];
+  const int npad = d.npad, q4 = npad / 4, t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  {
+    const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + k0) * npad);
+    int4 *dst = reinterpret_cast<int4 *>(seg + npad);
+    const int tot = rows * q4;
+    for (int b = 0; b < tot; b += 4 * 256) {
+      int4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i x = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(src + min(b + u * 256 + t, tot - 1)));
+        v[u] = make_int4(x.x, x.y, x.z, x.w);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (b + u * 256 + t < tot) dst[b + u * 256 + t] = v[u];
+    }
+    for (int c = t; c < npad; c += 256) seg[c] = k0 > 0 ? d.la[(int64_t)(cs + k0 - 1) * npad + c] : -1;
+  }
+  __syncthreads();
   const int64_t stride = d.la_rows + 64;  // FDT row stride
   int32_t *fdt = d.fdt + (int64_t)i * stride;
-  for (int c = threadIdx.x; c < d.n; c += blockDim.x) {
-    const int32_t *col = d.la + (int64_t)cs * d.npad + c;
-    int32_t prev = k0 > 0 ? col[(int64_t)(k0 - 1) * d.npad] : -1;
+  for (int c = wave; c < d.n; c += 4) {
+    const int32_t lo = seg[c], hi = seg[rows * npad + c];  // run (lo, hi]
     int32_t *out = fdt + d.chain_start[c];
-    int32_t k = k0;
-    // 8 rows of loads in flight per thread
-    for (; k + 8 <= k1; k += 8) {
-      int32_t v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(col + (int64_t)(k + u) * d.npad);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        for (; prev < v[u]; ) out[++prev] = k + u;
-    }
-    for (; k < k1; ++k) {
-      const int32_t v = col[(int64_t)k * d.npad];
-      for (; prev < v; ) out[++prev] = k;
+    for (int32_t j0 = lo + 1; j0 <= hi; j0 += 64) {
+      const int32_t j = j0 + lane;
+      if (j <= hi) {
+        // first segment row k (1-based in seg) with LA[k][c] >= j
+        int a = 1, z = rows;
+        while (a < z) {
+          const int m = (a + z) >> 1;
+          if (seg[m * npad + c] >= j) z = m;
+          else a = m + 1;
+        }
+        out[j] = k0 + a - 1;
+      }
     }
   }
 }
@@ -71,7 +106,7 @@ template <int TR_ROWS>
 __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   extern __shared__ int32_t tile[];  // [npad][TR_ROWS + 1]
   constexpr int IPP = 256 / TR_ROWS;  // columns i per pass
-  __shared__ int32_t rc[TR_ROWS], rj[TR_ROWS];
+  __shared__ int32_t rc[TR_ROWS], rj[TR_ROWS], rfast[TR_ROWS];
   const int t = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * TR_ROWS;
   const int64_t N = d.N;
@@ -81,8 +116,10 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   const int64_t row = min(row0 + ro, N - 1);
   if (t < TR_ROWS) {
     const int32_t e = d.chain_ids[row];
-    rc[t] = d.creator[e];
-    rj[t] = d.index[e];
+    const int32_t c = d.creator[e], j = d.index[e];
+    rc[t] = c;
+    rj[t] = j;
+    rfast[t] = j <= d.last_la[(int64_t)n * npad + c];  // every chain sees (c, j)
   }
   // phase 1: FDT[i][row0 .. row0+TR_ROWS) -> tile[i][*]; IPP columns per
   // pass, 4 passes of loads in flight
@@ -104,12 +141,13 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
     const int r = p / q4, i4 = (p - r * q4) * 4;
     if (row0 + r >= N) continue;
     const int32_t c = rc[r], j = rj[r];
+    const bool fast = rfast[r];
     int32_t o[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int ii = i4 + u;
       int32_t x = FD_NONE;
-      if (ii < n && j <= d.last_la[(int64_t)ii * npad + c]) x = tile[ii * (TR_ROWS + 1) + r];
+      if (ii < n && (fast || j <= d.last_la[(int64_t)ii * npad + c])) x = tile[ii * (TR_ROWS + 1) + r];
       o[u] = x;
     }
     *reinterpret_cast<int4 *>(d.fd + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
@@ -118,10 +156,10 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
 
 void launch_first_descendants(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
+  k_last_la_init<<<1, 256, 0, s>>>(d);
   k_last_la<<<d.n, 256, 0, s>>>(d);
-  const int wt = std::min(256, (d.n + 63) / 64 * 64);
-  dim3 g((unsigned)((d.max_chain_len + FD_SEG - 1) / FD_SEG), (unsigned)d.n);
-  k_fd_walk<<<g, wt, 0, s>>>(d);
+  dim3 g((unsigned)((d.max_chain_len + WSEG - 1) / WSEG), (unsigned)d.n);
+  k_fd_walk<<<g, 256, (size_t)(WSEG + 1) * d.npad * 4, s>>>(d);
   if (d.npad <= 512)
     k_fd_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
   else
@@ -129,6 +167,8 @@ void launch_first_descendants(const Dev &d, hipStream_t s) {
 }
 
 void configure_fd_kernels() {
+  (void)hipFuncSetAttribute((const void *)k_fd_walk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            150 * 1024);
   (void)hipFuncSetAttribute((const void *)k_fd_transpose<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             150 * 1024);
   (void)hipFuncSetAttribute((const void *)k_fd_transpose<32>, hipFuncAttributeMaxDynamicSharedMemorySize,

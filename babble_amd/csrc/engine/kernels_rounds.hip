@@ -34,42 +34,6 @@ constexpr int WROWS = 32;    // window rows per chain
 
 __device__ __forceinline__ int popc64(unsigned long long x) { return __popcll(x); }
 
-// stage `rows` rows of `q4` int4s (global row stride `gs` ints) into LDS
-// (row stride rs ints).  U loads per thread are issued before the first LDS
-// write, so a workgroup pays ~one L2 round trip per U*blockDim int4s
-// instead of one per blockDim (the loop body would otherwise wait on each).
-template <int U>
-__device__ __forceinline__ void stage_rows(int32_t *dst, int rs, const int32_t *src, int64_t gs,
-                                           int rows, int q4) {
-  const int total = rows * q4;
-  for (int b = threadIdx.x; b < total; b += U * blockDim.x) {
-    int4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = b + u * blockDim.x;
-      if (i < total) {
-        const int row = i / q4, c4 = i - row * q4;
-        v[u] = reinterpret_cast<const int4 *>(src + row * gs)[c4];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = b + u * blockDim.x;
-      if (i < total) {
-        const int row = i / q4, c4 = i - row * q4;
-        reinterpret_cast<int4 *>(dst + row * rs)[c4] = v[u];
-      }
-    }
-  }
-}
-
-// load rows [k0, k0+rows) of chain c (global rows cs+k) into LDS, stride rs
-template <int U>
-__device__ __forceinline__ void load_window(const Dev &d, int32_t *win, int rs, int32_t cs,
-                                            int32_t k0, int rows) {
-  stage_rows<U>(win, rs, d.la + (int64_t)(cs + k0) * d.npad, d.npad, rows, d.npad / 4);
-}
-
 // ---------------------------------------------------------------------------
 // k_round(p): one round-loop iteration, B[r+1][c] for one chain c per
 // workgroup.  Candidate q = (q, B[r][q]); its firstDescendants row is row
@@ -98,6 +62,8 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, rs = npad + SCAN_PAD, q4 = npad / 4;
   const int32_t *Bp = d.Bp + (int64_t)p * n;  // B[r]
+  const bool dg = d.diag != nullptr && t == 0;
+  const unsigned long long ts0 = dg ? stamp() : 0;
   // ---- loads that depend on nothing: state, B[r], chain tables ----
   const int done = d.state[ST_DONE];
   const int r = d.state[ST_CUR0 + p];
@@ -110,6 +76,7 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   if (done) return;
   const bool act = q < n && bq < lq;
   const int qpl = (q4 + LPC - 1) / LPC;  // pieces per lane (<= PIECES)
+  const unsigned long long ts1 = dg ? stamp() : 0;
   // ---- the one dependent gather: window rows of chain c and the
   // candidates' firstDescendants rows, all issued before any is consumed ----
   int rows = min(WROWS, max(0, len - k0));
@@ -143,6 +110,7 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
     reinterpret_cast<int4 *>(win + row * rs)[i - row * q4] = wsrc[i];
   }
   __syncthreads();
+  const unsigned long long ts2 = dg ? stamp() : 0;
   {
     const unsigned long long m = __ballot(act && part == 0);
     if (lane == 0 && m) atomicAdd(&sh_nc, __popcll(m));
@@ -205,6 +173,14 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
     }
     if (t <= WROWS) hist[t] = 0;
     __syncthreads();
+  }
+  if (dg) {
+    const unsigned long long te = stamp();
+    atomicAdd(&d.diag[DG_RD_B], ts1 - ts0);
+    atomicAdd(&d.diag[DG_RD_LOAD], ts2 - ts1);
+    atomicAdd(&d.diag[DG_RD_COMP], te - ts2);
+    atomicAdd(&d.diag[DG_RD_TOTAL], te - ts0);
+    atomicAdd(&d.diag[DG_RD_CALLS], 1ull);
   }
   if (t == 0) {
     if (sh_nc == 0) {  // R = r
@@ -338,6 +314,205 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_round2(p): the round-loop iteration for n <= 128 (npad <= 128), built so
+// that every load it starts with is independent of B[r]:
+//   * candfd[p][q]  -- the firstDescendants row of candidate q, written by
+//                      workgroup q of the previous iteration (it knew its new
+//                      boundary B[r][q] and had that row in LDS);
+//   * nextwin[p][c] -- LA rows B[r][c] .. +32 of chain c, likewise handed over.
+// 1024 threads: LPC lanes per candidate, 4 x 16-B pieces of its FD row per
+// lane in registers.  The search is over ROWS, for all candidates at once:
+// count(k) = #{q : window row k strongly sees q} is monotone in k, and
+// B[r+1][c] = the first k with count(k) >= SM.  A probe reads one window row
+// (every lane group reads the same 128 B per instruction: an LDS broadcast),
+// compares 16 columns per lane, sums over the group with DPP, and counts the
+// groups that reach SM with a ballot.  While the search runs, the rows the
+// next iteration will need (LA rows up to B[r][c]+64, FD rows of the window)
+// are loaded; afterwards the workgroup hands over candfd/nextwin for the new
+// boundary.  Windows that do not reach SM fall back to direct loads.
+constexpr int HW = 32;  // rows handed over per chain
+
+template <int LPC>
+__device__ __forceinline__ int group_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  if (LPC >= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+  return v;
+}
+
+// per-chain hand-off for round 0 (B[0] = 0)
+__global__ __launch_bounds__(256) void k_round2_init(Dev d) {
+  const int c = blockIdx.x, q4 = d.npad / 4;
+  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  if (len == 0) return;
+  const int rows = min(HW, len);
+  const int4 *la = reinterpret_cast<const int4 *>(d.la + (int64_t)cs * d.npad);
+  int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + (int64_t)c * HW * q4;
+  for (int i = threadIdx.x; i < rows * q4; i += blockDim.x) nw[i] = la[i];
+  const int4 *fd = reinterpret_cast<const int4 *>(d.fd + (int64_t)cs * d.npad);
+  int4 *cf = reinterpret_cast<int4 *>(d.candfd) + (int64_t)c * q4;
+  for (int i = threadIdx.x; i < q4; i += blockDim.x) cf[i] = fd[i];
+}
+
+template <int LPC>
+__global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
+  constexpr int PPL = 4;  // pieces per lane: LPC * PPL >= npad / 4
+  extern __shared__ __attribute__((aligned(16))) int4 sm4[];
+  __shared__ int32_t cntk[16];
+  const int t = threadIdx.x, lane = t & 63;
+  const int c = blockIdx.x;
+  const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
+  const int nwq = HW * q4;  // int4 per handed-over window (<= 1024)
+  int4 *win = sm4;              // [2 * HW][q4]: rows k0 .. k0 + 63
+  int4 *fdw = sm4 + 2 * nwq;    // [HW][q4]: FD rows k0 .. k0 + 31
+  const int32_t *Bp = d.Bp + (int64_t)p * n;
+  const bool dg = d.diag != nullptr && t == 0;
+  const unsigned long long ts0 = dg ? stamp() : 0;
+  // ---- independent loads ----
+  const int done = d.state[ST_DONE];
+  const int r = d.state[ST_CUR0 + p];
+  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  const int32_t k0 = Bp[c];
+  const int q = t / LPC, part = t % LPC;
+  int32_t bq = 0, lq = 0;
+  if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; }
+  int4 f[PPL];
+  {
+    const int4 *cf = reinterpret_cast<const int4 *>(d.candfd) + ((int64_t)p * n + min(q, n - 1)) * q4;
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) {
+      const int pc = part + LPC * u;
+      f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+    }
+  }
+  const int4 wv = reinterpret_cast<const int4 *>(d.nextwin)[((int64_t)p * n + c) * nwq + min(t, nwq - 1)];
+  if (done) return;
+  const bool act = q < n && bq < lq;
+  const int rows = min(HW, max(0, len - k0));
+  // ---- loads for the hand-off (consumed after the search) ----
+  const int rows2 = min(HW, max(0, len - k0 - HW));
+  const int4 xv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0 + HW) * q4 + min(t, max(rows2 * q4 - 1, 0))];
+  const int4 fv = reinterpret_cast<const int4 *>(d.fd)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
+  if (t < nwq) win[t] = wv;
+  if (t < 16) cntk[t] = 0;
+  __syncthreads();
+  const unsigned long long ts1 = dg ? stamp() : 0;
+  // count(row) into slot: groups whose candidate `row` strongly sees
+  auto probe = [&](const int4 *x4, int slot) {
+    int s = 0;
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) s += ge4(x4[min(part + LPC * u, q4 - 1)], f[u]);
+    s = group_sum<LPC>(s);
+    const unsigned long long m = __ballot(act && part == 0 && s >= sm);
+    if (lane == 0 && m) atomicAdd(&cntk[slot], __popcll(m));
+  };
+  {
+    const unsigned long long m = __ballot(act && part == 0);
+    if (lane == 0 && m) atomicAdd(&cntk[0], __popcll(m));
+  }
+  int slot = 1;
+  int32_t res = -1;  // window row of B[r+1][c], or -1
+  if (rows > 0) {
+    probe(win + (rows - 1) * q4, slot);
+    __syncthreads();
+    if (cntk[slot] >= sm) {
+      int lo = 0, hi = rows - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        ++slot;
+        probe(win + mid * q4, slot);
+        __syncthreads();
+        if (cntk[slot] >= sm) hi = mid;
+        else lo = mid + 1;
+      }
+      res = lo;
+    }
+  } else {
+    __syncthreads();
+  }
+  const int nc = cntk[0];
+  const unsigned long long ts2 = dg ? stamp() : 0;
+  int32_t result = len;
+  if (res >= 0) {
+    result = k0 + res;
+  } else if (nc > 0 && rows == HW) {
+    // SM not reached in the handed-over window (rare): later windows of
+    // chain c, loaded directly (slot counters are reused per row tested)
+    int4 *x4 = win;  // rows in LDS: row i of the current window at x4[i * q4]
+    for (int32_t wk = k0 + HW; wk < len && result == len; wk += HW) {
+      const int wr = min(HW, len - wk);
+      __syncthreads();
+      for (int i = t; i < wr * q4; i += blockDim.x)
+        x4[i] = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + wk) * q4 + i];
+      if (t < 16) cntk[t] = 0;
+      __syncthreads();
+      probe(x4 + (wr - 1) * q4, 1);
+      __syncthreads();
+      if (cntk[1] < sm) continue;
+      int lo = 0, hi = wr - 1, sl = 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        ++sl;
+        probe(x4 + mid * q4, sl);
+        __syncthreads();
+        if (cntk[sl] >= sm) hi = mid;
+        else lo = mid + 1;
+      }
+      result = wk + lo;
+    }
+    __syncthreads();
+  }
+  // ---- hand-off for the next iteration ----
+  if (nc > 0 && r + 1 < d.R_cap && result < len) {
+    const int32_t off = result - k0;
+    int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + ((int64_t)(p ^ 1) * n + c) * nwq;
+    int4 *cf = reinterpret_cast<int4 *>(d.candfd) + ((int64_t)(p ^ 1) * n + c) * q4;
+    if (off < HW) {  // both from the rows staged during the search
+      if (t < rows2 * q4) win[nwq + t] = xv;
+      if (t < rows * q4) fdw[t] = fv;
+      __syncthreads();
+      if (t < nwq) nw[t] = win[off * q4 + t];
+      if (t < q4) cf[t] = fdw[off * q4 + t];
+    } else {
+      const int4 *la = reinterpret_cast<const int4 *>(d.la) + (int64_t)(cs + result) * q4;
+      const int nr = min(HW, len - result);
+      if (t < nr * q4) nw[t] = la[t];
+      if (t < q4) cf[t] = reinterpret_cast<const int4 *>(d.fd)[(int64_t)(cs + result) * q4 + t];
+    }
+  }
+  if (dg) {
+    const unsigned long long te = stamp();
+    atomicAdd(&d.diag[DG_RD_B], ts1 - ts0);
+    atomicAdd(&d.diag[DG_RD_LOAD], 0ull);
+    atomicAdd(&d.diag[DG_RD_COMP], ts2 - ts1);
+    atomicAdd(&d.diag[DG_RD_TOTAL], te - ts0);
+    atomicAdd(&d.diag[DG_RD_CALLS], 1ull);
+  }
+  if (t == 0) {
+    if (nc == 0) {  // no candidates: R = r
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      return;
+    }
+    if (r + 1 >= d.R_cap) {
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      return;
+    }
+    d.Bp[(int64_t)(p ^ 1) * n + c] = result;
+    d.B[(int64_t)(r + 1) * n + c] = result;
+    if (c == 0) {
+      d.state[ST_CUR0 + (p ^ 1)] = r + 1;
+      d.state[ST_ITERS] = r + 1;
+    }
+  }
+}
+
+bool round2_eligible(const Dev &d) { return d.npad <= 128; }
+
+void launch_round_init(const Dev &d, hipStream_t s) {
+  if (round2_eligible(d)) k_round2_init<<<d.n, 256, 0, s>>>(d);
+}
+
 static int lanes_per_candidate(int npad) {
   const int q4 = npad / 4;
   int lpc = 1;
@@ -349,11 +524,18 @@ void configure_round_kernels() {
 #define CFG(K) (void)hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024)
   CFG(k_round<1>); CFG(k_round<2>); CFG(k_round<4>); CFG(k_round<8>); CFG(k_round<16>);
   CFG(k_round_wide<1>); CFG(k_round_wide<2>); CFG(k_round_wide<4>); CFG(k_round_wide<8>); CFG(k_round_wide<16>);
+  CFG(k_round2<4>); CFG(k_round2<8>);
 #undef CFG
 }
 
 // iteration parity p = round & 1 (ITER_BATCH is even, rounds start at 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
+  if (round2_eligible(d)) {
+    const size_t lds = (size_t)3 * HW * (d.npad / 4) * 16;
+    if (d.npad <= 64) k_round2<4><<<d.n, 1024, lds, s>>>(d, p);
+    else k_round2<8><<<d.n, 1024, lds, s>>>(d, p);
+    return;
+  }
   const size_t wbytes = (size_t)WROWS * (d.npad + SCAN_PAD) * 4;
   const int lpc = lanes_per_candidate(d.npad);
   const bool wide = d.n > 256 / lpc;
