@@ -93,7 +93,7 @@ int dalloc(bh_handle *h, T **p, size_t count) {
 void free_all(bh_handle *h) {
   Dev &d = h->d;
   void *ptrs[] = {d.creator, d.index, d.sp, d.op, d.ntx, d.coin, d.sigw, d.chain_start,
-                  d.chain_len, d.chain_ids, d.epos, d.opos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
+                  d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd};  // la_ev aliases fdt
@@ -347,6 +347,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   d.n = n;
   d.npad = (n + 3) & ~3;
   d.sm = 2 * n / 3 + 1;  // hashgraph.go:54
+  d.ring_log2 = n < 256 ? 14 : 12;  // sweep LDS: one workgroup per CU below 256 columns
   d.N = 0;
   const int64_t C = std::max<int64_t>(h->cap, 1);
   d.R_cap = (int32_t)std::min<int64_t>(C / d.sm + 2, INT32_MAX / 2);
@@ -358,7 +359,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   };
   A(&d.creator, C); A(&d.index, C); A(&d.sp, C); A(&d.op, C); A(&d.ntx, C);
   A(&d.coin, C); A(&d.sigw, (size_t)C * 8);
-  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C); A(&d.opos, C);
+  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C);
   d.la_rows = C;
   A(&d.la, (size_t)(C + 64) * d.npad);
   // the sweep's slabs (la_ev) are dead once permuted into la; the
@@ -378,6 +379,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.frame_cnt, R1); A(&d.frame_ofs, R1); A(&d.frame_cur, R1); A(&d.blk_of_frame, R1);
   A(&d.order, C); A(&d.cons_pos, C); A(&d.frame_ntx, R1); A(&d.counters, 4);
   if (rc == BH_OK) {
+    bh::configure_coord_kernels();
     bh::configure_round_kernels();
     bh::configure_fd_kernels();
     bh::configure_fame_kernels();

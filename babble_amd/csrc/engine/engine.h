@@ -7,8 +7,8 @@
 //   chain_ids                int32[N]       ids grouped by creator, ordered by index
 //   epos                     int32[N]       row of event e = chain_start[creator] + index
 //   la                       int32[N][npad] lastAncestors indexes (-1 = none), chain-major rows
-//   la_ev                    int4[npad/4][N] the sweep's output (one column group per slab,
-//                                           event order), permuted into `la` afterwards
+//   la_ev                    int32[n][N] the sweep's output (one column per slab, event
+//                                           order), permuted into `la` afterwards
 //   lt                       int32[N]       Lamport timestamp
 //   B                        int32[R_cap+1][n] first index on chain c with round >= r
 //   wids / wofs / wcnt       witnesses of each round (chain order)
@@ -25,9 +25,8 @@ namespace bh {
 
 constexpr int32_t UNSET = INT32_MIN;    // Go nil
 constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
-constexpr int RING = 8192;              // events held in the coordinate sweep's LDS ring
 constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
-constexpr int FRAME_LDS_MAX = 2048;     // frames sorted in LDS up to this size
+constexpr int FRAME_LDS_MAX = 8192;     // frames sorted in LDS up to this size (96 KiB)
 
 enum StateSlot {
   ST_CUR0 = 0,     // round r of the iteration with parity 0 (ST_CUR0 + 1: parity 1)
@@ -53,10 +52,11 @@ struct Dev {
   uint8_t *coin;
   uint32_t *sigw;
   // chains
-  int32_t *chain_start, *chain_len, *chain_ids, *epos, *opos;
+  int32_t *chain_start, *chain_len, *chain_ids, *epos;
   // coordinates
   int32_t *la, *lt;
-  int32_t *la_ev;  // [npad/4][la_rows+64][4] sweep output: column-group-major, event-major
+  int32_t *la_ev;  // [n][la_rows+64] sweep output: column-major, event order
+  int32_t ring_log2;  // the sweep's LDS value ring holds 1 << ring_log2 events
   uint8_t *depth, *chunk_maxd;
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds
@@ -101,6 +101,7 @@ __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_
 void configure_round_kernels();
 void configure_fame_kernels();
 void configure_order_kernels();
+void configure_coord_kernels();
 void launch_prep(const Dev &d, hipStream_t s);
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep
 void launch_chunk_depth(const Dev &d, hipStream_t s);

@@ -14,9 +14,10 @@
 // :1125-1231), ordered ByLamportTimestamp (event.go:332-347): Lamport
 // timestamp, then the signature's r as a big integer (8 big-endian words
 // here).  A block is emitted per non-empty frame (:1083-1107).  Implementation:
-// histogram of rr -> exclusive scan -> scatter into frame buckets -> one
-// workgroup per frame sorts its bucket (bitonic, keys staged in LDS; frames
-// larger than FRAME_LDS_MAX sort in place in HBM with the same network).
+// block-aggregated histogram of rr -> exclusive scan -> scatter into frame
+// buckets -> one workgroup per frame sorts its bucket (bitonic on 64-bit
+// prefix keys in LDS, exact fix-up of equal prefixes; frames larger than
+// FRAME_LDS_MAX take a slow in-HBM path).
 #include "engine.h"
 
 namespace bh {
@@ -55,14 +56,57 @@ __global__ __launch_bounds__(1024) void k_prefix(Dev d, int32_t R) {
   }
 }
 
-__global__ void k_frame_count(Dev d) {
-  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t rr = x < d.N ? d.rr[x] : UNSET;
-  // events received (in any round): they leave UndeterminedEvents
-  const unsigned long long m = __ballot(rr != UNSET);
-  if ((threadIdx.x & 63) == 0 && m)
-    atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[2]), (unsigned long long)__popcll(m));
-  if (rr != UNSET && rr < d.state[ST_P]) atomicAdd(&d.frame_cnt[rr], 1);
+// Frame histogram / scatter over 1024-event blocks: the round-received
+// values of a block span a few rounds, so each block histograms them in
+// LDS relative to the block minimum (64 bins) and issues one global atomic
+// per non-empty bin instead of one per event (per-event atomics on a few
+// hot bins serialise in the memory-side atomic units).
+constexpr int OB = 1024;   // events per block (256 threads x 4)
+constexpr int HB = 64;     // LDS bins per block
+
+__device__ __forceinline__ int32_t block_min(int32_t v, int32_t *sh) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+  if ((threadIdx.x & 63) == 0) atomicMin(sh, v);
+  __syncthreads();
+  return *sh;
+}
+
+__global__ __launch_bounds__(256) void k_frame_count(Dev d) {
+  __shared__ int32_t hist[HB], rmin_s;
+  __shared__ unsigned long long nrecv;
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * OB;
+  const int32_t P = d.state[ST_P];
+  if (t < HB) hist[t] = 0;
+  if (t == 0) { rmin_s = INT32_MAX; nrecv = 0; }
+  int32_t rr[4];
+  int32_t lo = INT32_MAX;
+  int recv = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t x = base + u * 256 + t;
+    rr[u] = x < d.N ? d.rr[x] : UNSET;
+    recv += rr[u] != UNSET;
+    if (rr[u] == UNSET || rr[u] >= P) rr[u] = -1;
+    else lo = min(lo, rr[u]);
+  }
+  __syncthreads();
+  const int32_t rmin = block_min(lo, &rmin_s);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) recv += __shfl_xor(recv, off);
+  if ((t & 63) == 0 && recv) atomicAdd(&nrecv, (unsigned long long)recv);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (rr[u] < 0) continue;
+    const int32_t b = rr[u] - rmin;
+    if (b < HB) atomicAdd(&hist[b], 1);
+    else atomicAdd(&d.frame_cnt[rr[u]], 1);
+  }
+  __syncthreads();
+  if (t < HB && hist[t]) atomicAdd(&d.frame_cnt[rmin + t], hist[t]);
+  // events received (in any round) leave UndeterminedEvents
+  if (t == 0 && nrecv) atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[2]), nrecv);
 }
 
 // exclusive scans of frame sizes and of non-empty flags (block indices)
@@ -94,101 +138,168 @@ __global__ __launch_bounds__(1024) void k_frame_scan(Dev d) {
   if (t == 1023) { d.state[ST_NCONS] = part[1023]; d.state[ST_NBLOCKS] = partb[1023]; }
 }
 
-__global__ void k_frame_scatter(Dev d) {
-  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= d.N) return;
-  const int32_t rr = d.rr[x];
-  if (rr == UNSET || rr >= d.state[ST_P]) return;
-  const int32_t slot = atomicAdd(&d.frame_cur[rr], 1);
-  d.order[d.frame_ofs[rr] + slot] = (int32_t)x;
-}
-
-// ByLamportTimestamp.Less; equal keys (same r, impossible for distinct
-// signatures) fall back to the id to stay deterministic
-struct Key {
-  int32_t lt;
-  uint32_t w[8];
-  int32_t id;
-};
-__device__ __forceinline__ bool key_less(const Key &a, const Key &b) {
-  if (a.lt != b.lt) return a.lt < b.lt;
+__global__ __launch_bounds__(256) void k_frame_scatter(Dev d) {
+  __shared__ int32_t hist[HB], basev[HB], rmin_s;
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * OB;
+  const int32_t P = d.state[ST_P];
+  if (t < HB) hist[t] = 0;
+  if (t == 0) rmin_s = INT32_MAX;
+  int32_t rr[4], slot[4];
+  int32_t lo = INT32_MAX;
 #pragma unroll
-  for (int q = 0; q < 8; ++q)
-    if (a.w[q] != b.w[q]) return a.w[q] < b.w[q];
-  return a.id < b.id;
-}
-__device__ __forceinline__ Key load_key(const Dev &d, int32_t e) {
-  Key k;
-  k.lt = d.lt[e];
-  const uint4 *s = reinterpret_cast<const uint4 *>(d.sigw + (int64_t)e * 8);
-  const uint4 a = s[0], b = s[1];
-  k.w[0] = a.x; k.w[1] = a.y; k.w[2] = a.z; k.w[3] = a.w;
-  k.w[4] = b.x; k.w[5] = b.y; k.w[6] = b.z; k.w[7] = b.w;
-  k.id = e;
-  return k;
-}
-
-// bitonic network in its "flip" form: every comparator puts the smaller key
-// at the lower index, so padding past `cnt` is never touched
-template <bool LDS>
-__device__ void bitonic(Key *keys, int32_t *ids, int32_t cnt, const Dev &d) {
-  int32_t p2 = 1;
-  while (p2 < cnt) p2 <<= 1;
-  for (int32_t k = 2; k <= p2; k <<= 1) {
-    for (int32_t j = k >> 1; j > 0; j >>= 1) {
-      for (int32_t i = threadIdx.x; i < p2; i += blockDim.x) {
-        int32_t partner;
-        if (j == (k >> 1)) partner = i ^ (k - 1);
-        else partner = i ^ j;
-        if (partner <= i || partner >= cnt) continue;
-        if (LDS) {
-          if (key_less(keys[partner], keys[i])) {
-            const Key tmp = keys[i];
-            keys[i] = keys[partner];
-            keys[partner] = tmp;
-          }
-        } else {
-          const int32_t a = ids[i], b = ids[partner];
-          if (key_less(load_key(d, b), load_key(d, a))) { ids[i] = b; ids[partner] = a; }
-        }
-      }
-      __syncthreads();
-    }
+  for (int u = 0; u < 4; ++u) {
+    const int64_t x = base + u * 256 + t;
+    rr[u] = x < d.N ? d.rr[x] : UNSET;
+    if (rr[u] == UNSET || rr[u] >= P) rr[u] = -1;
+    else lo = min(lo, rr[u]);
+  }
+  __syncthreads();
+  const int32_t rmin = block_min(lo, &rmin_s);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    slot[u] = -1;
+    if (rr[u] < 0) continue;
+    const int32_t b = rr[u] - rmin;
+    if (b < HB) slot[u] = atomicAdd(&hist[b], 1);                          // rank in the block
+    else slot[u] = d.frame_ofs[rr[u]] + atomicAdd(&d.frame_cur[rr[u]], 1);  // absolute (rare)
+  }
+  __syncthreads();
+  if (t < HB) basev[t] = hist[t] ? d.frame_ofs[rmin + t] + atomicAdd(&d.frame_cur[rmin + t], hist[t]) : 0;
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (rr[u] < 0) continue;
+    const int32_t b = rr[u] - rmin;
+    const int32_t pos = b < HB ? basev[b] + slot[u] : slot[u];
+    d.order[pos] = (int32_t)(base + u * 256 + t);
   }
 }
 
-__global__ __launch_bounds__(256) void k_frame_sort(Dev d) {
+// ByLamportTimestamp.Less (event.go:332-347): Lamport timestamp, then the
+// signature's r as a 256-bit big-endian integer; equal keys (same r, which
+// distinct signatures never share) fall back to the id to stay deterministic.
+// The sort runs on a 64-bit prefix key (LT, top 32 bits of r) and the id;
+// runs of equal prefixes are then put in full-key order.
+__device__ __forceinline__ uint64_t prefix_key(const Dev &d, int32_t e) {
+  return (uint64_t)(uint32_t)d.lt[e] << 32 | d.sigw[(int64_t)e * 8];
+}
+__device__ __forceinline__ bool full_less(const Dev &d, int32_t a, int32_t b) {
+  const int32_t la = d.lt[a], lb = d.lt[b];
+  if (la != lb) return la < lb;
+  const uint32_t *wa = d.sigw + (int64_t)a * 8, *wb = d.sigw + (int64_t)b * 8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (wa[q] != wb[q]) return wa[q] < wb[q];
+  return a < b;
+}
+__device__ __forceinline__ bool pair_less(uint64_t ka, int32_t ia, uint64_t kb, int32_t ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+// bitonic network in its "flip" form over p2 slots (slots >= cnt hold
+// +infinity keys).  Each wave owns 128 consecutive slots for the stages
+// whose partner distance is < 128, which then need no workgroup barrier
+// (a wave's LDS operations execute in order).
+__device__ __forceinline__ bool wave_local(int32_t k, int32_t j) { return j < 64 || k <= 128; }
+
+__device__ void bitonic_lds(uint64_t *key, int32_t *id, int32_t p2) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const bool one_per_thread = nt * 2 >= p2;  // comparator c = t: wave w owns slots [128w, 128w+128)
+  for (int32_t k = 2; k <= p2; k <<= 1) {
+    for (int32_t j = k >> 1; j > 0; j >>= 1) {
+      // comparator c: pair (i, partner) with i = the lower slot
+      for (int32_t c = t; c < p2 / 2; c += nt) {
+        const int32_t blk = c / j, off = c - blk * j;
+        const int32_t i = blk * 2 * j + off;
+        const int32_t partner = (j == (k >> 1)) ? (i ^ (k - 1)) : (i + j);
+        const int32_t lo = min(i, partner), hi = max(i, partner);
+        const uint64_t klo = key[lo], khi = key[hi];
+        const int32_t ilo = id[lo], ihi = id[hi];
+        if (pair_less(khi, ihi, klo, ilo)) {
+          key[lo] = khi; key[hi] = klo;
+          id[lo] = ihi; id[hi] = ilo;
+        }
+      }
+      // a barrier unless this stage and the next both stay inside each
+      // wave's own slots
+      int32_t nk = k, nj = j >> 1;
+      if (nj == 0) { nk = k << 1; nj = k; }
+      const bool keep = one_per_thread && wave_local(k, j) && nk <= p2 && wave_local(nk, nj);
+      if (!keep) __syncthreads();
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_frame_sort(Dev d) {
   extern __shared__ __attribute__((aligned(16))) unsigned char osm[];
   __shared__ unsigned long long sh_ntx, sh_loaded;
   const int32_t f = blockIdx.x;
   const int32_t cnt = d.frame_cnt[f];
   if (cnt == 0) return;
+  const int t = threadIdx.x, nt = blockDim.x;
   const int32_t off = d.frame_ofs[f];
   int32_t *ids = d.order + off;
-  if (threadIdx.x == 0) { sh_ntx = 0; sh_loaded = 0; }
+  if (t == 0) { sh_ntx = 0; sh_loaded = 0; }
   if (cnt <= FRAME_LDS_MAX) {
-    Key *keys = reinterpret_cast<Key *>(osm);
-    for (int32_t i = threadIdx.x; i < cnt; i += blockDim.x) keys[i] = load_key(d, ids[i]);
+    int32_t p2 = 64;
+    while (p2 < cnt) p2 <<= 1;
+    uint64_t *key = reinterpret_cast<uint64_t *>(osm);
+    int32_t *id = reinterpret_cast<int32_t *>(key + p2);
+    for (int32_t i = t; i < p2; i += nt) {
+      const int32_t e = i < cnt ? ids[i] : INT32_MAX;
+      key[i] = i < cnt ? prefix_key(d, e) : ~0ull;
+      id[i] = e;
+    }
     __syncthreads();
-    bitonic<true>(keys, nullptr, cnt, d);
-    for (int32_t i = threadIdx.x; i < cnt; i += blockDim.x) ids[i] = keys[i].id;
+    bitonic_lds(key, id, p2);
+    // runs of equal prefix keys: full 256-bit order (one thread per run)
+    for (int32_t i = t; i < cnt; i += nt) {
+      if ((i > 0 && key[i - 1] == key[i]) || i + 1 >= cnt || key[i + 1] != key[i]) continue;
+      int32_t e = i + 1;
+      while (e < cnt && key[e] == key[i]) ++e;
+      for (int32_t a = i + 1; a < e; ++a) {  // insertion sort of [i, e)
+        const int32_t v = id[a];
+        int32_t b = a - 1;
+        while (b >= i && full_less(d, v, id[b])) { id[b + 1] = id[b]; --b; }
+        id[b + 1] = v;
+      }
+    }
+    __syncthreads();
+    for (int32_t i = t; i < cnt; i += nt) ids[i] = id[i];
     __syncthreads();
   } else {
-    __syncthreads();
-    bitonic<false>(nullptr, ids, cnt, d);
+    // oversized frame: odd-even transposition passes in HBM with the full key
+    // (never seen on the benchmark DAGs; correctness path)
+    for (int32_t pass = 0; pass < cnt; ++pass) {
+      for (int32_t i = 2 * t + (pass & 1); i + 1 < cnt; i += 2 * nt) {
+        const int32_t a = ids[i], b = ids[i + 1];
+        if (full_less(d, b, a)) { ids[i] = b; ids[i + 1] = a; }
+      }
+      __threadfence_block();
+      __syncthreads();
+    }
   }
   unsigned long long ntx = 0, loaded = 0;
-  for (int32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+  for (int32_t i = t; i < cnt; i += nt) {
     const int32_t e = ids[i];
     d.cons_pos[e] = (int64_t)off + i;
-    const int32_t t = d.ntx[e];
-    ntx += t;
-    loaded += (d.index[e] == 0 || t > 0);  // IsLoaded, event.go:169-178
+    const int32_t tx = d.ntx[e];
+    ntx += tx;
+    loaded += (d.index[e] == 0 || tx > 0);  // IsLoaded, event.go:169-178
   }
-  if (ntx) atomicAdd(&sh_ntx, ntx);
-  if (loaded) atomicAdd(&sh_loaded, loaded);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ntx += __shfl_xor(ntx, o);
+    loaded += __shfl_xor(loaded, o);
+  }
+  if ((t & 63) == 0) {
+    if (ntx) atomicAdd(&sh_ntx, ntx);
+    if (loaded) atomicAdd(&sh_loaded, loaded);
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     d.frame_ntx[f] = (int64_t)sh_ntx;
     atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[0]), (unsigned long long)sh_ntx);
     atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[1]), (unsigned long long)sh_loaded);
@@ -197,18 +308,18 @@ __global__ __launch_bounds__(256) void k_frame_sort(Dev d) {
 
 void configure_order_kernels() {
   (void)hipFuncSetAttribute((const void *)k_frame_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            FRAME_LDS_MAX * sizeof(Key));
+                            FRAME_LDS_MAX * 12);
 }
 
 void launch_order(const Dev &d, int32_t R, hipStream_t s) {
   if (R <= 0) return;
   k_prefix<<<1, 1024, 0, s>>>(d, R);
-  const unsigned g = (unsigned)((d.N + 255) / 256);
+  const unsigned g = (unsigned)((d.N + OB - 1) / OB);
   k_frame_count<<<g, 256, 0, s>>>(d);
   k_frame_scan<<<1, 1024, 0, s>>>(d);
   k_frame_scatter<<<g, 256, 0, s>>>(d);
   // frames [0, P); P <= R.  Launch R blocks: frames >= P have cnt 0.
-  k_frame_sort<<<R, 256, FRAME_LDS_MAX * sizeof(Key), s>>>(d);
+  k_frame_sort<<<R, 1024, FRAME_LDS_MAX * 12, s>>>(d);
 }
 
 }  // namespace bh
