@@ -21,7 +21,7 @@ SYMBOLS = (
     "bh_decide_fame", "bh_decide_round_received", "bh_process_decided_rounds",
     "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
-    "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile",
+    "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
 )
 
 
@@ -79,5 +79,7 @@ def load():
     L.bh_get_stage_ms.argtypes = [P, C.POINTER(C.c_float), I32]
     L.bh_get_stage_ms.restype = I32
     L.bh_get_profile.argtypes = [P, C.POINTER(I64), C.POINTER(C.c_float)]
+    L.bh_get_profile_kernel.argtypes = [P]
+    L.bh_get_profile_kernel.restype = C.c_char_p
     _LIB = L
     return L

@@ -59,6 +59,7 @@ struct bh_handle {
   hipEvent_t ev[NSTAGE + 1]{};
   hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)
   float sweep_ms = 0;
+  const char *sweep_kernel = "";
   float stage_ms[NSTAGE]{};
   int64_t iters = 0;
   int64_t *d_counters_host = nullptr;
@@ -96,7 +97,7 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd};  // la_ev aliases fdt
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd, d.opdesc, d.lt_row};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -170,11 +171,23 @@ int stage_rounds(bh_handle *h) {
   hipStream_t s = h->stream;
   HIPCHK(h, hipEventRecord(h->ev[0], s));
   bh::launch_prep(d, s);
-  bh::launch_chunk_depth(d, s);
-  HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
-  bh::launch_la_sweep(d, s);
-  HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
-  bh::launch_permute(d, s);
+  // BH_SWEEP=chunk forces the chunked sweep (A/B and parity of both paths)
+  const bool force_chunk = getenv("BH_SWEEP") && !strcmp(getenv("BH_SWEEP"), "chunk");
+  if (bh::flow_eligible(d) && !force_chunk) {
+    bh::launch_flow_desc(d, s);
+    HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
+    bh::launch_flow(d, s);
+    HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
+    bh::launch_flow_transpose(d, s);
+    h->sweep_kernel = "k_flow";
+  } else {
+    bh::launch_chunk_depth(d, s);
+    HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
+    bh::launch_la_sweep(d, s);
+    HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
+    bh::launch_permute(d, s);
+    h->sweep_kernel = "k_la_sweep";
+  }
   bh::launch_first_descendants(d, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
@@ -366,6 +379,9 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   // firstDescendants walk output (fdt) reuses the same allocation
   A(&d.fdt, (size_t)(C + 64) * d.npad);
   d.la_ev = d.fdt;
+  d.la_col = d.fdt;
+  A(&d.opdesc, (size_t)C + 128);
+  A(&d.lt_row, (size_t)C + 64);
   A(&d.fd, (size_t)(C + 64) * d.npad);
   A(&d.last_la, (size_t)(n + 1) * d.npad);
   A(&d.nextwin, (size_t)2 * n * 32 * d.npad);
@@ -380,6 +396,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.order, C); A(&d.cons_pos, C); A(&d.frame_ntx, R1); A(&d.counters, 4);
   if (rc == BH_OK) {
     bh::configure_coord_kernels();
+    bh::configure_flow_kernels();
     bh::configure_round_kernels();
     bh::configure_fd_kernels();
     bh::configure_fame_kernels();
@@ -642,7 +659,8 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     d.N = N;
     if ((rc = set_chain_tables(h))) return rc;
     bh::launch_prep(d, h->stream);
-    bh::launch_coordinates(d, h->stream);
+    if (bh::flow_eligible(d)) bh::launch_flow_coordinates(d, h->stream);
+    else bh::launch_coordinates(d, h->stream);
     bh::launch_first_descendants(d, h->stream);
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
@@ -672,5 +690,7 @@ int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {
   if (sweep_ms) *sweep_ms = h->sweep_ms;
   return BH_OK;
 }
+
+const char *bh_get_profile_kernel(const bh_handle *h) { return h ? h->sweep_kernel : ""; }
 
 }  // extern "C"

@@ -57,6 +57,10 @@ struct Dev {
   int32_t *la, *lt;
   int32_t *la_ev;  // [n][la_rows+64] sweep output: column-major, event order
   int32_t ring_log2;  // the sweep's LDS value ring holds 1 << ring_log2 events
+  // chain dataflow (kernels_flow.hip)
+  int32_t *opdesc;  // [N] chain-major other-parent (creator << 22 | index), -1 = none
+  int32_t *la_col;  // [n][la_rows+64] column-major LA, chain-major rows (aliases la_ev)
+  int32_t *lt_row;  // [la_rows+64] LT by chain-major row
   uint8_t *depth, *chunk_maxd;
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds
@@ -102,6 +106,12 @@ void configure_round_kernels();
 void configure_fame_kernels();
 void configure_order_kernels();
 void configure_coord_kernels();
+void configure_flow_kernels();
+bool flow_eligible(const Dev &d);
+void launch_flow_coordinates(const Dev &d, hipStream_t s);  // LA + LT, chain dataflow
+void launch_flow_desc(const Dev &d, hipStream_t s);
+void launch_flow(const Dev &d, hipStream_t s);
+void launch_flow_transpose(const Dev &d, hipStream_t s);
 void launch_prep(const Dev &d, hipStream_t s);
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep
 void launch_chunk_depth(const Dev &d, hipStream_t s);

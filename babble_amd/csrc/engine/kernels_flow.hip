@@ -1,0 +1,249 @@
+// kernels_flow.hip -- event coordinates as a dataflow over creator chains.
+//
+// Reference: initEventCoordinates (hashgraph.go:439-507): LA[e][j] =
+// max(LA[sp][j], LA[op][j]), LA[e][creator] = index; _lamportTimestamp
+// (hashgraph.go:325-379): LT[e] = max(LT[sp], LT[op]) + 1.
+//
+// Mapping (n <= 128, chains shorter than 2^22): one workgroup per LA column
+// (plus one for LT), one LANE per creator chain.  Along a chain the
+// self-parent is the lane's previous event, so that half of the recurrence
+// stays in a register; the other-parent (d, j) is read from chain d's ring
+// of recent values in LDS, each slot tagged with the index it holds.  A lane
+// advances when the tag matches (the parent is done); otherwise it retries
+// on the next step.  Event (c, k) is thus computed at step LT(c, k) + 1:
+// the number of serial steps is the DAG's critical path (its Lamport depth),
+// and each step is one LDS round trip.  The chunked sweep in
+// kernels_coords.hip (used above these limits) needs ~2.2x more steps.
+//
+// Waves: ceil(n/64) compute waves (64 chains each) + one prefetch wave that
+// keeps every chain's ring of other-parent descriptors (packed (d << 22) |
+// j, or -1 for none, chain-major) filled by LDS-DMA, 64 entries per refill.
+// Values leave as one store per compute wave per step into column-major
+// LA (chain-major rows); a parent older than the value ring (tag past j) is
+// read back from there once its chain has published that its stores are
+// complete (checkpoint every 32 steps: s_waitcnt vmcnt(32) -- every step
+// issues exactly one store, so the stores of the last 32 steps are the 32
+// youngest operations and everything before the previous checkpoint is done).
+#include "engine.h"
+
+namespace bh {
+
+constexpr int FL_R = 64;     // value ring slots per chain (int2 {value, index})
+constexpr int FL_DR = 128;   // descriptor ring entries per chain
+constexpr int FL_MAXN = 128;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(3))) volatile int lds_vint;
+
+// Row n of the value ring is a sentinel chain: slot 63 = {-1, FL_NOOP}
+// always matches the "no other-parent" descriptor, slot 62 = {-1, -2} never
+// matches FL_WAIT (a lane without a loaded descriptor), slots 0..60 absorb
+// the ring writes of lanes that did not advance.
+constexpr int32_t FL_NOOP = 0x3FFFFF, FL_WAIT = 0x3FFFFE;
+
+// chain-major other-parent descriptors
+__global__ void k_flow_desc(Dev d) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  const int32_t o = d.op[e];
+  d.opdesc[d.epos[e]] = o < 0 ? (d.n << 22) | FL_NOOP : (d.creator[o] << 22) | d.index[o];
+}
+
+struct FlowLds {
+  int2 vring[FL_MAXN + 1][FL_R];   // 64.5 KiB
+  int32_t dring[FL_MAXN][FL_DR];   // 64 KiB
+  int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN];
+};
+
+template <bool LT>
+__device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = d.n;
+  const int nw = (n + 63) >> 6;  // compute waves
+  const int col = blockIdx.x;
+  const int64_t stride = d.la_rows + 64;
+  int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
+  for (int c = t; c < n; c += blockDim.x) {
+    L.filled[c] = 0;
+    L.consumed[c] = 0;
+    L.pub[c] = 0;
+    L.cs[c] = d.chain_start[c];
+    for (int s = 0; s < FL_R; ++s) L.vring[c][s] = make_int2(-1, -1);
+  }
+  if (t < FL_R) L.vring[n][t] = make_int2(-1, t == 63 ? FL_NOOP : -2);
+  __syncthreads();
+  lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub;
+
+  if (wave == nw) {
+    // ---------------- prefetch wave: descriptor rings ----------------
+    int32_t f[2] = {0, 0};  // entries filled, chains lane and lane + 64
+    int32_t len[2], cs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane + 64 * h;
+      len[h] = c < n ? d.chain_len[c] : 0;
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (;;) {
+      bool left = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        const int32_t cons = c < n ? consumed[c] : 0;
+        const bool need = f[h] < len[h] && f[h] - cons <= FL_DR - 64;
+        left |= f[h] < len[h];
+        unsigned long long m = __ballot(need);
+        while (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          const int cc = b + 64 * h;
+          const int32_t fc = __builtin_amdgcn_readlane(f[h], b);
+          const int32_t csc = __builtin_amdgcn_readlane(cs[h], b);
+          __builtin_amdgcn_global_load_lds((const void *)(d.opdesc + csc + fc + lane),
+                                           (lds_void_t *)&L.dring[cc][fc & (FL_DR - 1)], 4, 0, 0);
+        }
+        if (need) f[h] += 64;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        if (c < n) filled[c] = min(f[h], len[h]);
+      }
+      if (!__any(left)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return;
+  }
+  if (wave > nw) return;
+
+  // ---------------- compute waves: one chain per lane ----------------
+  // Per step: two LDS reads (the other-parent's ring slot, the next
+  // descriptor), one ring write and one store, all unconditional (lanes that
+  // do not advance write the sentinel row / the scratch rows), so the loop
+  // has no divergent branches; refills and read-backs sit behind
+  // wave-uniform tests.
+  const int c = wave * 64 + lane;
+  const bool valid = c < n;
+  const int32_t len = valid ? d.chain_len[c] : 0;
+  const int32_t cs = valid ? L.cs[c] : 0;
+  const int cc = valid ? c : 0;
+  const bool own = !LT && c == col;
+  int32_t *dummy = out + d.la_rows + lane;  // scratch rows: a not-ready lane's store
+  int2 *const wscratch = &L.vring[n][lane % 61];
+  const int32_t WAIT = (n << 22) | FL_WAIT;
+  int32_t k = 0, cur = -1, kcp = 0, lim = 0;
+  int32_t dsc = WAIT;  // descriptor of event k, or WAIT until it has landed
+  for (int32_t step = 0;; ++step) {
+    if ((step & 15) == 0) {  // refresh the fill level; publish progress
+      lim = valid ? filled[cc] : 0;
+      if ((step & 31) == 0) {
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // see the header
+        if (valid) { pub[c] = kcp; consumed[c] = k; }
+        kcp = k;
+      }
+      if (!__any(k < len)) break;
+    }
+    if (__builtin_expect(__any(dsc == WAIT && k < lim), 0))  // descriptor landed
+      if (dsc == WAIT && k < lim) dsc = L.dring[cc][k & (FL_DR - 1)];
+    const int32_t dd = (uint32_t)dsc >> 22, jj = dsc & 0x3FFFFF;
+    const int2 slot = L.vring[dd][jj & (FL_R - 1)];
+    const int32_t dn = L.dring[cc][(k + 1) & (FL_DR - 1)];
+    bool ready = slot.y == jj && dsc != WAIT;
+    int32_t val = slot.x;
+    if (__builtin_expect(__any(slot.y > jj), 0)) {
+      // the ring moved past j: read the value back once chain dd has
+      // published it (one inline-asm load with its own wait: a load the
+      // compiler sees in this loop would make it drain the per-step stores
+      // at every iteration)
+      if (slot.y > jj && pub[dd] > jj) {
+        const int32_t *fp = out + L.cs[dd] + jj;
+        asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
+        ready = true;
+      }
+    }
+    int32_t v = max(cur, val);
+    if (LT) v += 1;
+    else v = own ? k : v;  // LA[e][creator] = index
+    *(ready ? &L.vring[c][k & (FL_R - 1)] : wscratch) = make_int2(v, k);
+    *(ready ? out + cs + k : dummy) = v;  // exactly one store per step
+    cur = ready ? v : cur;
+    k += ready ? 1 : 0;
+    dsc = ready ? (k < lim ? dn : WAIT) : dsc;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (valid) { pub[c] = len; consumed[c] = len; }
+}
+
+__global__ __launch_bounds__(192) void k_flow(Dev d) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char flm[];
+  FlowLds &L = *reinterpret_cast<FlowLds *>(flm);
+  if ((int)blockIdx.x == d.n) flow_body<true>(d, L);
+  else flow_body<false>(d, L);
+}
+
+// column-major LA (chain-major rows) -> row-major LA; LT rows -> event ids
+template <int TR>
+__global__ __launch_bounds__(256) void k_flow_transpose(Dev d) {
+  extern __shared__ int32_t tile[];  // [npad][TR + 1]
+  constexpr int IPP = 256 / TR;
+  const int t = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * TR;
+  const int64_t N = d.N;
+  const int n = d.n, npad = d.npad;
+  const int64_t stride = d.la_rows + 64;
+  const int ro = t % TR;
+  const int64_t row = min(row0 + ro, N - 1);
+  if (t < TR && row0 + t < N) d.lt[d.chain_ids[row0 + t]] = d.lt_row[row0 + t];
+  for (int i = t / TR; i < n; i += 4 * IPP) {
+    int32_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(d.la_col + (int64_t)min(i + IPP * u, n - 1) * stride + row);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + IPP * u < n) tile[(i + IPP * u) * (TR + 1) + ro] = v[u];
+  }
+  __syncthreads();
+  const int q4 = npad / 4;
+  for (int p = t; p < TR * q4; p += blockDim.x) {
+    const int r = p / q4, i4 = (p - r * q4) * 4;
+    if (row0 + r >= N) continue;
+    int32_t o[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o[u] = i4 + u < n ? tile[(i4 + u) * (TR + 1) + r] : -1;
+    *reinterpret_cast<int4 *>(d.la + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+bool flow_eligible(const Dev &d) { return d.n <= FL_MAXN && d.max_chain_len < (1 << 22); }
+
+void launch_flow_desc(const Dev &d, hipStream_t s) {
+  if (d.N == 0) return;
+  k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
+}
+
+void launch_flow(const Dev &d, hipStream_t s) {
+  if (d.N == 0) return;
+  const int nw = (d.n + 63) / 64;
+  k_flow<<<d.n + 1, (nw + 1) * 64, sizeof(FlowLds), s>>>(d);
+}
+
+void launch_flow_transpose(const Dev &d, hipStream_t s) {
+  if (d.N == 0) return;
+  k_flow_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
+}
+
+void launch_flow_coordinates(const Dev &d, hipStream_t s) {
+  launch_flow_desc(d, s);
+  launch_flow(d, s);
+  launch_flow_transpose(d, s);
+}
+
+void configure_flow_kernels() {
+  (void)hipFuncSetAttribute((const void *)k_flow, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(FlowLds));
+  (void)hipFuncSetAttribute((const void *)k_flow_transpose<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            150 * 1024);
+}
+
+}  // namespace bh

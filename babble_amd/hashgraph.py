@@ -206,3 +206,7 @@ class Hashgraph:
         ms = C.c_float()
         self._check(self._L.bh_get_profile(self._h, C.byref(it), C.byref(ms)))
         return int(it.value), float(ms.value)
+
+    def profile_kernel(self):
+        """Name of the coordinate kernel the last run timed."""
+        return self._L.bh_get_profile_kernel(self._h).decode()

@@ -147,7 +147,7 @@ def main():
     value = total_ordered / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # roofline of the dominant kernel (coordinate sweep, k_la_sweep):
+    # roofline of the coordinate kernel (k_flow / k_la_sweep):
     # algorithmic bytes per event = 8*n (two parent LA rows) + 4*n (own row)
     # + 12 (LT of both parents + own); per launch x N events
     n = c["n"]
@@ -173,7 +173,7 @@ def main():
                    "participants": n, "events": N, "events_ordered_per_step": ordered,
                    "rounds": stats.last_round + 1, "blocks": stats.blocks,
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
-        "roofline": {"kernel": "k_la_sweep", "bound": "hbm", "achieved": achieved,
+        "roofline": {"kernel": hg.profile_kernel(), "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": None, "alg_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": sweep_avg_ms},

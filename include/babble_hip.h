@@ -118,6 +118,9 @@ int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap);
 /* kernel statistics of the last run for the roofline report: number of
  * round-loop iterations, coordinate sweep launches' average ms */
 int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms);
+/* name of the coordinate kernel the last run timed ("k_flow": chain
+ * dataflow; "k_la_sweep": chunked sweep); "" before the first run */
+const char *bh_get_profile_kernel(const bh_handle *h);
 
 #ifdef __cplusplus
 }

@@ -211,3 +211,81 @@ def test_large_properties():
     assert b["count"].sum() == len(order)
     assert b["ntx"].sum() == d.ntx[order].sum() == hg.consensus_transactions
     assert len(order) > 0.95 * N
+
+
+def _wild_dag(n, N, seed, back):
+    """A valid DAG that is not gossip-shaped: each event's other-parent is a
+    random event of another creator up to `back` events old (Babble accepts
+    any known event, checkOtherParent hashgraph.go:417-436).  Exercises
+    coordinate parents far outside the engines' on-chip rings."""
+    rng = np.random.default_rng(seed)
+    creator = np.empty(N, np.int32)
+    index = np.empty(N, np.int32)
+    sp = np.empty(N, np.int32)
+    op = np.empty(N, np.int32)
+    last = np.full(n, -1, np.int64)
+    cnt = np.zeros(n, np.int32)
+    for e in range(N):
+        c = e if e < n else int(rng.integers(n))
+        creator[e], index[e], sp[e] = c, cnt[c], last[c]
+        o = -1
+        if e >= n:
+            for _ in range(8):
+                cand = int(rng.integers(max(0, e - back), e))
+                if creator[cand] != c:
+                    o = cand
+                    break
+        op[e] = o
+        last[c] = e
+        cnt[c] += 1
+    hashes = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    sig = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    ntx = (rng.random(N) < 0.5).astype(np.int32)
+    return creator, index, sp, op, hashes, sig, ntx
+
+
+def _wild_parity(n, N, seed, back):
+    from babble_amd import Hashgraph
+    creator, index, sp, op, hashes, sig, ntx = _wild_dag(n, N, seed, back)
+    pid = np.sort(np.random.default_rng(seed + 1).choice(2**31 - 1, n, replace=False)).astype(np.int64)
+    o = Oracle(n, pid, capacity=N)
+    o.insert_dag(creator, index, sp, op, hashes, sig, ntx)
+    o.run_consensus()
+    hg = Hashgraph(pid, N)
+    spi = np.where(sp >= 0, index - 1, -1)
+    opc = np.where(op >= 0, pid[creator[np.maximum(op, 0)]], -1)
+    opi = np.where(op >= 0, index[np.maximum(op, 0)], -1)
+    st = hg.insert_events(pid[creator], index, spi, opc, opi, hashes, sig, ntx)
+    assert not st.any()
+    hg.run_consensus()
+    _compare(o, hg, f"wild n={n} N={N} back={back}")
+
+
+@pytest.mark.parametrize("n,N,seed,back", [
+    (8, 30_000, 21, 20_000),     # parents far behind the LDS rings (flow: 64/chain, sweep: 16K)
+    (24, 40_000, 22, 3_000),
+    (128, 40_000, 23, 30_000),
+    (64, 40_000, 24, 5_000),
+])
+def test_wild_dag_parity(n, N, seed, back):
+    _wild_parity(n, N, seed, back)
+
+
+@pytest.mark.parametrize("n,N,seed,lag", [(32, 40_000, 31, 0), (64, 40_000, 32, 21), (128, 40_000, 33, 0)])
+def test_chunk_sweep_parity(monkeypatch, n, N, seed, lag):
+    """The chunked coordinate sweep (used above the chain-dataflow limits)
+    forced on gossip DAGs the dataflow path would otherwise take."""
+    monkeypatch.setenv("BH_SWEEP", "chunk")
+    _random_parity(n, N, seed, lag)
+
+
+def test_chunk_sweep_wild(monkeypatch):
+    monkeypatch.setenv("BH_SWEEP", "chunk")
+    _wild_parity(8, 30_000, 41, 25_000)
+
+
+@pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
+def test_wide_parity(n, N, seed):
+    """More participants than the dataflow sweep / k_round2 / LDS fame
+    support: chunked sweep, k_round_wide, fame from HBM rows."""
+    _random_parity(n, N, seed)
