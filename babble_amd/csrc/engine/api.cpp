@@ -316,6 +316,8 @@ int stage_order(bh_handle *h) {
     if (hipMemcpy(g, d.diag, sizeof g, hipMemcpyDeviceToHost) == hipSuccess) {
       fprintf(stderr, "[bh diag] sweep: total %llu cyc, wait_desc %llu, wait_ring %llu, substeps %llu, far %llu, chunks %llu | mem: pref %llu store %llu idle %llu\n",
               g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]);
+      fprintf(stderr, "[bh diag] k_flow wave0: steps %llu, cycles %llu (%.1f/step)\n",
+              g[16], g[17], g[17] / (double)(g[16] ? g[16] : 1));
       const double nc = (double)(g[14] ? g[14] : 1);
       fprintf(stderr, "[bh diag] k_round: calls %llu, avg total %.0f cyc: loads %.0f, (unused) %.0f, search %.0f\n",
               g[14], g[13] / nc, g[10] / nc, g[11] / nc, g[12] / nc);

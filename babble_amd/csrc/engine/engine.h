@@ -97,6 +97,7 @@ enum DiagSlot {
   DG_SW_TOTAL = 0, DG_SW_WAIT_DESC, DG_SW_WAIT_RING, DG_SW_SUBSTEPS, DG_SW_FAR, DG_SW_CHUNKS,
   DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,
   DG_RD_B = 10, DG_RD_LOAD, DG_RD_COMP, DG_RD_TOTAL, DG_RD_CALLS,
+  DG_FL_STEPS = 16, DG_FL_CYC, DG_FL_ADV, DG_FL_FAR, DG_FL_WAITD,
   DG_COUNT = 32
 };
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }

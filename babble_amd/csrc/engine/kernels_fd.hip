@@ -44,14 +44,17 @@ __global__ void k_last_la_init(Dev d) {
 }
 
 // One workgroup per (chain i, 64-row segment).  The segment's LA rows (and
-// the row before it) are staged in LDS; column c then owns the FD entries
-// j in (LA[k0-1][c], LA[k0+63][c]], a contiguous run of FDT[i][row(c, j)].
-// A wave writes that run 64 entries per instruction (256 B coalesced), each
-// lane finding its k by binary search down column c in LDS.
+// the row before it) are staged in LDS transposed, one column per LDS row
+// (stride WSEG + 1: the 64 lanes of a wave searching one column hit
+// distinct banks); column c then owns the FD entries j in
+// (LA[k0-1][c], LA[k0+63][c]], a contiguous run of FDT[i][row(c, j)].  A
+// wave writes that run 64 entries per instruction (256 B coalesced), each
+// lane finding its k by binary search down column c.
 constexpr int WSEG = 64;
+constexpr int WST = WSEG + 1;  // LDS stride of a staged column (odd)
 
 __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
-  extern __shared__ int32_t seg[];  // [WSEG + 1][npad]: row 0 = LA[k0 - 1]
+  extern __shared__ int32_t seg[];  // [npad][WST]: seg[c][0] = LA[k0 - 1][c], seg[c][1 + k] = LA[k0 + k][c]
   const int i = blockIdx.y;
   const int32_t len = d.chain_len[i];
   const int32_t k0 = blockIdx.x * WSEG;
@@ -62,7 +65,6 @@ __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
   const int lane = t & 63, wave = t >> 6;
   {
     const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + k0) * npad);
-    int4 *dst = reinterpret_cast<int4 *>(seg + npad);
     const int tot = rows * q4;
     for (int b = 0; b < tot; b += 4 * 256) {
       int4 v[4];
@@ -73,25 +75,34 @@ __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
         v[u] = make_int4(x.x, x.y, x.z, x.w);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (b + u * 256 + t < tot) dst[b + u * 256 + t] = v[u];
+      for (int u = 0; u < 4; ++u) {
+        const int e = b + u * 256 + t;
+        if (e < tot) {
+          const int r = e / q4, c = (e - r * q4) * 4;
+          seg[(c + 0) * WST + 1 + r] = v[u].x;
+          seg[(c + 1) * WST + 1 + r] = v[u].y;
+          seg[(c + 2) * WST + 1 + r] = v[u].z;
+          seg[(c + 3) * WST + 1 + r] = v[u].w;
+        }
+      }
     }
-    for (int c = t; c < npad; c += 256) seg[c] = k0 > 0 ? d.la[(int64_t)(cs + k0 - 1) * npad + c] : -1;
+    for (int c = t; c < npad; c += 256) seg[c * WST] = k0 > 0 ? d.la[(int64_t)(cs + k0 - 1) * npad + c] : -1;
   }
   __syncthreads();
   const int64_t stride = d.la_rows + 64;  // FDT row stride
   int32_t *fdt = d.fdt + (int64_t)i * stride;
   for (int c = wave; c < d.n; c += 4) {
-    const int32_t lo = seg[c], hi = seg[rows * npad + c];  // run (lo, hi]
+    const int32_t *col = seg + c * WST;
+    const int32_t lo = col[0], hi = col[rows];  // run (lo, hi]
     int32_t *out = fdt + d.chain_start[c];
     for (int32_t j0 = lo + 1; j0 <= hi; j0 += 64) {
       const int32_t j = j0 + lane;
       if (j <= hi) {
-        // first segment row k (1-based in seg) with LA[k][c] >= j
+        // first segment row k (1-based) with LA[k][c] >= j
         int a = 1, z = rows;
         while (a < z) {
           const int m = (a + z) >> 1;
-          if (seg[m * npad + c] >= j) z = m;
+          if (col[m] >= j) z = m;
           else a = m + 1;
         }
         out[j] = k0 + a - 1;
@@ -159,7 +170,7 @@ void launch_first_descendants(const Dev &d, hipStream_t s) {
   k_last_la_init<<<1, 256, 0, s>>>(d);
   k_last_la<<<d.n, 256, 0, s>>>(d);
   dim3 g((unsigned)((d.max_chain_len + WSEG - 1) / WSEG), (unsigned)d.n);
-  k_fd_walk<<<g, 256, (size_t)(WSEG + 1) * d.npad * 4, s>>>(d);
+  k_fd_walk<<<g, 256, (size_t)WST * d.npad * 4, s>>>(d);
   if (d.npad <= 512)
     k_fd_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
   else

@@ -4,7 +4,7 @@
 // max(LA[sp][j], LA[op][j]), LA[e][creator] = index; _lamportTimestamp
 // (hashgraph.go:325-379): LT[e] = max(LT[sp], LT[op]) + 1.
 //
-// Mapping (n <= 128, chains shorter than 2^22): one workgroup per LA column
+// Mapping (n <= 128, chains shorter than 2^21): one workgroup per LA column
 // (plus one for LT), one LANE per creator chain.  Along a chain the
 // self-parent is the lane's previous event, so that half of the recurrence
 // stays in a register; the other-parent (d, j) is read from chain d's ring
@@ -15,15 +15,13 @@
 // and each step is one LDS round trip.  The chunked sweep in
 // kernels_coords.hip (used above these limits) needs ~2.2x more steps.
 //
-// Waves: ceil(n/64) compute waves (64 chains each) + one prefetch wave that
-// keeps every chain's ring of other-parent descriptors (packed (d << 22) |
-// j, or -1 for none, chain-major) filled by LDS-DMA, 64 entries per refill.
-// Values leave as one store per compute wave per step into column-major
-// LA (chain-major rows); a parent older than the value ring (tag past j) is
-// read back from there once its chain has published that its stores are
-// complete (checkpoint every 32 steps: s_waitcnt vmcnt(32) -- every step
-// issues exactly one store, so the stores of the last 32 steps are the 32
-// youngest operations and everything before the previous checkpoint is done).
+// Waves: ceil(n/64) compute waves (64 chains each), one prefetch wave that
+// keeps every chain's ring of other-parent descriptors (chain-major, packed
+// as below) filled by LDS-DMA, 64 entries per refill, and one store wave
+// that follows the value rings by tag and streams finished values to
+// column-major LA (chain-major rows).  A parent older than the value ring
+// (tag past j) is read back from there once the store wave has published
+// (after its vmcnt(0)) that the value is in HBM.
 #include "engine.h"
 
 namespace bh {
@@ -35,24 +33,43 @@ constexpr int FL_MAXN = 128;
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) volatile int lds_vint;
 
-// Row n of the value ring is a sentinel chain: slot 63 = {-1, FL_NOOP}
-// always matches the "no other-parent" descriptor, slot 62 = {-1, -2} never
-// matches FL_WAIT (a lane without a loaded descriptor), slots 0..60 absorb
-// the ring writes of lanes that did not advance.
-constexpr int32_t FL_NOOP = 0x3FFFFF, FL_WAIT = 0x3FFFFE;
+// Descriptor of an other-parent (d, j): bits [31:15] = LDS byte address of
+// its ring slot (d * FL_R + j % FL_R) * 8, bits [14:0] = j / FL_R (the slot's
+// tag when it holds j), so a step extracts both with one shift and one AND.
+// A ring slot is two dwords {value + 1 | (tag & 255) << 24, tag}: the tag
+// sits in both, so a read that races the slot's write and sees one dword
+// new and the other old fails the check (the slot's previous occupant had
+// tag - 1) and is simply retried on the next step.  Values are below 2^24
+// (LA indexes < 2^21; LT < N < 2^24).
+// Row n of the value ring is a sentinel chain: slot 63 = {0 | NOOP bits,
+// FL_NOOP} always matches the "no other-parent" descriptor (value -1),
+// slot 62 = {0, -2} never matches FL_WAIT (a lane without a loaded
+// descriptor), slots 0..60 absorb the ring writes of lanes that did not
+// advance.
+constexpr int32_t FL_NOOP = 0x7FFF, FL_WAIT = 0x7FFE;
+__host__ __device__ constexpr int32_t flow_desc(int32_t d, int32_t j, int32_t tag) {
+  return (((d * 64 + (j & 63)) * 8) << 15) | tag;
+}
+__device__ __forceinline__ int2 flow_slot(int32_t v, int32_t tag) {
+  return make_int2((int32_t)(((uint32_t)(v + 1) & 0xFFFFFFu) | ((uint32_t)tag << 24)), tag);
+}
+__device__ __forceinline__ bool flow_match(int2 s, int32_t tag) {
+  return s.y == tag && ((uint32_t)s.x >> 24) == ((uint32_t)tag & 255u);
+}
+__device__ __forceinline__ int32_t flow_value(int2 s) { return (int32_t)((uint32_t)s.x & 0xFFFFFFu) - 1; }
 
 // chain-major other-parent descriptors
 __global__ void k_flow_desc(Dev d) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.N) return;
   const int32_t o = d.op[e];
-  d.opdesc[d.epos[e]] = o < 0 ? (d.n << 22) | FL_NOOP : (d.creator[o] << 22) | d.index[o];
+  d.opdesc[d.epos[e]] = o < 0 ? flow_desc(d.n, 63, FL_NOOP) : flow_desc(d.creator[o], d.index[o], d.index[o] >> 6);
 }
 
 struct FlowLds {
   int2 vring[FL_MAXN + 1][FL_R];   // 64.5 KiB
   int32_t dring[FL_MAXN][FL_DR];   // 64 KiB
-  int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN];
+  int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN], stored[FL_MAXN];
 };
 
 template <bool LT>
@@ -67,12 +84,14 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
     L.filled[c] = 0;
     L.consumed[c] = 0;
     L.pub[c] = 0;
+    L.stored[c] = 0;
     L.cs[c] = d.chain_start[c];
     for (int s = 0; s < FL_R; ++s) L.vring[c][s] = make_int2(-1, -1);
   }
-  if (t < FL_R) L.vring[n][t] = make_int2(-1, t == 63 ? FL_NOOP : -2);
+  if (t < FL_R) L.vring[n][t] = t == 63 ? flow_slot(-1, FL_NOOP) : make_int2(0, -2);  // 0..60: scratch
   __syncthreads();
-  lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub;
+  lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub,
+           *stored = (lds_vint *)L.stored;
 
   if (wave == nw) {
     // ---------------- prefetch wave: descriptor rings ----------------
@@ -115,48 +134,91 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
     }
     return;
   }
-  if (wave > nw) return;
+  if (wave == nw + 1) {
+    // ---------------- store wave: rings -> HBM ----------------
+    // Follows every chain's ring by tag and streams the finished values to
+    // column-major LA; `stored` (slot reusable) bounds how far the compute
+    // lanes may run ahead, `pub` (store complete: after vmcnt(0)) tells far
+    // readers the value is in HBM.
+    int32_t sp[2] = {0, 0}, len[2], cs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane + 64 * h;
+      len[h] = c < n ? d.chain_len[c] : 0;
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (int pass = 1;; ++pass) {
+      bool left = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = min(lane + 64 * h, n);  // row n: sentinel, never matches below
+        for (int it = 0; it < 8; ++it) {
+          const int2 v = L.vring[c][sp[h] & (FL_R - 1)];
+          const bool ok = sp[h] < len[h] && flow_match(v, sp[h] >> 6);
+          if (!__any(ok)) break;
+          if (ok) {
+            out[cs[h] + sp[h]] = flow_value(v);
+            ++sp[h];
+          }
+        }
+        left |= sp[h] < len[h];
+        if (lane + 64 * h < n) stored[lane + 64 * h] = sp[h];
+      }
+      if ((pass & 7) == 0 || !__any(left)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (lane + 64 * h < n) pub[lane + 64 * h] = sp[h];
+      }
+      if (!__any(left)) break;
+    }
+    return;
+  }
+  if (wave > nw + 1) return;
 
   // ---------------- compute waves: one chain per lane ----------------
   // Per step: two LDS reads (the other-parent's ring slot, the next
-  // descriptor), one ring write and one store, all unconditional (lanes that
-  // do not advance write the sentinel row / the scratch rows), so the loop
-  // has no divergent branches; refills and read-backs sit behind
-  // wave-uniform tests.
+  // descriptor) and one ring write, all unconditional (lanes that do not
+  // advance write the sentinel row), so the loop has no divergent branches;
+  // refills and read-backs sit behind wave-uniform tests.  A lane may run
+  // at most 48 events ahead of the store wave (ring slot reuse).
+  static_assert(FL_R == 64, "descriptor packing assumes 64 ring slots");
   const int c = wave * 64 + lane;
   const bool valid = c < n;
   const int32_t len = valid ? d.chain_len[c] : 0;
-  const int32_t cs = valid ? L.cs[c] : 0;
   const int cc = valid ? c : 0;
   const bool own = !LT && c == col;
-  int32_t *dummy = out + d.la_rows + lane;  // scratch rows: a not-ready lane's store
-  int2 *const wscratch = &L.vring[n][lane % 61];
-  const int32_t WAIT = (n << 22) | FL_WAIT;
-  int32_t k = 0, cur = -1, kcp = 0, lim = 0;
-  int32_t dsc = WAIT;  // descriptor of event k, or WAIT until it has landed
-  for (int32_t step = 0;; ++step) {
-    if ((step & 15) == 0) {  // refresh the fill level; publish progress
-      lim = valid ? filled[cc] : 0;
-      if ((step & 31) == 0) {
-        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // see the header
-        if (valid) { pub[c] = kcp; consumed[c] = k; }
-        kcp = k;
-      }
+  const uint32_t ring_c = (uint32_t)(cc * FL_R * 8);           // LDS byte address of my ring
+  const uint32_t wscratch = (uint32_t)((n * FL_R + lane % 61) * 8);
+  const int32_t WAIT = flow_desc(n, 62, FL_WAIT);
+  char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
+  const int32_t *dring_c = &L.dring[cc][0];
+  int32_t k = 0, cur = -1, lim = 0;
+  int32_t dsc = WAIT;  // descriptor of event k, or WAIT until it may advance
+  const bool dg = d.diag != nullptr && col == 0 && wave == 0;
+  const unsigned long long t_start = dg ? stamp() : 0;
+  int32_t step = 0;
+  for (;; ++step) {
+    if ((step & 15) == 0) {  // refresh the limits, reload stalled descriptors
+      lim = valid ? min(filled[cc], stored[cc] + 48) : 0;
+      if (dsc == WAIT && k < lim) dsc = dring_c[k & (FL_DR - 1)];
+      if ((step & 63) == 0 && valid) consumed[c] = k;
       if (!__any(k < len)) break;
     }
-    if (__builtin_expect(__any(dsc == WAIT && k < lim), 0))  // descriptor landed
-      if (dsc == WAIT && k < lim) dsc = L.dring[cc][k & (FL_DR - 1)];
-    const int32_t dd = (uint32_t)dsc >> 22, jj = dsc & 0x3FFFFF;
-    const int2 slot = L.vring[dd][jj & (FL_R - 1)];
-    const int32_t dn = L.dring[cc][(k + 1) & (FL_DR - 1)];
-    bool ready = slot.y == jj && dsc != WAIT;
-    int32_t val = slot.x;
-    if (__builtin_expect(__any(slot.y > jj), 0)) {
+    const uint32_t sa = (uint32_t)dsc >> 15;
+    const int32_t tag = dsc & 0x7FFF;
+    const int2 slot = *reinterpret_cast<const int2 *>(lds + sa);
+    const int32_t kn = k + 1;
+    const int32_t dn = dring_c[kn & (FL_DR - 1)];
+    bool ready = flow_match(slot, tag);
+    int32_t val = flow_value(slot);
+    if (__builtin_expect(__any(slot.y > tag), 0)) {
       // the ring moved past j: read the value back once chain dd has
       // published it (one inline-asm load with its own wait: a load the
-      // compiler sees in this loop would make it drain the per-step stores
-      // at every iteration)
-      if (slot.y > jj && pub[dd] > jj) {
+      // compiler sees in this loop would make it drain stores/loads at every
+      // iteration)
+      const int32_t dd = (int32_t)(sa >> 9), jj = (tag << 6) | ((sa >> 3) & 63);
+      if (slot.y > tag && pub[dd] > jj) {
         const int32_t *fp = out + L.cs[dd] + jj;
         asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
         ready = true;
@@ -165,17 +227,20 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
     int32_t v = max(cur, val);
     if (LT) v += 1;
     else v = own ? k : v;  // LA[e][creator] = index
-    *(ready ? &L.vring[c][k & (FL_R - 1)] : wscratch) = make_int2(v, k);
-    *(ready ? out + cs + k : dummy) = v;  // exactly one store per step
+    const uint32_t wa = ready ? ring_c + ((k & (FL_R - 1)) << 3) : wscratch;
+    *reinterpret_cast<int2 *>(lds + wa) = flow_slot(v, k >> 6);
     cur = ready ? v : cur;
-    k += ready ? 1 : 0;
-    dsc = ready ? (k < lim ? dn : WAIT) : dsc;
+    dsc = ready ? (kn < lim ? dn : WAIT) : dsc;
+    k = ready ? kn : k;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (valid) { pub[c] = len; consumed[c] = len; }
+  if (valid) consumed[c] = len;
+  if (dg && lane == 0) {
+    d.diag[DG_FL_STEPS] = step;
+    d.diag[DG_FL_CYC] = stamp() - t_start;
+  }
 }
 
-__global__ __launch_bounds__(192) void k_flow(Dev d) {
+__global__ __launch_bounds__(256) void k_flow(Dev d) {
   extern __shared__ __attribute__((aligned(16))) unsigned char flm[];
   FlowLds &L = *reinterpret_cast<FlowLds *>(flm);
   if ((int)blockIdx.x == d.n) flow_body<true>(d, L);
@@ -215,7 +280,11 @@ __global__ __launch_bounds__(256) void k_flow_transpose(Dev d) {
   }
 }
 
-bool flow_eligible(const Dev &d) { return d.n <= FL_MAXN && d.max_chain_len < (1 << 22); }
+// 128 chains (one LDS ring row each + the sentinel row within a 17-bit
+// address), chains shorter than 2^21 (15-bit tags), values below 2^24
+bool flow_eligible(const Dev &d) {
+  return d.n <= FL_MAXN && d.max_chain_len < (1 << 21) && d.N < (1 << 24) - 1;
+}
 
 void launch_flow_desc(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
@@ -225,7 +294,7 @@ void launch_flow_desc(const Dev &d, hipStream_t s) {
 void launch_flow(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
-  k_flow<<<d.n + 1, (nw + 1) * 64, sizeof(FlowLds), s>>>(d);
+  k_flow<<<d.n + 1, (nw + 2) * 64, sizeof(FlowLds), s>>>(d);
 }
 
 void launch_flow_transpose(const Dev &d, hipStream_t s) {
