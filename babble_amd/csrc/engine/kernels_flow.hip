@@ -36,27 +36,32 @@ typedef __attribute__((address_space(3))) volatile int lds_vint;
 // Descriptor of an other-parent (d, j): bits [31:15] = LDS byte address of
 // its ring slot (d * FL_R + j % FL_R) * 8, bits [14:0] = j / FL_R (the slot's
 // tag when it holds j), so a step extracts both with one shift and one AND.
-// A ring slot is two dwords {value + 1 | (tag & 255) << 24, tag}: the tag
-// sits in both, so a read that races the slot's write and sees one dword
-// new and the other old fails the check (the slot's previous occupant had
-// tag - 1) and is simply retried on the next step.  Values are below 2^24
-// (LA indexes < 2^21; LT < N < 2^24).
-// Row n of the value ring is a sentinel chain: slot 63 = {0 | NOOP bits,
-// FL_NOOP} always matches the "no other-parent" descriptor (value -1),
-// slot 62 = {0, -2} never matches FL_WAIT (a lane without a loaded
-// descriptor), slots 0..60 absorb the ring writes of lanes that did not
-// advance.
+// A ring slot is two dwords {value + 1 | (tag & 255) << 24, descriptor of
+// the event it holds}: a consumer compares the second dword with its own
+// descriptor as is, and the tag sits in both dwords, so a read that races
+// the slot's write and sees one dword new and the other old fails the
+// check (the slot's previous occupant had tag - 1) and is simply retried on
+// the next step.  Values are carried biased by +1 (-1 = none) below 2^24
+// (LA indexes < 2^21; LT < N < 2^24); a later occupant of the slot has a
+// larger descriptor (same address, larger tag).
+// Row n of the value ring is a sentinel chain: slot 63 holds the "no
+// other-parent" event (value -1, always matches FL_NOOP), slot 62 = {0, 0}
+// never matches FL_WAIT (a lane without a loaded descriptor), slots 0..60
+// absorb the ring writes of lanes that did not advance.
 constexpr int32_t FL_NOOP = 0x7FFF, FL_WAIT = 0x7FFE;
 __host__ __device__ constexpr int32_t flow_desc(int32_t d, int32_t j, int32_t tag) {
   return (((d * 64 + (j & 63)) * 8) << 15) | tag;
 }
-__device__ __forceinline__ int2 flow_slot(int32_t v, int32_t tag) {
-  return make_int2((int32_t)(((uint32_t)(v + 1) & 0xFFFFFFu) | ((uint32_t)tag << 24)), tag);
+// slot of event k (biased value vb) of the chain whose ring starts at LDS byte ring_c
+__device__ __forceinline__ int2 flow_slot(int32_t vb, uint32_t ring_c, int32_t k) {
+  const uint32_t addr = ring_c + ((uint32_t)(k & 63) << 3);
+  return make_int2((int32_t)(((uint32_t)vb & 0xFFFFFFu) | ((uint32_t)k << 18 & 0xFF000000u)),
+                   (int32_t)(addr << 15 | (uint32_t)(k >> 6)));
 }
-__device__ __forceinline__ bool flow_match(int2 s, int32_t tag) {
-  return s.y == tag && ((uint32_t)s.x >> 24) == ((uint32_t)tag & 255u);
+__device__ __forceinline__ bool flow_match(int2 s, int32_t dsc) {
+  return s.y == dsc && ((uint32_t)s.x >> 24) == ((uint32_t)dsc & 255u);
 }
-__device__ __forceinline__ int32_t flow_value(int2 s) { return (int32_t)((uint32_t)s.x & 0xFFFFFFu) - 1; }
+__device__ __forceinline__ int32_t flow_vb(int2 s) { return (int32_t)((uint32_t)s.x & 0xFFFFFFu); }
 
 // chain-major other-parent descriptors
 __global__ void k_flow_desc(Dev d) {
@@ -86,9 +91,10 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
     L.pub[c] = 0;
     L.stored[c] = 0;
     L.cs[c] = d.chain_start[c];
-    for (int s = 0; s < FL_R; ++s) L.vring[c][s] = make_int2(-1, -1);
+    for (int s = 0; s < FL_R; ++s)  // "before event s": descriptor tag 0, value tag byte 255
+      L.vring[c][s] = make_int2((int32_t)0xFF000000u, flow_desc(c, s, 0));
   }
-  if (t < FL_R) L.vring[n][t] = t == 63 ? flow_slot(-1, FL_NOOP) : make_int2(0, -2);  // 0..60: scratch
+  if (t < FL_R) L.vring[n][t] = t == 63 ? make_int2((int32_t)0xFF000000u, flow_desc(n, 63, FL_NOOP)) : make_int2(0, 0);
   __syncthreads();
   lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub,
            *stored = (lds_vint *)L.stored;
@@ -154,10 +160,10 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
         const int c = min(lane + 64 * h, n);  // row n: sentinel, never matches below
         for (int it = 0; it < 8; ++it) {
           const int2 v = L.vring[c][sp[h] & (FL_R - 1)];
-          const bool ok = sp[h] < len[h] && flow_match(v, sp[h] >> 6);
+          const bool ok = sp[h] < len[h] && flow_match(v, flow_desc(c, sp[h], sp[h] >> 6));
           if (!__any(ok)) break;
           if (ok) {
-            out[cs[h] + sp[h]] = flow_value(v);
+            out[cs[h] + sp[h]] = flow_vb(v) - 1;
             ++sp[h];
           }
         }
@@ -180,8 +186,10 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
   // Per step: two LDS reads (the other-parent's ring slot, the next
   // descriptor) and one ring write, all unconditional (lanes that do not
   // advance write the sentinel row), so the loop has no divergent branches;
-  // refills and read-backs sit behind wave-uniform tests.  A lane may run
-  // at most 48 events ahead of the store wave (ring slot reuse).
+  // refills, read-backs and the exit test sit in a header every 8 steps (a
+  // lone wave issues in order, ~10 cycles per instruction: the step's
+  // instruction count is its cost).  A lane may run at most 48 events ahead
+  // of the store wave (ring slot reuse).
   static_assert(FL_R == 64, "descriptor packing assumes 64 ring slots");
   const int c = wave * 64 + lane;
   const bool valid = c < n;
@@ -193,46 +201,64 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
   const int32_t WAIT = flow_desc(n, 62, FL_WAIT);
   char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
   const int32_t *dring_c = &L.dring[cc][0];
-  int32_t k = 0, cur = -1, lim = 0;
+  int32_t k = 0, cur = 0, lim = 0;  // cur: value of event k-1, biased by +1
   int32_t dsc = WAIT;  // descriptor of event k, or WAIT until it may advance
   const bool dg = d.diag != nullptr && col == 0 && wave == 0;
   const unsigned long long t_start = dg ? stamp() : 0;
   int32_t step = 0;
-  for (;; ++step) {
-    if ((step & 15) == 0) {  // refresh the limits, reload stalled descriptors
-      lim = valid ? min(filled[cc], stored[cc] + 48) : 0;
-      if (dsc == WAIT && k < lim) dsc = dring_c[k & (FL_DR - 1)];
-      if ((step & 63) == 0 && valid) consumed[c] = k;
-      if (!__any(k < len)) break;
-    }
-    const uint32_t sa = (uint32_t)dsc >> 15;
-    const int32_t tag = dsc & 0x7FFF;
-    const int2 slot = *reinterpret_cast<const int2 *>(lds + sa);
-    const int32_t kn = k + 1;
-    const int32_t dn = dring_c[kn & (FL_DR - 1)];
-    bool ready = flow_match(slot, tag);
-    int32_t val = flow_value(slot);
-    if (__builtin_expect(__any(slot.y > tag), 0)) {
-      // the ring moved past j: read the value back once chain dd has
-      // published it (one inline-asm load with its own wait: a load the
-      // compiler sees in this loop would make it drain stores/loads at every
-      // iteration)
+  // one step of the chain: everything unconditional (a chain that does not
+  // advance writes the sentinel row); ~20 VALU ops
+#define FLOW_STEP()                                                               \
+  do {                                                                          \
+    const uint32_t sa_ = (uint32_t)dsc >> 15;                                   \
+    const int2 slot_ = *reinterpret_cast<const int2 *>(lds + sa_);             \
+    const int32_t kn_ = k + 1;                                                  \
+    const int32_t dn_ = dring_c[kn_ & (FL_DR - 1)];                              \
+    const bool ready_ = flow_match(slot_, dsc);                                 \
+    int32_t v_ = max(cur, flow_vb(slot_));                                      \
+    if (LT) v_ += 1;                                                            \
+    else v_ = own ? k + 1 : v_; /* LA[e][creator] = index */                    \
+    const uint32_t wa_ = ready_ ? ring_c + ((k & (FL_R - 1)) << 3) : wscratch;  \
+    *reinterpret_cast<int2 *>(lds + wa_) = flow_slot(v_, ring_c, k);           \
+    cur = ready_ ? v_ : cur;                                                    \
+    dsc = ready_ ? (kn_ < lim ? dn_ : WAIT) : dsc;                              \
+    k = ready_ ? kn_ : k;                                                       \
+  } while (0)
+  for (;; step += 8) {
+    // header, every 8 steps: limits, stalled descriptors, read-backs, exit
+    lim = valid ? min(filled[cc], stored[cc] + 48) : 0;
+    if (dsc == WAIT && k < lim) dsc = dring_c[k & (FL_DR - 1)];
+    if ((step & 63) == 0 && valid) consumed[c] = k;
+    if (!__any(k < len)) break;
+    {
+      // a parent the ring has moved past (tag beyond j): read it back once
+      // chain dd has published it, and take the step here (rare; one
+      // inline-asm load with its own wait, so the compiler never sees a load
+      // in flight across the loop)
+      const uint32_t sa = (uint32_t)dsc >> 15;
+      const int32_t tag = dsc & 0x7FFF;
+      const int2 slot = *reinterpret_cast<const int2 *>(lds + sa);
       const int32_t dd = (int32_t)(sa >> 9), jj = (tag << 6) | ((sa >> 3) & 63);
-      if (slot.y > tag && pub[dd] > jj) {
-        const int32_t *fp = out + L.cs[dd] + jj;
-        asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
-        ready = true;
+      const bool far = (uint32_t)slot.y > (uint32_t)dsc && pub[dd] > jj;
+      if (__builtin_expect(__any(far), 0)) {
+        if (far) {
+          const int32_t *fp = out + L.cs[dd] + jj;
+          int32_t val;
+          asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
+          int32_t v = max(cur, val + 1);
+          if (LT) v += 1;
+          else v = own ? k + 1 : v;
+          *reinterpret_cast<int2 *>(lds + ring_c + ((k & (FL_R - 1)) << 3)) = flow_slot(v, ring_c, k);
+          cur = v;
+          ++k;
+          dsc = k < lim ? dring_c[k & (FL_DR - 1)] : WAIT;
+        }
       }
     }
-    int32_t v = max(cur, val);
-    if (LT) v += 1;
-    else v = own ? k : v;  // LA[e][creator] = index
-    const uint32_t wa = ready ? ring_c + ((k & (FL_R - 1)) << 3) : wscratch;
-    *reinterpret_cast<int2 *>(lds + wa) = flow_slot(v, k >> 6);
-    cur = ready ? v : cur;
-    dsc = ready ? (kn < lim ? dn : WAIT) : dsc;
-    k = ready ? kn : k;
+    FLOW_STEP(); FLOW_STEP(); FLOW_STEP(); FLOW_STEP();
+    FLOW_STEP(); FLOW_STEP(); FLOW_STEP(); FLOW_STEP();
   }
+#undef FLOW_STEP
   if (valid) consumed[c] = len;
   if (dg && lane == 0) {
     d.diag[DG_FL_STEPS] = step;
@@ -241,8 +267,7 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
 }
 
 __global__ __launch_bounds__(256) void k_flow(Dev d) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char flm[];
-  FlowLds &L = *reinterpret_cast<FlowLds *>(flm);
+  __shared__ FlowLds L;  // static: the ring's LDS base is the constant 0
   if ((int)blockIdx.x == d.n) flow_body<true>(d, L);
   else flow_body<false>(d, L);
 }
@@ -294,7 +319,7 @@ void launch_flow_desc(const Dev &d, hipStream_t s) {
 void launch_flow(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
-  k_flow<<<d.n + 1, (nw + 2) * 64, sizeof(FlowLds), s>>>(d);
+  k_flow<<<d.n + 1, (nw + 2) * 64, 0, s>>>(d);
 }
 
 void launch_flow_transpose(const Dev &d, hipStream_t s) {
@@ -309,8 +334,6 @@ void launch_flow_coordinates(const Dev &d, hipStream_t s) {
 }
 
 void configure_flow_kernels() {
-  (void)hipFuncSetAttribute((const void *)k_flow, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(FlowLds));
   (void)hipFuncSetAttribute((const void *)k_flow_transpose<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             150 * 1024);
 }
