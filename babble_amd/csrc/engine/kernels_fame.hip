@@ -22,6 +22,30 @@ namespace bh {
 
 constexpr int FAME_MAXN = 128;  // LDS-staged rows up to this many participants
 
+// rows rowid[0..m) of src (row stride npad ints) into LDS dst (stride rs):
+// four independent 16-B loads in flight per thread, addresses from LDS
+__device__ __forceinline__ void fame_stage(int32_t *dst, int rs, const int32_t *src, const int32_t *rowid,
+                                           int m, int npad) {
+  const int q4 = npad / 4, tot = m * q4, nt = blockDim.x;
+  for (int b = threadIdx.x; b < tot; b += 4 * nt) {
+    int4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(b + u * nt, tot - 1);
+      const int row = i / q4;
+      v[u] = reinterpret_cast<const int4 *>(src + (int64_t)rowid[row] * npad)[i - row * q4];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = b + u * nt;
+      if (i < tot) {
+        const int row = i / q4;
+        reinterpret_cast<int4 *>(dst + row * rs)[i - row * q4] = v[u];
+      }
+    }
+  }
+}
+
 template <bool LDS_ROWS>
 __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
@@ -33,54 +57,63 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   unsigned long long *Vp = reinterpret_cast<unsigned long long *>(fsm);
   unsigned long long *Vc = Vp + n * WW;
   unsigned long long *S = Vc + n * WW;
-  int32_t *xs = reinterpret_cast<int32_t *>(S + n * WW);
-  int32_t *dec = xs + n;   // 0 undecided, 1 famous, 2 not famous
+  int32_t *xs = reinterpret_cast<int32_t *>(S + n * WW);  // W(r) event ids
+  int32_t *xc = xs + n;    // creator of x
+  int32_t *xk = xc + n;    // index of x
+  int32_t *dec = xk + n;   // 0 undecided, 1 famous, 2 not famous
   int32_t *nd = dec + n;   // decisions of the current j (bit0 yes, bit1 no)
-  int32_t *misc = nd + n;  // [0] undecided count, [1] error
-  int32_t *ly = misc + 4;               // LDS_ROWS: LA rows of W(j)
+  int32_t *rid = nd + n;   // [3][n] chain-major rows: W(r) (kept), then W(j-1) / W(j) alternating
+  int32_t *misc = rid + 3 * n;  // [0] undecided count, [1] error
+  int32_t *ly = misc + 4;                      // LDS_ROWS: LA rows of W(j)
   int32_t *fw = ly + (LDS_ROWS ? n * rs : 0);  // LDS_ROWS: FD rows of W(j-1)
 
   const int32_t nx = d.wcnt[r], xb = d.wofs[r];
-  for (int i = t; i < nx; i += nt) { xs[i] = d.wids[xb + i]; dec[i] = 0; }
+  for (int i = t; i < nx; i += nt) {
+    const int32_t e = d.wids[xb + i];
+    xs[i] = e;
+    xc[i] = d.creator[e];
+    xk[i] = d.index[e];
+    dec[i] = 0;
+    rid[i] = d.wrow[xb + i];  // rows of W(r), for minLA at the end
+  }
   if (t == 0) { misc[0] = nx; misc[1] = 0; }
   __syncthreads();
+  int cur = 1;  // rid[cur * n ..] (cur = 1 or 2): rows of the latest W(j)
 
   if (r + 1 < R) {
-    // ---- j = r+1: vote = see(y, x) ----
+    // ---- j = r+1: vote = see(y, x) = LA[y][creator(x)] >= index(x) ----
     int32_t ny = d.wcnt[r + 1], yb = d.wofs[r + 1];
+    for (int i = t; i < ny; i += nt) rid[n + i] = d.wrow[yb + i];
     for (int i = t; i < nx * WW; i += nt) Vp[i] = 0ull;
     __syncthreads();
+    if (LDS_ROWS) {
+      fame_stage(ly, rs, d.la, rid + n, ny, npad);
+      __syncthreads();
+    }
     for (int p = t; p < nx * ny; p += nt) {
       const int x = p / ny, y = p - x * ny;
-      const int32_t xe = xs[x], ye = d.wids[yb + y];
-      const bool v = d.la[(int64_t)d.epos[ye] * npad + d.creator[xe]] >= d.index[xe];
-      if (v) atomicOr(&Vp[x * WW + (y >> 6)], 1ull << (y & 63));
+      const int32_t a = LDS_ROWS ? ly[y * rs + xc[x]] : d.la[(int64_t)rid[n + y] * npad + xc[x]];
+      if (a >= xk[x]) atomicOr(&Vp[x * WW + (y >> 6)], 1ull << (y & 63));
     }
     __syncthreads();
     // ---- j >= r+2 ----
     for (int j = r + 2; j < R; ++j) {
       if (misc[0] == 0) break;
-      const int32_t nw = ny, wb = yb;  // W(j-1)
+      const int32_t nw = ny;  // W(j-1): rows rid[cur * n ..]
       ny = d.wcnt[j];
       yb = d.wofs[j];
-      for (int i = t; i < ny * WW; i += nt) { S[i] = 0ull; }
+      int32_t *wr_ = rid + cur * n, *yr_ = rid + (3 - cur) * n;
+      for (int i = t; i < ny; i += nt) yr_[i] = d.wrow[yb + i];
+      for (int i = t; i < ny * WW; i += nt) S[i] = 0ull;
       for (int i = t; i < nx * WW; i += nt) Vc[i] = 0ull;
       for (int i = t; i < nx; i += nt) nd[i] = 0;
+      __syncthreads();
       if (LDS_ROWS) {
-        const int q4 = npad / 4;
-        for (int q = t; q < ny * q4; q += nt) {
-          const int y = q / q4, c4 = q - y * q4;
-          const int32_t ye = d.wids[yb + y];
-          reinterpret_cast<int4 *>(ly + y * rs)[c4] =
-              reinterpret_cast<const int4 *>(d.la + (int64_t)d.epos[ye] * npad)[c4];
-        }
-        for (int q = t; q < nw * q4; q += nt) {
-          const int w = q / q4, c4 = q - w * q4;
-          reinterpret_cast<int4 *>(fw + w * rs)[c4] =
-              reinterpret_cast<const int4 *>(d.fd + (int64_t)d.wrow[wb + w] * npad)[c4];
-        }
+        fame_stage(ly, rs, d.la, yr_, ny, npad);
+        fame_stage(fw, rs, d.fd, wr_, nw, npad);
       }
       __syncthreads();
+      cur = 3 - cur;
       // S_j: 8x8 (y, w) tiles per thread, count columns with LA[y] >= FD[w]
       const int ty = (ny + 7) >> 3, tw = (nw + 7) >> 3;
       for (int tile = t; tile < ty * tw; tile += nt) {
@@ -94,8 +127,8 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
             yr[a] = ly + y * rs;
             wr[a] = fw + w * rs;
           } else {
-            yr[a] = d.la + (int64_t)d.epos[d.wids[yb + y]] * npad;
-            wr[a] = d.fd + (int64_t)d.wrow[wb + w] * npad;
+            yr[a] = d.la + (int64_t)yr_[y] * npad;
+            wr[a] = d.fd + (int64_t)wr_[w] * npad;
           }
         }
         int cnt[8][8];
@@ -176,13 +209,18 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
     if (misc[1]) d.state[ST_ERR] = 2;
   }
   // famous count and min LA over famous witnesses (see(w, x) for all w in FW)
+  if (LDS_ROWS) {
+    __syncthreads();
+    fame_stage(ly, rs, d.la, rid, nx, npad);  // rows of W(r) (rid[0..nx) kept)
+    __syncthreads();
+  }
   for (int c = t; c < npad; c += nt) {
     int32_t m = INT32_MAX;
     int cntf = 0;
     for (int x = 0; x < nx; ++x) {
       if (dec[x] != 1) continue;
       ++cntf;
-      m = min(m, d.la[(int64_t)d.epos[xs[x]] * npad + c]);
+      m = min(m, LDS_ROWS ? ly[x * rs + c] : d.la[(int64_t)rid[x] * npad + c]);
     }
     d.minla[(int64_t)r * npad + c] = m;
     if (c == 0) d.nfam[r] = cntf;
@@ -191,7 +229,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
 
 size_t fame_lds_bytes(int n, int npad, bool lds_rows) {
   const int WW = (n + 63) >> 6;
-  size_t b = (size_t)3 * n * WW * 8 + (size_t)3 * n * 4 + 16;
+  size_t b = (size_t)3 * n * WW * 8 + (size_t)8 * n * 4 + 16;
   if (lds_rows) b += (size_t)2 * n * (npad + 4) * 4;
   return b;
 }

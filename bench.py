@@ -154,6 +154,17 @@ def main():
     sweep_avg_ms = float(np.mean(sweep_ms))
     alg_bytes = N * (12 * n + 12)
     achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
+    # HBM traffic of that kernel per launch, from the committed PMC passes
+    # (tools/pmc.sh -> tools/pmc_summary.py -> profiles/pmc_traffic.json;
+    # FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction)
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            tr = json.load(f).get(hg.profile_kernel(), {})
+        if tr.get("participants") == n and tr.get("events") == N:
+            traffic = tr["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
     out = {
         "metric": METRIC,
         "value": value,
@@ -175,7 +186,7 @@ def main():
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
         "roofline": {"kernel": hg.profile_kernel(), "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": None, "alg_bytes_per_launch": alg_bytes,
+                     "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                      "avg_launch_ms": sweep_avg_ms},
         "stages_ms": dict(zip(["coordinates", "rounds", "fame", "round_received", "order"],
                               (stage_tot / args.steps).round(3).tolist())),
@@ -186,7 +197,8 @@ def main():
         cpu_sample = min(N, {1: 10_000, 2: 1_000_000, 3: 500_000, 4: 100_000, 5: 500_000}[args.cfg])
     if rank == 0 and world == 1 and cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args.cfg, cpu_sample, log)
-        out["speedup_vs_cpu"] = value / out["cpu_baseline"]["value"]
+        cv = out["cpu_baseline"]["value"]
+        out["speedup_vs_cpu"] = value / cv if cv > 0 else None
     else:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -1,0 +1,48 @@
+"""Summarise tools/pmc.sh counter passes into profiles/pmc_traffic.json.
+
+HBM bytes per launch of each kernel = FETCH_SIZE x 2 (gfx950 reports half
+the bytes of wide coalesced reads, MI355X_MICROARCH.md HBM section) +
+WRITE_SIZE, both in KiB per dispatch as rocprofv3 reports them (summed over
+XCDs).  usage: python tools/pmc_summary.py gpurun_out/pmc_c3 <participants> <events>
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_dispatch(path, counter):
+    acc = collections.defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        names[r["Dispatch_Id"]] = r["Kernel_Name"]
+    by_kernel = collections.defaultdict(list)
+    for dsp, v in acc.items():
+        by_kernel[names[dsp].split("(")[0].split("<")[0].replace("void ", "").replace("bh::", "")].append(v)
+    return {k: sum(v) / len(v) for k, v in by_kernel.items()}
+
+
+def main():
+    d, n, N = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    fetch = per_dispatch(os.path.join(d, "p0", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_dispatch(os.path.join(d, "p1", "run_counter_collection.csv"), "WRITE_SIZE")
+    out_path = os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json")
+    try:
+        out = json.load(open(out_path))
+    except (OSError, ValueError):
+        out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, 0.0) * 1024 * 2, write.get(k, 0.0) * 1024
+        out[k] = {"participants": n, "events": N, "fetch_bytes_corrected": f, "write_bytes": w,
+                  "hbm_bytes_per_launch": f + w,
+                  "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {os.path.basename(d)}"}
+        print(k, out[k])
+    json.dump(out, open(out_path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
