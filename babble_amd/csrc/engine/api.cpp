@@ -97,7 +97,8 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd, d.opdesc, d.lt_row};  // la_ev aliases fdt
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd, d.opdesc, d.lt_row, d.fdarch, d.wfrow,
+                  d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -161,6 +162,13 @@ int build_graph(bh_handle *h) {
   return BH_OK;
 }
 
+// the chain dataflow sweep where eligible; BH_SWEEP=chunk forces the chunked
+// sweep (A/B and parity of both paths)
+static bool use_flow(const bh::Dev &d) {
+  const char *e = getenv("BH_SWEEP");
+  return bh::flow_eligible(d) && !(e && !strcmp(e, "chunk"));
+}
+
 // stage 1: coordinates, Lamport timestamps, rounds, witnesses
 int stage_rounds(bh_handle *h) {
   int rc;
@@ -171,15 +179,15 @@ int stage_rounds(bh_handle *h) {
   hipStream_t s = h->stream;
   HIPCHK(h, hipEventRecord(h->ev[0], s));
   bh::launch_prep(d, s);
-  // BH_SWEEP=chunk forces the chunked sweep (A/B and parity of both paths)
-  const bool force_chunk = getenv("BH_SWEEP") && !strcmp(getenv("BH_SWEEP"), "chunk");
-  if (bh::flow_eligible(d) && !force_chunk) {
+  bool walked = false;
+  if (use_flow(d)) {
     bh::launch_flow_desc(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
     bh::launch_flow(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
     bh::launch_flow_transpose(d, s);
     h->sweep_kernel = "k_flow";
+    walked = true;
   } else {
     bh::launch_chunk_depth(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
@@ -188,7 +196,7 @@ int stage_rounds(bh_handle *h) {
     bh::launch_permute(d, s);
     h->sweep_kernel = "k_la_sweep";
   }
-  bh::launch_first_descendants(d, s);
+  bh::launch_first_descendants(d, s, walked);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
   h->coords_for = (int)d.N;
@@ -377,20 +385,25 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C);
   d.la_rows = C;
   A(&d.la, (size_t)(C + 64) * d.npad);
-  // the sweep's slabs (la_ev) are dead once permuted into la; the
-  // firstDescendants walk output (fdt) reuses the same allocation
-  A(&d.fdt, (size_t)(C + 64) * d.npad);
+  // the chunked sweep's slabs (la_ev) are dead once permuted into la; the
+  // firstDescendants walk output (fdt) reuses the same allocation.  The
+  // flow path's column-major LA (la_col) is read while FDT is written
+  // (k_flow_transpose walks as it transposes): its own allocation
+  A(&d.fdt, (size_t)(C + 128) * d.npad);  // whole 64-row tiles (fdt_pos)
   d.la_ev = d.fdt;
-  d.la_col = d.fdt;
+  if (n <= bh::FL_MAXN) A(&d.la_col, (size_t)(C + 64) * d.npad);
+  else d.la_col = d.fdt;
   A(&d.opdesc, (size_t)C + 128);
   A(&d.lt_row, (size_t)C + 64);
-  A(&d.fd, (size_t)(C + 64) * d.npad);
+  d.fd_cols = d.npad <= 128;
+  if (d.fd_cols) A(&d.fdarch, R1 * n * d.npad);
+  else A(&d.fd, (size_t)(C + 64) * d.npad);
   A(&d.last_la, (size_t)(n + 1) * d.npad);
   A(&d.nextwin, (size_t)2 * n * 32 * d.npad);
   A(&d.candfd, (size_t)2 * n * d.npad);
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
-  A(&d.wrow, (size_t)d.W_cap);
+  A(&d.wrow, (size_t)d.W_cap); A(&d.wfrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
@@ -661,9 +674,10 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     d.N = N;
     if ((rc = set_chain_tables(h))) return rc;
     bh::launch_prep(d, h->stream);
-    if (bh::flow_eligible(d)) bh::launch_flow_coordinates(d, h->stream);
+    const bool walked = use_flow(d);
+    if (walked) bh::launch_flow_coordinates(d, h->stream);
     else bh::launch_coordinates(d, h->stream);
-    bh::launch_first_descendants(d, h->stream);
+    bh::launch_first_descendants(d, h->stream, walked);
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
     h->stage = 0;
@@ -675,8 +689,12 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (last_ancestors)
     HIPCHK(h, hipMemcpy(last_ancestors, d.la + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
-  if (first_descendants)
+  if (first_descendants && d.fd_cols) {  // one column of FDT
+    HIPCHK(h, hipMemcpy2D(first_descendants, 4, d.fdt + bh::fdt_pos(row, 0, d.npad), 64 * 4, 4, (size_t)d.n,
+                          hipMemcpyDeviceToHost));
+  } else if (first_descendants) {
     HIPCHK(h, hipMemcpy(first_descendants, d.fd + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
+  }
   return BH_OK;
 }
 

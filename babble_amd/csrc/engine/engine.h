@@ -27,6 +27,7 @@ constexpr int32_t UNSET = INT32_MIN;    // Go nil
 constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
 constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 8192;     // frames sorted in LDS up to this size (96 KiB)
+constexpr int FL_MAXN = 128;            // participants the dataflow sweep (k_flow) handles
 
 enum StateSlot {
   ST_CUR0 = 0,     // round r of the iteration with parity 0 (ST_CUR0 + 1: parity 1)
@@ -40,6 +41,15 @@ enum StateSlot {
   ST_NBLOCKS = 9,
   ST_COUNT = 16
 };
+
+// FDT: firstDescendants by column, tiled by 64 chain-major rows --
+// [row / 64][column i][row % 64].  Runs of consecutive rows of one column
+// (what the walks write and the round loop's windows read) are contiguous,
+// and a window's 128 column segments share one or two 32 KiB tiles (a
+// [column][row] layout would put each in its own page).
+__host__ __device__ inline int64_t fdt_pos(int64_t row, int i, int npad) {
+  return (((row >> 6) * npad + i) << 6) + (row & 63);
+}
 
 struct Dev {
   int32_t n, npad, sm;
@@ -65,11 +75,18 @@ struct Dev {
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds
   int32_t *B, *wofs, *wcnt, *wids;
-  int32_t *wrow;   // [W] row of each witness's firstDescendants in fd
+  int32_t *wrow;   // [W] chain-major row of each witness (its LA row)
   int32_t *Bp;     // [2][n] B[r] / B[r+1] by round parity
   // firstDescendants of every event (updateAncestorFirstDescendant)
   int32_t *fd;      // [la_rows + 64][npad] chain-major rows
-  int32_t *fdt;     // [npad][la_rows + 64] walk output (shares la_ev's allocation)
+  int32_t *fdt;     // walk output, tiled by 64 chain-major rows (fdt_pos; shares la_ev's allocation)
+  // fd_cols (npad <= 128): FDT is complete (the walks write MaxInt32 where
+  // no event of a chain sees a row) and is the only per-event FD table; the
+  // round loop reads windows of it, fame the FD rows of witnesses archived
+  // per round (fdarch[r][c] = FD row of candidate (c, B[r][c])); no fd
+  int32_t fd_cols;
+  int32_t *fdarch;  // [R_cap + 1][n][npad]
+  int32_t *wfrow;   // [W] row of each witness's FD: fdarch row (fd_cols) or fd row
   int32_t *last_la; // [n][npad] LA row of each chain's last event
   int32_t max_chain_len;
   // round-loop hand-off (k_round2, npad <= 128), by round parity
@@ -126,6 +143,6 @@ void launch_fame(const Dev &d, int32_t R, hipStream_t s);
 void launch_round_received(const Dev &d, int32_t R, hipStream_t s);
 void launch_order(const Dev &d, int32_t R, hipStream_t s);
 void configure_fd_kernels();
-void launch_first_descendants(const Dev &d, hipStream_t s);  // fd from la
+void launch_first_descendants(const Dev &d, hipStream_t s, bool walked);  // fd from la (FDT already written by k_flow_transpose when walked)
 
 }  // namespace bh

@@ -63,7 +63,9 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   int32_t *dec = xk + n;   // 0 undecided, 1 famous, 2 not famous
   int32_t *nd = dec + n;   // decisions of the current j (bit0 yes, bit1 no)
   int32_t *rid = nd + n;   // [3][n] chain-major rows: W(r) (kept), then W(j-1) / W(j) alternating
-  int32_t *misc = rid + 3 * n;  // [0] undecided count, [1] error
+  int32_t *fid = rid + 3 * n;   // [3][n] FD rows of the same witnesses (wfrow)
+  int32_t *misc = fid + 3 * n;  // [0] undecided count, [1] error
+  const int32_t *fdrows = d.fd_cols ? d.fdarch : d.fd;
   int32_t *ly = misc + 4;                      // LDS_ROWS: LA rows of W(j)
   int32_t *fw = ly + (LDS_ROWS ? n * rs : 0);  // LDS_ROWS: FD rows of W(j-1)
 
@@ -75,6 +77,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
     xk[i] = d.index[e];
     dec[i] = 0;
     rid[i] = d.wrow[xb + i];  // rows of W(r), for minLA at the end
+    fid[i] = d.wfrow[xb + i];
   }
   if (t == 0) { misc[0] = nx; misc[1] = 0; }
   __syncthreads();
@@ -83,7 +86,10 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   if (r + 1 < R) {
     // ---- j = r+1: vote = see(y, x) = LA[y][creator(x)] >= index(x) ----
     int32_t ny = d.wcnt[r + 1], yb = d.wofs[r + 1];
-    for (int i = t; i < ny; i += nt) rid[n + i] = d.wrow[yb + i];
+    for (int i = t; i < ny; i += nt) {
+      rid[n + i] = d.wrow[yb + i];
+      fid[n + i] = d.wfrow[yb + i];
+    }
     for (int i = t; i < nx * WW; i += nt) Vp[i] = 0ull;
     __syncthreads();
     if (LDS_ROWS) {
@@ -102,15 +108,19 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
       const int32_t nw = ny;  // W(j-1): rows rid[cur * n ..]
       ny = d.wcnt[j];
       yb = d.wofs[j];
-      int32_t *wr_ = rid + cur * n, *yr_ = rid + (3 - cur) * n;
-      for (int i = t; i < ny; i += nt) yr_[i] = d.wrow[yb + i];
+      int32_t *yr_ = rid + (3 - cur) * n;
+      const int32_t *wr_ = fid + cur * n;
+      for (int i = t; i < ny; i += nt) {
+        yr_[i] = d.wrow[yb + i];
+        fid[(3 - cur) * n + i] = d.wfrow[yb + i];
+      }
       for (int i = t; i < ny * WW; i += nt) S[i] = 0ull;
       for (int i = t; i < nx * WW; i += nt) Vc[i] = 0ull;
       for (int i = t; i < nx; i += nt) nd[i] = 0;
       __syncthreads();
       if (LDS_ROWS) {
         fame_stage(ly, rs, d.la, yr_, ny, npad);
-        fame_stage(fw, rs, d.fd, wr_, nw, npad);
+        fame_stage(fw, rs, fdrows, wr_, nw, npad);
       }
       __syncthreads();
       cur = 3 - cur;
@@ -128,7 +138,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
             wr[a] = fw + w * rs;
           } else {
             yr[a] = d.la + (int64_t)yr_[y] * npad;
-            wr[a] = d.fd + (int64_t)wr_[w] * npad;
+            wr[a] = fdrows + (int64_t)wr_[w] * npad;
           }
         }
         int cnt[8][8];
@@ -229,7 +239,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
 
 size_t fame_lds_bytes(int n, int npad, bool lds_rows) {
   const int WW = (n + 63) >> 6;
-  size_t b = (size_t)3 * n * WW * 8 + (size_t)8 * n * 4 + 16;
+  size_t b = (size_t)3 * n * WW * 8 + (size_t)11 * n * 4 + 16;
   if (lds_rows) b += (size_t)2 * n * (npad + 4) * 4;
   return b;
 }

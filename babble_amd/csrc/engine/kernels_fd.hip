@@ -89,12 +89,13 @@ __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
     for (int c = t; c < npad; c += 256) seg[c * WST] = k0 > 0 ? d.la[(int64_t)(cs + k0 - 1) * npad + c] : -1;
   }
   __syncthreads();
-  const int64_t stride = d.la_rows + 64;  // FDT row stride
-  int32_t *fdt = d.fdt + (int64_t)i * stride;
+  const bool last = k0 + rows == len;
   for (int c = wave; c < d.n; c += 4) {
     const int32_t *col = seg + c * WST;
     const int32_t lo = col[0], hi = col[rows];  // run (lo, hi]
-    int32_t *out = fdt + d.chain_start[c];
+    const int64_t rc0 = d.chain_start[c];
+    if (last && d.fd_cols)  // rows (c, j) no event of chain i sees
+      for (int32_t j = hi + 1 + lane; j < d.chain_len[c]; j += 64) d.fdt[fdt_pos(rc0 + j, i, npad)] = FD_NONE;
     for (int32_t j0 = lo + 1; j0 <= hi; j0 += 64) {
       const int32_t j = j0 + lane;
       if (j <= hi) {
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
           if (col[m] >= j) z = m;
           else a = m + 1;
         }
-        out[j] = k0 + a - 1;
+        d.fdt[fdt_pos(rc0 + j, i, npad)] = k0 + a - 1;
       }
     }
   }
@@ -122,7 +123,6 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   const int64_t row0 = (int64_t)blockIdx.x * TR_ROWS;
   const int64_t N = d.N;
   const int n = d.n, npad = d.npad;
-  const int64_t stride = d.la_rows + 64;
   const int ro = t % TR_ROWS;
   const int64_t row = min(row0 + ro, N - 1);
   if (t < TR_ROWS) {
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int ii = min(i + IPP * u, n - 1);
-      v[u] = __builtin_nontemporal_load(d.fdt + (int64_t)ii * stride + row);
+      v[u] = __builtin_nontemporal_load(d.fdt + fdt_pos(row, ii, npad));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -165,12 +165,15 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   }
 }
 
-void launch_first_descendants(const Dev &d, hipStream_t s) {
+void launch_first_descendants(const Dev &d, hipStream_t s, bool walked) {
   if (d.N == 0) return;
+  if (!walked) {
+    dim3 g((unsigned)((d.max_chain_len + WSEG - 1) / WSEG), (unsigned)d.n);
+    k_fd_walk<<<g, 256, (size_t)WST * d.npad * 4, s>>>(d);
+  }
+  if (d.fd_cols) return;  // FDT complete; no chain-major rows
   k_last_la_init<<<1, 256, 0, s>>>(d);
   k_last_la<<<d.n, 256, 0, s>>>(d);
-  dim3 g((unsigned)((d.max_chain_len + WSEG - 1) / WSEG), (unsigned)d.n);
-  k_fd_walk<<<g, 256, (size_t)WST * d.npad * 4, s>>>(d);
   if (d.npad <= 512)
     k_fd_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
   else

@@ -28,7 +28,7 @@ namespace bh {
 
 constexpr int FL_R = 64;     // value ring slots per chain (int2 {value, index})
 constexpr int FL_DR = 128;   // descriptor ring entries per chain
-constexpr int FL_MAXN = 128;
+
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(3))) volatile int lds_vint;
@@ -272,36 +272,125 @@ __global__ __launch_bounds__(256) void k_flow(Dev d) {
   else flow_body<false>(d, L);
 }
 
-// column-major LA (chain-major rows) -> row-major LA; LT rows -> event ids
-template <int TR>
-__global__ __launch_bounds__(256) void k_flow_transpose(Dev d) {
-  extern __shared__ int32_t tile[];  // [npad][TR + 1]
-  constexpr int IPP = 256 / TR;
+// column-major LA (chain-major rows) -> row-major LA; LT rows -> event
+// ids; and the firstDescendants walk (kernels_fd.hip) on the same tile:
+// the TR rows staged column-major are exactly what the walk searches, so
+// FDT is produced here without a second pass over LA.  A tile may span
+// chain boundaries; each run of rows of one chain is a walk segment whose
+// column c owns FD entries j in (LA[row before][c], LA[last row][c]].
+template <int TR, int BT>
+__global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
+  extern __shared__ int32_t tile[];  // [npad][TR + 1], then prev[npad]
+  __shared__ int32_t rc[TR], rj[TR];
+  __shared__ uint64_t segmask;
+  __shared__ int32_t cstart[FL_MAXN + 16], clen[FL_MAXN + 16];
+  constexpr int IPP = BT / TR;  // columns per load pass
+  constexpr int LU = 16;        // load passes in flight
   const int t = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * TR;
   const int64_t N = d.N;
   const int n = d.n, npad = d.npad;
   const int64_t stride = d.la_rows + 64;
   const int ro = t % TR;
+  const int rows = (int)min<int64_t>(TR, N - row0);
   const int64_t row = min(row0 + ro, N - 1);
-  if (t < TR && row0 + t < N) d.lt[d.chain_ids[row0 + t]] = d.lt_row[row0 + t];
-  for (int i = t / TR; i < n; i += 4 * IPP) {
-    int32_t v[4];
+  int32_t *prev = tile + npad * (TR + 1);
+  if (t < TR) {
+    const int32_t e = d.chain_ids[row];
+    if (t < rows) d.lt[e] = d.lt_row[row0 + t];
+    rc[t] = d.creator[e];
+    rj[t] = d.index[e];
+  }
+  for (int i = t; i < n; i += BT) prev[i] = row0 > 0 ? d.la_col[(int64_t)i * stride + row0 - 1] : -1;
+  for (int i = t; i < n; i += BT) {
+    cstart[i] = d.chain_start[i];
+    clen[i] = d.chain_len[i];
+  }
+  for (int i = t / TR; i < n; i += LU * IPP) {
+    int32_t v[LU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(d.la_col + (int64_t)min(i + IPP * u, n - 1) * stride + row);
+    for (int u = 0; u < LU; ++u) v[u] = __builtin_nontemporal_load(d.la_col + (int64_t)min(i + IPP * u, n - 1) * stride + row);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < LU; ++u)
       if (i + IPP * u < n) tile[(i + IPP * u) * (TR + 1) + ro] = v[u];
   }
   __syncthreads();
+  if (t < 64) {  // segment starts: row 0 and every chain change
+    const bool st = t < rows && t < TR && (t == 0 || rc[t] != rc[t - 1]);
+    const uint64_t m = __ballot(st);
+    if (t == 0) segmask = m;
+  }
   const int q4 = npad / 4;
   for (int p = t; p < TR * q4; p += blockDim.x) {
     const int r = p / q4, i4 = (p - r * q4) * 4;
-    if (row0 + r >= N) continue;
+    if (r >= rows) continue;
     int32_t o[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) o[u] = i4 + u < n ? tile[(i4 + u) * (TR + 1) + r] : -1;
     *reinterpret_cast<int4 *>(d.la + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+  const uint64_t segs = segmask;
+  const int lane = t & 63, wave = t >> 6;
+  for (uint64_t m = segs; m; m &= m - 1) {
+    const int ra = __builtin_ctzll(m);
+    const uint64_t rest = m & (m - 1);
+    const int rb = rest ? __builtin_ctzll(rest) : rows;  // segment rows [ra, rb)
+    const int32_t i = rc[ra], ka = rj[ra];
+    if (ka + (rb - ra) == clen[i] && d.fd_cols)  // chain i ends here: rows it never sees
+      for (int c = wave; c < n; c += BT / 64) {
+        const int32_t hi = tile[c * (TR + 1) + rb - 1];
+        for (int32_t j = hi + 1 + lane; j < clen[c]; j += 64) d.fdt[fdt_pos(cstart[c] + j, i, npad)] = FD_NONE;
+      }
+    // four columns per pass: their binary searches (at most 6 halvings of
+    // a <= 64-row segment) interleave, so LDS latency is paid once per
+    // four columns; the first 64 entries of each run here, longer runs'
+    // remainders after
+    for (int c0 = wave * 4; c0 < n; c0 += BT / 16) {
+      int32_t lo[4], hi[4], a[4], z[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = min(c0 + u, n - 1);
+        const int32_t *col = tile + c * (TR + 1);
+        lo[u] = ka == 0 ? -1 : (ra == 0 ? prev[c] : col[ra - 1]);
+        hi[u] = c0 + u < n ? col[rb - 1] : lo[u];
+        a[u] = ra;
+        z[u] = rb - 1;
+      }
+#pragma unroll
+      for (int st = 0; st < 6; ++st) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int mm = (a[u] + z[u]) >> 1;
+          const bool ge = tile[(c0 + u) * (TR + 1) + mm] >= lo[u] + 1 + lane;
+          const bool go = a[u] < z[u];
+          z[u] = go && ge ? mm : z[u];
+          a[u] = go && !ge ? mm + 1 : a[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int32_t j = lo[u] + 1 + lane;
+        if (j <= hi[u]) d.fdt[fdt_pos(cstart[c0 + u] + j, i, npad)] = ka + a[u] - ra;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (hi[u] - lo[u] <= 64) continue;
+        const int32_t *col = tile + (c0 + u) * (TR + 1);
+        for (int32_t j0 = lo[u] + 65; j0 <= hi[u]; j0 += 64) {
+          const int32_t j = j0 + lane;
+          if (j <= hi[u]) {
+            int aa = ra, zz = rb - 1;
+            while (aa < zz) {
+              const int mm = (aa + zz) >> 1;
+              if (col[mm] >= j) zz = mm;
+              else aa = mm + 1;
+            }
+            d.fdt[fdt_pos(cstart[c0 + u] + j, i, npad)] = ka + aa - ra;
+          }
+        }
+      }
+    }
   }
 }
 
@@ -324,7 +413,7 @@ void launch_flow(const Dev &d, hipStream_t s) {
 
 void launch_flow_transpose(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
-  k_flow_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
+  k_flow_transpose<64, 512><<<(unsigned)((d.N + 63) / 64), 512, (size_t)d.npad * 66 * 4, s>>>(d);
 }
 
 void launch_flow_coordinates(const Dev &d, hipStream_t s) {
@@ -334,7 +423,7 @@ void launch_flow_coordinates(const Dev &d, hipStream_t s) {
 }
 
 void configure_flow_kernels() {
-  (void)hipFuncSetAttribute((const void *)k_flow_transpose<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void *)k_flow_transpose<64, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             150 * 1024);
 }
 

@@ -350,9 +350,9 @@ __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
   const int4 *la = reinterpret_cast<const int4 *>(d.la + (int64_t)cs * d.npad);
   int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + (int64_t)c * HW * q4;
   for (int i = threadIdx.x; i < rows * q4; i += blockDim.x) nw[i] = la[i];
-  const int4 *fd = reinterpret_cast<const int4 *>(d.fd + (int64_t)cs * d.npad);
-  int4 *cf = reinterpret_cast<int4 *>(d.candfd) + (int64_t)c * q4;
-  for (int i = threadIdx.x; i < q4; i += blockDim.x) cf[i] = fd[i];
+  // candidate (c, 0): its FD row gathered from the FDT columns
+  int32_t *cf = d.candfd + (int64_t)c * d.npad;
+  for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs, i, d.npad)] : FD_NONE;
 }
 
 template <int LPC>
@@ -365,7 +365,8 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int nwq = HW * q4;  // int4 per handed-over window (<= 1024)
   int4 *win = sm4;              // [2 * HW][q4]: rows k0 .. k0 + 63
-  int4 *fdw = sm4 + 2 * nwq;    // [HW][q4]: FD rows k0 .. k0 + 31
+  int32_t *fdw = reinterpret_cast<int32_t *>(sm4 + 2 * nwq);  // [npad][FDS]: FD rows rb .. rb + 31 by column
+  constexpr int FDS = HW + 4;
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   const bool dg = d.diag != nullptr && t == 0;
   const unsigned long long ts0 = dg ? stamp() : 0;
@@ -389,11 +390,24 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int4 wv = reinterpret_cast<const int4 *>(d.nextwin)[((int64_t)p * n + c) * nwq + min(t, nwq - 1)];
   if (done) return;
   const bool act = q < n && bq < lq;
+  // archive this round's candidate FD row of chain c for fame (the group
+  // of chain c holds it in registers; the stores drain during the search)
+  if (q == c && act && r < d.R_cap) {
+    int4 *fa = reinterpret_cast<int4 *>(d.fdarch) + ((int64_t)r * n + c) * q4;
+#pragma unroll
+    for (int u = 0; u < PPL; ++u)
+      if (part + LPC * u < q4) fa[part + LPC * u] = f[u];
+  }
   const int rows = min(HW, max(0, len - k0));
   // ---- loads for the hand-off (consumed after the search) ----
   const int rows2 = min(HW, max(0, len - k0 - HW));
   const int4 xv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0 + HW) * q4 + min(t, max(rows2 * q4 - 1, 0))];
-  const int4 fv = reinterpret_cast<const int4 *>(d.fd)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
+  // FD rows rb .. rb + 31 (rb = the window's first row rounded down to 4)
+  // from the FDT tiles: 16 B = 4 rows of one column per thread, 8 threads
+  // per column
+  const int64_t rb = (int64_t)(cs + k0) & ~(int64_t)3;
+  const int fi = min(t >> 3, n - 1), fp = (t & 7) * 4;
+  const int4 fv = *reinterpret_cast<const int4 *>(d.fdt + fdt_pos(rb + fp, fi, npad));
   if (t < nwq) win[t] = wv;
   if (t < 16) cntk[t] = 0;
   __syncthreads();
@@ -467,18 +481,19 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   if (nc > 0 && r + 1 < d.R_cap && result < len) {
     const int32_t off = result - k0;
     int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + ((int64_t)(p ^ 1) * n + c) * nwq;
-    int4 *cf = reinterpret_cast<int4 *>(d.candfd) + ((int64_t)(p ^ 1) * n + c) * q4;
-    if (off < HW) {  // both from the rows staged during the search
+    int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
+    const int frel = (int)(cs + result - rb);  // row of the candidate in fdw
+    if (off < HW && frel < HW) {  // both from the rows staged during the search
       if (t < rows2 * q4) win[nwq + t] = xv;
-      if (t < rows * q4) fdw[t] = fv;
+      if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
       __syncthreads();
       if (t < nwq) nw[t] = win[off * q4 + t];
-      if (t < q4) cf[t] = fdw[off * q4 + t];
+      if (t < npad) cf[t] = t < n ? fdw[t * FDS + frel] : FD_NONE;
     } else {
       const int4 *la = reinterpret_cast<const int4 *>(d.la) + (int64_t)(cs + result) * q4;
       const int nr = min(HW, len - result);
       if (t < nr * q4) nw[t] = la[t];
-      if (t < q4) cf[t] = reinterpret_cast<const int4 *>(d.fd)[(int64_t)(cs + result) * q4 + t];
+      if (t < npad) cf[t] = t < n ? d.fdt[fdt_pos(cs + result, t, npad)] : FD_NONE;
     }
   }
   if (dg) {
@@ -507,7 +522,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
 }
 
-bool round2_eligible(const Dev &d) { return d.npad <= 128; }
+bool round2_eligible(const Dev &d) { return d.fd_cols != 0; }
 
 void launch_round_init(const Dev &d, hipStream_t s) {
   if (round2_eligible(d)) k_round2_init<<<d.n, 256, 0, s>>>(d);
@@ -531,7 +546,7 @@ void configure_round_kernels() {
 // iteration parity p = round & 1 (ITER_BATCH is even, rounds start at 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
-    const size_t lds = (size_t)3 * HW * (d.npad / 4) * 16;
+    const size_t lds = (size_t)2 * HW * (d.npad / 4) * 16 + (size_t)d.npad * (HW + 4) * 4;
     if (d.npad <= 64) k_round2<4><<<d.n, 1024, lds, s>>>(d, p);
     else k_round2<8><<<d.n, 1024, lds, s>>>(d, p);
     return;
@@ -603,7 +618,8 @@ __global__ __launch_bounds__(64) void k_wfill(Dev d) {
     if (w) {
       const int32_t k = j + popc64(m & ((1ull << lane) - 1ull));
       d.wids[k] = d.chain_ids[d.chain_start[q] + b0];
-      d.wrow[k] = d.chain_start[q] + b0;  // the witness's FD row
+      d.wrow[k] = d.chain_start[q] + b0;  // the witness's LA row
+      d.wfrow[k] = d.fd_cols ? r * n + q : d.chain_start[q] + b0;  // and its FD row
     }
     j += popc64(m);
   }

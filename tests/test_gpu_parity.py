@@ -289,3 +289,32 @@ def test_wide_parity(n, N, seed):
     """More participants than the dataflow sweep / k_round2 / LDS fame
     support: chunked sweep, k_round_wide, fame from HBM rows."""
     _random_parity(n, N, seed)
+
+
+@pytest.mark.parametrize("sweep", ["flow", "chunk"])
+@pytest.mark.parametrize("n,N,seed,lag", [(16, 4_000, 61, 2), (128, 20_000, 62, 0)])
+def test_coordinates_random(monkeypatch, sweep, n, N, seed, lag):
+    """lastAncestors / firstDescendants (hashgraph.go:478-544) of sampled
+    events -- every chain's last events included, whose FD entries are
+    MaxInt32 for the chains that have not seen them yet -- against the
+    oracle, through both coordinate sweeps."""
+    from babble_amd.dag import Dag
+    if sweep == "chunk":
+        monkeypatch.setenv("BH_SWEEP", "chunk")
+    d = Dag(n, N, seed, lagging=lag, sig_mode=0)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    hg = _engine(n, d.participant_ids, N)
+    assert not hg.insert_dag(d).any()
+    rng = np.random.default_rng(seed)
+    last = [int(np.nonzero(d.creator == c)[0][-1]) for c in range(n)]
+    first = [int(np.nonzero(d.creator == c)[0][0]) for c in range(n)]
+    sample = sorted(set(last + first + rng.integers(0, N, 150).tolist()))
+    nmax = 0
+    for e in sample:
+        la_r, fd_r = o.coordinates(e)
+        la_g, fd_g = hg.coordinates(e)
+        assert np.array_equal(la_r, la_g), (e, la_r, la_g)
+        assert np.array_equal(fd_r, fd_g), (e, fd_r, fd_g)
+        nmax += int((np.asarray(fd_r) == 2**31 - 1).sum())
+    assert nmax > 0  # the unseen tails were exercised
