@@ -186,7 +186,7 @@ int stage_rounds(bh_handle *h) {
     bh::launch_flow(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
     bh::launch_flow_transpose(d, s);
-    h->sweep_kernel = "k_flow";
+    h->sweep_kernel = bh::flow32_eligible(d) ? "k_flow32" : "k_flow";
     walked = true;
   } else {
     bh::launch_chunk_depth(d, s);
@@ -249,6 +249,7 @@ int stage_rounds(bh_handle *h) {
   if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
   h->R = st[bh::ST_ROUNDS];
   h->iters = st[bh::ST_ITERS];
+  if (st[bh::ST_FLOWOVF]) bh::launch_flow_lt_fallback(d, s);  // LT only feeds the frame order
   bh::launch_witness_tables(d, h->R, s);
   bh::launch_assign_rounds(d, s);
   HIPCHK(h, hipGetLastError());
@@ -320,8 +321,15 @@ int stage_order(bh_handle *h) {
   float sms = 0;
   if (hipEventElapsedTime(&sms, h->ev_sweep[0], h->ev_sweep[1]) == hipSuccess) h->sweep_ms = sms;
   if (d.diag) {  // diagnostic run only: phase counters to stderr, then reset
-    unsigned long long g[bh::DG_COUNT];
-    if (hipMemcpy(g, d.diag, sizeof g, hipMemcpyDeviceToHost) == hipSuccess) {
+    std::vector<unsigned long long> gv(bh::DG_COUNT);
+    unsigned long long *g = gv.data();
+    if (hipMemcpy(g, d.diag, bh::DG_COUNT * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      if (const char *tp = getenv("BH_TIMELINE")) {  // k_round2 stamps for offline analysis
+        if (FILE *f = fopen(tp, "wb")) {
+          fwrite(g + bh::DG_TL, 8, bh::DG_COUNT - bh::DG_TL, f);
+          fclose(f);
+        }
+      }
       fprintf(stderr, "[bh diag] sweep: total %llu cyc, wait_desc %llu, wait_ring %llu, substeps %llu, far %llu, chunks %llu | mem: pref %llu store %llu idle %llu\n",
               g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]);
       fprintf(stderr, "[bh diag] k_flow wave0: steps %llu, cycles %llu (%.1f/step)\n",
@@ -370,7 +378,8 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   d.n = n;
   d.npad = (n + 3) & ~3;
   d.sm = 2 * n / 3 + 1;  // hashgraph.go:54
-  d.ring_log2 = n < 256 ? 14 : 12;  // sweep LDS: one workgroup per CU below 256 columns
+  d.ring_log2 = n < 256 ? 14 : 12;
+  d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;  // sweep LDS: one workgroup per CU below 256 columns
   d.N = 0;
   const int64_t C = std::max<int64_t>(h->cap, 1);
   d.R_cap = (int32_t)std::min<int64_t>(C / d.sm + 2, INT32_MAX / 2);
@@ -393,7 +402,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   d.la_ev = d.fdt;
   if (n <= bh::FL_MAXN) A(&d.la_col, (size_t)(C + 64) * d.npad);
   else d.la_col = d.fdt;
-  A(&d.opdesc, (size_t)C + 128);
+  A(&d.opdesc, (size_t)2 * (C + 128));  // k_flow32: int2 entries
   A(&d.lt_row, (size_t)C + 64);
   d.fd_cols = d.npad <= 128;
   if (d.fd_cols) A(&d.fdarch, R1 * n * d.npad);

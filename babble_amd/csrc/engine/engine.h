@@ -39,6 +39,7 @@ enum StateSlot {
   ST_ITERS = 7,    // round-loop iterations executed
   ST_FLAGGED = 8,  // candidates that needed the exact witness resolution
   ST_NBLOCKS = 9,
+  ST_FLOWOVF = 10,  // k_flow32: a Lamport timestamp reached 2^21 (LT recomputed by k_flow)
   ST_COUNT = 16
 };
 
@@ -71,6 +72,7 @@ struct Dev {
   int32_t *opdesc;  // [N] chain-major other-parent (creator << 22 | index), -1 = none
   int32_t *la_col;  // [n][la_rows+64] column-major LA, chain-major rows (aliases la_ev)
   int32_t *lt_row;  // [la_rows+64] LT by chain-major row
+  int32_t flow_ltclamp;  // k_flow32 LT limit (2^21 - 256; BH_FLOW_LTCLAMP lowers it to test the fallback)
   uint8_t *depth, *chunk_maxd;
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds
@@ -115,8 +117,10 @@ enum DiagSlot {
   DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,
   DG_RD_B = 10, DG_RD_LOAD, DG_RD_COMP, DG_RD_TOTAL, DG_RD_CALLS,
   DG_FL_STEPS = 16, DG_FL_CYC, DG_FL_ADV, DG_FL_FAR, DG_FL_WAITD,
-  DG_COUNT = 32
+  DG_TL = 32,  // k_round2 timeline: rounds TL_R0 .. TL_R0+TL_NR, [r][c][4] realtime stamps
+  DG_COUNT = 32 + 64 * 128 * 4
 };
+constexpr int TL_R0 = 1000, TL_NR = 64;
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
 
 // launchers (kernels_*.hip)
@@ -129,6 +133,8 @@ bool flow_eligible(const Dev &d);
 void launch_flow_coordinates(const Dev &d, hipStream_t s);  // LA + LT, chain dataflow
 void launch_flow_desc(const Dev &d, hipStream_t s);
 void launch_flow(const Dev &d, hipStream_t s);
+bool flow32_eligible(const Dev &d);
+void launch_flow_lt_fallback(const Dev &d, hipStream_t s);
 void launch_flow_transpose(const Dev &d, hipStream_t s);
 void launch_prep(const Dev &d, hipStream_t s);
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep

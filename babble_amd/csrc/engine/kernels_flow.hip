@@ -24,6 +24,9 @@
 // (after its vmcnt(0)) that the value is in HBM.
 #include "engine.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace bh {
 
 constexpr int FL_R = 64;     // value ring slots per chain (int2 {value, index})
@@ -78,11 +81,11 @@ struct FlowLds {
 };
 
 template <bool LT>
-__device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
+__device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L, int col0) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = d.n;
   const int nw = (n + 63) >> 6;  // compute waves
-  const int col = blockIdx.x;
+  const int col = blockIdx.x + col0;
   const int64_t stride = d.la_rows + 64;
   int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
   for (int c = t; c < n; c += blockDim.x) {
@@ -266,10 +269,236 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_flow(Dev d) {
+__global__ __launch_bounds__(256) void k_flow(Dev d, int col0) {
   __shared__ FlowLds L;  // static: the ring's LDS base is the constant 0
-  if ((int)blockIdx.x == d.n) flow_body<true>(d, L);
-  else flow_body<false>(d, L);
+  if ((int)blockIdx.x + col0 == d.n) flow_body<true>(d, L, col0);
+  else flow_body<false>(d, L, col0);
+}
+
+// ---------------------------------------------------------------------------
+// k_flow32: the same dataflow with ONE-dword ring slots, for chains shorter
+// than F2_MAXLEN (2^17 - 128) and Lamport timestamps below 2^21.
+//   slot       = generation (k / 64, 11 bits) << 21 | value + 1 (21 bits)
+//   descriptor = generation << 21 | LDS byte address of the slot
+// A parent is ready when (slot ^ descriptor) < 2^21: one XOR and one
+// compare, and a dword cannot be read torn.  Each descriptor-ring entry
+// carries the next event's other-parent descriptor AND the current event's
+// own slot descriptor (entry k + 1 = {op(k + 1), own(k)}), both prepared by
+// k_flow_desc32, so a step spends no instructions encoding its write: 17
+// VALU per step against 21 for k_flow (a lone wave issues one VALU per 8
+// cycles on gfx950, tools/micro/lat.hip).  LT values that would reach 2^21
+// are clamped (the generation bits stay intact, every lane keeps making
+// progress) and flagged in ST_FLOWOVF; the host then recomputes LT with
+// k_flow (LT workgroup only).
+constexpr int F2_DR = 64;                   // descriptor-ring entries (int2) per chain
+constexpr uint32_t F2_VMASK = 0x1FFFFFu;    // value bits
+constexpr uint32_t F2_GMASK = 0xFFE00000u;  // generation bits
+constexpr uint32_t F2_GNOOP = 0x7FF, F2_GWAIT = 0x7FE, F2_GINIT = 0x7FF;
+constexpr int32_t F2_MAXLEN = 0x7FE * 64;   // generations of real events stay <= 0x7FD
+constexpr int32_t F2_LTCLAMP = (1 << 21) - 256;
+
+__host__ __device__ constexpr uint32_t f2_desc(int32_t dch, int32_t j) {
+  return ((uint32_t)(j >> 6) << 21) | (uint32_t)(dch * 256 + (j & 63) * 4);
+}
+// sentinel row n: slot 63 = "no other-parent" (value -1), slot 62 never matches
+__host__ __device__ constexpr uint32_t f2_noop(int n) { return (F2_GNOOP << 21) | (uint32_t)(n * 256 + 63 * 4); }
+__host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 21) | (uint32_t)(n * 256 + 62 * 4); }
+
+// opw[row] = {descriptor of the row's other-parent, own slot of the row
+// before it}; the .y of a chain's first row holds the previous chain's last
+// own slot (the chain reads it as entry len)
+__global__ void k_flow_desc32(Dev d) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  int2 *opw = reinterpret_cast<int2 *>(d.opdesc);
+  const int32_t o = d.op[e], p = d.epos[e];
+  opw[p].x = (int32_t)(o < 0 ? f2_noop(d.n) : f2_desc(d.creator[o], d.index[o]));
+  opw[p + 1].y = (int32_t)f2_desc(d.creator[e], d.index[e]);
+}
+
+struct FlowLds32 {
+  uint32_t vring[FL_MAXN + 1][64];  // 33 KiB, LDS offset 0
+  int2 dring[FL_MAXN][F2_DR];       // 64 KiB
+  int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN], stored[FL_MAXN];
+};
+
+template <bool LT>
+__device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = d.n;
+  const int nw = (n + 63) >> 6;
+  const int col = blockIdx.x;
+  const int64_t stride = d.la_rows + 64;
+  int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
+  for (int c = t; c < n; c += blockDim.x) {
+    L.filled[c] = 0;
+    L.consumed[c] = 0;
+    L.pub[c] = 0;
+    L.stored[c] = 0;
+    L.cs[c] = d.chain_start[c];
+    for (int s = 0; s < 64; ++s) L.vring[c][s] = F2_GINIT << 21;  // matches no real event
+  }
+  if (t < 64) L.vring[n][t] = t == 63 ? (F2_GNOOP << 21) : 0u;
+  __syncthreads();
+  lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub,
+           *stored = (lds_vint *)L.stored;
+  const int2 *opw = reinterpret_cast<const int2 *>(d.opdesc);
+
+  if (wave == nw) {
+    // ---------------- prefetch wave: descriptor rings, 32 entries per DMA ----------------
+    int32_t f[2] = {0, 0}, tot[2], cs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane + 64 * h;
+      const int32_t len = c < n ? d.chain_len[c] : 0;
+      tot[h] = len > 0 ? len + 1 : 0;  // entry len carries the last event's own slot
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (;;) {
+      bool left = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        const int32_t cons = c < n ? consumed[c] : 0;
+        const bool need = f[h] < tot[h] && f[h] - cons <= F2_DR - 32;
+        left |= f[h] < tot[h];
+        unsigned long long m = __ballot(need);
+        while (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          const int cc = b + 64 * h;
+          const int32_t fc = __builtin_amdgcn_readlane(f[h], b);
+          const int32_t csc = __builtin_amdgcn_readlane(cs[h], b);
+          __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const int32_t *>(opw + csc + fc) + lane),
+                                           (lds_void_t *)&L.dring[cc][fc & (F2_DR - 1)], 4, 0, 0);
+        }
+        if (need) f[h] += 32;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        if (c < n) filled[c] = min(f[h], tot[h]);
+      }
+      if (!__any(left)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return;
+  }
+  if (wave == nw + 1) {
+    // ---------------- store wave: rings -> HBM ----------------
+    int32_t sp[2] = {0, 0}, len[2], cs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane + 64 * h;
+      len[h] = c < n ? d.chain_len[c] : 0;
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (int pass = 1;; ++pass) {
+      bool left = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = min(lane + 64 * h, n);
+        for (int it = 0; it < 8; ++it) {
+          const uint32_t v = L.vring[c][sp[h] & 63];
+          const bool ok = sp[h] < len[h] && (v ^ ((uint32_t)(sp[h] >> 6) << 21)) < (1u << 21);
+          if (!__any(ok)) break;
+          if (ok) {
+            out[cs[h] + sp[h]] = (int32_t)(v & F2_VMASK) - 1;
+            ++sp[h];
+          }
+        }
+        left |= sp[h] < len[h];
+        if (lane + 64 * h < n) stored[lane + 64 * h] = sp[h];
+      }
+      if ((pass & 7) == 0 || !__any(left)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (lane + 64 * h < n) pub[lane + 64 * h] = sp[h];
+      }
+      if (!__any(left)) break;
+    }
+    return;
+  }
+  if (wave > nw + 1) return;
+
+  // ---------------- compute waves: one chain per lane ----------------
+  const int c = wave * 64 + lane;
+  const bool valid = c < n;
+  const int32_t len = valid ? d.chain_len[c] : 0;
+  const int cc = valid ? c : 0;
+  const int32_t inc = LT ? 1 : (c == col ? 1 : 0);  // LT + 1; LA[e][creator] = index
+  const uint32_t wscratch = (uint32_t)((n * 64 + lane % 61) * 4);
+  const uint32_t WAIT = f2_wait(n);
+  char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
+  const int2 *dring_c = &L.dring[cc][0];
+  int32_t k = 0, cur = 0, lim = 0;  // cur: value of event k-1 + 1
+  uint32_t dsc = WAIT;
+  const int32_t ltclamp = min(d.flow_ltclamp, F2_LTCLAMP);
+  const bool dg = d.diag != nullptr && col == 0 && wave == 0;
+  const unsigned long long t_start = dg ? stamp() : 0;
+  int32_t step = 0;
+#define F2_STEP()                                                                   \
+  do {                                                                              \
+    const uint32_t slot_ = *reinterpret_cast<const uint32_t *>(lds + (dsc & 0xFFFFu)); \
+    const int32_t kn_ = k + 1;                                                      \
+    const int2 e_ = dring_c[kn_ & (F2_DR - 1)];                                     \
+    const bool ready_ = (slot_ ^ dsc) < (1u << 21);                                 \
+    const int32_t v_ = max(cur, (int32_t)(slot_ & F2_VMASK)) + inc;                 \
+    const uint32_t wa_ = ready_ ? ((uint32_t)e_.y & 0xFFFFu) : wscratch;            \
+    *reinterpret_cast<uint32_t *>(lds + wa_) = ((uint32_t)e_.y & F2_GMASK) | (uint32_t)v_; \
+    cur = ready_ ? v_ : cur;                                                        \
+    dsc = ready_ ? (kn_ < lim ? (uint32_t)e_.x : WAIT) : dsc;                       \
+    k = ready_ ? kn_ : k;                                                           \
+  } while (0)
+  for (;; step += 8) {
+    // header: limits (entry k + 1 must be loaded: it holds k's own slot),
+    // stalled descriptors, LT clamp, read-backs, exit
+    lim = valid ? min(filled[cc] - 1, stored[cc] + 48) : 0;
+    if (dsc == WAIT && k < lim) dsc = (uint32_t)dring_c[k & (F2_DR - 1)].x;
+    if (valid) consumed[c] = k;
+    if (LT && __builtin_expect(__any(cur > ltclamp), 0)) {
+      if (cur > ltclamp) {
+        cur = ltclamp;
+        d.state[ST_FLOWOVF] = 1;
+      }
+    }
+    if (!__any(k < len)) break;
+    {
+      const uint32_t sa = dsc & 0xFFFFu;
+      const uint32_t slot = *reinterpret_cast<const uint32_t *>(lds + sa);
+      const int32_t dd = (int32_t)(sa >> 8), jj = (int32_t)((dsc >> 21) << 6) | (int32_t)((sa >> 2) & 63);
+      const bool far = (slot & F2_GMASK) > (dsc & F2_GMASK) && pub[dd] > jj;
+      if (__builtin_expect(__any(far), 0)) {
+        if (far) {
+          const int32_t *fp = out + L.cs[dd] + jj;
+          int32_t val;
+          asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
+          const int32_t v = max(cur, val + 1) + inc;
+          const uint32_t wd = (uint32_t)dring_c[(k + 1) & (F2_DR - 1)].y;
+          *reinterpret_cast<uint32_t *>(lds + (wd & 0xFFFFu)) = (wd & F2_GMASK) | (uint32_t)v;
+          cur = v;
+          ++k;
+          dsc = k < lim ? (uint32_t)dring_c[k & (F2_DR - 1)].x : WAIT;
+        }
+      }
+    }
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+  }
+#undef F2_STEP
+  if (valid) consumed[c] = len;
+  if (dg && lane == 0) {
+    d.diag[DG_FL_STEPS] = step;
+    d.diag[DG_FL_CYC] = stamp() - t_start;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_flow32(Dev d) {
+  __shared__ FlowLds32 L;  // static: the ring's LDS base is the constant 0
+  if ((int)blockIdx.x == d.n) flow32_body<true>(d, L);
+  else flow32_body<false>(d, L);
 }
 
 // column-major LA (chain-major rows) -> row-major LA; LT rows -> event
@@ -400,15 +629,34 @@ bool flow_eligible(const Dev &d) {
   return d.n <= FL_MAXN && d.max_chain_len < (1 << 21) && d.N < (1 << 24) - 1;
 }
 
+// one-dword slots: chains short enough for 11-bit generations
+// (BH_SWEEP=flow64 forces the two-dword kernel)
+bool flow32_eligible(const Dev &d) {
+  const char *e = getenv("BH_SWEEP");
+  return flow_eligible(d) && d.max_chain_len <= F2_MAXLEN && !(e && !strcmp(e, "flow64"));
+}
+
 void launch_flow_desc(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
-  k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
+  if (flow32_eligible(d)) k_flow_desc32<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
+  else k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
 }
 
 void launch_flow(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
-  k_flow<<<d.n + 1, (nw + 2) * 64, 0, s>>>(d);
+  if (flow32_eligible(d)) k_flow32<<<d.n + 1, (nw + 2) * 64, 0, s>>>(d);
+  else k_flow<<<d.n + 1, (nw + 2) * 64, 0, s>>>(d, 0);
+}
+
+// LT overflowed k_flow32's 21-bit values (ST_FLOWOVF): recompute LT with
+// the two-dword kernel's LT workgroup alone, then the rows' timestamps
+void launch_flow_lt_fallback(const Dev &d, hipStream_t s) {
+  if (d.N == 0) return;
+  const int nw = (d.n + 63) / 64;
+  k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
+  k_flow<<<1, (nw + 2) * 64, 0, s>>>(d, d.n);
+  launch_flow_transpose(d, s);
 }
 
 void launch_flow_transpose(const Dev &d, hipStream_t s) {

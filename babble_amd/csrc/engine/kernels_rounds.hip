@@ -370,6 +370,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   const bool dg = d.diag != nullptr && t == 0;
   const unsigned long long ts0 = dg ? stamp() : 0;
+  const unsigned long long rt0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
   // ---- independent loads ----
   const int done = d.state[ST_DONE];
   const int r = d.state[ST_CUR0 + p];
@@ -447,6 +448,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
   const int nc = cntk[0];
   const unsigned long long ts2 = dg ? stamp() : 0;
+  const unsigned long long rt2 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
   int32_t result = len;
   if (res >= 0) {
     result = k0 + res;
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     __syncthreads();
   }
   // ---- hand-off for the next iteration ----
+  unsigned long long rthb = 0;
   if (nc > 0 && r + 1 < d.R_cap && result < len) {
     const int32_t off = result - k0;
     int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + ((int64_t)(p ^ 1) * n + c) * nwq;
@@ -487,6 +490,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       if (t < rows2 * q4) win[nwq + t] = xv;
       if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
       __syncthreads();
+      if (dg) rthb = __builtin_amdgcn_s_memrealtime();
       if (t < nwq) nw[t] = win[off * q4 + t];
       if (t < npad) cf[t] = t < n ? fdw[t * FDS + frel] : FD_NONE;
     } else {
@@ -498,6 +502,12 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
   if (dg) {
     const unsigned long long te = stamp();
+    if (r >= TL_R0 && r < TL_R0 + TL_NR && c < 128) {
+      unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
+      const unsigned long long fl = (unsigned long long)(min(result - k0, 255) & 255) |
+                                    (unsigned long long)(res < 0) << 8 | (unsigned long long)(nc > 0) << 9;
+      tl[0] = rt0 | fl << 52; tl[1] = rt2; tl[2] = rthb; tl[3] = __builtin_amdgcn_s_memrealtime();
+    }
     atomicAdd(&d.diag[DG_RD_B], ts1 - ts0);
     atomicAdd(&d.diag[DG_RD_LOAD], 0ull);
     atomicAdd(&d.diag[DG_RD_COMP], ts2 - ts1);

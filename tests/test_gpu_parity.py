@@ -318,3 +318,21 @@ def test_coordinates_random(monkeypatch, sweep, n, N, seed, lag):
         assert np.array_equal(fd_r, fd_g), (e, fd_r, fd_g)
         nmax += int((np.asarray(fd_r) == 2**31 - 1).sum())
     assert nmax > 0  # the unseen tails were exercised
+
+
+def test_flow32_lt_fallback(monkeypatch):
+    """k_flow32 carries values in 21 bits; Lamport timestamps beyond its
+    limit are flagged and recomputed by the two-dword kernel.  A lowered
+    limit (BH_FLOW_LTCLAMP, read at handle creation) forces that path on a
+    DAG whose timestamps exceed it."""
+    monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
+    hg = _random_parity(16, 20_000, 71, 2)
+    assert hg.results()["lamport"].max() > 300
+
+
+def test_flow64_parity(monkeypatch):
+    """The two-dword dataflow kernel (chains of 2^17 .. 2^21 events) forced
+    on DAGs the one-dword kernel would take."""
+    monkeypatch.setenv("BH_SWEEP", "flow64")
+    _random_parity(128, 40_000, 72, 0)
+    _wild_parity(24, 30_000, 73, 20_000)
