@@ -97,7 +97,7 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.nextwin, d.candfd, d.opdesc, d.lt_row, d.fdarch, d.wfrow,
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.fdarch, d.wfrow,
                   d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -408,7 +408,6 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   if (d.fd_cols) A(&d.fdarch, R1 * n * d.npad);
   else A(&d.fd, (size_t)(C + 64) * d.npad);
   A(&d.last_la, (size_t)(n + 1) * d.npad);
-  A(&d.nextwin, (size_t)2 * n * 32 * d.npad);
   A(&d.candfd, (size_t)2 * n * d.npad);
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);

@@ -92,7 +92,6 @@ struct Dev {
   int32_t *last_la; // [n][npad] LA row of each chain's last event
   int32_t max_chain_len;
   // round-loop hand-off (k_round2, npad <= 128), by round parity
-  int32_t *nextwin;  // [2][n][32][npad] LA rows B[r][c] .. +32 of each chain
   int32_t *candfd;   // [2][n][npad] FD row of each chain's candidate (c, B[r][c])
   int32_t *state;
   int32_t *round;

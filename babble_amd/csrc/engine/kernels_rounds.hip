@@ -320,17 +320,17 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
 //   * candfd[p][q]  -- the firstDescendants row of candidate q, written by
 //                      workgroup q of the previous iteration (it knew its new
 //                      boundary B[r][q] and had that row in LDS);
-//   * nextwin[p][c] -- LA rows B[r][c] .. +32 of chain c, likewise handed over.
+//   * LA rows B[r][c] .. +32 of chain c -- read straight from la: the
+//     previous iteration's window covered them, so they come from L2 / MALL.
 // 1024 threads: LPC lanes per candidate, 4 x 16-B pieces of its FD row per
 // lane in registers.  The search is over ROWS, for all candidates at once:
 // count(k) = #{q : window row k strongly sees q} is monotone in k, and
 // B[r+1][c] = the first k with count(k) >= SM.  A probe reads one window row
 // (every lane group reads the same 128 B per instruction: an LDS broadcast),
 // compares 16 columns per lane, sums over the group with DPP, and counts the
-// groups that reach SM with a ballot.  While the search runs, the rows the
-// next iteration will need (LA rows up to B[r][c]+64, FD rows of the window)
-// are loaded; afterwards the workgroup hands over candfd/nextwin for the new
-// boundary.  Windows that do not reach SM fall back to direct loads.
+// groups that reach SM with a ballot.  While the search runs, the FD rows of
+// the window are loaded; afterwards the workgroup hands over candfd for the
+// new boundary.  Windows that do not reach SM fall back to direct loads.
 constexpr int HW = 32;  // rows handed over per chain
 
 template <int LPC>
@@ -346,10 +346,7 @@ __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
   const int c = blockIdx.x, q4 = d.npad / 4;
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
   if (len == 0) return;
-  const int rows = min(HW, len);
-  const int4 *la = reinterpret_cast<const int4 *>(d.la + (int64_t)cs * d.npad);
-  int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + (int64_t)c * HW * q4;
-  for (int i = threadIdx.x; i < rows * q4; i += blockDim.x) nw[i] = la[i];
+  (void)q4;
   // candidate (c, 0): its FD row gathered from the FDT columns
   int32_t *cf = d.candfd + (int64_t)c * d.npad;
   for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs, i, d.npad)] : FD_NONE;
@@ -364,8 +361,8 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int nwq = HW * q4;  // int4 per handed-over window (<= 1024)
-  int4 *win = sm4;              // [2 * HW][q4]: rows k0 .. k0 + 63
-  int32_t *fdw = reinterpret_cast<int32_t *>(sm4 + 2 * nwq);  // [npad][FDS]: FD rows rb .. rb + 31 by column
+  int4 *win = sm4;              // [HW][q4]: LA rows k0 .. k0 + 31
+  int32_t *fdw = reinterpret_cast<int32_t *>(sm4 + nwq);  // [npad][FDS]: FD rows rb .. rb + 31 by column
   constexpr int FDS = HW + 4;
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   const bool dg = d.diag != nullptr && t == 0;
@@ -388,7 +385,8 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
     }
   }
-  const int4 wv = reinterpret_cast<const int4 *>(d.nextwin)[((int64_t)p * n + c) * nwq + min(t, nwq - 1)];
+  const int rows = min(HW, max(0, len - k0));
+  const int4 wv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
   if (done) return;
   const bool act = q < n && bq < lq;
   // archive this round's candidate FD row of chain c for fame (the group
@@ -399,17 +397,14 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     for (int u = 0; u < PPL; ++u)
       if (part + LPC * u < q4) fa[part + LPC * u] = f[u];
   }
-  const int rows = min(HW, max(0, len - k0));
   // ---- loads for the hand-off (consumed after the search) ----
-  const int rows2 = min(HW, max(0, len - k0 - HW));
-  const int4 xv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0 + HW) * q4 + min(t, max(rows2 * q4 - 1, 0))];
   // FD rows rb .. rb + 31 (rb = the window's first row rounded down to 4)
   // from the FDT tiles: 16 B = 4 rows of one column per thread, 8 threads
   // per column
   const int64_t rb = (int64_t)(cs + k0) & ~(int64_t)3;
   const int fi = min(t >> 3, n - 1), fp = (t & 7) * 4;
   const int4 fv = *reinterpret_cast<const int4 *>(d.fdt + fdt_pos(rb + fp, fi, npad));
-  if (t < nwq) win[t] = wv;
+  if (t < rows * q4) win[t] = wv;
   if (t < 16) cntk[t] = 0;
   __syncthreads();
   const unsigned long long ts1 = dg ? stamp() : 0;
@@ -483,20 +478,14 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   unsigned long long rthb = 0;
   if (nc > 0 && r + 1 < d.R_cap && result < len) {
     const int32_t off = result - k0;
-    int4 *nw = reinterpret_cast<int4 *>(d.nextwin) + ((int64_t)(p ^ 1) * n + c) * nwq;
     int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
     const int frel = (int)(cs + result - rb);  // row of the candidate in fdw
     if (off < HW && frel < HW) {  // both from the rows staged during the search
-      if (t < rows2 * q4) win[nwq + t] = xv;
       if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
       __syncthreads();
       if (dg) rthb = __builtin_amdgcn_s_memrealtime();
-      if (t < nwq) nw[t] = win[off * q4 + t];
       if (t < npad) cf[t] = t < n ? fdw[t * FDS + frel] : FD_NONE;
     } else {
-      const int4 *la = reinterpret_cast<const int4 *>(d.la) + (int64_t)(cs + result) * q4;
-      const int nr = min(HW, len - result);
-      if (t < nr * q4) nw[t] = la[t];
       if (t < npad) cf[t] = t < n ? d.fdt[fdt_pos(cs + result, t, npad)] : FD_NONE;
     }
   }
@@ -507,12 +496,15 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       const unsigned long long fl = (unsigned long long)(min(result - k0, 255) & 255) |
                                     (unsigned long long)(res < 0) << 8 | (unsigned long long)(nc > 0) << 9;
       tl[0] = rt0 | fl << 52; tl[1] = rt2; tl[2] = rthb; tl[3] = __builtin_amdgcn_s_memrealtime();
+    } else if (r < TL_R0 - 64 || r >= TL_R0 + TL_NR + 64) {
+      // phase counters (device-scope atomics from every workgroup: they
+      // stretch the round by several us, so none near the timeline window)
+      atomicAdd(&d.diag[DG_RD_B], ts1 - ts0);
+      atomicAdd(&d.diag[DG_RD_LOAD], 0ull);
+      atomicAdd(&d.diag[DG_RD_COMP], ts2 - ts1);
+      atomicAdd(&d.diag[DG_RD_TOTAL], te - ts0);
+      atomicAdd(&d.diag[DG_RD_CALLS], 1ull);
     }
-    atomicAdd(&d.diag[DG_RD_B], ts1 - ts0);
-    atomicAdd(&d.diag[DG_RD_LOAD], 0ull);
-    atomicAdd(&d.diag[DG_RD_COMP], ts2 - ts1);
-    atomicAdd(&d.diag[DG_RD_TOTAL], te - ts0);
-    atomicAdd(&d.diag[DG_RD_CALLS], 1ull);
   }
   if (t == 0) {
     if (nc == 0) {  // no candidates: R = r
@@ -556,7 +548,7 @@ void configure_round_kernels() {
 // iteration parity p = round & 1 (ITER_BATCH is even, rounds start at 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
-    const size_t lds = (size_t)2 * HW * (d.npad / 4) * 16 + (size_t)d.npad * (HW + 4) * 4;
+    const size_t lds = (size_t)HW * (d.npad / 4) * 16 + (size_t)d.npad * (HW + 4) * 4;
     if (d.npad <= 64) k_round2<4><<<d.n, 1024, lds, s>>>(d, p);
     else k_round2<8><<<d.n, 1024, lds, s>>>(d, p);
     return;
