@@ -424,20 +424,28 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   int slot = 1;
   int32_t res = -1;  // window row of B[r+1][c], or -1
   if (rows > 0) {
-    probe(win + (rows - 1) * q4, slot);
-    __syncthreads();
-    if (cntk[slot] >= sm) {
-      int lo = 0, hi = rows - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        ++slot;
-        probe(win + mid * q4, slot);
-        __syncthreads();
-        if (cntk[slot] >= sm) hi = mid;
-        else lo = mid + 1;
+    // binary search assuming the window's last row reaches SM (count is
+    // monotone); that row is probed only if the search ends on it unverified
+    int lo = 0, hi = rows - 1;
+    bool hi_ok = false;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      probe(win + mid * q4, slot);
+      __syncthreads();
+      if (cntk[slot] >= sm) {
+        hi = mid;
+        hi_ok = true;
+      } else {
+        lo = mid + 1;
       }
-      res = lo;
+      ++slot;
     }
+    if (!hi_ok) {
+      probe(win + hi * q4, slot);
+      __syncthreads();
+      hi_ok = cntk[slot] >= sm;
+    }
+    if (hi_ok) res = lo;
   } else {
     __syncthreads();
   }
