@@ -452,7 +452,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
     dsc = ready_ ? (kn_ < lim ? (uint32_t)e_.x : WAIT) : dsc;                       \
     k = ready_ ? kn_ : k;                                                           \
   } while (0)
-  for (;; step += 16) {
+  for (;; step += 32) {
     // header: limits (entry k + 1 must be loaded: it holds k's own slot),
     // stalled descriptors, LT clamp, read-backs, exit
     lim = valid ? min(filled[cc] - 1, stored[cc] + 48) : 0;
@@ -484,6 +484,10 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
         }
       }
     }
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
     F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
     F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
     F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
