@@ -277,8 +277,9 @@ __global__ __launch_bounds__(256) void k_flow(Dev d, int col0) {
 
 // ---------------------------------------------------------------------------
 // k_flow32: the same dataflow with ONE-dword ring slots, for chains shorter
-// than F2_MAXLEN (2^17 - 128) and Lamport timestamps below 2^21.
-//   slot       = generation (k / 64, 11 bits) << 21 | value + 1 (21 bits)
+// than F2_MAXLEN (2^18 - 256) and Lamport timestamps below 2^21.  Rings hold
+// 128 events per chain (66 KiB).
+//   slot       = generation (k / 128, 11 bits) << 21 | value + 1 (21 bits)
 //   descriptor = generation << 21 | LDS byte address of the slot
 // A parent is ready when (slot ^ descriptor) < 2^21: one XOR and one
 // compare, and a dword cannot be read torn.  Each descriptor-ring entry
@@ -294,15 +295,16 @@ constexpr int F2_DR = 64;                   // descriptor-ring entries (int2) pe
 constexpr uint32_t F2_VMASK = 0x1FFFFFu;    // value bits
 constexpr uint32_t F2_GMASK = 0xFFE00000u;  // generation bits
 constexpr uint32_t F2_GNOOP = 0x7FF, F2_GWAIT = 0x7FE, F2_GINIT = 0x7FF;
-constexpr int32_t F2_MAXLEN = 0x7FE * 64;   // generations of real events stay <= 0x7FD
+constexpr int F2_R = 128;                   // value-ring slots per chain
+constexpr int32_t F2_MAXLEN = 0x7FE * F2_R;  // generations of real events stay <= 0x7FD
 constexpr int32_t F2_LTCLAMP = (1 << 21) - 256;
 
 __host__ __device__ constexpr uint32_t f2_desc(int32_t dch, int32_t j) {
-  return ((uint32_t)(j >> 6) << 21) | (uint32_t)(dch * 256 + (j & 63) * 4);
+  return ((uint32_t)(j >> 7) << 21) | (uint32_t)(dch * F2_R * 4 + (j & (F2_R - 1)) * 4);
 }
-// sentinel row n: slot 63 = "no other-parent" (value -1), slot 62 never matches
-__host__ __device__ constexpr uint32_t f2_noop(int n) { return (F2_GNOOP << 21) | (uint32_t)(n * 256 + 63 * 4); }
-__host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 21) | (uint32_t)(n * 256 + 62 * 4); }
+// sentinel row n: slot R-1 = "no other-parent" (value -1), slot R-2 never matches
+__host__ __device__ constexpr uint32_t f2_noop(int n) { return (F2_GNOOP << 21) | (uint32_t)((n * F2_R + F2_R - 1) * 4); }
+__host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 21) | (uint32_t)((n * F2_R + F2_R - 2) * 4); }
 
 // opw[row] = {descriptor of the row's other-parent, own slot of the row
 // before it}; the .y of a chain's first row holds the previous chain's last
@@ -317,7 +319,7 @@ __global__ void k_flow_desc32(Dev d) {
 }
 
 struct FlowLds32 {
-  uint32_t vring[FL_MAXN + 1][64];  // 33 KiB, LDS offset 0
+  uint32_t vring[FL_MAXN + 1][F2_R];  // 66 KiB, LDS offset 0
   int2 dring[FL_MAXN][F2_DR];       // 64 KiB
   int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN], stored[FL_MAXN];
 };
@@ -336,9 +338,9 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
     L.pub[c] = 0;
     L.stored[c] = 0;
     L.cs[c] = d.chain_start[c];
-    for (int s = 0; s < 64; ++s) L.vring[c][s] = F2_GINIT << 21;  // matches no real event
+    for (int s = 0; s < F2_R; ++s) L.vring[c][s] = F2_GINIT << 21;  // matches no real event
   }
-  if (t < 64) L.vring[n][t] = t == 63 ? (F2_GNOOP << 21) : 0u;
+  for (int s = t; s < F2_R; s += blockDim.x) L.vring[n][s] = s == F2_R - 1 ? (F2_GNOOP << 21) : 0u;
   __syncthreads();
   lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub,
            *stored = (lds_vint *)L.stored;
@@ -400,8 +402,8 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
       for (int h = 0; h < 2; ++h) {
         const int c = min(lane + 64 * h, n);
         for (int it = 0; it < 8; ++it) {
-          const uint32_t v = L.vring[c][sp[h] & 63];
-          const bool ok = sp[h] < len[h] && (v ^ ((uint32_t)(sp[h] >> 6) << 21)) < (1u << 21);
+          const uint32_t v = L.vring[c][sp[h] & (F2_R - 1)];
+          const bool ok = sp[h] < len[h] && (v ^ ((uint32_t)(sp[h] >> 7) << 21)) < (1u << 21);
           if (!__any(ok)) break;
           if (ok) {
             out[cs[h] + sp[h]] = (int32_t)(v & F2_VMASK) - 1;
@@ -429,7 +431,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   const int32_t len = valid ? d.chain_len[c] : 0;
   const int cc = valid ? c : 0;
   const int32_t inc = LT ? 1 : (c == col ? 1 : 0);  // LT + 1; LA[e][creator] = index
-  const uint32_t wscratch = (uint32_t)((n * 64 + lane % 61) * 4);
+  const uint32_t wscratch = (uint32_t)((n * F2_R + lane) * 4);
   const uint32_t WAIT = f2_wait(n);
   char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
   const int2 *dring_c = &L.dring[cc][0];
@@ -441,12 +443,12 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   int32_t step = 0;
 #define F2_STEP()                                                                   \
   do {                                                                              \
-    const uint32_t slot_ = *reinterpret_cast<const uint32_t *>(lds + (dsc & 0xFFFFu)); \
+    const uint32_t slot_ = *reinterpret_cast<const uint32_t *>(lds + (dsc & 0x1FFFFu)); \
     const int32_t kn_ = k + 1;                                                      \
     const int2 e_ = dring_c[kn_ & (F2_DR - 1)];                                     \
     const bool ready_ = (slot_ ^ dsc) < (1u << 21);                                 \
     const int32_t v_ = max(cur, (int32_t)(slot_ & F2_VMASK)) + inc;                 \
-    const uint32_t wa_ = ready_ ? ((uint32_t)e_.y & 0xFFFFu) : wscratch;            \
+    const uint32_t wa_ = ready_ ? ((uint32_t)e_.y & 0x1FFFFu) : wscratch;           \
     *reinterpret_cast<uint32_t *>(lds + wa_) = ((uint32_t)e_.y & F2_GMASK) | (uint32_t)v_; \
     cur = ready_ ? v_ : cur;                                                        \
     dsc = ready_ ? (kn_ < lim ? (uint32_t)e_.x : WAIT) : dsc;                       \
@@ -455,7 +457,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   for (;; step += 32) {
     // header: limits (entry k + 1 must be loaded: it holds k's own slot),
     // stalled descriptors, LT clamp, read-backs, exit
-    lim = valid ? min(filled[cc] - 1, stored[cc] + 48) : 0;
+    lim = valid ? min(filled[cc] - 1, stored[cc] + F2_R - 16) : 0;
     if (dsc == WAIT && k < lim) dsc = (uint32_t)dring_c[k & (F2_DR - 1)].x;
     if (valid) consumed[c] = k;
     if (LT && __builtin_expect(__any(cur > ltclamp), 0)) {
@@ -466,9 +468,9 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
     }
     if (!__any(k < len)) break;
     {
-      const uint32_t sa = dsc & 0xFFFFu;
+      const uint32_t sa = dsc & 0x1FFFFu;
       const uint32_t slot = *reinterpret_cast<const uint32_t *>(lds + sa);
-      const int32_t dd = (int32_t)(sa >> 8), jj = (int32_t)((dsc >> 21) << 6) | (int32_t)((sa >> 2) & 63);
+      const int32_t dd = (int32_t)(sa >> 9), jj = (int32_t)((dsc >> 21) << 7) | (int32_t)((sa >> 2) & (F2_R - 1));
       const bool far = (slot & F2_GMASK) > (dsc & F2_GMASK) && pub[dd] > jj;
       if (__builtin_expect(__any(far), 0)) {
         if (far) {
@@ -477,7 +479,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
           asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
           const int32_t v = max(cur, val + 1) + inc;
           const uint32_t wd = (uint32_t)dring_c[(k + 1) & (F2_DR - 1)].y;
-          *reinterpret_cast<uint32_t *>(lds + (wd & 0xFFFFu)) = (wd & F2_GMASK) | (uint32_t)v;
+          *reinterpret_cast<uint32_t *>(lds + (wd & 0x1FFFFu)) = (wd & F2_GMASK) | (uint32_t)v;
           cur = v;
           ++k;
           dsc = k < lim ? (uint32_t)dring_c[k & (F2_DR - 1)].x : WAIT;
