@@ -296,15 +296,18 @@ constexpr uint32_t F2_VMASK = 0x1FFFFFu;    // value bits
 constexpr uint32_t F2_GMASK = 0xFFE00000u;  // generation bits
 constexpr uint32_t F2_GNOOP = 0x7FF, F2_GWAIT = 0x7FE, F2_GINIT = 0x7FF;
 constexpr int F2_R = 128;                   // value-ring slots per chain
+// ring rows padded by one slot / one entry: lanes polling rings of
+// different chains at similar indices hit different LDS banks
+constexpr int F2_RS = F2_R + 1, F2_DRS = F2_DR + 1;
 constexpr int32_t F2_MAXLEN = 0x7FE * F2_R;  // generations of real events stay <= 0x7FD
 constexpr int32_t F2_LTCLAMP = (1 << 21) - 256;
 
 __host__ __device__ constexpr uint32_t f2_desc(int32_t dch, int32_t j) {
-  return ((uint32_t)(j >> 7) << 21) | (uint32_t)(dch * F2_R * 4 + (j & (F2_R - 1)) * 4);
+  return ((uint32_t)(j >> 7) << 21) | (uint32_t)((dch * F2_RS + (j & (F2_R - 1))) * 4);
 }
 // sentinel row n: slot R-1 = "no other-parent" (value -1), slot R-2 never matches
-__host__ __device__ constexpr uint32_t f2_noop(int n) { return (F2_GNOOP << 21) | (uint32_t)((n * F2_R + F2_R - 1) * 4); }
-__host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 21) | (uint32_t)((n * F2_R + F2_R - 2) * 4); }
+__host__ __device__ constexpr uint32_t f2_noop(int n) { return (F2_GNOOP << 21) | (uint32_t)((n * F2_RS + F2_R - 1) * 4); }
+__host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 21) | (uint32_t)((n * F2_RS + F2_R - 2) * 4); }
 
 // opw[row] = {descriptor of the row's other-parent, own slot of the row
 // before it}; the .y of a chain's first row holds the previous chain's last
@@ -319,8 +322,8 @@ __global__ void k_flow_desc32(Dev d) {
 }
 
 struct FlowLds32 {
-  uint32_t vring[FL_MAXN + 1][F2_R];  // 66 KiB, LDS offset 0
-  int2 dring[FL_MAXN][F2_DR];       // 64 KiB
+  uint32_t vring[FL_MAXN + 1][F2_RS];  // 66 KiB, LDS offset 0
+  int2 dring[FL_MAXN][F2_DRS];        // 66 KiB
   int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN], stored[FL_MAXN];
 };
 
@@ -431,7 +434,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   const int32_t len = valid ? d.chain_len[c] : 0;
   const int cc = valid ? c : 0;
   const int32_t inc = LT ? 1 : (c == col ? 1 : 0);  // LT + 1; LA[e][creator] = index
-  const uint32_t wscratch = (uint32_t)((n * F2_R + lane) * 4);
+  const uint32_t wscratch = (uint32_t)((n * F2_RS + lane) * 4);
   const uint32_t WAIT = f2_wait(n);
   char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
   const int2 *dring_c = &L.dring[cc][0];
@@ -470,7 +473,8 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
     {
       const uint32_t sa = dsc & 0x1FFFFu;
       const uint32_t slot = *reinterpret_cast<const uint32_t *>(lds + sa);
-      const int32_t dd = (int32_t)(sa >> 9), jj = (int32_t)((dsc >> 21) << 7) | (int32_t)((sa >> 2) & (F2_R - 1));
+      const int32_t si = (int32_t)(sa >> 2), dd = si / F2_RS;
+      const int32_t jj = (int32_t)((dsc >> 21) << 7) | (si - dd * F2_RS);
       const bool far = (slot & F2_GMASK) > (dsc & F2_GMASK) && pub[dd] > jj;
       if (__builtin_expect(__any(far), 0)) {
         if (far) {
