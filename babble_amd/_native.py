@@ -7,7 +7,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbabble_hip.so")
+# BH_LIB_PATH: an alternative build of the same library (A/B of kernel
+# variants in one GPU session); the in-tree build by default
+LIB_PATH = os.environ.get("BH_LIB_PATH") or os.path.join(_HERE, "libbabble_hip.so")
 
 BH_OK = 0
 ERRORS = {

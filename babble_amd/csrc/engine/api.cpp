@@ -97,7 +97,7 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.fdarch, d.wfrow,
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm,
                   d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -405,13 +405,17 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.opdesc, (size_t)2 * (C + 128));  // k_flow32: int2 entries
   A(&d.lt_row, (size_t)C + 64);
   d.fd_cols = d.npad <= 128;
-  if (d.fd_cols) A(&d.fdarch, R1 * n * d.npad);
-  else A(&d.fd, (size_t)(C + 64) * d.npad);
+  if (d.fd_cols) {
+    A(&d.ssm, R1 * n * 16);
+    d.round_lpc = d.npad <= 64 ? 4 : 8;
+  } else {
+    A(&d.fd, (size_t)(C + 64) * d.npad);
+  }
   A(&d.last_la, (size_t)(n + 1) * d.npad);
   A(&d.candfd, (size_t)2 * n * d.npad);
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
-  A(&d.wrow, (size_t)d.W_cap); A(&d.wfrow, (size_t)d.W_cap);
+  A(&d.wrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);

@@ -84,11 +84,13 @@ struct Dev {
   int32_t *fdt;     // walk output, tiled by 64 chain-major rows (fdt_pos; shares la_ev's allocation)
   // fd_cols (npad <= 128): FDT is complete (the walks write MaxInt32 where
   // no event of a chain sees a row) and is the only per-event FD table; the
-  // round loop reads windows of it, fame the FD rows of witnesses archived
-  // per round (fdarch[r][c] = FD row of candidate (c, B[r][c])); no fd
+  // round loop reads windows of it and hands fame its stronglySee results
+  // as ballots (ssm); no fd
   int32_t fd_cols;
-  int32_t *fdarch;  // [R_cap + 1][n][npad]
-  int32_t *wfrow;   // [W] row of each witness's FD: fdarch row (fd_cols) or fd row
+  // [n][R_cap + 1][16 waves] k_round2 ballots: lane (q * LPC) % 64 of wave
+  // q * LPC / 64 = candidate (c, B[r][c]) strongly sees (q, B[r-1][q])
+  unsigned long long *ssm;
+  int32_t round_lpc;  // LPC of k_round2 (4 or 8)
   int32_t *last_la; // [n][npad] LA row of each chain's last event
   int32_t max_chain_len;
   // round-loop hand-off (k_round2, npad <= 128), by round parity

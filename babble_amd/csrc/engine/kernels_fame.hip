@@ -63,9 +63,8 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   int32_t *dec = xk + n;   // 0 undecided, 1 famous, 2 not famous
   int32_t *nd = dec + n;   // decisions of the current j (bit0 yes, bit1 no)
   int32_t *rid = nd + n;   // [3][n] chain-major rows: W(r) (kept), then W(j-1) / W(j) alternating
-  int32_t *fid = rid + 3 * n;   // [3][n] FD rows of the same witnesses (wfrow)
-  int32_t *misc = fid + 3 * n;  // [0] undecided count, [1] error
-  const int32_t *fdrows = d.fd_cols ? d.fdarch : d.fd;
+  int32_t *misc = rid + 3 * n;  // [0] undecided count, [1] error
+  const int32_t *fdrows = d.fd;
   int32_t *ly = misc + 4;                      // LDS_ROWS: LA rows of W(j)
   int32_t *fw = ly + (LDS_ROWS ? n * rs : 0);  // LDS_ROWS: FD rows of W(j-1)
 
@@ -77,7 +76,6 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
     xk[i] = d.index[e];
     dec[i] = 0;
     rid[i] = d.wrow[xb + i];  // rows of W(r), for minLA at the end
-    fid[i] = d.wfrow[xb + i];
   }
   if (t == 0) { misc[0] = nx; misc[1] = 0; }
   __syncthreads();
@@ -86,10 +84,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   if (r + 1 < R) {
     // ---- j = r+1: vote = see(y, x) = LA[y][creator(x)] >= index(x) ----
     int32_t ny = d.wcnt[r + 1], yb = d.wofs[r + 1];
-    for (int i = t; i < ny; i += nt) {
-      rid[n + i] = d.wrow[yb + i];
-      fid[n + i] = d.wfrow[yb + i];
-    }
+    for (int i = t; i < ny; i += nt) rid[n + i] = d.wrow[yb + i];
     for (int i = t; i < nx * WW; i += nt) Vp[i] = 0ull;
     __syncthreads();
     if (LDS_ROWS) {
@@ -108,12 +103,8 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
       const int32_t nw = ny;  // W(j-1): rows rid[cur * n ..]
       ny = d.wcnt[j];
       yb = d.wofs[j];
-      int32_t *yr_ = rid + (3 - cur) * n;
-      const int32_t *wr_ = fid + cur * n;
-      for (int i = t; i < ny; i += nt) {
-        yr_[i] = d.wrow[yb + i];
-        fid[(3 - cur) * n + i] = d.wfrow[yb + i];
-      }
+      int32_t *wr_ = rid + cur * n, *yr_ = rid + (3 - cur) * n;
+      for (int i = t; i < ny; i += nt) yr_[i] = d.wrow[yb + i];
       for (int i = t; i < ny * WW; i += nt) S[i] = 0ull;
       for (int i = t; i < nx * WW; i += nt) Vc[i] = 0ull;
       for (int i = t; i < nx; i += nt) nd[i] = 0;
@@ -124,15 +115,18 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
       }
       __syncthreads();
       cur = 3 - cur;
-      // S_j: 8x8 (y, w) tiles per thread, count columns with LA[y] >= FD[w]
+      // S_j: 8x8 (y, w) tiles per thread, count columns with LA[y] >= FD[w].
+      // A tile's w rows are strided by tw (w = wt + b * tw), so the lanes of
+      // a wave (consecutive wt) read consecutive LDS rows: distinct banks;
+      // its y rows are shared by the wave (broadcast)
       const int ty = (ny + 7) >> 3, tw = (nw + 7) >> 3;
       for (int tile = t; tile < ty * tw; tile += nt) {
-        const int y0 = (tile / tw) * 8, w0 = (tile % tw) * 8;
+        const int y0 = (tile / tw) * 8, wt = tile % tw;
         const int32_t *yr[8];
         const int32_t *wr[8];
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
-          const int y = min(y0 + a, ny - 1), w = min(w0 + a, nw - 1);
+          const int y = min(y0 + a, ny - 1), w = min(wt + a * tw, nw - 1);
           if (LDS_ROWS) {
             yr[a] = ly + y * rs;
             wr[a] = fw + w * rs;
@@ -166,7 +160,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
           if (y >= ny) continue;
 #pragma unroll
           for (int b = 0; b < 8; ++b) {
-            const int w = w0 + b;
+            const int w = wt + b * tw;
             if (w < nw && cnt[a][b] >= sm) atomicOr(&S[y * WW + (w >> 6)], 1ull << (w & 63));
           }
         }
@@ -237,9 +231,185 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_fame_masks (n <= 128, the k_round2 path): DecideFame from the round
+// loop's results.  The stronglySee rows fame needs -- S_j[y] over W(j-1)
+// for y in W(j) -- are exactly what k_round2 evaluated when its search
+// verified y's row against the candidates of round j-1 (ssm); the first
+// votes see(y, x) for y in W(r+1) are LA[y][c(x)] >= k(x).  Sets are 128-bit
+// masks indexed by CHAIN (a round has at most one witness per chain), so
+// voting is AND + popcount: one workgroup per round r, thread (x, half)
+// owns the vote word of witness x over 64 chains of W(j).
+__device__ __forceinline__ uint32_t fame_wmask_word(const Dev &d, int j, int w) {
+  // word w of the W(j) chain mask: B[j][q] < len_q and B[j+1][q] > B[j][q]
+  uint32_t m = 0;
+  for (int b = 0; b < 32; ++b) {
+    const int q = w * 32 + b;
+    if (q >= d.n) break;
+    const int32_t b0 = d.B[(int64_t)j * d.n + q], b1 = d.B[(int64_t)(j + 1) * d.n + q];
+    if (b0 < d.chain_len[q] && b1 > b0) m |= 1u << b;
+  }
+  return m;
+}
+
+// the k_round2 ballots of (chain c, round j) packed into a 128-bit chain mask
+__device__ __forceinline__ uint32_t fame_ballot_word(const unsigned long long *b, int lpc, int w) {
+  uint32_t word = 0;
+  if (lpc == 8) {  // 8 candidates per wave: bits 0, 8, .., 56
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long m = b[w * 4 + k];
+      word |= (uint32_t)(((m & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56) << (8 * k);
+    }
+  } else {  // 16 per wave: bits 0, 4, .., 60
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      unsigned long long m = b[w * 2 + k] & 0x1111111111111111ull;
+      m = (m | (m >> 3)) & 0x0303030303030303ull;
+      m = (m | (m >> 6)) & 0x000F000F000F000Full;
+      m = (m | (m >> 12)) & 0x000000FF000000FFull;
+      m = (m | (m >> 24)) & 0xFFFFull;
+      word |= (uint32_t)m << (16 * k);
+    }
+  }
+  return word;
+}
+
+__global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R) {
+  __shared__ uint32_t V[2][128][4];  // votes: [cur][x chain][word over W(j-1) chains]
+  __shared__ uint32_t S[128][4];     // ssm rows of W(j), restricted to W(j-1)
+  __shared__ uint32_t wx[4], wp[4], wc[4];  // W(r), W(j-1), W(j)
+  __shared__ int32_t dec[128], nd[128], yev[128], xev[128], xk[128];
+  __shared__ int32_t misc[2];  // [0] undecided, [1] conflicting decisions
+  __shared__ int32_t frow[128];  // LA rows of famous witnesses
+  __shared__ int32_t nfam_s;
+  const int r = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+  const int n = d.n, npad = d.npad, sm = d.sm;
+  if (t < 4) wx[t] = fame_wmask_word(d, r, t);
+  for (int q = t; q < 128; q += nt) {
+    dec[q] = 0;
+    nd[q] = 0;
+    xev[q] = -1;
+    xk[q] = 0;
+    yev[q] = 0;  // j = r+1: LA row of y
+    if (q < n) {
+      const int32_t b0 = d.B[(int64_t)r * n + q];
+      if (b0 < d.chain_len[q]) xev[q] = d.chain_ids[d.chain_start[q] + b0];
+      xk[q] = b0;
+      if (r + 1 < R) yev[q] = d.chain_start[q] + min(d.B[(int64_t)(r + 1) * n + q], d.chain_len[q] - 1);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    misc[0] = __popc(wx[0]) + __popc(wx[1]) + __popc(wx[2]) + __popc(wx[3]);
+    misc[1] = 0;
+  }
+  const int x = t & 127, h = t >> 7;  // vote words 2h, 2h+1 of witness x
+  const bool isx = (wx[x >> 5] >> (x & 31)) & 1u;
+  int cur = 0;
+  if (r + 1 < R) {
+    // ---- j = r+1: vote(y, x) = see(y, x) ----
+    if (t < 4) wc[t] = fame_wmask_word(d, r + 1, t);
+    __syncthreads();
+    {
+      uint32_t v0 = 0, v1 = 0;
+      const int xc = min(x, n - 1);
+      for (int b = 0; b < 64; ++b) {
+        const int y = h * 64 + b;
+        if (y >= n || !((wc[y >> 5] >> (y & 31)) & 1u)) continue;
+        if (d.la[(int64_t)yev[y] * npad + xc] >= xk[xc]) {
+          if (b < 32) v0 |= 1u << b;
+          else v1 |= 1u << (b - 32);
+        }
+      }
+      V[0][x][2 * h] = v0;
+      V[0][x][2 * h + 1] = v1;
+    }
+    __syncthreads();
+    // ---- j >= r+2 ----
+    for (int j = r + 2; j < R; ++j) {
+      if (misc[0] == 0) break;
+      if (t < 4) {
+        wp[t] = wc[t];
+        wc[t] = fame_wmask_word(d, j, t);
+      }
+      __syncthreads();
+      for (int y = t; y < n; y += nt) {
+        const bool isy = (wc[y >> 5] >> (y & 31)) & 1u;
+        yev[y] = isy ? d.chain_ids[d.chain_start[y] + d.B[(int64_t)j * n + y]] : -1;
+        const unsigned long long *b = d.ssm + ((int64_t)y * (d.R_cap + 1) + j) * 16;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) S[y][w] = isy ? fame_ballot_word(b, d.round_lpc, w) & wp[w] : 0u;
+      }
+      __syncthreads();
+      const int diff = j - r;
+      const bool normal = (diff % n) != 0;
+      if (isx && !dec[x]) {
+        uint32_t v0 = 0, v1 = 0;
+        int decide = 0;
+        for (int b = 0; b < 64; ++b) {
+          const int y = h * 64 + b;
+          if (y >= n || !((wc[y >> 5] >> (y & 31)) & 1u)) continue;
+          int yays = 0, tot = 0;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            yays += __popc(S[y][w] & V[cur][x][w]);
+            tot += __popc(S[y][w]);
+          }
+          const int nays = tot - yays;
+          const bool v = yays >= nays;
+          const int tt = v ? yays : nays;
+          bool vote;
+          if (normal) {
+            if (tt >= sm) decide |= v ? 1 : 2;
+            vote = v;
+          } else {
+            vote = tt >= sm ? v : d.coin[yev[y]] != 0;
+          }
+          if (vote) {
+            if (b < 32) v0 |= 1u << b;
+            else v1 |= 1u << (b - 32);
+          }
+        }
+        V[cur ^ 1][x][2 * h] = v0;
+        V[cur ^ 1][x][2 * h + 1] = v1;
+        if (decide) atomicOr(&nd[x], decide);
+      }
+      __syncthreads();
+      if (t < 128 && isx && dec[x] == 0 && nd[x]) {
+        if (nd[x] == 3) misc[1] = 1;  // conflicting decisions: impossible without forks
+        dec[x] = nd[x] == 1 ? 1 : 2;
+        atomicSub(&misc[0], 1);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  // ---- publish ----
+  __syncthreads();
+  if (t < 128 && isx) d.fame[xev[x]] = (int8_t)dec[x];
+  if (t == 0) {
+    d.decided[r] = misc[0] == 0 ? 1 : 0;
+    if (misc[1]) d.state[ST_ERR] = 2;
+    int m = 0;
+    for (int q = 0; q < n; ++q)
+      if (((wx[q >> 5] >> (q & 31)) & 1u) && dec[q] == 1) frow[m++] = d.chain_start[q] + d.B[(int64_t)r * n + q];
+    nfam_s = m;
+  }
+  __syncthreads();
+  // famous count and min LA over famous witnesses (roundReceived)
+  const int nf = nfam_s;
+  for (int c = t; c < npad; c += nt) {
+    int32_t m = INT32_MAX;
+    for (int i = 0; i < nf; ++i) m = min(m, d.la[(int64_t)frow[i] * npad + c]);
+    d.minla[(int64_t)r * npad + c] = m;
+    if (c == 0) d.nfam[r] = nf;
+  }
+}
+
 size_t fame_lds_bytes(int n, int npad, bool lds_rows) {
   const int WW = (n + 63) >> 6;
-  size_t b = (size_t)3 * n * WW * 8 + (size_t)11 * n * 4 + 16;
+  size_t b = (size_t)3 * n * WW * 8 + (size_t)8 * n * 4 + 16;
   if (lds_rows) b += (size_t)2 * n * (npad + 4) * 4;
   return b;
 }
@@ -253,6 +423,10 @@ void configure_fame_kernels() {
 
 void launch_fame(const Dev &d, int32_t R, hipStream_t s) {
   if (R <= 0) return;
+  if (d.fd_cols) {  // masks from the k_round2 loop
+    k_fame_masks<<<R, 256, 0, s>>>(d, R);
+    return;
+  }
   const bool lds = d.n <= FAME_MAXN;
   const size_t bytes = fame_lds_bytes(d.n, d.npad, lds);
   if (lds)

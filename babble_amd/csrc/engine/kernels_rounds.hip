@@ -357,7 +357,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   constexpr int PPL = 4;  // pieces per lane: LPC * PPL >= npad / 4
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
   __shared__ int32_t cntk[16];
-  const int t = threadIdx.x, lane = t & 63;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int nwq = HW * q4;  // int4 per handed-over window (<= 1024)
@@ -389,14 +389,6 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int4 wv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
   if (done) return;
   const bool act = q < n && bq < lq;
-  // archive this round's candidate FD row of chain c for fame (the group
-  // of chain c holds it in registers; the stores drain during the search)
-  if (q == c && act && r < d.R_cap) {
-    int4 *fa = reinterpret_cast<int4 *>(d.fdarch) + ((int64_t)r * n + c) * q4;
-#pragma unroll
-    for (int u = 0; u < PPL; ++u)
-      if (part + LPC * u < q4) fa[part + LPC * u] = f[u];
-  }
   // ---- loads for the hand-off (consumed after the search) ----
   // FD rows rb .. rb + 31 (rb = the window's first row rounded down to 4)
   // from the FDT tiles: 16 B = 4 rows of one column per thread, 8 threads
@@ -416,6 +408,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     s = group_sum<LPC>(s);
     const unsigned long long m = __ballot(act && part == 0 && s >= sm);
     if (lane == 0 && m) atomicAdd(&cntk[slot], __popcll(m));
+    return m;  // this wave's candidates the row strongly sees (fame's S_j)
   };
   {
     const unsigned long long m = __ballot(act && part == 0);
@@ -423,6 +416,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
   int slot = 1;
   int32_t res = -1;  // window row of B[r+1][c], or -1
+  unsigned long long ssb = 0;  // this wave's ballot of the probe that verified the answer row
   if (rows > 0) {
     // binary search assuming the window's last row reaches SM (count is
     // monotone); that row is probed only if the search ends on it unverified
@@ -430,18 +424,19 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     bool hi_ok = false;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      probe(win + mid * q4, slot);
+      const unsigned long long m = probe(win + mid * q4, slot);
       __syncthreads();
       if (cntk[slot] >= sm) {
         hi = mid;
         hi_ok = true;
+        ssb = m;
       } else {
         lo = mid + 1;
       }
       ++slot;
     }
     if (!hi_ok) {
-      probe(win + hi * q4, slot);
+      ssb = probe(win + hi * q4, slot);
       __syncthreads();
       hi_ok = cntk[slot] >= sm;
     }
@@ -466,17 +461,22 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
         x4[i] = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + wk) * q4 + i];
       if (t < 16) cntk[t] = 0;
       __syncthreads();
-      probe(x4 + (wr - 1) * q4, 1);
+      const unsigned long long ml = probe(x4 + (wr - 1) * q4, 1);
       __syncthreads();
       if (cntk[1] < sm) continue;
       int lo = 0, hi = wr - 1, sl = 1;
+      ssb = ml;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         ++sl;
-        probe(x4 + mid * q4, sl);
+        const unsigned long long m = probe(x4 + mid * q4, sl);
         __syncthreads();
-        if (cntk[sl] >= sm) hi = mid;
-        else lo = mid + 1;
+        if (cntk[sl] >= sm) {
+          hi = mid;
+          ssb = m;
+        } else {
+          lo = mid + 1;
+        }
       }
       result = wk + lo;
     }
@@ -496,6 +496,12 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     } else {
       if (t < npad) cf[t] = t < n ? d.fdt[fdt_pos(cs + result, t, npad)] : FD_NONE;
     }
+    // fame's input for the new candidate y = (c, result): SS(y, q) over
+    // the candidates q of round r = the ballots of the probe that verified
+    // y's row.  Raw ballots, one aligned 8-B word per wave (fame packs the
+    // LPC-strided bits), chain-major [c][round]; issued last, since a later
+    // vmcnt wait would include them
+    if (lane == 0) d.ssm[((int64_t)c * (d.R_cap + 1) + r + 1) * 16 + wave] = ssb;
   }
   if (dg) {
     const unsigned long long te = stamp();
@@ -628,8 +634,7 @@ __global__ __launch_bounds__(64) void k_wfill(Dev d) {
     if (w) {
       const int32_t k = j + popc64(m & ((1ull << lane) - 1ull));
       d.wids[k] = d.chain_ids[d.chain_start[q] + b0];
-      d.wrow[k] = d.chain_start[q] + b0;  // the witness's LA row
-      d.wfrow[k] = d.fd_cols ? r * n + q : d.chain_start[q] + b0;  // and its FD row
+      d.wrow[k] = d.chain_start[q] + b0;  // the witness's LA / FD row
     }
     j += popc64(m);
   }
