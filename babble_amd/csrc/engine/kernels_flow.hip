@@ -528,7 +528,14 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
   constexpr int IPP = BT / TR;  // columns per load pass
   constexpr int LU = 16;        // load passes in flight
   const int t = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * TR;
+  // XCD-aware tile order: workgroup b runs on XCD b % 8, so give each XCD a
+  // contiguous range of tiles -- a tile's "row before" (the previous tile's
+  // last row) is then usually already in that XCD's L2
+  // (the grid is rounded up to a multiple of 8 workgroups)
+  const uint32_t per = gridDim.x / 8;
+  const int64_t tix = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (tix * TR >= d.N) return;
+  const int64_t row0 = tix * TR;
   const int64_t N = d.N;
   const int n = d.n, npad = d.npad;
   const int64_t stride = d.la_rows + 64;
@@ -673,7 +680,8 @@ void launch_flow_lt_fallback(const Dev &d, hipStream_t s) {
 
 void launch_flow_transpose(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
-  k_flow_transpose<64, 512><<<(unsigned)((d.N + 63) / 64), 512, (size_t)d.npad * 66 * 4, s>>>(d);
+  const unsigned tiles = (unsigned)((d.N + 63) / 64);
+  k_flow_transpose<64, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 66 * 4, s>>>(d);
 }
 
 void launch_flow_coordinates(const Dev &d, hipStream_t s) {
