@@ -554,10 +554,13 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
     cstart[i] = d.chain_start[i];
     clen[i] = d.chain_len[i];
   }
-  for (int i = t / TR; i < n; i += LU * IPP) {
+  // column i of a load is uniform per wave (TR = 64): scalar base address,
+  // 32-bit lane offset
+  for (int i = __builtin_amdgcn_readfirstlane(t / TR); i < n; i += LU * IPP) {
     int32_t v[LU];
 #pragma unroll
-    for (int u = 0; u < LU; ++u) v[u] = __builtin_nontemporal_load(d.la_col + (int64_t)min(i + IPP * u, n - 1) * stride + row);
+    for (int u = 0; u < LU; ++u)
+      v[u] = i + IPP * u < n ? __builtin_nontemporal_load(d.la_col + (int64_t)(i + IPP * u) * stride + row) : 0;
 #pragma unroll
     for (int u = 0; u < LU; ++u)
       if (i + IPP * u < n) tile[(i + IPP * u) * (TR + 1) + ro] = v[u];
@@ -568,14 +571,19 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
     const uint64_t m = __ballot(st);
     if (t == 0) segmask = m;
   }
-  const int q4 = npad / 4;
-  for (int p = t; p < TR * q4; p += blockDim.x) {
-    const int r = p / q4, i4 = (p - r * q4) * 4;
-    if (r >= rows) continue;
-    int32_t o[4];
+  {
+    // rows out: thread = (row r0 + k * rpp, 4 columns i4); one division
+    const int q4 = npad / 4, rpp = BT / q4;
+    if (t < rpp * q4) {
+      const int r0 = t / q4, i4 = (t - r0 * q4) * 4;
+      int4 *dst = reinterpret_cast<int4 *>(d.la + row0 * npad + i4);
+      for (int r = r0; r < rows; r += rpp) {
+        int32_t o[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) o[u] = i4 + u < n ? tile[(i4 + u) * (TR + 1) + r] : -1;
-    *reinterpret_cast<int4 *>(d.la + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
+        for (int u = 0; u < 4; ++u) o[u] = i4 + u < n ? tile[(i4 + u) * (TR + 1) + r] : -1;
+        dst[(int64_t)r * q4] = make_int4(o[0], o[1], o[2], o[3]);
+      }
+    }
   }
   __syncthreads();
   const uint64_t segs = segmask;
