@@ -220,7 +220,9 @@ int stage_rounds(bh_handle *h) {
   hipEvent_t done_ev[2];
   HIPCHK(h, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
   HIPCHK(h, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
-  int32_t *pin = h->pinned_state;
+  // the round kernels store 1 into the mapped word pin[0] when the loop ends
+  volatile int32_t *pin = h->pinned_state;
+  pin[0] = 0;
   bool done = false;
 
   const int64_t max_batches = (int64_t)d.R_cap / ITER_BATCH + 2;
@@ -231,13 +233,11 @@ int stage_rounds(bh_handle *h) {
     } else {
       HIPCHK(h, hipGraphLaunch(h->graph, s));
     }
-    HIPCHK(h, hipMemcpyAsync(pin + (b & 1) * bh::ST_COUNT, d.state, bh::ST_COUNT * 4,
-                             hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
 
     if (b > 0) {
       HIPCHK(h, hipEventSynchronize(done_ev[(b - 1) & 1]));
-      if (pin[((b - 1) & 1) * bh::ST_COUNT + bh::ST_DONE]) done = true;
+      if (pin[0]) done = true;
     }
   }
   HIPCHK(h, hipStreamSynchronize(s));
@@ -430,7 +430,9 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
     bh::configure_order_kernels();
   }
   if (rc == BH_OK && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = BH_ERR_DEVICE;
-  if (rc == BH_OK && hipHostMalloc((void **)&h->pinned_state, 2 * bh::ST_COUNT * 4, 0) != hipSuccess)
+  if (rc == BH_OK && hipHostMalloc((void **)&h->pinned_state, 2 * bh::ST_COUNT * 4, hipHostMallocMapped) != hipSuccess)
+    rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipHostGetDevicePointer((void **)&d.hdone, h->pinned_state, 0) != hipSuccess)
     rc = BH_ERR_DEVICE;
   for (auto &e : h->ev)
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;

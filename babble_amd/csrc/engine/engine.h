@@ -72,6 +72,7 @@ struct Dev {
   int32_t *opdesc;  // [N] chain-major other-parent (creator << 22 | index), -1 = none
   int32_t *la_col;  // [n][la_rows+64] column-major LA, chain-major rows (aliases la_ev)
   int32_t *lt_row;  // [la_rows+64] LT by chain-major row
+  int32_t *hdone;  // mapped pinned host word: set when the round loop is done
   int32_t flow_ltclamp;  // k_flow32 LT limit (2^21 - 256; BH_FLOW_LTCLAMP lowers it to test the fallback)
   uint8_t *depth, *chunk_maxd;
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)

@@ -30,6 +30,14 @@
 
 namespace bh {
 
+// the round loop's end, told to the host through mapped pinned memory (a
+// system-scope store), so the host polls it between graph replays instead of
+// copying the state back after every batch
+__device__ __forceinline__ void signal_done(const Dev &d) {
+  if (d.hdone) __hip_atomic_store(d.hdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+
 constexpr int WROWS = 32;    // window rows per chain
 
 __device__ __forceinline__ int popc64(unsigned long long x) { return __popcll(x); }
@@ -184,11 +192,11 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   }
   if (t == 0) {
     if (sh_nc == 0) {  // R = r
-      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
       return;
     }
     if (r + 1 >= d.R_cap) {
-      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
       return;
     }
     d.Bp[(int64_t)(p ^ 1) * n + c] = result;
@@ -298,11 +306,11 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
   }
   if (t == 0) {
     if (sh_nc == 0) {
-      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
       return;
     }
     if (r + 1 >= d.R_cap) {
-      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
       return;
     }
     d.Bp[(int64_t)(p ^ 1) * n + c] = result;
@@ -522,11 +530,11 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
   if (t == 0) {
     if (nc == 0) {  // no candidates: R = r
-      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
       return;
     }
     if (r + 1 >= d.R_cap) {
-      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; }
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
       return;
     }
     d.Bp[(int64_t)(p ^ 1) * n + c] = result;
