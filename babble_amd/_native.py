@@ -24,6 +24,7 @@ SYMBOLS = (
     "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
+    "bh_hash_bodies",
 )
 
 
@@ -83,5 +84,7 @@ def load():
     L.bh_get_profile.argtypes = [P, C.POINTER(I64), C.POINTER(C.c_float)]
     L.bh_get_profile_kernel.argtypes = [P]
     L.bh_get_profile_kernel.restype = C.c_char_p
+    L.bh_hash_bodies.argtypes = [P, VP, VP, I64, VP]
+    L.bh_hash_bodies.restype = C.c_int
     _LIB = L
     return L

@@ -56,6 +56,8 @@ struct bh_handle {
   hipGraphExec_t graph = nullptr;
   Dev graph_dev{};
   int32_t *pinned_state = nullptr;
+  uint8_t *sha_buf = nullptr;  // bh_hash_bodies scratch
+  size_t sha_cap = 0;
   hipEvent_t ev[NSTAGE + 1]{};
   hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)
   float sweep_ms = 0;
@@ -102,6 +104,7 @@ void free_all(bh_handle *h) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
+  if (h->sha_buf) (void)hipFree(h->sha_buf);
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
   for (auto &e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -726,5 +729,46 @@ int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {
 }
 
 const char *bh_get_profile_kernel(const bh_handle *h) { return h ? h->sweep_kernel : ""; }
+
+int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, int64_t count,
+                   uint8_t *digests) {
+  if (!h) return BH_ERR_INVALID;
+  if (count < 0 || (count > 0 && (!bytes || !offsets || !digests)))
+    return h->fail(BH_ERR_INVALID, "bh_hash_bodies: null buffer or negative count");
+  if (count == 0) return BH_OK;
+  (void)hipSetDevice(h->device);
+  const int64_t base = offsets[0], total = offsets[count] - base;
+  std::vector<int64_t> off((size_t)count);
+  std::vector<int32_t> len((size_t)count);
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t l = offsets[i + 1] - offsets[i];
+    if (l < 0 || l > INT32_MAX / 8) return h->fail(BH_ERR_INVALID, "bh_hash_bodies: offsets not ascending");
+    off[(size_t)i] = offsets[i] - base;
+    len[(size_t)i] = (int32_t)l;
+  }
+  // one device buffer: bytes (+128 B of read slack for the block loads),
+  // offsets, lengths, digests; kept for the next call
+  const size_t nb = ((size_t)total + 128 + 15) & ~(size_t)15;
+  const size_t need = nb + (size_t)count * (8 + 4 + 32);
+  if (need > h->sha_cap) {
+    if (h->sha_buf) (void)hipFree(h->sha_buf);
+    h->sha_buf = nullptr;
+    h->sha_cap = 0;
+    HIPCHK(h, hipMalloc((void **)&h->sha_buf, need));
+    h->sha_cap = need;
+  }
+  uint8_t *db = h->sha_buf;
+  int64_t *doff = reinterpret_cast<int64_t *>(db + nb);
+  int32_t *dlen = reinterpret_cast<int32_t *>(doff + count);
+  uint8_t *dout = reinterpret_cast<uint8_t *>(dlen + count);
+  HIPCHK(h, hipMemcpyAsync(db, bytes + base, (size_t)total, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(doff, off.data(), (size_t)count * 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(dlen, len.data(), (size_t)count * 4, hipMemcpyHostToDevice, h->stream));
+  bh::launch_sha256(db, doff, dlen, count, dout, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemcpyAsync(digests, dout, (size_t)count * 32, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
 
 }  // extern "C"

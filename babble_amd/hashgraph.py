@@ -210,3 +210,16 @@ class Hashgraph:
     def profile_kernel(self):
         """Name of the coordinate kernel the last run timed."""
         return self._L.bh_get_profile_kernel(self._h).decode()
+
+    def hash_bodies(self, bodies):
+        """Event.Hash() (event.go:50-56) of each body on the device: SHA-256
+        of the Go-JSON bytes.  bodies: a sequence of bytes; returns [n, 32] u8."""
+        lens = np.fromiter((len(b) for b in bodies), np.int64, len(bodies))
+        offsets = np.zeros(len(bodies) + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        data = np.frombuffer(b"".join(bodies), np.uint8) if len(bodies) else np.zeros(1, np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        out = np.empty((len(bodies), 32), np.uint8)
+        self._check(self._L.bh_hash_bodies(self._h, _ptr(data), _ptr(offsets), len(bodies), _ptr(out)))
+        return out

@@ -118,9 +118,17 @@ int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap);
 /* kernel statistics of the last run for the roofline report: number of
  * round-loop iterations, coordinate sweep launches' average ms */
 int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms);
-/* name of the coordinate kernel the last run timed ("k_flow": chain
- * dataflow; "k_la_sweep": chunked sweep); "" before the first run */
+/* name of the coordinate kernel the last run timed ("k_flow32" / "k_flow":
+ * chain dataflow; "k_la_sweep": chunked sweep); "" before the first run */
 const char *bh_get_profile_kernel(const bh_handle *h);
+/* SHA-256 of a batch of event bodies on the device:
+ * Event.Hash() = SHA-256 of the body's Go-JSON bytes (event.go:50-56), the
+ * digest InsertEvent keys, verifies and takes the coin from
+ * (hashgraph.go:716-721, 1526-1535).  Body i is bytes[offsets[i] ..
+ * offsets[i+1]) (offsets: count + 1 ascending entries); digests receives
+ * 32 * count bytes.  Runs on the handle's device and stream, synchronously. */
+int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, int64_t count,
+                   uint8_t *digests);
 
 #ifdef __cplusplus
 }
