@@ -24,7 +24,7 @@ SYMBOLS = (
     "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
-    "bh_hash_bodies",
+    "bh_hash_bodies", "bh_verify_signatures",
 )
 
 
@@ -86,5 +86,7 @@ def load():
     L.bh_get_profile_kernel.restype = C.c_char_p
     L.bh_hash_bodies.argtypes = [P, VP, VP, I64, VP]
     L.bh_hash_bodies.restype = C.c_int
+    L.bh_verify_signatures.argtypes = [P, VP, VP, VP, VP, I64, VP, I32, VP]
+    L.bh_verify_signatures.restype = C.c_int
     _LIB = L
     return L

@@ -771,4 +771,37 @@ int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, i
   return BH_OK;
 }
 
+int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig_r, const uint8_t *sig_s,
+                         const int32_t *keys, int64_t count, const uint8_t *pubkeys, int32_t n_keys,
+                         uint8_t *ok) {
+  if (!h) return BH_ERR_INVALID;
+  if (count < 0 || n_keys <= 0 || (count > 0 && (!hashes || !sig_r || !sig_s || !keys || !pubkeys || !ok)))
+    return h->fail(BH_ERR_INVALID, "bh_verify_signatures: null buffer or bad count");
+  if (count == 0) return BH_OK;
+  for (int64_t i = 0; i < count; ++i)
+    if (keys[i] < 0 || keys[i] >= n_keys) return h->fail(BH_ERR_INVALID, "bh_verify_signatures: key index out of range");
+  (void)hipSetDevice(h->device);
+  const size_t need = (size_t)count * (3 * 32 + 4 + 1) + (size_t)n_keys * 64 + 64;
+  if (need > h->sha_cap) {  // shares the hashing scratch buffer
+    if (h->sha_buf) (void)hipFree(h->sha_buf);
+    h->sha_buf = nullptr;
+    h->sha_cap = 0;
+    HIPCHK(h, hipMalloc((void **)&h->sha_buf, need));
+    h->sha_cap = need;
+  }
+  uint8_t *dh = h->sha_buf, *dr = dh + count * 32, *ds = dr + count * 32;
+  int32_t *dk = reinterpret_cast<int32_t *>(ds + count * 32);
+  uint8_t *dp = reinterpret_cast<uint8_t *>(dk + count), *dok = dp + (size_t)n_keys * 64;
+  HIPCHK(h, hipMemcpyAsync(dh, hashes, (size_t)count * 32, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(dr, sig_r, (size_t)count * 32, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(ds, sig_s, (size_t)count * 32, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(dk, keys, (size_t)count * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(dp, pubkeys, (size_t)n_keys * 64, hipMemcpyHostToDevice, h->stream));
+  bh::launch_ecdsa_verify(dh, dr, ds, dk, dp, count, dok, h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemcpyAsync(ok, dok, (size_t)count, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
+
 }  // extern "C"

@@ -139,6 +139,8 @@ bool flow32_eligible(const Dev &d);
 void launch_flow_lt_fallback(const Dev &d, hipStream_t s);
 void launch_sha256(const uint8_t *data, const int64_t *off, const int32_t *len, int64_t count, uint8_t *out,
                    hipStream_t s);  // kernels_sha.hip
+void launch_ecdsa_verify(const uint8_t *hash, const uint8_t *r, const uint8_t *s, const int32_t *key,
+                         const uint8_t *pub, int64_t count, uint8_t *ok, hipStream_t st);  // kernels_ecdsa.hip
 void launch_flow_transpose(const Dev &d, hipStream_t s);
 void launch_prep(const Dev &d, hipStream_t s);
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep

@@ -223,3 +223,16 @@ class Hashgraph:
         out = np.empty((len(bodies), 32), np.uint8)
         self._check(self._L.bh_hash_bodies(self._h, _ptr(data), _ptr(offsets), len(bodies), _ptr(out)))
         return out
+
+    def verify_signatures(self, hashes, sig_r, sig_s, keys, pubkeys):
+        """Event.Verify() (event.go:194-209) of a batch on the device: ECDSA
+        P-256 with Go ecdsa.Verify semantics.  hashes / sig_r / sig_s: [m, 32]
+        u8 big-endian; keys: [m] index into pubkeys [k, 64] (x || y).
+        Returns [m] bool."""
+        hashes, sig_r, sig_s = (np.ascontiguousarray(a, np.uint8) for a in (hashes, sig_r, sig_s))
+        keys = np.ascontiguousarray(keys, np.int32)
+        pubkeys = np.ascontiguousarray(pubkeys, np.uint8)
+        out = np.zeros(len(keys), np.uint8)
+        self._check(self._L.bh_verify_signatures(self._h, _ptr(hashes), _ptr(sig_r), _ptr(sig_s), _ptr(keys),
+                                                 len(keys), _ptr(pubkeys), len(pubkeys), _ptr(out)))
+        return out.astype(bool)

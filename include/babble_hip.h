@@ -129,6 +129,15 @@ const char *bh_get_profile_kernel(const bh_handle *h);
  * 32 * count bytes.  Runs on the handle's device and stream, synchronously. */
 int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, int64_t count,
                    uint8_t *digests);
+/* ECDSA P-256 verification of a batch of event signatures on the device
+ * (SURVEY 8(f) row 2): Event.Verify() (event.go:194-209) -> Go
+ * ecdsa.Verify(pub, hash, r, s) (crypto/utils.go:43-51).  Signature i:
+ * 32-byte big-endian hash / r / s at 32 * i, signed by public key
+ * keys[i] of pubkeys (64 bytes each: x || y big-endian, on the curve);
+ * ok[i] = 1 if it verifies, else 0.  Synchronous, on the handle's stream. */
+int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig_r, const uint8_t *sig_s,
+                         const int32_t *keys, int64_t count, const uint8_t *pubkeys, int32_t n_keys,
+                         uint8_t *ok);
 
 #ifdef __cplusplus
 }

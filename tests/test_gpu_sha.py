@@ -40,3 +40,39 @@ def test_sha256_event_bodies():
 
 def test_sha256_empty_batch():
     assert _hg().hash_bodies([]).shape == (0, 32)
+
+
+def _ecdsa_inputs(n=8, N=2000, seed=93):
+    from babble_amd.dag import Dag
+    d = Dag(n, N, seed, sig_mode=1)
+    pub = np.ascontiguousarray(d.pubkeys[:, 1:65])  # drop the 0x04 prefix
+    return d, pub
+
+
+def test_ecdsa_verify_generator_signatures():
+    """Every event signature of a sig_mode=1 DAG verifies (real ECDSA P-256
+    signatures over the body digests, pinned by test_host's pure-Python
+    verify); the same signatures checked against the wrong key, a flipped
+    hash bit, a perturbed s, and out-of-range r / s do not."""
+    d, pub = _ecdsa_inputs()
+    hg = _hg(8)
+    keys = d.creator.astype(np.int32)
+    ok = hg.verify_signatures(d.hash, d.sig_r, d.sig_s, keys, pub)
+    assert ok.all(), np.nonzero(~ok)[0][:10]
+    bad_key = hg.verify_signatures(d.hash, d.sig_r, d.sig_s, (keys + 1) % 8, pub)
+    assert not bad_key.any()
+    h2 = d.hash.copy()
+    h2[:, 31] ^= 1
+    assert not hg.verify_signatures(h2, d.sig_r, d.sig_s, keys, pub).any()
+    s2 = d.sig_s.copy()
+    s2[:, 31] ^= 4
+    assert not hg.verify_signatures(d.hash, d.sig_r, s2, keys, pub).any()
+    q = bytes.fromhex("FFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551")
+    edge = np.zeros((4, 32), np.uint8)
+    edge[1] = np.frombuffer(q, np.uint8)  # r = n
+    edge[2, 31] = 1
+    edge[3] = 0xFF
+    for e in range(4):  # r or s in {0, n, 1 (wrong), 2^256-1}
+        rr = np.repeat(edge[e:e + 1], 4, 0)
+        assert not hg.verify_signatures(d.hash[:4], rr, d.sig_s[:4], keys[:4], pub).any()
+        assert not hg.verify_signatures(d.hash[:4], d.sig_r[:4], rr, keys[:4], pub).any()

@@ -1,6 +1,7 @@
-"""Throughput of bh_hash_bodies (device SHA-256 of Go-JSON event bodies,
-SURVEY 8(f) row 2) against hashlib on one host core.  One JSON line.
-usage: python tools/bench_sha.py [--events N] [--reps R]"""
+"""Throughput of the insert-side crypto on the device:
+bh_hash_bodies (SHA-256 of Go-JSON event bodies) against hashlib on one host
+core, and bh_verify_signatures (ECDSA P-256) on real signatures.  Two JSON
+lines.  usage: python tools/bench_sha.py [--events N] [--reps R] [--sigs M]"""
 import argparse
 import hashlib
 import json
@@ -17,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=400_000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sigs", type=int, default=50_000)
     a = ap.parse_args()
     from babble_amd import Hashgraph
     from babble_amd.dag import Dag
@@ -39,6 +41,18 @@ def main():
                       "value": a.events / dt, "unit": "bodies/s", "bytes": nbytes,
                       "gb_per_s_pcie_inclusive": nbytes / dt / 1e9,
                       "cpu_hashlib_1core": cpu, "events": a.events}))
+    if a.sigs > 0:
+        ds = Dag(128, a.sigs, 0xBABB1E03, sig_mode=1)
+        pub = np.ascontiguousarray(ds.pubkeys[:, 1:65])
+        keys = ds.creator.astype(np.int32)
+        ok = hg.verify_signatures(ds.hash, ds.sig_r, ds.sig_s, keys, pub)
+        assert ok.all()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            hg.verify_signatures(ds.hash, ds.sig_r, ds.sig_s, keys, pub)
+        dt = (time.perf_counter() - t0) / a.reps
+        print(json.dumps({"metric": "event signatures verified/sec (ECDSA P-256, host buffers in and out)",
+                          "value": a.sigs / dt, "unit": "signatures/s", "signatures": a.sigs}))
 
 
 if __name__ == "__main__":
