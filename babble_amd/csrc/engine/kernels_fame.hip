@@ -11,48 +11,24 @@
 // entries, so every round is decided independently: one workgroup per round
 // r keeps the votes of all x in W(r) as bitsets over the voters (n/64 words),
 // and tallies with popcount(S_j[y] & V_{j-1}[x]), where S_j[y] is the bitset
-// of the W(j-1) witnesses y strongly sees.  S_j is an n x n x n integer
-// compare-and-count, register-tiled 8x8 per thread from LDS-staged LA rows
-// (voters) and firstDescendants rows (voted).  The workgroup then publishes
-// the round's decided flag, its famous count and min over famous witnesses
-// of LA (what DecideRoundReceived needs, hashgraph.go:968-1001).
+// of the W(j-1) witnesses y strongly sees.  For n <= 128 S_j comes from the
+// round loop's ballots (k_fame_masks, below); for larger n it is an
+// n x n x n integer compare-and-count, register-tiled 8x8 per thread over
+// LA rows (voters) and firstDescendants rows (voted) (k_fame).  The
+// workgroup then publishes the round's decided flag, its famous count and
+// min over famous witnesses of LA (what DecideRoundReceived needs,
+// hashgraph.go:968-1001).
 #include "engine.h"
 
 namespace bh {
 
-constexpr int FAME_MAXN = 128;  // LDS-staged rows up to this many participants
-
-// rows rowid[0..m) of src (row stride npad ints) into LDS dst (stride rs):
-// four independent 16-B loads in flight per thread, addresses from LDS
-__device__ __forceinline__ void fame_stage(int32_t *dst, int rs, const int32_t *src, const int32_t *rowid,
-                                           int m, int npad) {
-  const int q4 = npad / 4, tot = m * q4, nt = blockDim.x;
-  for (int b = threadIdx.x; b < tot; b += 4 * nt) {
-    int4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = min(b + u * nt, tot - 1);
-      const int row = i / q4;
-      v[u] = reinterpret_cast<const int4 *>(src + (int64_t)rowid[row] * npad)[i - row * q4];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = b + u * nt;
-      if (i < tot) {
-        const int row = i / q4;
-        reinterpret_cast<int4 *>(dst + row * rs)[i - row * q4] = v[u];
-      }
-    }
-  }
-}
-
-template <bool LDS_ROWS>
+// DecideFame for n > 128 (the k_round / k_round_wide path, where the round
+// loop keeps no ballots): S_j recomputed from LA / FD rows read from HBM
 __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   const int r = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const int n = d.n, npad = d.npad, sm = d.sm;
   const int WW = (n + 63) >> 6;       // words per voter bitset
-  const int rs = npad + 4;            // LDS row stride (ints)
   // carve
   unsigned long long *Vp = reinterpret_cast<unsigned long long *>(fsm);
   unsigned long long *Vc = Vp + n * WW;
@@ -65,8 +41,6 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   int32_t *rid = nd + n;   // [3][n] chain-major rows: W(r) (kept), then W(j-1) / W(j) alternating
   int32_t *misc = rid + 3 * n;  // [0] undecided count, [1] error
   const int32_t *fdrows = d.fd;
-  int32_t *ly = misc + 4;                      // LDS_ROWS: LA rows of W(j)
-  int32_t *fw = ly + (LDS_ROWS ? n * rs : 0);  // LDS_ROWS: FD rows of W(j-1)
 
   const int32_t nx = d.wcnt[r], xb = d.wofs[r];
   for (int i = t; i < nx; i += nt) {
@@ -87,13 +61,9 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
     for (int i = t; i < ny; i += nt) rid[n + i] = d.wrow[yb + i];
     for (int i = t; i < nx * WW; i += nt) Vp[i] = 0ull;
     __syncthreads();
-    if (LDS_ROWS) {
-      fame_stage(ly, rs, d.la, rid + n, ny, npad);
-      __syncthreads();
-    }
     for (int p = t; p < nx * ny; p += nt) {
       const int x = p / ny, y = p - x * ny;
-      const int32_t a = LDS_ROWS ? ly[y * rs + xc[x]] : d.la[(int64_t)rid[n + y] * npad + xc[x]];
+      const int32_t a = d.la[(int64_t)rid[n + y] * npad + xc[x]];
       if (a >= xk[x]) atomicOr(&Vp[x * WW + (y >> 6)], 1ull << (y & 63));
     }
     __syncthreads();
@@ -109,16 +79,9 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
       for (int i = t; i < nx * WW; i += nt) Vc[i] = 0ull;
       for (int i = t; i < nx; i += nt) nd[i] = 0;
       __syncthreads();
-      if (LDS_ROWS) {
-        fame_stage(ly, rs, d.la, yr_, ny, npad);
-        fame_stage(fw, rs, fdrows, wr_, nw, npad);
-      }
-      __syncthreads();
       cur = 3 - cur;
-      // S_j: 8x8 (y, w) tiles per thread, count columns with LA[y] >= FD[w].
-      // A tile's w rows are strided by tw (w = wt + b * tw), so the lanes of
-      // a wave (consecutive wt) read consecutive LDS rows: distinct banks;
-      // its y rows are shared by the wave (broadcast)
+      // S_j: 8x8 (y, w) tiles per thread, count columns with LA[y] >= FD[w]
+      // (w rows strided by tw: w = wt + b * tw)
       const int ty = (ny + 7) >> 3, tw = (nw + 7) >> 3;
       for (int tile = t; tile < ty * tw; tile += nt) {
         const int y0 = (tile / tw) * 8, wt = tile % tw;
@@ -127,13 +90,8 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
 #pragma unroll
         for (int a = 0; a < 8; ++a) {
           const int y = min(y0 + a, ny - 1), w = min(wt + a * tw, nw - 1);
-          if (LDS_ROWS) {
-            yr[a] = ly + y * rs;
-            wr[a] = fw + w * rs;
-          } else {
-            yr[a] = d.la + (int64_t)yr_[y] * npad;
-            wr[a] = fdrows + (int64_t)wr_[w] * npad;
-          }
+          yr[a] = d.la + (int64_t)yr_[y] * npad;
+          wr[a] = fdrows + (int64_t)wr_[w] * npad;
         }
         int cnt[8][8];
 #pragma unroll
@@ -213,18 +171,13 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
     if (misc[1]) d.state[ST_ERR] = 2;
   }
   // famous count and min LA over famous witnesses (see(w, x) for all w in FW)
-  if (LDS_ROWS) {
-    __syncthreads();
-    fame_stage(ly, rs, d.la, rid, nx, npad);  // rows of W(r) (rid[0..nx) kept)
-    __syncthreads();
-  }
   for (int c = t; c < npad; c += nt) {
     int32_t m = INT32_MAX;
     int cntf = 0;
     for (int x = 0; x < nx; ++x) {
       if (dec[x] != 1) continue;
       ++cntf;
-      m = min(m, LDS_ROWS ? ly[x * rs + c] : d.la[(int64_t)rid[x] * npad + c]);
+      m = min(m, d.la[(int64_t)rid[x] * npad + c]);
     }
     d.minla[(int64_t)r * npad + c] = m;
     if (c == 0) d.nfam[r] = cntf;
@@ -407,18 +360,13 @@ __global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R) {
   }
 }
 
-size_t fame_lds_bytes(int n, int npad, bool lds_rows) {
+size_t fame_lds_bytes(int n) {
   const int WW = (n + 63) >> 6;
-  size_t b = (size_t)3 * n * WW * 8 + (size_t)8 * n * 4 + 16;
-  if (lds_rows) b += (size_t)2 * n * (npad + 4) * 4;
-  return b;
+  return (size_t)3 * n * WW * 8 + (size_t)8 * n * 4 + 16;
 }
 
 void configure_fame_kernels() {
-  (void)hipFuncSetAttribute((const void *)k_fame<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            150 * 1024);
-  (void)hipFuncSetAttribute((const void *)k_fame<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            150 * 1024);
+  (void)hipFuncSetAttribute((const void *)k_fame, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
 }
 
 void launch_fame(const Dev &d, int32_t R, hipStream_t s) {
@@ -427,12 +375,7 @@ void launch_fame(const Dev &d, int32_t R, hipStream_t s) {
     k_fame_masks<<<R, 256, 0, s>>>(d, R);
     return;
   }
-  const bool lds = d.n <= FAME_MAXN;
-  const size_t bytes = fame_lds_bytes(d.n, d.npad, lds);
-  if (lds)
-    k_fame<true><<<R, 256, bytes, s>>>(d, R);
-  else
-    k_fame<false><<<R, 256, bytes, s>>>(d, R);
+  k_fame<<<R, 256, fame_lds_bytes(d.n), s>>>(d, R);
 }
 
 }  // namespace bh
