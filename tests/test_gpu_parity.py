@@ -336,3 +336,29 @@ def test_flow64_parity(monkeypatch):
     monkeypatch.setenv("BH_SWEEP", "flow64")
     _random_parity(128, 40_000, 72, 0)
     _wild_parity(24, 30_000, 73, 20_000)
+
+
+@pytest.mark.parametrize("n,N,seed,lag,step", [(4, 3000, 5, 0, 97), (9, 8000, 14, 3, 400), (32, 30_000, 21, 0, 3000)])
+def test_gossip_schedule_every_call(n, N, seed, lag, step):
+    """The live node's schedule (node.go:583-603 -> core.go:337-369):
+    RunConsensus after every gossip batch.  After EVERY call the engine's
+    state (rounds, fame, roundReceived, order, blocks, PendingRounds,
+    LastConsensusRound, counters, UndeterminedEvents) equals the oracle run
+    on the same schedule."""
+    from babble_amd.dag import Dag
+    d = Dag(n, N, seed, lagging=lag, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = _engine(n, d.participant_ids, N)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        st = hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi],
+                              opi[lo:hi], d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])
+        assert not np.asarray(st).any()
+        hg.run_consensus()
+        _compare(o, hg, f"after events [0, {hi})")
