@@ -38,7 +38,17 @@ struct bh_handle {
   int64_t cap = 0;
   // host mirrors (insert bookkeeping: ParticipantEventsCache + checks)
   std::vector<int64_t> pids;
-  std::unordered_map<int64_t, int32_t> slot_of;
+  // participant ID -> slot: open addressing, power-of-two table >= 4n,
+  // linear probing (one or two probes per lookup on the insert loop)
+  std::vector<int64_t> slot_key;
+  std::vector<int32_t> slot_val;
+  uint64_t slot_mask = 0;
+  int32_t slot_find(int64_t id) const {
+    for (uint64_t i = ((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 32 & slot_mask;; i = (i + 1) & slot_mask) {
+      if (slot_val[i] < 0) return -1;
+      if (slot_key[i] == id) return slot_val[i];
+    }
+  }
   std::vector<std::vector<int32_t>> chain;  // ids by creator, by index
   std::vector<int32_t> h_creator, h_index, h_sp, h_op, h_ntx;
   std::vector<uint8_t> h_coin;
@@ -374,7 +384,19 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   }
   h->device = cfg->device;
   h->pids.assign(cfg->participant_ids, cfg->participant_ids + n);
-  for (int i = 0; i < n; ++i) h->slot_of[h->pids[i]] = i;
+  {
+    size_t sz = 8;
+    while (sz < (size_t)n * 4) sz <<= 1;
+    h->slot_key.assign(sz, 0);
+    h->slot_val.assign(sz, -1);
+    h->slot_mask = sz - 1;
+    for (int i = 0; i < n; ++i) {
+      uint64_t j = ((uint64_t)h->pids[i] * 0x9E3779B97F4A7C15ull) >> 32 & h->slot_mask;
+      while (h->slot_val[j] >= 0) j = (j + 1) & h->slot_mask;
+      h->slot_key[j] = h->pids[i];
+      h->slot_val[j] = i;
+    }
+  }
   h->chain.resize(n);
   h->cap = cfg->max_events;
   Dev &d = h->d;
@@ -472,14 +494,21 @@ int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t
     return h->fail(BH_ERR_INVALID, "null field in bh_events");
   int first = BH_OK;
   int64_t acc = 0;
+  {  // geometric growth, sized for the whole batch up front
+    const size_t need = h->h_creator.size() + (size_t)std::max<int64_t>(ev->count, 0);
+    if (need > h->h_creator.capacity()) {
+      const size_t to = std::max(need, 2 * h->h_creator.capacity());
+      for (auto *v : {&h->h_creator, &h->h_index, &h->h_sp, &h->h_op, &h->h_ntx}) v->reserve(to);
+      h->h_coin.reserve(to);
+      h->h_sigw.reserve(to * 8);
+    }
+  }
   for (int64_t i = 0; i < ev->count; ++i) {
     int code = BH_OK;
-    int32_t c = -1, op = -1;
-    auto it = h->slot_of.find(ev->creator_id[i]);
-    if (it == h->slot_of.end()) {
+    int32_t c = h->slot_find(ev->creator_id[i]), op = -1;
+    if (c < 0) {
       code = BH_ERR_UNKNOWN_PARTICIPANT;
     } else {
-      c = it->second;
       const auto &ch = h->chain[c];
       const int32_t last = (int32_t)ch.size() - 1;  // base Root index is -1
       // checkSelfParent (hashgraph.go:398-414): self-parent must be the
@@ -489,10 +518,10 @@ int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t
       else if (ev->index[i] != last + 1) code = BH_ERR_SKIPPED_INDEX;
       else if (ev->other_parent_index[i] >= 0 || ev->other_parent_creator_id[i] >= 0) {
         // checkOtherParent (hashgraph.go:417-436) via ReadWireInfo's lookup
-        auto io = h->slot_of.find(ev->other_parent_creator_id[i]);
-        if (io == h->slot_of.end()) code = BH_ERR_OTHER_PARENT;
+        const int32_t oslot = h->slot_find(ev->other_parent_creator_id[i]);
+        if (oslot < 0) code = BH_ERR_OTHER_PARENT;
         else {
-          const auto &oc = h->chain[io->second];
+          const auto &oc = h->chain[oslot];
           const int32_t k = ev->other_parent_index[i];
           if (k < 0 || k >= (int32_t)oc.size()) code = BH_ERR_OTHER_PARENT;
           else op = oc[k];
@@ -522,9 +551,9 @@ int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t
     h->h_ntx.push_back(ev->n_transactions[i]);
     h->h_coin.push_back(ev->hash[i * 32 + 16] != 0 ? 1 : 0);
     const uint8_t *rb = ev->sig_r + i * 32;
-    for (int q = 0; q < 8; ++q)
-      h->h_sigw.push_back((uint32_t)rb[4 * q] << 24 | (uint32_t)rb[4 * q + 1] << 16 |
-                          (uint32_t)rb[4 * q + 2] << 8 | rb[4 * q + 3]);
+    uint32_t w[8];  // big-endian words of r
+    memcpy(w, rb, 32);
+    for (int q = 0; q < 8; ++q) h->h_sigw.push_back(__builtin_bswap32(w[q]));
     ch.push_back(id);
     if (ev->index[i] == 0 || ev->n_transactions[i] > 0) h->loaded_total++;
     ++acc;
