@@ -362,3 +362,22 @@ def test_gossip_schedule_every_call(n, N, seed, lag, step):
         assert not np.asarray(st).any()
         hg.run_consensus()
         _compare(o, hg, f"after events [0, {hi})")
+
+
+def test_participant_lookup_rejects_unknown_ids():
+    """ParticipantEvents lookups (rolling_index / peers): an unknown creator is
+    UnknownParticipant, an unknown other-parent creator is OtherParent; IDs
+    spread over the int64 range (the open-addressing table's probing)."""
+    from babble_amd import Hashgraph, HashgraphError
+    ids = np.array(sorted([0, 3, 11, 12, 13, 1 << 31, 1 << 40, (1 << 62) + 5]), np.int64)
+    hg = Hashgraph(ids, 64)
+    for c, pid in enumerate(ids):
+        hg.insert_event(int(pid), 0, -1, -1, -1, bytes([c + 1] * 32), bytes([c + 1] * 32), 0)
+    with pytest.raises(HashgraphError) as ei:
+        hg.insert_event(4, 0, -1, -1, -1, bytes(32), bytes(32), 0)
+    assert ei.value.kind == "UnknownParticipant"
+    with pytest.raises(HashgraphError) as ei:
+        hg.insert_event(int(ids[0]), 1, 0, 99, 0, bytes(32), bytes(32), 0)
+    assert ei.value.kind == "OtherParent"
+    hg.insert_event(int(ids[0]), 1, 0, int(ids[-1]), 0, bytes([77] * 32), bytes([77] * 32), 0)
+    assert hg.stats().n_events == len(ids) + 1
