@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("BH_LIB_PATH") or os.path.join(_HERE, "libbabble_hip.s
 BH_OK = 0
 ERRORS = {
     1: "SelfParent", 2: "OtherParent", 3: "UnknownParticipant", 4: "SkippedIndex",
-    5: "Capacity", 6: "State", 7: "Invalid", 8: "Device",
+    5: "Capacity", 6: "State", 7: "Invalid", 8: "Device", 9: "KeyNotFound",
 }
 
 # exported symbols, in include/babble_hip.h order (checked by tests)
@@ -23,14 +23,15 @@ SYMBOLS = (
     "bh_decide_fame", "bh_decide_round_received", "bh_process_decided_rounds",
     "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
-    "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
+    "bh_get_round_info", "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
     "bh_hash_bodies", "bh_verify_signatures",
 )
 
 
 class Config(C.Structure):
     _fields_ = [("n_participants", C.c_int32), ("participant_ids", C.POINTER(C.c_int64)),
-                ("max_events", C.c_int64), ("device", C.c_int32)]
+                ("max_events", C.c_int64), ("device", C.c_int32),
+                ("n_devices", C.c_int32), ("device_ids", C.POINTER(C.c_int32))]
 
 
 class Events(C.Structure):
@@ -46,6 +47,12 @@ class Stats(C.Structure):
                 ("consensus_transactions", C.c_int64), ("pending_loaded_events", C.c_int64),
                 ("undetermined_events", C.c_int64), ("blocks", C.c_int64),
                 ("pending_rounds", C.c_int32)]
+
+
+class RoundInfo(C.Structure):
+    _fields_ = [("round", C.c_int32), ("n_events", C.c_int32), ("n_witnesses", C.c_int32),
+                ("n_consensus", C.c_int32), ("queued", C.c_int8), ("witnesses_decided", C.c_int8),
+                ("pending", C.c_int8), ("pending_decided", C.c_int8)]
 
 
 _LIB = None
@@ -78,6 +85,8 @@ def load():
     L.bh_get_pending_rounds.restype = I32
     L.bh_get_undetermined.argtypes = [P, VP, I64]
     L.bh_get_undetermined.restype = I64
+    L.bh_get_round_info.argtypes = [P, I32, C.POINTER(RoundInfo), VP, VP, I32]
+    L.bh_get_round_info.restype = C.c_int
     L.bh_get_coordinates.argtypes = [P, I64, VP, VP]
     L.bh_get_stage_ms.argtypes = [P, C.POINTER(C.c_float), I32]
     L.bh_get_stage_ms.restype = I32

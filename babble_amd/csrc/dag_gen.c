@@ -10,10 +10,21 @@
 #include <openssl/obj_mac.h>
 #include <openssl/sha.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
+
+/* SHA-256 through the low-level interface: OpenSSL 3's one-shot SHA256()
+ * fetches the digest under a global lock on every call, which serialises
+ * the worker threads */
+static void sha256(const uint8_t *in, size_t len, uint8_t *out) {
+  SHA256_CTX c;
+  SHA256_Init(&c);
+  SHA256_Update(&c, in, len);
+  SHA256_Final(out, &c);
+}
 
 uint32_t bg_fnv1a32(const uint8_t *data, int64_t len) {
   uint32_t h = 2166136261u;
@@ -131,10 +142,10 @@ static void *sig_worker(void *arg) {
       in[0] = 'r';
       memcpy(in + 1, &j->seed, 8);
       memcpy(in + 9, d->hash + (size_t)e * 32, 32);
-      SHA256(in, sizeof in, d->sig_r + (size_t)e * 32);
+      sha256(in, sizeof in, d->sig_r + (size_t)e * 32);
       d->sig_r[(size_t)e * 32] &= 0x7F; /* < q */
       in[0] = 's';
-      SHA256(in, sizeof in, d->sig_s + (size_t)e * 32);
+      sha256(in, sizeof in, d->sig_s + (size_t)e * 32);
       d->sig_s[(size_t)e * 32] &= 0x7F;
     }
     return NULL;
@@ -149,7 +160,7 @@ static void *sig_worker(void *arg) {
     const uint8_t *hsh = d->hash + (size_t)e * 32;
     memcpy(buf + 8, hsh, 32);
     uint8_t kb[32];
-    SHA256(buf, 40, kb);
+    sha256(buf, 40, kb);
     BN_bin2bn(kb, 32, k);
     BN_nnmod(k, k, q, ctx);
     if (BN_is_zero(k)) BN_one(k);
@@ -168,6 +179,28 @@ static void *sig_worker(void *arg) {
   BN_free(q); BN_free(k); BN_free(kinv); BN_free(r); BN_free(s); BN_free(e_bn); BN_free(x); BN_free(t);
   BN_CTX_free(ctx);
   EC_GROUP_free(g);
+  return NULL;
+}
+
+typedef struct {
+  bg_dag *d;
+  uint8_t *done;
+  int t, T;
+} hash_job;
+
+static void *hash_worker(void *arg) {
+  hash_job *j = (hash_job *)arg;
+  bg_dag *d = j->d;
+  char jb[1024];
+  for (int64_t e = j->t; e < d->N; e += j->T) {
+    const int32_t sp = d->self_parent[e], op = d->other_parent[e];
+    while ((sp >= 0 && !__atomic_load_n(&j->done[sp], __ATOMIC_ACQUIRE)) ||
+           (op >= 0 && !__atomic_load_n(&j->done[op], __ATOMIC_ACQUIRE)))
+      sched_yield();
+    int32_t l = bg_body_json(d, e, jb);
+    sha256((const uint8_t *)jb, (size_t)l, d->hash + (size_t)e * 32);
+    __atomic_store_n(&j->done[e], 1, __ATOMIC_RELEASE);
+  }
   return NULL;
 }
 
@@ -209,7 +242,7 @@ int bg_generate(const bg_params *p, bg_dag *out) {
     memcpy(in, "babble-hip", 10);
     memcpy(in + 10, &p->seed, 8);
     memcpy(in + 18, &i, 4);
-    SHA256(in, sizeof in, d32);
+    sha256(in, sizeof in, d32);
     priv_raw[i] = BN_bin2bn(d32, 32, NULL);
     BN_nnmod(priv_raw[i], priv_raw[i], q, ctx);
     if (BN_is_zero(priv_raw[i])) BN_one(priv_raw[i]);
@@ -279,19 +312,25 @@ int bg_generate(const bg_params *p, bg_dag *out) {
   }
   free(head); free(seq); free(last); free(w);
 
-  /* hashes, in topological order (parents' hex strings are in the body) */
-  char *jb = (char *)malloc(1024);
-  for (int64_t e = 0; e < N; e++) {
-    int32_t l = bg_body_json(out, e, jb);
-    SHA256((const uint8_t *)jb, (size_t)l, out->hash + (size_t)e * 32);
-  }
-  free(jb);
-
-  /* signatures, in parallel */
   int T = p->threads > 0 ? p->threads : (int)sysconf(_SC_NPROCESSORS_ONLN);
   if (T > 16) T = 16;
   if (T < 1) T = 1;
   pthread_t th[16];
+
+  /* hashes: a body holds its parents' hex hashes, so event e waits for its
+   * parents' (always lower ids).  Thread t hashes e = t, t + T, ... in
+   * order, spinning on the parents' done flags: the lowest unfinished
+   * event always has its parents done, so the threads cannot deadlock. */
+  hash_job hj[16];
+  uint8_t *done = (uint8_t *)calloc((size_t)N, 1);
+  for (int t = 0; t < T; t++) {
+    hj[t].d = out; hj[t].done = done; hj[t].t = t; hj[t].T = T;
+    pthread_create(&th[t], NULL, hash_worker, &hj[t]);
+  }
+  for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+  free(done);
+
+  /* signatures, in parallel */
   sig_job jobs[16];
   for (int t = 0; t < T; t++) {
     jobs[t].d = out; jobs[t].seed = p->seed; jobs[t].sig_mode = p->sig_mode;

@@ -55,13 +55,25 @@ struct bh_handle {
   std::vector<uint32_t> h_sigw;
   int64_t uploaded = 0;  // events already on the device
   int64_t loaded_total = 0;
-  // stage bookkeeping: 0 none, 1 rounds, 2 fame, 3 rr, 4 processed
-  int stage = 0;
+  // The Go Hashgraph's state persists across calls: InsertEvent appends to
+  // UndeterminedEvents and changes nothing else; each pass updates its own
+  // part (hashgraph.go:714-1122).  The engine keeps the same split.
+  //   n_div   events covered by the last DivideRounds (round / witness / LT)
+  //   n_rr    events covered by the last DecideRoundReceived
+  //   R       rounds (Store.LastRound() + 1)
+  //   P       processed prefix: LastConsensusRound + 1
+  //   pend_dec  PendingRounds' decided flags for rounds [P, R): sticky, as
+  //             updatePendingRounds only ever sets them (hashgraph.go:689-695)
+  int stage = 0;  // last pass run: 0 none, 1 rounds, 2 fame, 3 rr, 4 processed
   int coords_for = -1;  // N the device coordinates were computed for
+  int64_t n_div = 0, n_rr = 0;
   int32_t R = 0, P = 0;
-  int64_t ncons = 0, cons_txs = 0, cons_loaded = 0, nreceived = 0;
+  std::vector<int8_t> pend_dec;     // indexed by round, meaningful for [P, R)
+  std::vector<int8_t> decided_h;    // last fame pass: round r's witnesses all decided
+  int64_t nundet = 0;               // undetermined among [0, n_rr) after the last rr pass
+  int32_t R_rr = 0;                 // R at the last rr pass (frame_cnt covers [0, R_rr))
+  int64_t ncons = 0, cons_txs = 0, cons_loaded = 0;
   std::vector<Block> blocks;
-  std::vector<int8_t> decided_h;
   // round-loop graph
   hipGraphExec_t graph = nullptr;
   Dev graph_dev{};
@@ -109,7 +121,7 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm,
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm,
                   d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -216,11 +228,8 @@ int stage_rounds(bh_handle *h) {
   if (d.N == 0) {
     HIPCHK(h, hipEventRecord(h->ev[2], s));
     h->R = 0;
+    h->n_div = 0;
     h->stage = 1;
-    h->decided_h.clear();
-    h->P = 0;
-    h->blocks.clear();
-    h->ncons = h->cons_txs = h->cons_loaded = h->nreceived = 0;
     return BH_OK;
   }
   bh::launch_round_init(d, s);
@@ -264,14 +273,14 @@ int stage_rounds(bh_handle *h) {
   h->iters = st[bh::ST_ITERS];
   if (st[bh::ST_FLOWOVF]) bh::launch_flow_lt_fallback(d, s);  // LT only feeds the frame order
   bh::launch_witness_tables(d, h->R, s);
-  bh::launch_assign_rounds(d, s);
+  bh::launch_assign_rounds(d, h->n_div, h->P, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[2], s));
+  h->n_div = d.N;
+  // rounds new to this call join PendingRounds undecided (hashgraph.go:809-815;
+  // every round >= LastConsensusRound is queued when it first appears)
+  h->pend_dec.resize((size_t)h->R, 0);
   h->stage = 1;
-  h->decided_h.assign((size_t)h->R, 0);
-  h->P = 0;
-  h->blocks.clear();
-  h->ncons = h->cons_txs = h->cons_loaded = h->nreceived = 0;
   return BH_OK;
 }
 
@@ -280,21 +289,31 @@ int stage_fame(bh_handle *h) {
   bh::launch_fame(h->d, h->R, h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
+  h->decided_h.assign((size_t)h->R, 0);
   if (h->R > 0)
     HIPCHK(h, hipMemcpyAsync(h->decided_h.data(), h->d.decided, (size_t)h->R, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int32_t err = 0;
   HIPCHK(h, hipMemcpy(&err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost));
   if (err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
+  // updatePendingRounds (hashgraph.go:689-695): set, never cleared
+  for (int32_t r = h->P; r < h->R; ++r)
+    if (h->decided_h[(size_t)r]) h->pend_dec[(size_t)r] = 1;
   h->stage = 2;
   return BH_OK;
 }
 
 int stage_rr(bh_handle *h) {
   if (h->stage < 2) return h->fail(BH_ERR_STATE, "DecideRoundReceived before DecideFame");
-  bh::launch_round_received(h->d, h->R, h->stream);
+  bh::launch_round_received(h->d, h->R, h->P, h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[4], h->stream));
+  int64_t und = 0;
+  HIPCHK(h, hipMemcpyAsync(&und, h->d.counters + 3, 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->nundet = und;
+  h->n_rr = h->n_div;
+  h->R_rr = h->R;
   h->stage = 3;
   return BH_OK;
 }
@@ -303,7 +322,14 @@ int stage_order(bh_handle *h) {
   if (h->stage < 3) return h->fail(BH_ERR_STATE, "ProcessDecidedRounds before DecideRoundReceived");
   Dev &d = h->d;
   hipStream_t s = h->stream;
+  // ProcessDecidedRounds (hashgraph.go:1041-1122): PendingRounds in order
+  // while their (sticky) decided flag is set
+  int32_t P1 = h->P;
+  while (P1 < h->R && h->pend_dec[(size_t)P1]) ++P1;
+  h->pinned_state[bh::ST_COUNT] = P1;  // pinned staging word (the first ST_COUNT hold the loop's done flag)
+  HIPCHK(h, hipMemcpyAsync(d.state + bh::ST_P, h->pinned_state + bh::ST_COUNT, 4, hipMemcpyHostToDevice, s));
   bh::launch_order(d, h->R, s);
+  bh::launch_trap_processed(d, h->P, P1, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[5], s));
   HIPCHK(h, hipStreamSynchronize(s));
@@ -311,11 +337,10 @@ int stage_order(bh_handle *h) {
   int64_t ctr[4];
   HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
   HIPCHK(h, hipMemcpy(ctr, d.counters, sizeof ctr, hipMemcpyDeviceToHost));
-  h->P = st[bh::ST_P];
+  h->P = P1;
   h->ncons = st[bh::ST_NCONS];
   h->cons_txs = ctr[0];
   h->cons_loaded = ctr[1];
-  h->nreceived = ctr[2];
   h->blocks.clear();
   if (h->P > 0) {
     std::vector<int32_t> cnt(h->P), ofs(h->P);
@@ -365,6 +390,7 @@ extern "C" {
 int bh_create(const bh_config *cfg, bh_handle **out) {
   if (!cfg || !out || cfg->n_participants < 1 || cfg->max_events < 0 || !cfg->participant_ids)
     return BH_ERR_INVALID;
+  if (cfg->n_devices > 1) return BH_ERR_INVALID;  // sharded handles: not in this build
   *out = nullptr;
   bh_handle *h = new bh_handle();
   const int n = cfg->n_participants;
@@ -442,7 +468,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
-  A(&d.round, C); A(&d.witness, C); A(&d.fame, C);
+  A(&d.round, C); A(&d.witness, C); A(&d.fame, C); A(&d.trapped, C); A(&d.blocked, R1);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
   A(&d.frame_cnt, R1); A(&d.frame_ofs, R1); A(&d.frame_cur, R1); A(&d.blk_of_frame, R1);
   A(&d.order, C); A(&d.cons_pos, C); A(&d.frame_ntx, R1); A(&d.counters, 4);
@@ -465,6 +491,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.state, 0, bh::ST_COUNT * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.counters, 0, 4 * 8) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipMemset(d.blocked, 0, R1 * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && getenv("BH_DIAG") && atoi(getenv("BH_DIAG"))) {
     rc = dalloc(h, &d.diag, bh::DG_COUNT);
     if (rc == BH_OK && hipMemset(d.diag, 0, bh::DG_COUNT * 8) != hipSuccess) rc = BH_ERR_DEVICE;
@@ -559,8 +586,7 @@ int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t
     ++acc;
   }
   if (n_accepted) *n_accepted = acc;
-  if (acc) {
-    h->stage = 0;
+  if (acc) {  // InsertEvent touches no pass's results (hashgraph.go:714-761)
     (void)hipSetDevice(h->device);
     int rc = upload(h);
     if (rc) return rc;
@@ -607,61 +633,52 @@ int bh_get_stats(bh_handle *h, bh_stats *o) {
   if (!h || !o) return BH_ERR_INVALID;
   memset(o, 0, sizeof *o);
   o->n_events = (int64_t)h->h_creator.size();
-  o->last_round = h->stage >= 1 ? h->R - 1 : -1;
-  o->last_consensus_round = h->stage >= 4 && h->P > 0 ? h->P - 1 : -1;
-  o->consensus_events = h->stage >= 4 ? h->ncons : 0;
-  o->consensus_transactions = h->stage >= 4 ? h->cons_txs : 0;
-  o->pending_loaded_events = h->loaded_total - (h->stage >= 4 ? h->cons_loaded : 0);
-  o->undetermined_events = o->n_events - (h->stage >= 4 ? h->nreceived : 0);
-  if (h->stage == 3) {  // received but not yet processed: count on demand
-    int64_t k = bh_get_undetermined(h, nullptr, 0);
-    o->undetermined_events = k;
-  }
+  o->last_round = h->R - 1;
+  o->last_consensus_round = h->P - 1;
+  o->consensus_events = h->ncons;
+  o->consensus_transactions = h->cons_txs;
+  o->pending_loaded_events = h->loaded_total - h->cons_loaded;
+  // received by the last DecideRoundReceived, plus everything inserted since
+  o->undetermined_events = h->nundet + (o->n_events - h->n_rr);
   o->blocks = (int64_t)h->blocks.size();
-  o->pending_rounds = h->stage >= 1 ? h->R - (h->stage >= 4 ? h->P : 0) : 0;
+  o->pending_rounds = h->R - h->P;
   return BH_OK;
 }
 
 int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round, int8_t *witness,
                       int32_t *lamport, int32_t *round_received, int8_t *fame, int64_t *consensus_pos) {
   if (!h || first < 0 || count < 0 || first + count > (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
+  if (count == 0) return BH_OK;
   (void)hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const Dev &d = h->d;
-  const size_t k = (size_t)count;
-  if (count == 0) return BH_OK;
-  auto fill32 = [&](int32_t *p) { std::fill(p, p + k, INT32_MIN); };
-  if (round) {
-    if (h->stage >= 1) HIPCHK(h, hipMemcpy(round, d.round + first, k * 4, hipMemcpyDeviceToHost));
-    else fill32(round);
-  }
-  if (lamport) {
-    if (h->stage >= 1) HIPCHK(h, hipMemcpy(lamport, d.lt + first, k * 4, hipMemcpyDeviceToHost));
-    else fill32(lamport);
-  }
-  if (witness) {
-    if (h->stage >= 1) HIPCHK(h, hipMemcpy(witness, d.witness + first, k, hipMemcpyDeviceToHost));
-    else std::fill(witness, witness + k, 0);
-  }
-  if (fame) {
-    if (h->stage >= 1) HIPCHK(h, hipMemcpy(fame, d.fame + first, k, hipMemcpyDeviceToHost));
-    else std::fill(fame, fame + k, -1);
-  }
+  // events [first, first + k) were divided; the rest are not (Go: nil fields)
+  const int64_t k = std::max<int64_t>(0, std::min<int64_t>(count, h->n_div - first));
+  const size_t rest = (size_t)(count - k);
+  auto get = [&](void *dst, const void *src, size_t esz) -> hipError_t {
+    return k > 0 ? hipMemcpy(dst, (const char *)src + (size_t)first * esz, (size_t)k * esz, hipMemcpyDeviceToHost)
+                 : hipSuccess;
+  };
+  if (round) { HIPCHK(h, get(round, d.round, 4)); std::fill(round + k, round + k + rest, INT32_MIN); }
+  if (lamport) { HIPCHK(h, get(lamport, d.lt, 4)); std::fill(lamport + k, lamport + k + rest, INT32_MIN); }
+  if (witness) { HIPCHK(h, get(witness, d.witness, 1)); std::fill(witness + k, witness + k + rest, 0); }
+  if (fame) { HIPCHK(h, get(fame, d.fame, 1)); std::fill(fame + k, fame + k + rest, -1); }
   if (round_received) {
-    if (h->stage >= 3) HIPCHK(h, hipMemcpy(round_received, d.rr + first, k * 4, hipMemcpyDeviceToHost));
-    else fill32(round_received);
+    HIPCHK(h, get(round_received, d.rr, 4));
+    std::fill(round_received + k, round_received + k + rest, INT32_MIN);
   }
   if (consensus_pos) {
-    if (h->stage >= 4) HIPCHK(h, hipMemcpy(consensus_pos, d.cons_pos + first, k * 8, hipMemcpyDeviceToHost));
-    else std::fill(consensus_pos, consensus_pos + k, -1);
+    HIPCHK(h, get(consensus_pos, d.cons_pos, 8));
+    std::fill(consensus_pos + k, consensus_pos + k + rest, -1);
   }
   return BH_OK;
 }
 
 int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *ids) {
   if (!h || !ids || first < 0 || count < 0) return BH_ERR_INVALID;
-  if (h->stage < 4 || first + count > h->ncons) return h->fail(BH_ERR_INVALID, "range beyond consensus");
+  if (first + count > h->ncons) return h->fail(BH_ERR_INVALID, "range beyond consensus");
   (void)hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   if (count) HIPCHK(h, hipMemcpy(ids, h->d.order + first, (size_t)count * 4, hipMemcpyDeviceToHost));
   return BH_OK;
 }
@@ -680,12 +697,11 @@ int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_rec
 }
 
 int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap) {
-  if (!h || h->stage < 1) return 0;
-  const int32_t lo = h->stage >= 4 ? h->P : 0;
-  const int32_t cnt = h->R - lo;
+  if (!h) return 0;
+  const int32_t cnt = h->R - h->P;
   for (int32_t i = 0; i < cnt && i < cap; ++i) {
-    if (index) index[i] = lo + i;
-    if (decided) decided[i] = h->stage >= 2 ? h->decided_h[(size_t)(lo + i)] : 0;
+    if (index) index[i] = h->P + i;
+    if (decided) decided[i] = h->pend_dec[(size_t)(h->P + i)];
   }
   return cnt;
 }
@@ -693,20 +709,58 @@ int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int
 int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap) {
   if (!h) return 0;
   const int64_t N = (int64_t)h->h_creator.size();
-  if (h->stage < 3) {
-    for (int64_t i = 0; i < N && i < cap; ++i) ids[i] = (int32_t)i;
-    return N;
-  }
-  std::vector<int32_t> rr((size_t)N);
+  const int64_t total = h->nundet + (N - h->n_rr);
+  if (!ids || cap <= 0) return total;
+  std::vector<int32_t> rr((size_t)h->n_rr);
   (void)hipSetDevice(h->device);
-  if (N && hipMemcpy(rr.data(), h->d.rr, (size_t)N * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipStreamSynchronize(h->stream) != hipSuccess) return -1;
+  if (h->n_rr && hipMemcpy(rr.data(), h->d.rr, (size_t)h->n_rr * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   int64_t k = 0;
-  for (int64_t i = 0; i < N; ++i)
-    if (rr[(size_t)i] == INT32_MIN) {
-      if (ids && k < cap) ids[k] = (int32_t)i;
-      ++k;
+  for (int64_t i = 0; i < h->n_rr && k < cap; ++i)
+    if (rr[(size_t)i] == INT32_MIN) ids[k++] = (int32_t)i;
+  for (int64_t i = h->n_rr; i < N && k < cap; ++i) ids[k++] = (int32_t)i;
+  return total;
+}
+
+int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *witness_ids, int8_t *fame,
+                      int32_t cap) {
+  if (!h || !info) return BH_ERR_INVALID;
+  if (r < 0 || r >= h->R) return h->fail(BH_ERR_KEY_NOT_FOUND, "GetRound %d: Not Found", r);
+  (void)hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const Dev &d = h->d;
+  const int n = d.n;
+  memset(info, 0, sizeof *info);
+  info->round = r;
+  // round r on chain c = indexes [B[r][c], B[r+1][c]) (B[R][c] = chain length)
+  std::vector<int32_t> b((size_t)2 * n), len((size_t)n);
+  HIPCHK(h, hipMemcpy(b.data(), d.B + (int64_t)r * n, (size_t)2 * n * 4, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(len.data(), d.chain_len, (size_t)n * 4, hipMemcpyDeviceToHost));
+  int64_t ne = 0;
+  for (int c = 0; c < n; ++c) ne += std::min(b[(size_t)(n + c)], len[(size_t)c]) - std::min(b[(size_t)c], len[(size_t)c]);
+  info->n_events = (int32_t)ne;
+  int32_t wofs = 0, wcnt = 0;
+  HIPCHK(h, hipMemcpy(&wofs, d.wofs + r, 4, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpy(&wcnt, d.wcnt + r, 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> w((size_t)wcnt);
+  std::vector<int8_t> f((size_t)wcnt);
+  if (wcnt) HIPCHK(h, hipMemcpy(w.data(), d.wids + wofs, (size_t)wcnt * 4, hipMemcpyDeviceToHost));
+  bool all = true;
+  for (int32_t i = 0; i < wcnt; ++i) {
+    HIPCHK(h, hipMemcpy(&f[(size_t)i], d.fame + w[(size_t)i], 1, hipMemcpyDeviceToHost));
+    all = all && f[(size_t)i] != 0;
+    if (i < cap) {
+      if (witness_ids) witness_ids[i] = w[(size_t)i];
+      if (fame) fame[i] = f[(size_t)i];
     }
-  return k;
+  }
+  info->n_witnesses = wcnt;
+  info->witnesses_decided = all ? 1 : 0;
+  if (r < h->R_rr) HIPCHK(h, hipMemcpy(&info->n_consensus, d.frame_cnt + r, 4, hipMemcpyDeviceToHost));
+  info->queued = 1;  // every round >= LastConsensusRound is queued when it first appears
+  info->pending = r >= h->P ? 1 : 0;
+  info->pending_decided = r >= h->P ? h->pend_dec[(size_t)r] : 0;
+  return BH_OK;
 }
 
 int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_t *first_descendants) {

@@ -103,12 +103,20 @@ struct Dev {
   int8_t *decided;
   int32_t *nfam, *minla;
   int32_t *rr;
+  // per-sync schedule (hashgraph.go:809-815, roundInfo.go:35):
+  // a witness whose round was already processed when it arrived (or was
+  // still undecided when its round was processed) is never decided again --
+  // its fame stays Undefined and its round never again reports
+  // WitnessesDecided.  trapped[e] marks such witnesses, blocked[r] counts
+  // them per round.
+  int8_t *trapped;
+  int32_t *blocked;
   // frames
   int32_t *frame_cnt, *frame_ofs, *frame_cur, *blk_of_frame;
   int32_t *order;
   int64_t *cons_pos;
   int64_t *frame_ntx;
-  int64_t *counters;  // [0] consensus txs, [1] loaded consensus events, [2] received
+  int64_t *counters;  // [0] consensus txs, [1] loaded consensus events, [2] unused, [3] undetermined
   // diagnostic phase counters (BH_DIAG=1 builds the buffer; null otherwise).
   // Only a separate diagnostic run reads them; no result depends on them.
   unsigned long long *diag;
@@ -150,10 +158,19 @@ void launch_permute(const Dev &d, hipStream_t s);  // sweep slabs -> chain-major
 void launch_round_init(const Dev &d, hipStream_t s);  // hand-off buffers for round 0
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
 void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wcnt/wrow
-void launch_assign_rounds(const Dev &d, hipStream_t s);
+// per-event round / witness; events >= n_prev (inserted since the last
+// division) also get their initial fame / rr / consensus position, and are
+// marked trapped when they are witnesses of a round < P (already processed)
+void launch_assign_rounds(const Dev &d, int64_t n_prev, int32_t P, hipStream_t s);
 void launch_fame(const Dev &d, int32_t R, hipStream_t s);
-void launch_round_received(const Dev &d, int32_t R, hipStream_t s);
+// rr of events still undetermined (rr already set is kept); rounds < P are
+// live-decided iff no trapped witness; counters[3] = undetermined after it;
+// frame_cnt[r] = events received in r (every r < R)
+void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s);
+// frames / order / blocks of rounds [0, P): ST_P holds P (set by the host)
 void launch_order(const Dev &d, int32_t R, hipStream_t s);
+// witnesses of rounds [P0, P1) still Undefined when those rounds were processed
+void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s);
 void configure_fd_kernels();
 void launch_first_descendants(const Dev &d, hipStream_t s, bool walked);  // fd from la (FDT already written by k_flow_transpose when walked)
 

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   }
   // ---- publish ----
   __syncthreads();
-  for (int x = t; x < nx; x += nt) d.fame[xs[x]] = (int8_t)dec[x];
+  for (int x = t; x < nx; x += nt) d.fame[xs[x]] = d.trapped[xs[x]] ? 0 : (int8_t)dec[x];  // trapped: Undefined
   __syncthreads();
   if (t == 0) {
     d.decided[r] = misc[0] == 0 ? 1 : 0;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R) {
   }
   // ---- publish ----
   __syncthreads();
-  if (t < 128 && isx) d.fame[xev[x]] = (int8_t)dec[x];
+  if (t < 128 && isx) d.fame[xev[x]] = d.trapped[xev[x]] ? 0 : (int8_t)dec[x];  // trapped: Undefined (A.12)
   if (t == 0) {
     d.decided[r] = misc[0] == 0 ? 1 : 0;
     if (misc[1]) d.state[ST_ERR] = 2;

@@ -22,37 +22,41 @@
 
 namespace bh {
 
-__global__ void k_round_received(Dev d, int32_t R) {
+// Only events still undetermined are visited: an event received by an earlier
+// call has left UndeterminedEvents for good (hashgraph.go:1028-1033).  A
+// round is "decided" here as DecideRoundReceived reads it, live:
+// RoundInfo.WitnessesDecided (roundInfo.go:78-85) -- for a processed round
+// (< P) that is "no trapped witness", for a pending one the fame pass's flag.
+__global__ __launch_bounds__(256) void k_round_received(Dev d, int32_t R, int32_t P) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= d.N) return;
-  const int32_t r = d.round[x], c = d.creator[x], k = d.index[x];
-  int32_t res = UNSET;
-  for (int32_t i = r + 1; i < R; ++i) {
-    if (!d.decided[i]) break;
-    if (d.nfam[i] > 0 && k <= d.minla[(int64_t)i * d.npad + c]) { res = i; break; }
+  int und = 0;
+  if (x < d.N) {
+    int32_t res = d.rr[x];
+    if (res == UNSET) {
+      const int32_t r = d.round[x], c = d.creator[x], k = d.index[x];
+      for (int32_t i = r + 1; i < R; ++i) {
+        const bool live = i < P ? d.blocked[i] == 0 : d.decided[i] != 0;
+        if (!live) break;
+        if (d.nfam[i] > 0 && k <= d.minla[(int64_t)i * d.npad + c]) { res = i; break; }
+      }
+      if (res != UNSET) d.rr[x] = res;
+    }
+    und = res == UNSET;
   }
-  d.rr[x] = res;
-}
-
-void launch_round_received(const Dev &d, int32_t R, hipStream_t s) {
-  if (d.N == 0) return;
-  k_round_received<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d, R);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) und += __shfl_xor(und, off);
+  if ((threadIdx.x & 63) == 0 && und)
+    atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[3]), (unsigned long long)und);
 }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_prefix(Dev d, int32_t R) {
-  __shared__ int32_t p;
-  if (threadIdx.x == 0) p = R;
-  __syncthreads();
-  for (int32_t r = threadIdx.x; r < R; r += blockDim.x)
-    if (!d.decided[r]) atomicMin(&p, r);
-  __syncthreads();
-  for (int32_t r = threadIdx.x; r < R; r += blockDim.x) { d.frame_cnt[r] = 0; d.frame_cur[r] = 0; }
+// ProcessDecidedRounds bookkeeping: P (the processed prefix) is decided on
+// the host from PendingRounds' sticky decided flags and stored in ST_P
+__global__ __launch_bounds__(1024) void k_order_init(Dev d, int32_t R) {
+  for (int32_t r = threadIdx.x; r < R; r += blockDim.x) d.frame_cur[r] = 0;
   if (threadIdx.x == 0) {
-    d.state[ST_P] = p;
     d.counters[0] = 0;
     d.counters[1] = 0;
-    d.counters[2] = 0;
   }
 }
 
@@ -74,28 +78,21 @@ __device__ __forceinline__ int32_t block_min(int32_t v, int32_t *sh) {
 
 __global__ __launch_bounds__(256) void k_frame_count(Dev d) {
   __shared__ int32_t hist[HB], rmin_s;
-  __shared__ unsigned long long nrecv;
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * OB;
-  const int32_t P = d.state[ST_P];
   if (t < HB) hist[t] = 0;
-  if (t == 0) { rmin_s = INT32_MAX; nrecv = 0; }
+  if (t == 0) rmin_s = INT32_MAX;
   int32_t rr[4];
   int32_t lo = INT32_MAX;
-  int recv = 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int64_t x = base + u * 256 + t;
     rr[u] = x < d.N ? d.rr[x] : UNSET;
-    recv += rr[u] != UNSET;
-    if (rr[u] == UNSET || rr[u] >= P) rr[u] = -1;
+    if (rr[u] == UNSET) rr[u] = -1;
     else lo = min(lo, rr[u]);
   }
   __syncthreads();
   const int32_t rmin = block_min(lo, &rmin_s);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) recv += __shfl_xor(recv, off);
-  if ((t & 63) == 0 && recv) atomicAdd(&nrecv, (unsigned long long)recv);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     if (rr[u] < 0) continue;
@@ -105,8 +102,6 @@ __global__ __launch_bounds__(256) void k_frame_count(Dev d) {
   }
   __syncthreads();
   if (t < HB && hist[t]) atomicAdd(&d.frame_cnt[rmin + t], hist[t]);
-  // events received (in any round) leave UndeterminedEvents
-  if (t == 0 && nrecv) atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[2]), nrecv);
 }
 
 // exclusive scans of frame sizes and of non-empty flags (block indices)
@@ -236,6 +231,7 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d) {
   extern __shared__ __attribute__((aligned(16))) unsigned char osm[];
   __shared__ unsigned long long sh_ntx, sh_loaded;
   const int32_t f = blockIdx.x;
+  if (f >= d.state[ST_P]) return;  // received in a round not yet processed
   const int32_t cnt = d.frame_cnt[f];
   if (cnt == 0) return;
   const int t = threadIdx.x, nt = blockDim.x;
@@ -311,14 +307,21 @@ void configure_order_kernels() {
                             FRAME_LDS_MAX * 12);
 }
 
+void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s) {
+  (void)hipMemsetAsync(d.counters + 3, 0, 8, s);
+  if (R > 0) (void)hipMemsetAsync(d.frame_cnt, 0, (size_t)R * 4, s);
+  if (d.N == 0) return;
+  k_round_received<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d, R, P);
+  if (R > 0) k_frame_count<<<(unsigned)((d.N + OB - 1) / OB), 256, 0, s>>>(d);
+}
+
 void launch_order(const Dev &d, int32_t R, hipStream_t s) {
   if (R <= 0) return;
-  k_prefix<<<1, 1024, 0, s>>>(d, R);
+  k_order_init<<<1, 1024, 0, s>>>(d, R);
   const unsigned g = (unsigned)((d.N + OB - 1) / OB);
-  k_frame_count<<<g, 256, 0, s>>>(d);
   k_frame_scan<<<1, 1024, 0, s>>>(d);
   k_frame_scatter<<<g, 256, 0, s>>>(d);
-  // frames [0, P); P <= R.  Launch R blocks: frames >= P have cnt 0.
+  // frames [0, P); P <= R.  Launch R blocks: frames >= P return at once.
   k_frame_sort<<<R, 1024, FRAME_LDS_MAX * 12, s>>>(d);
 }
 

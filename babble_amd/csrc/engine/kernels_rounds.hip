@@ -657,8 +657,14 @@ void launch_witness_tables(const Dev &d, int R, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // per-event round / witness from the boundary table (DivideRounds output,
-// hashgraph.go:782-827): round(x) = max r with B[r][c] <= k.
-__global__ void k_assign(Dev d) {
+// hashgraph.go:782-827): round(x) = max r with B[r][c] <= k.  Round and
+// witness of an event depend only on its ancestors, so events divided by an
+// earlier call get the same values again; only events inserted since
+// (e >= n_prev) get their initial fame (Undefined for a witness), round
+// received (nil) and consensus position.  A new witness of a round that is
+// already processed (r < P) is never queued again (hashgraph.go:809-815) and
+// so never decided: it is trapped.
+__global__ void k_assign(Dev d, int64_t n_prev, int32_t P) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.N) return;
   const int32_t R = d.state[ST_ROUNDS];
@@ -673,14 +679,40 @@ __global__ void k_assign(Dev d) {
   d.round[e] = lo;
   const bool w = d.B[(int64_t)lo * n + c] == k;
   d.witness[e] = w ? 1 : 0;
-  d.fame[e] = w ? 0 : -1;
-  d.rr[e] = UNSET;
-  d.cons_pos[e] = -1;
+  if (e >= n_prev) {
+    d.fame[e] = w ? 0 : -1;
+    d.rr[e] = UNSET;
+    d.cons_pos[e] = -1;
+    const bool trap = w && lo < P;
+    d.trapped[e] = trap ? 1 : 0;
+    if (trap) atomicAdd(&d.blocked[lo], 1);
+  }
 }
 
-void launch_assign_rounds(const Dev &d, hipStream_t s) {
+void launch_assign_rounds(const Dev &d, int64_t n_prev, int32_t P, hipStream_t s) {
   if (d.N == 0) return;
-  k_assign<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
+  k_assign<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d, n_prev, P);
+}
+
+// witnesses of the rounds just processed, [P0, P1), that were still
+// Undefined: ProcessDecidedRounds went by the pending round's sticky decided
+// flag (hashgraph.go:689-695, 1054-1056) and the round leaves PendingRounds
+// for good, so DecideFame never visits them again
+__global__ __launch_bounds__(64) void k_trap_processed(Dev d, int32_t P0) {
+  const int32_t r = P0 + blockIdx.x;
+  const int32_t b = d.wofs[r], cnt = d.wcnt[r];
+  for (int i = threadIdx.x; i < cnt; i += 64) {
+    const int32_t w = d.wids[b + i];
+    if (d.fame[w] == 0 && !d.trapped[w]) {
+      d.trapped[w] = 1;
+      atomicAdd(&d.blocked[r], 1);
+    }
+  }
+}
+
+void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s) {
+  if (P1 <= P0) return;
+  k_trap_processed<<<(unsigned)(P1 - P0), 64, 0, s>>>(d, P0);
 }
 
 }  // namespace bh

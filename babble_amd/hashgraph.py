@@ -45,7 +45,7 @@ class Hashgraph:
         self.participant_ids = ids
         self.n = len(ids)
         cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
-                             int(device))
+                             int(device), 0, None)
         h = C.c_void_p()
         rc = self._L.bh_create(C.byref(cfg), C.byref(h))
         if rc != _native.BH_OK:
@@ -190,6 +190,22 @@ class Hashgraph:
                                               _ptr(out["ntx"])))
         return out
 
+    def round_info(self, r):
+        """Store.GetRound(r) + RoundInfo accessors (inmem_store.go:185-211,
+        roundInfo.go:33-128).  Raises HashgraphError(KeyNotFound) for a
+        round that does not exist.  Returns a dict with the witnesses (event
+        ids, participant order) and their Trilean fame."""
+        info = _native.RoundInfo()
+        cap = self.n
+        wid = np.empty(cap, np.int32)
+        fame = np.empty(cap, np.int8)
+        self._check(self._L.bh_get_round_info(self._h, int(r), C.byref(info), _ptr(wid), _ptr(fame), cap))
+        k = info.n_witnesses
+        return dict(round=info.round, n_events=info.n_events, n_consensus=info.n_consensus,
+                    witnesses=wid[:k].copy(), fame=fame[:k].copy(), queued=bool(info.queued),
+                    witnesses_decided=bool(info.witnesses_decided), pending=bool(info.pending),
+                    pending_decided=bool(info.pending_decided))
+
     def coordinates(self, event_id):
         la = np.empty(self.n, np.int32)
         fd = np.empty(self.n, np.int32)
@@ -229,10 +245,18 @@ class Hashgraph:
         P-256 with Go ecdsa.Verify semantics.  hashes / sig_r / sig_s: [m, 32]
         u8 big-endian; keys: [m] index into pubkeys [k, 64] (x || y).
         Returns [m] bool."""
+        keys = np.ascontiguousarray(keys, np.int32).reshape(-1)
+        m = len(keys)
         hashes, sig_r, sig_s = (np.ascontiguousarray(a, np.uint8) for a in (hashes, sig_r, sig_s))
-        keys = np.ascontiguousarray(keys, np.int32)
+        if any(a.size != 32 * m for a in (hashes, sig_r, sig_s)):
+            raise ValueError("hashes / sig_r / sig_s must hold 32 bytes per signature")
         pubkeys = np.ascontiguousarray(pubkeys, np.uint8)
-        out = np.zeros(len(keys), np.uint8)
+        if pubkeys.size == 0 or pubkeys.size % 64:
+            raise ValueError("pubkeys must be [k, 64] bytes (x || y)")
+        pubkeys = pubkeys.reshape(-1, 64)
+        if m and (keys.min() < 0 or keys.max() >= len(pubkeys)):
+            raise ValueError("key index out of range")
+        out = np.zeros(m, np.uint8)
         self._check(self._L.bh_verify_signatures(self._h, _ptr(hashes), _ptr(sig_r), _ptr(sig_s), _ptr(keys),
                                                  len(keys), _ptr(pubkeys), len(pubkeys), _ptr(out)))
         return out.astype(bool)

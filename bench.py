@@ -47,6 +47,29 @@ def sum_over_ranks(x, dist=None):
     return float(t.item())
 
 
+def _pmc_table(n, N):
+    """Per-kernel PMC HBM bytes of this config (tools/pmc.sh ->
+    tools/pmc_summary.py -> profiles/pmc_traffic.json), or {}."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    cfg = tab.get(f"n{n}_N{N}", {})
+    return cfg if all("hbm_bytes_per_step" in v for v in cfg.values()) else {}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cfg, sample_events, log):
     """CPU restatement of the reference Go path (oracle/, 1 thread) on the
     first `sample_events` events of the same DAG (a valid DAG prefix)."""
@@ -66,7 +89,8 @@ def cpu_baseline(cfg, sample_events, log):
     ordered = len(o.consensus_order())
     o.close()
     log(f"cpu baseline: {ordered} events ordered in {dt:.2f}s")
-    return dict(value=ordered / dt, unit="events/s", cores=1, kind="port",
+    return dict(value=ordered / dt, unit="events/s", cores=1, kind="port", cpu_model=_cpu_model(),
+                nproc=os.cpu_count(), threads_used=1,
                 sample=f"first {sample_events} events of the cfg{cfg} DAG (prefix), batch schedule "
                        f"(coordinates+DivideRounds+DecideFame+DecideRoundReceived+ProcessDecidedRounds), "
                        f"C restatement of hashgraph.go, 1 thread, {ordered} events ordered in {dt:.2f}s")
@@ -147,44 +171,33 @@ def main():
     value = total_ordered / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
-    # roofline of the coordinate kernel (k_flow / k_la_sweep):
-    # algorithmic bytes per event = 8*n (two parent LA rows) + 4*n (own row)
-    # + 12 (LT of both parents + own); per launch x N events
     n = c["n"]
-    sweep_avg_ms = float(np.mean(sweep_ms))
-    alg_bytes = N * (12 * n + 12)
-    achieved = alg_bytes / (sweep_avg_ms * 1e-3) / 1e9
-    # HBM traffic of that kernel per launch, from the committed PMC passes
-    # (tools/pmc.sh -> tools/pmc_summary.py -> profiles/pmc_traffic.json;
-    # FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction)
-    traffic = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
-            tr = json.load(f).get(hg.profile_kernel(), {})
-        if tr.get("participants") == n and tr.get("events") == N:
-            traffic = tr["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        pass
-    # roofline of the round loop (the dominant kernel by total time at every
-    # config: one launch per round).  Algorithmic bytes per launch: each of
-    # the n workgroups streams every candidate's FD row (n x npad int32),
-    # its chain's 32-row LA window and 32-row FD window (32 x npad int32
-    # each), from L2/MALL; average launch duration = the rounds stage (HIP
-    # events, graph replay) / iterations, launch gaps included
     npad = (n + 3) & ~3
-    round_kernel = "k_round2" if npad <= 128 else "k_round"
-    round_alg = n * (n * npad * 4 + 2 * 32 * npad * 4)
+    stages = dict(zip(["coordinates", "rounds", "fame", "round_received", "order"],
+                      (stage_tot / args.steps).round(3).tolist()))
+    pmc = _pmc_table(n, N)
+    # roofline: the path is integer and
+    # HBM-bound; algorithmic bytes per ordered event B(n) = 12n + 96 (two
+    # parent LA rows read, own row written, per-event scalars, sort key and
+    # value, signature tie-break) against the 8 TB/s HBM peak
+    B = 12 * n + 96
+    achieved = value * B / 1e9
+    traffic_step = sum(v["hbm_bytes_per_step"] for v in pmc.values()) if pmc else None
+    # the dominant kernel: the round loop (one launch per round; N / launches
+    # events per launch), timed live by HIP events around its graph replays
+    round_kernel = "k_round2" if npad <= 128 else "k_round_wide"
     rounds_ms = float(stage_tot[1] / args.steps)
     round_avg_ms = rounds_ms / max(iters, 1)
-    round_achieved = round_alg / (round_avg_ms * 1e-3) / 1e9
-    round_traffic = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
-            tr = json.load(f).get(round_kernel, {})
-        if tr.get("participants") == n and tr.get("events") == N:
-            round_traffic = tr["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        pass
+    ev_per_launch = N / max(iters, 1)
+    dom_alg = ev_per_launch * B
+    dom_achieved = dom_alg / (round_avg_ms * 1e-3) / 1e9
+    dom = pmc.get(round_kernel) if pmc else None
+    # the L2-level view of the same kernel (round 1's figure): each of the n
+    # workgroups streams every candidate's FD row and its 32-row LA / FD
+    # windows from L2 / MALL -- not HBM bytes, reported under its own key
+    l2_bytes = n * (n * npad * 4 + 2 * 32 * npad * 4)
+    sweep_avg_ms = float(np.mean(sweep_ms))
+    coord_alg = N * (12 * n + 12)
     out = {
         "metric": METRIC,
         "value": value,
@@ -204,18 +217,28 @@ def main():
                    "participants": n, "events": N, "events_ordered_per_step": ordered,
                    "rounds": stats.last_round + 1, "blocks": stats.blocks,
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
-        "roofline": {"kernel": round_kernel, "bound": "hbm", "achieved": round_achieved,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round_achieved / HBM_PEAK_GBS,
-                     "traffic": round_traffic, "alg_bytes_per_launch": round_alg,
-                     "avg_launch_ms": round_avg_ms, "launches": iters,
-                     "note": "latency-bound per round (a serial chain of rounds); bytes come from L2/MALL"},
-        "roofline_coordinates": {"kernel": hg.profile_kernel(), "bound": "hbm", "achieved": achieved,
-                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                                 "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
-                                 "avg_launch_ms": sweep_avg_ms,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_step,
+                     "scope": "whole step: events ordered/s x B(n), SURVEY 8(d)",
+                     "alg_bytes_per_event": B, "alg_bytes_per_step": ordered * B,
+                     "traffic_total_note": "PMC HBM bytes of every kernel of one step "
+                                           "(profiles/pmc_traffic.json; FETCH_SIZE x 2 + WRITE_SIZE)",
+                     "dominant_kernel": {
+                         "kernel": round_kernel, "launches": iters, "avg_launch_ms": round_avg_ms,
+                         "events_per_launch": ev_per_launch, "alg_bytes_per_launch": dom_alg,
+                         "achieved": dom_achieved, "frac": dom_achieved / HBM_PEAK_GBS,
+                         "traffic": dom["hbm_bytes_per_launch"] if dom else None,
+                         "note": "latency-bound: rounds are a serial chain, one launch each"},
+                     "l2_level": {"kernel": round_kernel, "bytes_per_launch": l2_bytes,
+                                  "GBps": l2_bytes / (round_avg_ms * 1e-3) / 1e9,
+                                  "note": "candidate FD rows + LA/FD windows re-read by every workgroup "
+                                          "from L2/MALL; not HBM traffic"}},
+        "roofline_coordinates": {"kernel": hg.profile_kernel(), "avg_launch_ms": sweep_avg_ms,
+                                 "alg_bytes_per_launch": coord_alg,
+                                 "achieved": coord_alg / (sweep_avg_ms * 1e-3) / 1e9,
+                                 "traffic": (pmc.get(hg.profile_kernel()) or {}).get("hbm_bytes_per_launch"),
                                  "note": "bound by the DAG's critical path x per-step issue, not bandwidth"},
-        "stages_ms": dict(zip(["coordinates", "rounds", "fame", "round_received", "order"],
-                              (stage_tot / args.steps).round(3).tolist())),
+        "stages_ms": stages,
         "round_loop_iterations": iters,
     }
     cpu_sample = args.cpu_sample

@@ -22,6 +22,7 @@
 //   Store.ConsensusEvents / LastBlockIndex         ConsensusEvents() / Blocks()
 //   Event.round / lamportTimestamp / ...           EventMeta(id) / Coordinates(id)
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <optional>
 #include <stdexcept>
@@ -70,6 +71,15 @@ struct PendingRound {
   bool decided;
 };
 
+// RoundInfo (roundInfo.go:33-128) as Store.GetRound returns it
+struct RoundInfo {
+  int32_t round = 0;
+  int32_t n_events = 0, n_consensus = 0;
+  bool queued = false, witnesses_decided = false, pending = false, pending_decided = false;
+  std::vector<int32_t> witnesses;  // event ids, participant order
+  std::vector<int8_t> fame;        // Trilean: 0 Undefined, 1 True, 2 False
+};
+
 struct Block {  // block.go:100-123 (bodies are reassembled by the caller)
   int64_t index;
   int32_t round_received;
@@ -83,7 +93,7 @@ class Hashgraph {
   // NewHashgraph (hashgraph.go:43-73); ids are the peers' IDs in ascending
   // order (peers.go:63-73), max_events the store capacity.
   Hashgraph(const std::vector<int64_t> &participant_ids, int64_t max_events, int device = 0) {
-    bh_config cfg{(int32_t)participant_ids.size(), participant_ids.data(), max_events, device};
+    bh_config cfg{(int32_t)participant_ids.size(), participant_ids.data(), max_events, device, 0, nullptr};
     const int rc = bh_create(&cfg, &h_);
     if (rc != BH_OK) {
       std::string msg = h_ ? bh_last_error(h_) : "bh_create failed";
@@ -197,6 +207,33 @@ class Hashgraph {
     m.famous = fame;
     m.consensus_position = pos;
     return m;
+  }
+
+  // Store.GetRound (inmem_store.go:185-191): throws KeyNotFound for a round
+  // that does not exist
+  RoundInfo GetRound(int32_t r) const {
+    bh_round_info info{};
+    const int cap = 4096;
+    std::vector<int32_t> w(cap);
+    std::vector<int8_t> f(cap);
+    check(bh_get_round_info(h_, r, &info, w.data(), f.data(), cap));
+    RoundInfo out;
+    out.round = info.round;
+    out.n_events = info.n_events;
+    out.n_consensus = info.n_consensus;
+    out.queued = info.queued != 0;
+    out.witnesses_decided = info.witnesses_decided != 0;
+    out.pending = info.pending != 0;
+    out.pending_decided = info.pending_decided != 0;
+    const int k = std::min(info.n_witnesses, cap);
+    out.witnesses.assign(w.begin(), w.begin() + k);
+    out.fame.assign(f.begin(), f.begin() + k);
+    return out;
+  }
+  // Store.RoundWitnesses (inmem_store.go:205-211): [] for a missing round
+  std::vector<int32_t> RoundWitnesses(int32_t r) const {
+    if (r < 0 || r > LastRound()) return {};
+    return GetRound(r).witnesses;
   }
 
   // lastAncestors / firstDescendants indexes of one event (event.go:115-116),

@@ -28,7 +28,8 @@ enum {
   BH_ERR_CAPACITY = 5,      /* more events than bh_config.max_events */
   BH_ERR_STATE = 6,         /* pass called before its prerequisites */
   BH_ERR_INVALID = 7,       /* bad argument */
-  BH_ERR_DEVICE = 8         /* HIP runtime error / no device / kernel fault */
+  BH_ERR_DEVICE = 8,        /* HIP runtime error / no device / kernel fault */
+  BH_ERR_KEY_NOT_FOUND = 9  /* StoreErr KeyNotFound (common/errors.go:8), e.g. GetRound */
 };
 
 typedef struct bh_handle bh_handle;
@@ -39,7 +40,13 @@ typedef struct {
   int32_t n_participants;
   const int64_t *participant_ids; /* peer IDs, ascending (peers.go:63-73, 118-129) */
   int64_t max_events;             /* capacity; the reference's cacheSize must be >= #events */
-  int32_t device;                 /* HIP device ordinal */
+  int32_t device;                 /* HIP device ordinal (when n_devices <= 1) */
+  /* Devices the handle shards its passes over: each
+   * holds the whole DAG; coordinate columns, fame rounds and frames are
+   * split between them and exchanged device to device.  n_devices <= 1:
+   * one device, `device`.  Ordinals may repeat (shards sharing a device). */
+  int32_t n_devices;
+  const int32_t *device_ids;
 } bh_config;
 
 /* A batch of events in topological order, in the reference's compact wire
@@ -106,8 +113,28 @@ int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_rec
                   int64_t *first_event, int64_t *n_events, int64_t *n_transactions);
 /* Hashgraph.PendingRounds: returns the count, fills up to cap entries */
 int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap);
-/* Hashgraph.UndeterminedEvents (insertion order): returns the count */
+/* Hashgraph.UndeterminedEvents (insertion order): returns the count, fills
+ * up to cap ids (ids may be NULL) */
 int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap);
+
+/* Store.GetRound(r) / RoundWitnesses(r) (inmem_store.go:185-211) and the
+ * RoundInfo accessors (roundInfo.go:33-128).  BH_ERR_KEY_NOT_FOUND for a
+ * round that does not exist (r < 0 or r > LastRound).  Witnesses are listed
+ * in participant (ID) order -- Go returns them in map order -- with their
+ * Trilean fame (0 Undefined, 1 True, 2 False) in fame[]; up to cap entries
+ * (witness_ids / fame nullable), info->n_witnesses gives the count. */
+typedef struct {
+  int32_t round;
+  int32_t n_events;          /* events whose round is r (RoundInfo.Events also lists the n_consensus ones) */
+  int32_t n_witnesses;       /* len(RoundInfo.Witnesses()) */
+  int32_t n_consensus;       /* len(RoundInfo.ConsensusEvents()): events received in r */
+  int8_t queued;             /* RoundInfo.queued */
+  int8_t witnesses_decided;  /* RoundInfo.WitnessesDecided() */
+  int8_t pending;            /* r is in Hashgraph.PendingRounds */
+  int8_t pending_decided;    /* that entry's Decided flag (0 when not pending) */
+} bh_round_info;
+int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *witness_ids, int8_t *fame,
+                      int32_t cap);
 /* lastAncestors / firstDescendants indexes of one event (event.go:115-116) */
 int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors,
                        int32_t *first_descendants);

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from kat import KatDag, kat_names
-from oracle_py import Oracle
+from oracle_py import UNSET, Oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -181,8 +181,11 @@ def test_empty_and_tiny():
 
 
 def test_large_properties():
-    """C2 size (1M events, 32 peers): size-independent properties, plus
-    parity of the first-processed prefix against the oracle on a 200k prefix."""
+    """C2 size (1M events, 32 peers): size-independent properties of the
+    whole-DAG run -- the Lamport recurrence, round monotonicity along both
+    parents, the witness definition, the frame sort key order and the
+    block / transaction conservation.  (Bit-exact parity at full sizes is
+    test_full_size_prefix_parity.)"""
     from babble_amd.dag import Dag
     from babble_amd import Hashgraph
     n, N = 32, 1_000_000
@@ -211,6 +214,77 @@ def test_large_properties():
     assert b["count"].sum() == len(order)
     assert b["ntx"].sum() == d.ntx[order].sum() == hg.consensus_transactions
     assert len(order) > 0.95 * N
+
+
+def test_wide_512_parity():
+    """C4's width (512 participants, SM = 342) against the oracle, bit-exact:
+    the chunked coordinate sweep, k_round_wide and fame from HBM rows."""
+    _random_parity(512, 40_000, 0xBABB1E04, 0)
+
+
+def _prefix_check(cfg, prefix):
+    """Full-size DAG of BASELINE config `cfg` (the DAG bench.py times) through
+    the engine, against the oracle on its first `prefix` events.
+
+    Round, witness and Lamport timestamp of an event depend only on its
+    ancestors, which precede it in insertion order, so they must agree on
+    every prefix event.  A witness's votes depend only on the voters'
+    ancestry, so a fame the prefix run decided is the full run's fame; an
+    event received in a round the prefix run processed is received there in
+    the full run, and those frames -- hence the consensus order and blocks up
+    to the prefix run's last processed round -- are identical.  The engine is
+    also run on the prefix itself and compared with the oracle in full."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    d = Dag.config(cfg, sig_mode=0)
+    N, n = d.N, d.n
+    o = Oracle(n, d.participant_ids, capacity=prefix)
+    o.insert_dag(*(a[:prefix] for a in (d.creator, d.index, d.self_parent, d.other_parent, d.hash,
+                                        d.sig_r, d.ntx)))
+    o.run_consensus()
+    ref = o.results()
+    # the engine on the prefix: full state parity
+    hp = Hashgraph(d.participant_ids, prefix)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    assert not hp.insert_events(pid[d.creator[:prefix]], d.index[:prefix], spi[:prefix], opc_id[:prefix],
+                                opi[:prefix], d.hash[:prefix], d.sig_r[:prefix], d.ntx[:prefix]).any()
+    hp.run_consensus()
+    _compare(o, hp, f"cfg{cfg} prefix {prefix}")
+    hp.close()
+    # the engine on the whole DAG
+    hg = Hashgraph(d.participant_ids, N)
+    assert not hg.insert_dag(d).any()
+    hg.run_consensus()
+    got = hg.results(0, prefix)
+    for k in ("round", "witness", "lamport"):
+        bad = np.nonzero(ref[k] != got[k])[0]
+        assert len(bad) == 0, f"cfg{cfg} {k}: {len(bad)} mismatches, first {bad[:8]}"
+    dec = (ref["witness"] == 1) & (ref["fame"] != 0)
+    assert dec.sum() > 0
+    assert np.array_equal(ref["fame"][dec], got["fame"][dec]), f"cfg{cfg} decided fame"
+    rcv = ref["round_received"] != UNSET
+    assert np.array_equal(ref["round_received"][rcv], got["round_received"][rcv]), f"cfg{cfg} rr"
+    oo = o.consensus_order()
+    assert len(oo) > 0.75 * prefix
+    assert np.array_equal(oo, hg.consensus_order()[:len(oo)]), f"cfg{cfg} consensus order"
+    assert np.array_equal(ref["cons_pos"][rcv], got["cons_pos"][rcv])
+    ob, gb = o.blocks(), hg.blocks()
+    k = len(ob["round_received"])
+    for f in ("round_received", "first", "count", "ntx"):
+        assert np.array_equal(ob[f], gb[f][:k]), f"cfg{cfg} blocks.{f}"
+    st = hg.stats()
+    assert st.consensus_events > 0.95 * N and st.last_consensus_round >= o.last_consensus_round()
+    hg.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cfg,prefix", [(3, 200_000), (5, 200_000), (4, 100_000)])
+def test_full_size_prefix_parity(cfg, prefix):
+    """BASELINE configs C3 (128 peers, 10M events: the bench DAG), C5 (64 peers,
+    21 lagging, 2M) and C4 (512 peers, 20M) at full size."""
+    _prefix_check(cfg, prefix)
 
 
 def _wild_dag(n, N, seed, back):

@@ -1,0 +1,181 @@
+"""The live node's schedule through the engine: RunConsensus after every
+gossip batch (node.go:583-603 -> core.go:337-369), the state the Go
+Hashgraph keeps between calls, and the RoundInfo query surface.
+
+The reference's Hashgraph is a state machine: InsertEvent only appends to
+UndeterminedEvents, each pass updates its own part, and PendingRounds'
+`queued` / sticky `decided` flags make the result depend on the call
+schedule (hashgraph.go:689-695, 809-815; roundInfo.go:35).  The
+oracle replays the Go state machine literally; every comparison here is
+against the oracle run on the same schedule, bit-exact."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from kat import KatDag
+from oracle_py import UNSET, Oracle
+from test_gpu_parity import _compare, _insert_kat
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _wire_batches(d):
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+
+    def batch(lo, hi):
+        return (pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi], opi[lo:hi],
+                d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])
+    return batch
+
+
+def _schedule(n, N, seed, lagging, lag_div, step, check_every=True):
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    d = Dag(n, N, seed, lagging=lagging, lag_div=lag_div, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not np.asarray(hg.insert_events(*batch(lo, hi))).any()
+        hg.run_consensus()
+        if check_every or hi == N:
+            _compare(o, hg, f"after events [0, {hi})")
+    return d, o, hg
+
+
+def test_queued_trap_fixture():
+    """SURVEY A.12 on a seeded lagging-peer DAG (tests/golden/trap_schedule.json):
+    a lagging peer's witness lands in a round that was already processed, so
+    it is never queued again -- its fame stays Undefined, its round never
+    again reports WitnessesDecided, and an older undetermined event of the
+    same peer is never received (hashgraph.go:809-815, 984-986).  The batch
+    schedule decides both.  The engine must follow the per-sync schedule."""
+    with open(os.path.join(GOLDEN, "trap_schedule.json")) as f:
+        fx = json.load(f)
+    d, o, hg = _schedule(fx["n"], fx["N"], fx["seed"], fx["lagging"], fx["lag_div"], fx["step"])
+    res = hg.results()
+    for e, want in fx["per_sync"]["fame"].items():
+        assert res["fame"][int(e)] == want, e
+    for e, want in fx["per_sync"]["round_received"].items():
+        assert res["round_received"][int(e)] == (UNSET if want is None else want), e
+    w = int(fx["trapped_witness"])
+    info = hg.round_info(int(res["round"][w]))
+    assert w in info["witnesses"].tolist() and not info["witnesses_decided"]
+    assert not info["pending"]
+
+
+@pytest.mark.parametrize("n,N,seed,lag,div,step", [
+    (5, 4000, 1003, 1, 40, 3),
+    (9, 6000, 1014, 3, 80, 7),
+    (13, 6000, 1021, 4, 300, 17),
+])
+def test_lagging_schedules(n, N, seed, lag, div, step):
+    """Per-sync schedules with strongly lagging peers, state compared after
+    every RunConsensus call."""
+    _schedule(n, N, seed, lag, div, step)
+
+
+def test_state_between_insert_and_run():
+    """InsertEvent leaves every pass's results in place: between an insert and
+    the next RunConsensus the counters, the consensus order, PendingRounds and
+    the per-event fields read what the Go Hashgraph holds at that point
+    (undetermined grows by the new events; nothing else changes)."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    n, N, step = 8, 9000, 1500
+    d = Dag(n, N, 404, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        hg.insert_events(*batch(lo, hi))
+        _compare(o, hg, f"after inserting [0, {hi}), before RunConsensus")
+        o.run_consensus()
+        hg.run_consensus()
+        _compare(o, hg, f"after RunConsensus on [0, {hi})")
+
+
+def test_stepwise_passes_across_calls():
+    """The four passes called one at a time on every call of a schedule
+    (core.go:337-369 calls them in sequence); the state after EACH pass
+    equals the oracle's."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    n, N, step = 6, 5000, 700
+    d = Dag(n, N, 505, lagging=1, lag_div=30, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    batch = _wire_batches(d)
+    passes = (("divide_rounds", "divide_rounds"), ("decide_fame", "decide_fame"),
+              ("decide_round_received", "decide_round_received"),
+              ("process_decided_rounds", "process_decided_rounds"))
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        hg.insert_events(*batch(lo, hi))
+        for go, ours in passes:
+            getattr(o, go)()
+            getattr(hg, ours)()
+            _compare(o, hg, f"[0, {hi}) after {go}")
+
+
+def test_round_info_kat():
+    """TestDivideRounds' per-round witness sets (hashgraph_test.go:746-828) and
+    TestDecideFame's fame (:1267-1343) through Store.GetRound / RoundInfo;
+    GetRound of a missing round is KeyNotFound (inmem_store.go:185-191)."""
+    from babble_amd import Hashgraph, HashgraphError
+    d = KatDag("kat_round")
+    hg = Hashgraph(d.participant_ids, 64)
+    _insert_kat(hg, d)
+    hg.divide_rounds()
+    ex = d.expect["divide_rounds"]
+    assert hg.last_round() == ex["last_round"]
+    for r, ws in ex["witnesses"].items():
+        info = hg.round_info(int(r))
+        assert sorted(d.names[i] for i in info["witnesses"]) == sorted(ws), r
+        assert info["queued"] and info["pending"]
+    with pytest.raises(HashgraphError) as ei:
+        hg.round_info(ex["last_round"] + 1)
+    assert ei.value.kind == "KeyNotFound"
+
+    d = KatDag("kat_consensus")
+    hg = Hashgraph(d.participant_ids, 64)
+    _insert_kat(hg, d)
+    o = Oracle(d.n, d.participant_ids, capacity=64)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    hg.divide_rounds()
+    o.divide_rounds()
+    hg.decide_fame()
+    o.decide_fame()
+    famous = d.expect["famous"]
+    seen = set()
+    ores = o.results()
+    for r in range(hg.last_round() + 1):
+        info = hg.round_info(r)
+        for w, f in zip(info["witnesses"].tolist(), info["fame"].tolist()):
+            assert f == ores["fame"][w], (r, d.names[w])
+            name = d.names[w]
+            if name in famous:
+                assert f == (1 if famous[name] else 2), name
+                seen.add(name)
+        assert info["witnesses_decided"] == all(f != 0 for f in info["fame"].tolist())
+    assert seen == set(famous)
+    hg.decide_round_received()
+    o.decide_round_received()
+    ores = o.results()
+    for r in range(hg.last_round() + 1):
+        assert hg.round_info(r)["n_consensus"] == int(np.sum(ores["round_received"] == r)), r

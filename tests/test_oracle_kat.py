@@ -223,3 +223,32 @@ def test_incremental_schedule_equals_batch_random(n, N, seed, lag, step):
         inc.insert_dag(*(a[lo:lo + step] for a in args))
         inc.run_consensus()
     _same_state(_state(batch), _state(inc))
+
+
+def test_queued_trap_fixture_oracle():
+    """tests/golden/trap_schedule.json: on the per-sync schedule
+    the late witness stays Undefined and the older lagging event is never
+    received; one batch run decides both (hashgraph.go:809-815, 984-986)."""
+    import json
+    import os
+    from babble_amd.dag import Dag
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "trap_schedule.json")) as f:
+        fx = json.load(f)
+    d = Dag(fx["n"], fx["N"], fx["seed"], lagging=fx["lagging"], lag_div=fx["lag_div"], sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    b = Oracle(fx["n"], d.participant_ids, capacity=fx["N"])
+    b.insert_dag(*args)
+    b.run_consensus()
+    o = Oracle(fx["n"], d.participant_ids, capacity=fx["N"])
+    for lo in range(0, fx["N"], fx["step"]):
+        o.insert_dag(*(a[lo:lo + fx["step"]] for a in args))
+        o.run_consensus()
+    for which, orc in (("per_sync", o), ("batch", b)):
+        res = orc.results()
+        for e, want in fx[which]["fame"].items():
+            assert res["fame"][int(e)] == want, (which, e)
+        for e, want in fx[which]["round_received"].items():
+            assert res["round_received"][int(e)] == (UNSET if want is None else want), (which, e)
+        assert len(orc.consensus_order()) == fx[which]["consensus_events"], which
+    w = fx["trapped_witness"]
+    assert o.results()["witness"][w] == 1

@@ -27,7 +27,7 @@ for s in "$@"; do
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
-    pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_flow|k_fd_walk|k_fd_transpose|k_fame|k_round2" --cfg 3 ;;
+    pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_" --cfg 3 ;;
     pmct) step pmc_t 900 bash tools/pmc.sh t "k_flow_transpose|k_fd_transpose" --cfg 3 ;;
     prof3) step prof_c3 900 bash tools/prof.sh c3 --cfg 3 --steps 3 --warmup 1 ;;
   esac
