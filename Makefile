@@ -13,7 +13,7 @@ babble_amd/libbabble_gen.so: babble_amd/csrc/dag_gen.c babble_amd/csrc/dag_gen.h
 	$(CC) -O2 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
 
 babble_amd/libbabble_hip.so: $(ENGINE_SRC) $(ENGINE_HDR)
-	$(HIPCC) $(HIPFLAGS) -Iinclude -shared -o $@ $(ENGINE_SRC)
+	$(HIPCC) $(HIPFLAGS) -Iinclude -shared -o $@ $(ENGINE_SRC) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle/liboracle.so: oracle/hg_oracle.c oracle/hg_oracle.h
 	$(MAKE) -C oracle

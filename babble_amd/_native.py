@@ -24,7 +24,7 @@ SYMBOLS = (
     "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_round_info", "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
-    "bh_hash_bodies", "bh_verify_signatures",
+    "bh_hash_bodies", "bh_verify_signatures", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
 )
 
 
@@ -97,5 +97,11 @@ def load():
     L.bh_hash_bodies.restype = C.c_int
     L.bh_verify_signatures.argtypes = [P, VP, VP, VP, VP, I64, VP, I32, VP]
     L.bh_verify_signatures.restype = C.c_int
+    L.bh_comm_unique_id.argtypes = [VP]
+    L.bh_comm_unique_id.restype = C.c_int
+    L.bh_comm_init.argtypes = [P, I32, I32, VP]
+    L.bh_comm_init.restype = C.c_int
+    L.bh_shard_range.argtypes = [I64, I32, I32, C.POINTER(I64), C.POINTER(I64)]
+    L.bh_shard_range.restype = None
     _LIB = L
     return L

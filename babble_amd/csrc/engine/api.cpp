@@ -1,10 +1,23 @@
 // api.cpp -- C ABI of libbabble_hip (include/babble_hip.h): host state of the
 // drop-in Hashgraph, insert validation, stage orchestration on one HIP
-// stream, result queries.  No CPU fallback: every consensus stage runs as
-// HIP kernels on the device; without a device bh_create fails.
+// stream per shard, result queries.  No CPU fallback: every consensus stage
+// runs as HIP kernels on the device; without a device bh_create fails.
+//
+// Sharding.  A handle may be one shard of a group of
+// `world` shards, each holding the whole DAG on its own device (or sharing
+// one): an in-process group (bh_config.device_ids, shard 0 is the handle the
+// caller holds and owns the others) or one shard per process joined by an
+// RCCL communicator (bh_comm_init).  Each pass runs the same kernels on
+// every shard; the split parts -- LA columns of the coordinate dataflow,
+// DecideFame rounds, frame sorts -- cover the shard's range only and are
+// then exchanged (peer copies over xGMI in-process, ncclBroadcast per range
+// across processes), so every shard ends each pass with identical arrays.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -87,6 +100,14 @@ struct bh_handle {
   float stage_ms[NSTAGE]{};
   int64_t iters = 0;
   int64_t *d_counters_host = nullptr;
+  // sharding
+  int32_t rank = 0, world = 1;
+  std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
+  ncclComm_t comm = nullptr;       // multi-process group (bh_comm_init)
+  bool shard_cols = false;         // split the coordinate dataflow's LA columns (else every shard computes all)
+  float xchg_ms = 0;               // exchange time of the last pass sequence (host wall, incl. waits)
+  std::vector<int32_t> wofs_h;     // [R + 1] witness offsets (fame exchange ranges; launch size)
+  std::vector<int32_t> fofs_h;     // [P + 1] frame offsets (order exchange ranges)
 
   int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -121,7 +142,8 @@ void free_all(bh_handle *h) {
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
-                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm,
+                  d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm,
                   d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -133,6 +155,7 @@ void free_all(bh_handle *h) {
   for (auto &e : h->ev_sweep)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->comm) (void)ncclCommDestroy(h->comm);
 }
 
 // upload events inserted since the last upload
@@ -194,25 +217,132 @@ static bool use_flow(const bh::Dev &d) {
   return bh::flow_eligible(d) && !(e && !strcmp(e, "chunk"));
 }
 
+// ---------------------------------------------------------------------------
+// shards: ranges, local execution, exchanges
+
+// [lo, hi) of `items` owned by shard `rank` of `world`: contiguous, sizes
+// differ by at most one (bh_shard_range exposes it to the tests)
+inline void shard_range(int64_t items, int32_t world, int32_t rank, int64_t *lo, int64_t *hi) {
+  *lo = items * rank / world;
+  *hi = items * (rank + 1) / world;
+}
+
+// the shards this process drives for handle h
+inline std::vector<bh_handle *> local_shards(bh_handle *h) {
+  return h->group.empty() ? std::vector<bh_handle *>{h} : h->group;
+}
+
+// run fn on every local shard: one host thread per shard of an in-process
+// group (each on its own device and stream; the round loop polls its device
+// from the host), inline otherwise.  The first failure is reported on h.
+template <class F>
+int run_local(bh_handle *h, F fn) {
+  if (h->group.size() <= 1) return fn(h);
+  const size_t G = h->group.size();
+  std::vector<int> rc(G, BH_OK);
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < G; ++i)
+    th.emplace_back([&, i] {
+      bh_handle *s = h->group[i];
+      if (hipSetDevice(s->device) != hipSuccess) { rc[i] = s->fail(BH_ERR_DEVICE, "hipSetDevice"); return; }
+      rc[i] = fn(s);
+    });
+  for (auto &t : th) t.join();
+  for (size_t i = 0; i < G; ++i)
+    if (rc[i] != BH_OK) {
+      if (h->group[i] != h) h->err = "shard " + std::to_string(i) + ": " + h->group[i]->err;
+      (void)hipSetDevice(h->device);
+      return rc[i];
+    }
+  (void)hipSetDevice(h->device);
+  return BH_OK;
+}
+
+// All-gather of per-shard byte ranges of one device buffer (same layout on
+// every shard): shard r owns [off[r], off[r] + len[r]) of the buffer `sel`
+// selects; afterwards every shard holds every range.  In-process: each
+// shard's stream waits for the owner's work, then peer-copies the range
+// (xGMI between devices, a device copy on a shared one).  Across processes:
+// one ncclBroadcast per owner, in place, grouped.
+template <class Sel>
+int exchange(bh_handle *h, Sel sel, const std::vector<size_t> &off, const std::vector<size_t> &len) {
+  if (h->world <= 1) return BH_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (h->comm) {
+    uint8_t *base = reinterpret_cast<uint8_t *>(sel(h));
+    if (ncclGroupStart() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupStart");
+    for (int r = 0; r < h->world; ++r)
+      if (len[r] && ncclBroadcast(base + off[r], base + off[r], len[r], ncclChar, r, h->comm, h->stream) != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return h->fail(BH_ERR_DEVICE, "ncclBroadcast");
+      }
+    if (ncclGroupEnd() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupEnd");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  } else {
+    const size_t G = h->group.size();
+    std::vector<hipEvent_t> ready(G);
+    for (size_t r = 0; r < G; ++r) {
+      bh_handle *o = h->group[r];
+      HIPCHK(h, hipSetDevice(o->device));
+      HIPCHK(h, hipEventCreateWithFlags(&ready[r], hipEventDisableTiming));
+      HIPCHK(h, hipEventRecord(ready[r], o->stream));
+    }
+    for (size_t t = 0; t < G; ++t) {
+      bh_handle *dst = h->group[t];
+      HIPCHK(h, hipSetDevice(dst->device));
+      uint8_t *db = reinterpret_cast<uint8_t *>(sel(dst));
+      for (size_t r = 0; r < G; ++r) {
+        if (r == t || !len[r]) continue;
+        bh_handle *src = h->group[r];
+        HIPCHK(h, hipStreamWaitEvent(dst->stream, ready[r], 0));
+        HIPCHK(h, hipMemcpyPeerAsync(db + off[r], dst->device, reinterpret_cast<uint8_t *>(sel(src)) + off[r],
+                                     src->device, len[r], dst->stream));
+      }
+    }
+    for (size_t t = 0; t < G; ++t) {
+      HIPCHK(h, hipSetDevice(h->group[t]->device));
+      HIPCHK(h, hipStreamSynchronize(h->group[t]->stream));
+      (void)hipEventDestroy(ready[t]);
+    }
+    HIPCHK(h, hipSetDevice(h->device));
+  }
+  h->xchg_ms += std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return BH_OK;
+}
+
+// per-shard ranges of a table of `items` entries of `esz` bytes each
+std::vector<size_t> range_bytes(const bh_handle *h, int64_t items, size_t esz, bool lengths,
+                                const std::vector<int32_t> *ofs = nullptr) {
+  std::vector<size_t> v((size_t)h->world);
+  for (int r = 0; r < h->world; ++r) {
+    int64_t lo, hi;
+    shard_range(items, h->world, r, &lo, &hi);
+    if (ofs) { lo = (*ofs)[(size_t)lo]; hi = (*ofs)[(size_t)hi]; }  // item ranges -> entry ranges
+    v[(size_t)r] = lengths ? (size_t)(hi - lo) * esz : (size_t)lo * esz;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
 // stage 1: coordinates, Lamport timestamps, rounds, witnesses
-int stage_rounds(bh_handle *h) {
+
+// coordinates up to the dataflow kernel (this shard's LA columns when split)
+int rounds_coords(bh_handle *h) {
   int rc;
   if ((rc = upload(h))) return rc;
   Dev &d = h->d;
   d.N = (int64_t)h->h_creator.size();
+  h->xchg_ms = 0;
   if ((rc = set_chain_tables(h))) return rc;
   hipStream_t s = h->stream;
   HIPCHK(h, hipEventRecord(h->ev[0], s));
   bh::launch_prep(d, s);
-  bool walked = false;
   if (use_flow(d)) {
     bh::launch_flow_desc(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
     bh::launch_flow(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
-    bh::launch_flow_transpose(d, s);
     h->sweep_kernel = bh::flow32_eligible(d) ? "k_flow32" : "k_flow";
-    walked = true;
   } else {
     bh::launch_chunk_depth(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
@@ -221,6 +351,17 @@ int stage_rounds(bh_handle *h) {
     bh::launch_permute(d, s);
     h->sweep_kernel = "k_la_sweep";
   }
+  HIPCHK(h, hipGetLastError());
+  return BH_OK;
+}
+
+// the rest: LA rows + firstDescendants, the round loop, witness tables
+int rounds_loop(bh_handle *h) {
+  int rc;
+  Dev &d = h->d;
+  hipStream_t s = h->stream;
+  const bool walked = use_flow(d);
+  if (walked) bh::launch_flow_transpose(d, s);
   bh::launch_first_descendants(d, s, walked);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
@@ -229,6 +370,7 @@ int stage_rounds(bh_handle *h) {
     HIPCHK(h, hipEventRecord(h->ev[2], s));
     h->R = 0;
     h->n_div = 0;
+    h->wofs_h.assign(1, 0);
     h->stage = 1;
     return BH_OK;
   }
@@ -276,6 +418,9 @@ int stage_rounds(bh_handle *h) {
   bh::launch_assign_rounds(d, h->n_div, h->P, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[2], s));
+  h->wofs_h.resize((size_t)h->R + 1);
+  HIPCHK(h, hipMemcpyAsync(h->wofs_h.data(), d.wofs, ((size_t)h->R + 1) * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
   h->n_div = d.N;
   // rounds new to this call join PendingRounds undecided (hashgraph.go:809-815;
   // every round >= LastConsensusRound is queued when it first appears)
@@ -284,9 +429,33 @@ int stage_rounds(bh_handle *h) {
   return BH_OK;
 }
 
-int stage_fame(bh_handle *h) {
+int stage_rounds(bh_handle *h) {
+  int rc;
+  if ((rc = run_local(h, rounds_coords))) return rc;
+  if (h->world > 1 && h->shard_cols && use_flow(h->d)) {
+    // LA columns: shard r computed columns [col0, col0 + ncol), each a
+    // contiguous (la_rows + 64)-int32 run of la_col
+    const size_t colb = (size_t)(h->d.la_rows + 64) * 4;
+    std::vector<size_t> off = range_bytes(h, h->d.n, colb, false), len = range_bytes(h, h->d.n, colb, true);
+    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.la_col; }, off, len))) return rc;
+  }
+  return run_local(h, rounds_loop);
+}
+
+// ---------------------------------------------------------------------------
+// stage 2: DecideFame -- this shard's rounds, then exchanged
+
+int fame_local(bh_handle *h) {
   if (h->stage < 1) return h->fail(BH_ERR_STATE, "DecideFame before DivideRounds");
-  bh::launch_fame(h->d, h->R, h->stream);
+  int64_t r0, r1;
+  shard_range(h->R, h->world, h->rank, &r0, &r1);
+  bh::launch_fame(h->d, h->R, (int32_t)r0, (int32_t)r1, h->stream);
+  HIPCHK(h, hipGetLastError());
+  return BH_OK;
+}
+
+int fame_finish(bh_handle *h) {
+  bh::launch_fame_scatter(h->d, h->wofs_h[(size_t)h->R], h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
   h->decided_h.assign((size_t)h->R, 0);
@@ -303,7 +472,35 @@ int stage_fame(bh_handle *h) {
   return BH_OK;
 }
 
-int stage_rr(bh_handle *h) {
+int stage_fame(bh_handle *h) {
+  int rc;
+  if ((rc = run_local(h, fame_local))) return rc;
+  if (h->world > 1) {
+    const int64_t R = h->R;
+    const int npad = h->d.npad;
+    struct {
+      void *(*sel)(bh_handle *);
+      size_t esz;
+      bool by_witness;
+    } parts[] = {
+        {[](bh_handle *x) -> void * { return x->d.wfame; }, 1, true},
+        {[](bh_handle *x) -> void * { return x->d.decided; }, 1, false},
+        {[](bh_handle *x) -> void * { return x->d.nfam; }, 4, false},
+        {[](bh_handle *x) -> void * { return x->d.minla; }, (size_t)npad * 4, false},
+    };
+    for (auto &pt : parts) {
+      const std::vector<int32_t> *ofs = pt.by_witness ? &h->wofs_h : nullptr;
+      if ((rc = exchange(h, pt.sel, range_bytes(h, R, pt.esz, false, ofs), range_bytes(h, R, pt.esz, true, ofs))))
+        return rc;
+    }
+  }
+  return run_local(h, fame_finish);
+}
+
+// ---------------------------------------------------------------------------
+// stage 3: DecideRoundReceived (every shard, every event)
+
+int stage_rr_local(bh_handle *h) {
   if (h->stage < 2) return h->fail(BH_ERR_STATE, "DecideRoundReceived before DecideFame");
   bh::launch_round_received(h->d, h->R, h->P, h->stream);
   HIPCHK(h, hipGetLastError());
@@ -318,38 +515,67 @@ int stage_rr(bh_handle *h) {
   return BH_OK;
 }
 
-int stage_order(bh_handle *h) {
+int stage_rr(bh_handle *h) { return run_local(h, stage_rr_local); }
+
+// ---------------------------------------------------------------------------
+// stage 4: ProcessDecidedRounds -- frames sorted by range, then exchanged
+
+// P after this call: PendingRounds walked in order while their (sticky)
+// decided flag is set (hashgraph.go:1041-1122)
+int32_t next_prefix(const bh_handle *h) {
+  int32_t P1 = h->P;
+  while (P1 < h->R && h->pend_dec[(size_t)P1]) ++P1;
+  return P1;
+}
+
+int order_local(bh_handle *h) {
   if (h->stage < 3) return h->fail(BH_ERR_STATE, "ProcessDecidedRounds before DecideRoundReceived");
   Dev &d = h->d;
   hipStream_t s = h->stream;
-  // ProcessDecidedRounds (hashgraph.go:1041-1122): PendingRounds in order
-  // while their (sticky) decided flag is set
-  int32_t P1 = h->P;
-  while (P1 < h->R && h->pend_dec[(size_t)P1]) ++P1;
+  const int32_t P1 = next_prefix(h);
   h->pinned_state[bh::ST_COUNT] = P1;  // pinned staging word (the first ST_COUNT hold the loop's done flag)
   HIPCHK(h, hipMemcpyAsync(d.state + bh::ST_P, h->pinned_state + bh::ST_COUNT, 4, hipMemcpyHostToDevice, s));
-  bh::launch_order(d, h->R, s);
+  bh::launch_order_buckets(d, h->R, s);
+  int64_t f0, f1;
+  shard_range(P1, h->world, h->rank, &f0, &f1);
+  bh::launch_order_sort(d, (int32_t)f0, (int32_t)f1, s);
+  HIPCHK(h, hipGetLastError());
+  if (h->world > 1) {  // frame offsets: the order exchange's ranges
+    h->fofs_h.resize((size_t)P1 + 1);
+    if (P1 > 0) HIPCHK(h, hipMemcpyAsync(h->fofs_h.data(), d.frame_ofs, (size_t)P1 * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(h->fofs_h.data() + P1, d.state + bh::ST_NCONS, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+  }
+  return BH_OK;
+}
+
+int order_finish(bh_handle *h) {
+  Dev &d = h->d;
+  hipStream_t s = h->stream;
+  const int32_t P1 = next_prefix(h);
+  if (h->world > 1) bh::launch_cons_pos(d, h->fofs_h[(size_t)P1], s);  // frames sorted elsewhere arrived
   bh::launch_trap_processed(d, h->P, P1, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[5], s));
   HIPCHK(h, hipStreamSynchronize(s));
   int32_t st[bh::ST_COUNT];
-  int64_t ctr[4];
   HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(ctr, d.counters, sizeof ctr, hipMemcpyDeviceToHost));
   h->P = P1;
   h->ncons = st[bh::ST_NCONS];
-  h->cons_txs = ctr[0];
-  h->cons_loaded = ctr[1];
+  h->cons_txs = h->cons_loaded = 0;
   h->blocks.clear();
   if (h->P > 0) {
-    std::vector<int32_t> cnt(h->P), ofs(h->P);
+    std::vector<int32_t> cnt(h->P), ofs(h->P), ld(h->P);
     std::vector<int64_t> ntx(h->P);
     HIPCHK(h, hipMemcpy(cnt.data(), d.frame_cnt, h->P * 4, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemcpy(ofs.data(), d.frame_ofs, h->P * 4, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemcpy(ntx.data(), d.frame_ntx, h->P * 8, hipMemcpyDeviceToHost));
-    for (int32_t r = 0; r < h->P; ++r)
+    HIPCHK(h, hipMemcpy(ld.data(), d.frame_loaded, h->P * 4, hipMemcpyDeviceToHost));
+    for (int32_t r = 0; r < h->P; ++r) {
       if (cnt[r] > 0) h->blocks.push_back(Block{r, ofs[r], cnt[r], ntx[r]});
+      h->cons_txs += ntx[r];
+      h->cons_loaded += ld[r];
+    }
   }
   h->stage = 4;
   for (int i = 0; i < NSTAGE; ++i) {
@@ -382,16 +608,80 @@ int stage_order(bh_handle *h) {
   return BH_OK;
 }
 
+int stage_order(bh_handle *h) {
+  int rc;
+  if ((rc = run_local(h, order_local))) return rc;
+  if (h->world > 1) {
+    const int32_t P1 = next_prefix(h);
+    // order: frame f's sorted events at [frame_ofs[f], frame_ofs[f + 1])
+    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.order; },
+                       range_bytes(h, P1, 4, false, &h->fofs_h), range_bytes(h, P1, 4, true, &h->fofs_h))))
+      return rc;
+    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.frame_ntx; }, range_bytes(h, P1, 8, false),
+                       range_bytes(h, P1, 8, true))))
+      return rc;
+    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.frame_loaded; }, range_bytes(h, P1, 4, false),
+                       range_bytes(h, P1, 4, true))))
+      return rc;
+  }
+  return run_local(h, order_finish);
+}
+
 }  // namespace
 
 // ===========================================================================
 extern "C" {
 
+static int create_one(const bh_config *cfg, int device, bh_handle **out);
+
+void bh_destroy(bh_handle *h);
+
 int bh_create(const bh_config *cfg, bh_handle **out) {
   if (!cfg || !out || cfg->n_participants < 1 || cfg->max_events < 0 || !cfg->participant_ids)
     return BH_ERR_INVALID;
-  if (cfg->n_devices > 1) return BH_ERR_INVALID;  // sharded handles: not in this build
   *out = nullptr;
+  if (cfg->n_devices <= 1) return create_one(cfg, cfg->n_devices == 1 && cfg->device_ids ? cfg->device_ids[0] : cfg->device, out);
+  if (!cfg->device_ids) return BH_ERR_INVALID;
+  // in-process shard group: shard 0 is the handle returned, it owns the rest
+  const int G = cfg->n_devices;
+  std::vector<bh_handle *> g((size_t)G, nullptr);
+  for (int r = 0; r < G; ++r) {
+    const int rc = create_one(cfg, cfg->device_ids[r], &g[(size_t)r]);
+    if (rc != BH_OK) {
+      for (bh_handle *x : g) bh_destroy(x);
+      return rc;
+    }
+  }
+  // BH_SHARD_COORDS=columns splits the coordinate dataflow's LA columns
+  // between shards and all-gathers them; by default every shard runs the
+  // whole dataflow (it is bound by the DAG's critical path, not by its
+  // columns, so splitting saves no time and the gather costs (G-1)/G of LA)
+  const char *sc = getenv("BH_SHARD_COORDS");
+  const bool cols = sc && !strcmp(sc, "columns");
+  for (int r = 0; r < G; ++r) {
+    bh_handle *x = g[(size_t)r];
+    x->rank = r;
+    x->world = G;
+    x->shard_cols = cols;
+    int64_t c0 = 0, c1 = x->d.n;
+    if (cols) shard_range(x->d.n, G, r, &c0, &c1);
+    x->d.col0 = (int32_t)c0;
+    x->d.ncol = (int32_t)(c1 - c0);
+    // peer access between the group's devices (xGMI); same-device pairs need none
+    (void)hipSetDevice(x->device);
+    for (int q = 0; q < G; ++q)
+      if (cfg->device_ids[q] != x->device) {
+        const hipError_t e = hipDeviceEnablePeerAccess(cfg->device_ids[q], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      }
+  }
+  g[0]->group = g;
+  (void)hipSetDevice(g[0]->device);
+  *out = g[0];
+  return BH_OK;
+}
+
+static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   bh_handle *h = new bh_handle();
   const int n = cfg->n_participants;
   for (int i = 1; i < n; ++i)
@@ -400,15 +690,15 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
       return BH_ERR_INVALID;  // peers must be ID-sorted (peers.go:63-73)
     }
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device) {
+  if (device < 0 || hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) {
     delete h;
     return BH_ERR_DEVICE;
   }
-  if (hipSetDevice(cfg->device) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess) {
     delete h;
     return BH_ERR_DEVICE;
   }
-  h->device = cfg->device;
+  h->device = device;
   h->pids.assign(cfg->participant_ids, cfg->participant_ids + n);
   {
     size_t sz = 8;
@@ -432,6 +722,8 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   d.ring_log2 = n < 256 ? 14 : 12;
   d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;  // sweep LDS: one workgroup per CU below 256 columns
   d.N = 0;
+  d.col0 = 0;
+  d.ncol = n;
   const int64_t C = std::max<int64_t>(h->cap, 1);
   d.R_cap = (int32_t)std::min<int64_t>(C / d.sm + 2, INT32_MAX / 2);
   d.W_cap = C + n;
@@ -469,6 +761,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
   A(&d.wrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C); A(&d.trapped, C); A(&d.blocked, R1);
+  A(&d.wfame, (size_t)d.W_cap); A(&d.frame_loaded, R1);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
   A(&d.frame_cnt, R1); A(&d.frame_ofs, R1); A(&d.frame_cur, R1); A(&d.blk_of_frame, R1);
   A(&d.order, C); A(&d.cons_pos, C); A(&d.frame_ntx, R1); A(&d.counters, 4);
@@ -507,6 +800,13 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
 
 void bh_destroy(bh_handle *h) {
   if (!h) return;
+  if (!h->group.empty() && h->group[0] == h)  // an in-process group's owner
+    for (size_t r = 1; r < h->group.size(); ++r) {
+      bh_handle *x = h->group[r];
+      (void)hipSetDevice(x->device);
+      free_all(x);
+      delete x;
+    }
   (void)hipSetDevice(h->device);
   free_all(h);
   delete h;
@@ -514,8 +814,25 @@ void bh_destroy(bh_handle *h) {
 
 const char *bh_last_error(const bh_handle *h) { return h ? h->err.c_str() : "null handle"; }
 
+static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted);
+
 int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted) {
   if (!h || !ev) return BH_ERR_INVALID;
+  if (h->group.size() <= 1) return insert_one(h, ev, status, n_accepted);
+  // every shard holds the whole DAG: the same batch, validated the same way
+  int rc = BH_OK;
+  for (size_t r = 0; r < h->group.size(); ++r) {
+    bh_handle *x = h->group[r];
+    (void)hipSetDevice(x->device);
+    const int q = r == 0 ? insert_one(x, ev, status, n_accepted) : insert_one(x, ev, nullptr, nullptr);
+    if (r == 0) rc = q;
+    else if (q == BH_ERR_DEVICE) rc = h->fail(q, "shard %zu: %s", r, x->err.c_str());
+  }
+  (void)hipSetDevice(h->device);
+  return rc;
+}
+
+static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted) {
   if (!ev->creator_id || !ev->index || !ev->self_parent_index || !ev->other_parent_creator_id ||
       !ev->other_parent_index || !ev->hash || !ev->sig_r || !ev->n_transactions)
     return h->fail(BH_ERR_INVALID, "null field in bh_events");
@@ -625,8 +942,49 @@ int bh_run_consensus(bh_handle *h) {
 }
 int bh_synchronize(bh_handle *h) {
   if (!h) return BH_ERR_INVALID;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (bh_handle *x : local_shards(h)) {
+    HIPCHK(h, hipSetDevice(x->device));
+    HIPCHK(h, hipStreamSynchronize(x->stream));
+  }
+  HIPCHK(h, hipSetDevice(h->device));
   return BH_OK;
+}
+
+int bh_comm_unique_id(uint8_t *id) {
+  if (!id) return BH_ERR_INVALID;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return BH_ERR_DEVICE;
+  memcpy(id, u.internal, sizeof u.internal);
+  return BH_OK;
+}
+
+int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id) {
+  if (!h || !id || world < 1 || rank < 0 || rank >= world || !h->group.empty() || h->comm)
+    return BH_ERR_INVALID;
+  if (h->n_div || !h->h_creator.empty()) return h->fail(BH_ERR_STATE, "bh_comm_init after events were inserted");
+  (void)hipSetDevice(h->device);
+  if (world > 1) {
+    ncclUniqueId u;
+    memcpy(u.internal, id, sizeof u.internal);
+    if (ncclCommInitRank(&h->comm, world, u, rank) != ncclSuccess)
+      return h->fail(BH_ERR_DEVICE, "ncclCommInitRank(%d of %d) failed", rank, world);
+  }
+  h->rank = rank;
+  h->world = world;
+  const char *sc = getenv("BH_SHARD_COORDS");  // see bh_create
+  h->shard_cols = sc && !strcmp(sc, "columns");
+  int64_t c0 = 0, c1 = h->d.n;
+  if (h->shard_cols) shard_range(h->d.n, world, rank, &c0, &c1);
+  h->d.col0 = (int32_t)c0;
+  h->d.ncol = (int32_t)(c1 - c0);
+  return BH_OK;
+}
+
+void bh_shard_range(int64_t items, int32_t world, int32_t rank, int64_t *lo, int64_t *hi) {
+  int64_t a = 0, b = 0;
+  if (world >= 1 && rank >= 0 && rank < world && items >= 0) shard_range(items, world, rank, &a, &b);
+  if (lo) *lo = a;
+  if (hi) *hi = b;
 }
 
 int bh_get_stats(bh_handle *h, bh_stats *o) {
@@ -775,9 +1133,12 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     if ((rc = set_chain_tables(h))) return rc;
     bh::launch_prep(d, h->stream);
     const bool walked = use_flow(d);
-    if (walked) bh::launch_flow_coordinates(d, h->stream);
-    else bh::launch_coordinates(d, h->stream);
-    bh::launch_first_descendants(d, h->stream, walked);
+    Dev full = d;  // every LA column, whatever this shard's share of the dataflow
+    full.col0 = 0;
+    full.ncol = d.n;
+    if (walked) bh::launch_flow_coordinates(full, h->stream);
+    else bh::launch_coordinates(full, h->stream);
+    bh::launch_first_descendants(full, h->stream, walked);
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
     h->stage = 0;
@@ -801,7 +1162,8 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
 int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap) {
   if (!h) return 0;
   for (int i = 0; i < NSTAGE && i < cap; ++i) ms[i] = h->stage_ms[i];
-  return NSTAGE;
+  if (cap > NSTAGE) ms[NSTAGE] = h->xchg_ms;
+  return NSTAGE + 1;
 }
 
 int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {

@@ -72,6 +72,7 @@ struct Dev {
   int32_t *opdesc;  // [N] chain-major other-parent (creator << 22 | index), -1 = none
   int32_t *la_col;  // [n][la_rows+64] column-major LA, chain-major rows (aliases la_ev)
   int32_t *lt_row;  // [la_rows+64] LT by chain-major row
+  int32_t col0, ncol;  // k_flow / k_flow32: this shard's LA columns [col0, col0 + ncol) (+ the LT workgroup)
   int32_t *hdone;  // mapped pinned host word: set when the round loop is done
   int32_t flow_ltclamp;  // k_flow32 LT limit (2^21 - 256; BH_FLOW_LTCLAMP lowers it to test the fallback)
   uint8_t *depth, *chunk_maxd;
@@ -101,6 +102,7 @@ struct Dev {
   int8_t *witness, *fame;
   // fame / received
   int8_t *decided;
+  int8_t *wfame;   // [W] fame of witness wofs[r] + i (chain order), as the fame pass decides it
   int32_t *nfam, *minla;
   int32_t *rr;
   // per-sync schedule (hashgraph.go:809-815, roundInfo.go:35):
@@ -116,6 +118,7 @@ struct Dev {
   int32_t *order;
   int64_t *cons_pos;
   int64_t *frame_ntx;
+  int32_t *frame_loaded;  // [R] loaded events per frame (IsLoaded, event.go:169-178)
   int64_t *counters;  // [0] consensus txs, [1] loaded consensus events, [2] unused, [3] undetermined
   // diagnostic phase counters (BH_DIAG=1 builds the buffer; null otherwise).
   // Only a separate diagnostic run reads them; no result depends on them.
@@ -162,13 +165,22 @@ void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wc
 // division) also get their initial fame / rr / consensus position, and are
 // marked trapped when they are witnesses of a round < P (already processed)
 void launch_assign_rounds(const Dev &d, int64_t n_prev, int32_t P, hipStream_t s);
-void launch_fame(const Dev &d, int32_t R, hipStream_t s);
+// DecideFame of rounds [r0, r1) into wfame / decided / nfam / minla
+void launch_fame(const Dev &d, int32_t R, int32_t r0, int32_t r1, hipStream_t s);
+// wfame -> per-event fame (trapped witnesses stay Undefined); W witnesses
+void launch_fame_scatter(const Dev &d, int32_t W, hipStream_t s);
 // rr of events still undetermined (rr already set is kept); rounds < P are
 // live-decided iff no trapped witness; counters[3] = undetermined after it;
 // frame_cnt[r] = events received in r (every r < R)
 void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s);
-// frames / order / blocks of rounds [0, P): ST_P holds P (set by the host)
-void launch_order(const Dev &d, int32_t R, hipStream_t s);
+// frames / order / blocks of rounds [0, P): ST_P holds P (set by the host).
+// launch_order_buckets: frame offsets and unsorted frame buckets of every
+// frame; launch_order_sort: sort frames [f0, f1), their tx / loaded counts
+// and consensus positions
+void launch_order_buckets(const Dev &d, int32_t R, hipStream_t s);
+void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s);
+// cons_pos[order[i]] = i for i < ncons (after frames sorted elsewhere arrive)
+void launch_cons_pos(const Dev &d, int64_t ncons, hipStream_t s);
 // witnesses of rounds [P0, P1) still Undefined when those rounds were processed
 void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s);
 void configure_fd_kernels();

@@ -24,9 +24,9 @@ namespace bh {
 
 // DecideFame for n > 128 (the k_round / k_round_wide path, where the round
 // loop keeps no ballots): S_j recomputed from LA / FD rows read from HBM
-__global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
+__global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R, int32_t r0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
-  const int r = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+  const int r = r0 + (int)blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const int n = d.n, npad = d.npad, sm = d.sm;
   const int WW = (n + 63) >> 6;       // words per voter bitset
   // carve
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void k_fame(Dev d, int32_t R) {
   }
   // ---- publish ----
   __syncthreads();
-  for (int x = t; x < nx; x += nt) d.fame[xs[x]] = d.trapped[xs[x]] ? 0 : (int8_t)dec[x];  // trapped: Undefined
+  for (int x = t; x < nx; x += nt) d.wfame[xb + x] = (int8_t)dec[x];
   __syncthreads();
   if (t == 0) {
     d.decided[r] = misc[0] == 0 ? 1 : 0;
@@ -228,7 +228,7 @@ __device__ __forceinline__ uint32_t fame_ballot_word(const unsigned long long *b
   return word;
 }
 
-__global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R) {
+__global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R, int32_t r0) {
   __shared__ uint32_t V[2][128][4];  // votes: [cur][x chain][word over W(j-1) chains]
   __shared__ uint32_t S[128][4];     // ssm rows of W(j), restricted to W(j-1)
   __shared__ uint32_t wx[4], wp[4], wc[4];  // W(r), W(j-1), W(j)
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R) {
   __shared__ int32_t misc[2];  // [0] undecided, [1] conflicting decisions
   __shared__ int32_t frow[128];  // LA rows of famous witnesses
   __shared__ int32_t nfam_s;
-  const int r = blockIdx.x, t = threadIdx.x, nt = blockDim.x;
+  const int r = r0 + (int)blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const int n = d.n, npad = d.npad, sm = d.sm;
   if (t < 4) wx[t] = fame_wmask_word(d, r, t);
   for (int q = t; q < 128; q += nt) {
@@ -340,7 +340,12 @@ __global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R) {
   }
   // ---- publish ----
   __syncthreads();
-  if (t < 128 && isx) d.fame[xev[x]] = d.trapped[xev[x]] ? 0 : (int8_t)dec[x];  // trapped: Undefined (A.12)
+  if (t < 128 && isx) {  // witness x's position in W(r): the witnesses of lower chains before it
+    int rank = 0;
+    for (int w = 0; w < (x >> 5); ++w) rank += __popc(wx[w]);
+    rank += __popc(wx[x >> 5] & ((1u << (x & 31)) - 1u));
+    d.wfame[d.wofs[r] + rank] = (int8_t)dec[x];
+  }
   if (t == 0) {
     d.decided[r] = misc[0] == 0 ? 1 : 0;
     if (misc[1]) d.state[ST_ERR] = 2;
@@ -369,13 +374,27 @@ void configure_fame_kernels() {
   (void)hipFuncSetAttribute((const void *)k_fame, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
 }
 
-void launch_fame(const Dev &d, int32_t R, hipStream_t s) {
-  if (R <= 0) return;
+void launch_fame(const Dev &d, int32_t R, int32_t r0, int32_t r1, hipStream_t s) {
+  if (r1 <= r0) return;
   if (d.fd_cols) {  // masks from the k_round2 loop
-    k_fame_masks<<<R, 256, 0, s>>>(d, R);
+    k_fame_masks<<<r1 - r0, 256, 0, s>>>(d, R, r0);
     return;
   }
-  k_fame<<<R, 256, fame_lds_bytes(d.n), s>>>(d, R);
+  k_fame<<<r1 - r0, 256, fame_lds_bytes(d.n), s>>>(d, R, r0);
+}
+
+// per-event fame from the witness-ordered results; a trapped witness
+//  stays Undefined whatever the votes say
+__global__ void k_fame_scatter(Dev d, int32_t W) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= W) return;
+  const int32_t e = d.wids[i];
+  d.fame[e] = d.trapped[e] ? 0 : d.wfame[i];
+}
+
+void launch_fame_scatter(const Dev &d, int32_t W, hipStream_t s) {
+  if (W <= 0) return;
+  k_fame_scatter<<<(unsigned)((W + 255) / 256), 256, 0, s>>>(d, W);
 }
 
 }  // namespace bh

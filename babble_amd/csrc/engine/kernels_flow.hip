@@ -81,11 +81,10 @@ struct FlowLds {
 };
 
 template <bool LT>
-__device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L, int col0) {
+__device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L, int col) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = d.n;
   const int nw = (n + 63) >> 6;  // compute waves
-  const int col = blockIdx.x + col0;
   const int64_t stride = d.la_rows + 64;
   int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
   for (int c = t; c < n; c += blockDim.x) {
@@ -269,10 +268,12 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L, int col0) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_flow(Dev d, int col0) {
+// workgroups 0 .. ncol-1: this shard's columns col0 + b; workgroup ncol (or
+// every workgroup when lt_only): the Lamport timestamps
+__global__ __launch_bounds__(256) void k_flow(Dev d, int lt_only) {
   __shared__ FlowLds L;  // static: the ring's LDS base is the constant 0
-  if ((int)blockIdx.x + col0 == d.n) flow_body<true>(d, L, col0);
-  else flow_body<false>(d, L, col0);
+  if (lt_only || (int)blockIdx.x == d.ncol) flow_body<true>(d, L, d.n);
+  else flow_body<false>(d, L, d.col0 + (int)blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -332,7 +333,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = d.n;
   const int nw = (n + 63) >> 6;
-  const int col = blockIdx.x;
+  const int col = d.col0 + (int)blockIdx.x;  // this shard's columns; the LT workgroup is the last
   const int64_t stride = d.la_rows + 64;
   int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
   for (int c = t; c < n; c += blockDim.x) {
@@ -509,7 +510,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
 
 __global__ __launch_bounds__(256) void k_flow32(Dev d) {
   __shared__ FlowLds32 L;  // static: the ring's LDS base is the constant 0
-  if ((int)blockIdx.x == d.n) flow32_body<true>(d, L);
+  if ((int)blockIdx.x == d.ncol) flow32_body<true>(d, L);
   else flow32_body<false>(d, L);
 }
 
@@ -672,8 +673,8 @@ void launch_flow_desc(const Dev &d, hipStream_t s) {
 void launch_flow(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
-  if (flow32_eligible(d)) k_flow32<<<d.n + 1, (nw + 2) * 64, 0, s>>>(d);
-  else k_flow<<<d.n + 1, (nw + 2) * 64, 0, s>>>(d, 0);
+  if (flow32_eligible(d)) k_flow32<<<d.ncol + 1, (nw + 2) * 64, 0, s>>>(d);
+  else k_flow<<<d.ncol + 1, (nw + 2) * 64, 0, s>>>(d, 0);
 }
 
 // LT overflowed k_flow32's 21-bit values (ST_FLOWOVF): recompute LT with
@@ -682,7 +683,7 @@ void launch_flow_lt_fallback(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
   k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
-  k_flow<<<1, (nw + 2) * 64, 0, s>>>(d, d.n);
+  k_flow<<<1, (nw + 2) * 64, 0, s>>>(d, 1);
   launch_flow_transpose(d, s);
 }
 

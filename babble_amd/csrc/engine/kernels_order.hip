@@ -227,13 +227,15 @@ __device__ void bitonic_lds(uint64_t *key, int32_t *id, int32_t p2) {
   __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_frame_sort(Dev d) {
+__global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char osm[];
   __shared__ unsigned long long sh_ntx, sh_loaded;
-  const int32_t f = blockIdx.x;
-  if (f >= d.state[ST_P]) return;  // received in a round not yet processed
+  const int32_t f = f0 + (int32_t)blockIdx.x;
   const int32_t cnt = d.frame_cnt[f];
-  if (cnt == 0) return;
+  if (cnt == 0) {
+    if (threadIdx.x == 0) { d.frame_ntx[f] = 0; d.frame_loaded[f] = 0; }
+    return;
+  }
   const int t = threadIdx.x, nt = blockDim.x;
   const int32_t off = d.frame_ofs[f];
   int32_t *ids = d.order + off;
@@ -297,8 +299,7 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d) {
   __syncthreads();
   if (t == 0) {
     d.frame_ntx[f] = (int64_t)sh_ntx;
-    atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[0]), (unsigned long long)sh_ntx);
-    atomicAdd(reinterpret_cast<unsigned long long *>(&d.counters[1]), (unsigned long long)sh_loaded);
+    d.frame_loaded[f] = (int32_t)sh_loaded;
   }
 }
 
@@ -315,14 +316,27 @@ void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s) {
   if (R > 0) k_frame_count<<<(unsigned)((d.N + OB - 1) / OB), 256, 0, s>>>(d);
 }
 
-void launch_order(const Dev &d, int32_t R, hipStream_t s) {
+void launch_order_buckets(const Dev &d, int32_t R, hipStream_t s) {
   if (R <= 0) return;
   k_order_init<<<1, 1024, 0, s>>>(d, R);
   const unsigned g = (unsigned)((d.N + OB - 1) / OB);
   k_frame_scan<<<1, 1024, 0, s>>>(d);
   k_frame_scatter<<<g, 256, 0, s>>>(d);
-  // frames [0, P); P <= R.  Launch R blocks: frames >= P return at once.
-  k_frame_sort<<<R, 1024, FRAME_LDS_MAX * 12, s>>>(d);
+}
+
+void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s) {
+  if (f1 <= f0) return;
+  k_frame_sort<<<f1 - f0, 1024, FRAME_LDS_MAX * 12, s>>>(d, f0);
+}
+
+__global__ void k_cons_pos(Dev d, int64_t ncons) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < ncons) d.cons_pos[d.order[i]] = i;
+}
+
+void launch_cons_pos(const Dev &d, int64_t ncons, hipStream_t s) {
+  if (ncons <= 0) return;
+  k_cons_pos<<<(unsigned)((ncons + 255) / 256), 256, 0, s>>>(d, ncons);
 }
 
 }  // namespace bh

@@ -36,21 +36,55 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
 
+def comm_unique_id():
+    """RCCL id for Hashgraph.comm_init (rank 0 makes it, every rank passes it)."""
+    L = _native.load()
+    buf = (C.c_uint8 * 128)()
+    rc = L.bh_comm_unique_id(buf)
+    if rc != _native.BH_OK:
+        raise HashgraphError(rc, "ncclGetUniqueId failed")
+    return bytes(buf)
+
+
+def shard_range(items, world, rank):
+    """[lo, hi) of `items` owned by shard `rank` of `world` -- the engine's
+    split rule for LA columns, fame rounds and frames (bh_shard_range)."""
+    L = _native.load()
+    lo, hi = C.c_int64(), C.c_int64()
+    L.bh_shard_range(int(items), int(world), int(rank), C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
+
+
 class Hashgraph:
-    def __init__(self, participant_ids, max_events, device=0):
+    def __init__(self, participant_ids, max_events, device=0, devices=None):
+        """devices: a list of HIP ordinals to shard the passes over in this
+        process (repeats allowed: shards sharing one device); None = one
+        device, `device`."""
         self._L = _native.load()
         ids = np.ascontiguousarray(participant_ids, dtype=np.int64)
         if np.any(np.diff(ids) <= 0):
             raise ValueError("participant ids must be sorted ascending (peers.go:63-73)")
         self.participant_ids = ids
         self.n = len(ids)
-        cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
-                             int(device), 0, None)
+        if devices is not None:
+            self._devs = np.ascontiguousarray(devices, dtype=np.int32)
+            cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
+                                 int(self._devs[0]), len(self._devs),
+                                 self._devs.ctypes.data_as(C.POINTER(C.c_int32)))
+        else:
+            cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
+                                 int(device), 0, None)
         h = C.c_void_p()
         rc = self._L.bh_create(C.byref(cfg), C.byref(h))
         if rc != _native.BH_OK:
             raise HashgraphError(rc, "bh_create failed (no HIP device or out of memory)")
         self._h = h
+
+    def comm_init(self, rank, world, uid):
+        """Make this handle shard `rank` of `world` processes (RCCL); call
+        before inserting events.  Every pass is then collective."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._check(self._L.bh_comm_init(self._h, int(rank), int(world), buf))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -213,6 +247,8 @@ class Hashgraph:
         return la, fd
 
     def stage_ms(self):
+        """[coordinates, rounds, fame, round_received, order, exchange] ms of
+        the last run (device events; exchange: host wall time)."""
         buf = (C.c_float * 8)()
         k = self._L.bh_get_stage_ms(self._h, buf, 8)
         return [float(buf[i]) for i in range(k)]

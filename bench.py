@@ -6,8 +6,12 @@ ProcessDecidedRounds (frame sort + blocks), all in libbabble_hip on one GPU.
 The DAG (generation, hashing, signing, H2D copy) is prepared before the timed
 region.  Workload: BASELINE.json's headline config C3 (128 participants,
 10M-event random-gossip DAG).  Multi-GPU: one process per GPU, each orders
-its own DAG (replicas, weak scaling; the reference has no sharded path and
-the engine's passes need no exchange between independent DAGs).
+the same DAG as one shard of a group (strong scaling): DecideFame rounds
+and frame sorts are split between the ranks and exchanged with RCCL
+(ncclBroadcast per range, over xGMI); the coordinate dataflow and the
+round loop -- both serial latency chains -- run on every rank
+(BH_SHARD_COORDS=columns splits the LA columns and all-gathers them
+instead).  --mode replicas runs independent DAGs per rank (weak scaling).
 
 usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--events N]
        torchrun ... bench.py --gpus N ...
@@ -106,6 +110,8 @@ def main():
     ap.add_argument("--sig", type=int, default=0, help="1 = deterministic ECDSA signatures")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="events for the CPU baseline (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--mode", choices=("shards", "replicas"), default="shards",
+                    help="N>1: shard one DAG over the ranks (strong) or order one DAG per rank (weak)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,15 +128,20 @@ def main():
         if not args.quiet and rank == 0:
             print(*a, file=sys.stderr, flush=True)
 
-    from babble_amd import Hashgraph
+    from babble_amd import Hashgraph, comm_unique_id
     from babble_amd.dag import CONFIGS, Dag
     c = CONFIGS[args.cfg]
     N = args.events or c["N"]
+    sharded = world > 1 and args.mode == "shards"
     t0 = time.perf_counter()
-    dag = Dag.config(args.cfg, N=N, sig_mode=args.sig, rank=rank)
+    dag = Dag.config(args.cfg, N=N, sig_mode=args.sig, rank=0 if sharded else rank)
     log(f"generated cfg{args.cfg} n={c['n']} N={N} in {time.perf_counter() - t0:.1f}s")
     t0 = time.perf_counter()
     hg = Hashgraph(dag.participant_ids, N, device=local)
+    if sharded:  # one RCCL communicator of the engine's own, id from rank 0
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        hg.comm_init(rank, world, obj[0])
     st = hg.insert_dag(dag)
     assert not st.any(), "generator produced a rejected event"
     hg.synchronize()
@@ -152,7 +163,7 @@ def main():
     for w in range(args.warmup):
         hg.run_consensus()
         log(f"warmup {w}: stages_ms={['%.2f' % x for x in hg.stage_ms()]}")
-    sweep_ms, stage_tot = [], np.zeros(5)
+    sweep_ms, stage_tot = [], np.zeros(6)
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -166,14 +177,15 @@ def main():
     elapsed = max_over_ranks(elapsed, dist)
     stats = hg.stats()
     ordered = stats.consensus_events
-    total_ordered = sum_over_ranks(ordered * args.steps, dist)
+    # whole-job events ordered: one DAG per step when sharded, one per rank per step as replicas
+    total_ordered = ordered * args.steps if (sharded or world == 1) else sum_over_ranks(ordered * args.steps, dist)
     iters, _ = hg.profile()
     value = total_ordered / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
 
     n = c["n"]
     npad = (n + 3) & ~3
-    stages = dict(zip(["coordinates", "rounds", "fame", "round_received", "order"],
+    stages = dict(zip(["coordinates", "rounds", "fame", "round_received", "order", "exchange"],
                       (stage_tot / args.steps).round(3).tolist()))
     pmc = _pmc_table(n, N)
     # roofline: the path is integer and
@@ -207,7 +219,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -216,7 +228,10 @@ def main():
                                f"DivideRounds + DecideFame + DecideRoundReceived + ProcessDecidedRounds",
                    "participants": n, "events": N, "events_ordered_per_step": ordered,
                    "rounds": stats.last_round + 1, "blocks": stats.blocks,
-                   "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
+                   "parallelism": (f"{world} shards (RCCL): fame rounds + frame sorts split, coordinates "
+                                   f"{os.environ.get('BH_SHARD_COORDS', 'replicated') if os.environ.get('BH_SHARD_COORDS') == 'columns' else 'replicated'}"
+                                   f", round loop replicated") if sharded else
+                                  (f"replicas x{world}" if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_step,
                      "scope": "whole step: events ordered/s x B(n), SURVEY 8(d)",

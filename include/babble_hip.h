@@ -140,7 +140,8 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors,
                        int32_t *first_descendants);
 /* device milliseconds of the last run, per stage:
  * [0] coordinates+lamport, [1] rounds+witnesses, [2] fame, [3] round received,
- * [4] frames/order/blocks; returns the number of stages */
+ * [4] frames/order/blocks, [5] shard exchanges (host wall time, 0 for one
+ * shard); returns the number of entries */
 int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap);
 /* kernel statistics of the last run for the roofline report: number of
  * round-loop iterations, coordinate sweep launches' average ms */
@@ -165,6 +166,17 @@ int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, i
 int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig_r, const uint8_t *sig_s,
                          const int32_t *keys, int64_t count, const uint8_t *pubkeys, int32_t n_keys,
                          uint8_t *ok);
+
+/* Sharding across processes: one shard per process,
+ * each holding the whole DAG, joined by an RCCL communicator.  Rank 0 makes
+ * the id, every rank passes the same bytes (NCCL_UNIQUE_ID_BYTES = 128)
+ * before inserting any event.  Every pass is then collective: all ranks must
+ * call the same passes in the same order. */
+int bh_comm_unique_id(uint8_t *id);
+int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id);
+/* The split rule every shard uses for LA columns, fame rounds and frames:
+ * shard `rank` of `world` owns [items*rank/world, items*(rank+1)/world). */
+void bh_shard_range(int64_t items, int32_t world, int32_t rank, int64_t *lo, int64_t *hi);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,96 @@
+"""Sharded passes through the C ABI: an
+in-process shard group on ONE device (device_ids = [0, 0] / [0, 0, 0]) runs
+exactly the split kernels and device-to-device exchanges a multi-GPU group
+runs over xGMI, and must match the single-shard engine -- and the oracle --
+bit for bit: LA columns (BH_SHARD_COORDS=columns) or replicated coordinates,
+fame by round ranges, frames sorted by range."""
+import numpy as np
+import pytest
+
+from oracle_py import Oracle
+from test_gpu_parity import _compare
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_engine(a, b, where):
+    ra, rb = a.results(), b.results()
+    for k in ra:
+        assert np.array_equal(ra[k], rb[k]), f"{where}: {k}"
+    assert np.array_equal(a.consensus_order(), b.consensus_order()), where
+    ba, bb = a.blocks(), b.blocks()
+    for k in ba:
+        assert np.array_equal(ba[k], bb[k]), f"{where}: blocks.{k}"
+    assert a.pending_rounds == b.pending_rounds, where
+    sa, sb = a.stats(), b.stats()
+    for f, _ in sa._fields_:
+        assert getattr(sa, f) == getattr(sb, f), f"{where}: stats.{f}"
+
+
+@pytest.mark.parametrize("coords", ["replicate", "columns"])
+@pytest.mark.parametrize("n,N,seed,lag,devs", [
+    (32, 40_000, 81, 0, [0, 0]),
+    (64, 40_000, 82, 21, [0, 0, 0]),
+    (128, 60_000, 83, 0, [0, 0]),
+    (7, 5_000, 84, 2, [0, 0, 0, 0, 0]),   # more shards than some ranges have items
+])
+def test_group_matches_single_and_oracle(monkeypatch, coords, n, N, seed, lag, devs):
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_SHARD_COORDS", coords)
+    d = Dag(n, N, seed, lagging=lag, sig_mode=0)
+    one = Hashgraph(d.participant_ids, N)
+    grp = Hashgraph(d.participant_ids, N, devices=devs)
+    assert not one.insert_dag(d).any() and not grp.insert_dag(d).any()
+    one.run_consensus()
+    grp.run_consensus()
+    _same_engine(one, grp, f"{coords} n={n} shards={len(devs)}")
+    assert grp.stage_ms()[5] > 0  # the exchanges ran
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    _compare(o, grp, f"group {coords} vs oracle")
+
+
+def test_group_wide_chunked():
+    """n > 128: the chunked sweep (coordinates always replicated), k_round_wide,
+    fame from HBM rows split by round."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    n, N = 160, 20_000
+    d = Dag(n, N, 85, sig_mode=0)
+    one = Hashgraph(d.participant_ids, N)
+    grp = Hashgraph(d.participant_ids, N, devices=[0, 0])
+    one.insert_dag(d)
+    grp.insert_dag(d)
+    one.run_consensus()
+    grp.run_consensus()
+    _same_engine(one, grp, "wide")
+
+
+def test_group_per_sync_schedule(monkeypatch):
+    """The per-sync schedule with the A.12 trap on a 2-shard group: the
+    persistent state (pending flags, trapped witnesses, undetermined events)
+    stays identical on every shard across calls."""
+    import json
+    import os
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    from test_gpu_schedule import GOLDEN, _wire_batches
+    monkeypatch.setenv("BH_SHARD_COORDS", "columns")
+    with open(os.path.join(GOLDEN, "trap_schedule.json")) as f:
+        fx = json.load(f)
+    n, N, step = fx["n"], fx["N"], fx["step"] * 7
+    d = Dag(n, N, fx["seed"], lagging=fx["lagging"], lag_div=fx["lag_div"], sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    grp = Hashgraph(d.participant_ids, N, devices=[0, 0])
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        grp.insert_events(*batch(lo, hi))
+        grp.run_consensus()
+        if hi % (step * 20) == 0 or hi == N:
+            _compare(o, grp, f"group after [0, {hi})")
