@@ -100,6 +100,19 @@ struct bh_handle {
   float stage_ms[NSTAGE]{};
   int64_t iters = 0;
   int64_t *d_counters_host = nullptr;
+  // segment pipeline: coordinates of prefix s + 1 on
+  // stream2 while the round loop runs prefix s on `stream`
+  hipStream_t stream2 = nullptr;
+  int32_t *seg_zero = nullptr;   // [n] zeros: seg_lo of a one-segment view
+  int32_t *segbuf = nullptr;     // [2 parities][lo, len][n]
+  int32_t *seg_stage = nullptr;  // pinned staging of segbuf, same layout
+  hipGraphExec_t seg_graph[2] = {nullptr, nullptr};
+  Dev seg_graph_dev[2]{};
+  std::vector<hipEvent_t> seg_ev;  // per segment: coordinates done, k_flow32 start / end
+  int32_t segments_used = 1;
+  int32_t *tlist = nullptr, *tlist_stage = nullptr;  // [2 parities][tlist_cap] segment tile lists
+  int64_t tlist_cap = 0;
+  std::vector<int32_t> cstart_h;  // chain_start as uploaded
   // sharding
   int32_t rank = 0, world = 1;
   std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
@@ -155,6 +168,16 @@ void free_all(bh_handle *h) {
   for (auto &e : h->ev_sweep)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->stream2) (void)hipStreamDestroy(h->stream2);
+  for (auto &g : h->seg_graph)
+    if (g) (void)hipGraphExecDestroy(g);
+  for (auto &e : h->seg_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->seg_zero) (void)hipFree(h->seg_zero);
+  if (h->segbuf) (void)hipFree(h->segbuf);
+  if (h->seg_stage) (void)hipHostFree(h->seg_stage);
+  if (h->tlist) (void)hipFree(h->tlist);
+  if (h->tlist_stage) (void)hipHostFree(h->tlist_stage);
   if (h->comm) (void)ncclCommDestroy(h->comm);
 }
 
@@ -188,25 +211,68 @@ int set_chain_tables(bh_handle *h) {
     mx = std::max(mx, len[c]);
   }
   h->d.max_chain_len = mx;
+  h->cstart_h = start;
   HIPCHK(h, hipMemcpyAsync(h->d.chain_start, start.data(), n * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->d.chain_len, len.data(), n * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return BH_OK;
 }
 
-int build_graph(bh_handle *h) {
-  if (h->graph && memcmp(&h->graph_dev, &h->d, sizeof(Dev)) == 0) return BH_OK;
-  if (h->graph) {
-    (void)hipGraphExecDestroy(h->graph);
-    h->graph = nullptr;
+// the round loop's iterations as one graph of ITER_BATCH launches for the
+// view v, cached per slot (kernel arguments are captured by value)
+int build_graph(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_dev) {
+  if (*graph && memcmp(graph_dev, &v, sizeof(Dev)) == 0) return BH_OK;
+  if (*graph) {
+    (void)hipGraphExecDestroy(*graph);
+    *graph = nullptr;
   }
   hipGraph_t g;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-  for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(h->d, i & 1, h->stream);
+  for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(v, i & 1, h->stream);
   HIPCHK(h, hipStreamEndCapture(h->stream, &g));
-  HIPCHK(h, hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0));
+  HIPCHK(h, hipGraphInstantiate(graph, g, nullptr, nullptr, 0));
   (void)hipGraphDestroy(g);
-  h->graph_dev = h->d;
+  *graph_dev = v;
+  return BH_OK;
+}
+
+// the round loop on h->stream for view v, its inputs set up already:
+// replays batches of iterations, checking completion one batch behind so
+// the device never idles on the host round trip.  Returns the loop state.
+int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_dev, int32_t *st) {
+  int rc;
+  hipStream_t s = h->stream;
+  // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
+  // captured graph (profiling / A-B; results are identical)
+  static const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
+  if (!no_graph && (rc = build_graph(h, v, graph, graph_dev))) return rc;
+  hipEvent_t done_ev[2];
+  HIPCHK(h, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
+  HIPCHK(h, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
+  // the round kernels store 1 into the mapped word pin[0] when the loop ends
+  volatile int32_t *pin = h->pinned_state;
+  pin[0] = 0;
+  bool done = false;
+  const int64_t max_batches = (int64_t)v.R_cap / ITER_BATCH + 2;
+  for (int64_t b = 0; b < max_batches && !done; ++b) {
+    if (no_graph) {
+      for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(v, i & 1, s);
+      HIPCHK(h, hipGetLastError());
+    } else {
+      HIPCHK(h, hipGraphLaunch(*graph, s));
+    }
+    HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
+    if (b > 0) {
+      HIPCHK(h, hipEventSynchronize(done_ev[(b - 1) & 1]));
+      if (pin[0]) done = true;
+    }
+  }
+  HIPCHK(h, hipStreamSynchronize(s));
+  (void)hipEventDestroy(done_ev[0]);
+  (void)hipEventDestroy(done_ev[1]);
+  HIPCHK(h, hipMemcpy(st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
+  if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
+  if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
   return BH_OK;
 }
 
@@ -332,7 +398,11 @@ int rounds_coords(bh_handle *h) {
   if ((rc = upload(h))) return rc;
   Dev &d = h->d;
   d.N = (int64_t)h->h_creator.size();
+  d.rows = d.N;
+  d.e0 = 0;
+  d.seg_lo = h->seg_zero;
   h->xchg_ms = 0;
+  h->segments_used = 1;
   if ((rc = set_chain_tables(h))) return rc;
   hipStream_t s = h->stream;
   HIPCHK(h, hipEventRecord(h->ev[0], s));
@@ -356,6 +426,8 @@ int rounds_coords(bh_handle *h) {
 }
 
 // the rest: LA rows + firstDescendants, the round loop, witness tables
+int rounds_tail(bh_handle *h, const int32_t *st);
+
 int rounds_loop(bh_handle *h) {
   int rc;
   Dev &d = h->d;
@@ -375,42 +447,15 @@ int rounds_loop(bh_handle *h) {
     return BH_OK;
   }
   bh::launch_round_init(d, s);
-  // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
-  // captured graph (profiling / A-B; results are identical)
-  static const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
-  if (!no_graph && (rc = build_graph(h))) return rc;
-  // replay batches of iterations; check completion one batch behind so the
-  // device never idles on the host round trip
-  hipEvent_t done_ev[2];
-  HIPCHK(h, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
-  HIPCHK(h, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
-  // the round kernels store 1 into the mapped word pin[0] when the loop ends
-  volatile int32_t *pin = h->pinned_state;
-  pin[0] = 0;
-  bool done = false;
-
-  const int64_t max_batches = (int64_t)d.R_cap / ITER_BATCH + 2;
-  for (int64_t b = 0; b < max_batches && !done; ++b) {
-    if (no_graph) {
-      for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(d, i & 1, s);
-      HIPCHK(h, hipGetLastError());
-    } else {
-      HIPCHK(h, hipGraphLaunch(h->graph, s));
-    }
-    HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
-
-    if (b > 0) {
-      HIPCHK(h, hipEventSynchronize(done_ev[(b - 1) & 1]));
-      if (pin[0]) done = true;
-    }
-  }
-  HIPCHK(h, hipStreamSynchronize(s));
-  (void)hipEventDestroy(done_ev[0]);
-  (void)hipEventDestroy(done_ev[1]);
   int32_t st[bh::ST_COUNT];
-  HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
-  if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
-  if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
+  if ((rc = run_round_loop(h, d, &h->graph, &h->graph_dev, st))) return rc;
+  return rounds_tail(h, st);
+}
+
+// after the loop: witness tables, per-event rounds, PendingRounds
+int rounds_tail(bh_handle *h, const int32_t *st) {
+  Dev &d = h->d;
+  hipStream_t s = h->stream;
   h->R = st[bh::ST_ROUNDS];
   h->iters = st[bh::ST_ITERS];
   if (st[bh::ST_FLOWOVF]) bh::launch_flow_lt_fallback(d, s);  // LT only feeds the frame order
@@ -429,8 +474,164 @@ int rounds_loop(bh_handle *h) {
   return BH_OK;
 }
 
+// Coordinates and rounds as a pipeline over K insertion-order prefixes
+// (segments): the coordinate kernels of prefix s + 1 run on stream2 while
+// the round loop runs prefix s on `stream`, resuming at the last round the
+// previous prefix fixed (k_resume_point).  Single shard, chain dataflow
+// path (k_flow32, n <= 128) only.
+int segments_for(const bh_handle *h) {
+  const Dev &d = h->d;
+  if (h->world > 1 || !use_flow(d) || !bh::flow32_eligible(d) || !d.fd_cols) return 1;
+  // measured at C3 (10M events): 4 segments 73.4 ms, 8 segments 72.4 ms,
+  // one 84.3 ms (profiles/r2_segments.log)
+  int K = d.N >= 4000000 ? 8 : d.N >= 1000000 ? 4 : 1;
+  if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(K, d.N / 4096 + 1));
+}
+
+int rounds_pipelined(bh_handle *h, int K) {
+  int rc;
+  Dev &d = h->d;  // the whole prefix: every segment's view derives from it
+  const int n = d.n;
+  hipStream_t sr = h->stream, sc = h->stream2;
+  h->segments_used = K;
+  if ((int)h->seg_ev.size() < 3 * K) {
+    for (int i = (int)h->seg_ev.size(); i < 3 * K; ++i) {
+      hipEvent_t e;
+      HIPCHK(h, hipEventCreate(&e));
+      h->seg_ev.push_back(e);
+    }
+  }
+  // the coordinate stream starts after everything queued on the main one
+  HIPCHK(h, hipEventRecord(h->ev[0], sr));
+  HIPCHK(h, hipStreamWaitEvent(sc, h->ev[0], 0));
+  bh::launch_prep(d, sc);
+  const int64_t N = d.N;
+  std::vector<int64_t> Ns((size_t)K + 1, 0);
+  for (int k = 1; k <= K; ++k) Ns[(size_t)k] = N * k / K;
+  // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
+  auto lens_at = [&](int64_t bound, int32_t *out) {
+    for (int c = 0; c < n; ++c) {
+      const auto &ch = h->chain[(size_t)c];
+      out[c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)std::min<int64_t>(bound, INT32_MAX)) - ch.begin());
+    }
+  };
+  auto view = [&](int k) {  // segment k: events [Ns[k], Ns[k + 1])
+    Dev v = d;
+    v.seg_lo = h->segbuf + (size_t)(k & 1) * 2 * n;
+    v.chain_len = v.seg_lo + n;
+    v.N = Ns[(size_t)k + 1];
+    v.e0 = Ns[(size_t)k];
+    v.rows = N;
+    return v;
+  };
+  auto coords = [&](int k) -> int {
+    Dev v = view(k);
+    int32_t *stg = h->seg_stage + (size_t)(k & 1) * 2 * n;
+    lens_at(Ns[(size_t)k], stg);
+    lens_at(Ns[(size_t)k + 1], stg + n);
+    HIPCHK(h, hipMemcpyAsync(v.seg_lo, stg, (size_t)2 * n * 4, hipMemcpyHostToDevice, sc));
+    // the 64-row tiles holding the segment's rows: each chain's run
+    // [start + lo, start + hi), in layout order, shared boundary tiles once
+    int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
+    int64_t nt = 0;
+    for (int c = 0; c < n; ++c) {
+      if (stg[n + c] <= stg[c]) continue;
+      const int64_t a = ((int64_t)h->cstart_h[(size_t)c] + stg[c]) >> 6, b = ((int64_t)h->cstart_h[(size_t)c] + stg[n + c] - 1) >> 6;
+      for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
+    }
+    int32_t *dtl = h->tlist + (size_t)(k & 1) * h->tlist_cap;
+    if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
+    v.tile_list = dtl;
+    v.ntiles = nt;
+    bh::launch_flow_desc(v, sc);
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
+    bh::launch_flow(v, sc);
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
+    bh::launch_flow_transpose(v, sc);
+    bh::launch_fd_idle(v, sc);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));
+    if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));  // the coordinate pipeline's end
+    return BH_OK;
+  };
+  if ((rc = coords(0))) return rc;
+  int32_t st[bh::ST_COUNT];
+  hipEvent_t sr_mark;  // the loop stream's progress, for segbuf reuse by stream2
+  HIPCHK(h, hipEventCreateWithFlags(&sr_mark, hipEventDisableTiming));
+  // BH_SEG_DEBUG=1: per-segment timings to stderr; BH_SEG_SERIAL=1: no overlap (A/B)
+  static const bool dbg = getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG"));
+  static const bool serial = getenv("BH_SEG_SERIAL") && atoi(getenv("BH_SEG_SERIAL"));
+  hipEvent_t lt0 = nullptr, lt1 = nullptr;
+  if (dbg) {
+    HIPCHK(h, hipEventCreate(&lt0));
+    HIPCHK(h, hipEventCreate(&lt1));
+  }
+  for (int k = 0; k < K; ++k) {
+    HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * k], 0));
+    if (serial) HIPCHK(h, hipStreamSynchronize(sr));
+    if (k + 1 < K) {
+      // segment k + 1 reuses the segbuf parity of k - 1, last read by its
+      // resume point on the loop stream
+      HIPCHK(h, hipEventRecord(sr_mark, sr));
+      HIPCHK(h, hipStreamWaitEvent(sc, sr_mark, 0));
+      if ((rc = coords(k + 1))) { (void)hipEventDestroy(sr_mark); return rc; }
+    }
+    Dev rv = d;  // the loop's view: only the prefix lengths differ from d
+    rv.chain_len = view(k).chain_len;
+    if (serial) HIPCHK(h, hipStreamSynchronize(sc));
+    if (dbg) HIPCHK(h, hipEventRecord(lt0, sr));
+    if (k == 0) bh::launch_round_init(rv, sr);
+    else bh::launch_round_resume(rv, sr);
+    if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], st))) {
+      (void)hipEventDestroy(sr_mark);
+      return rc;
+    }
+    if (k + 1 < K) bh::launch_resume_point(rv, st[bh::ST_ROUNDS], sr);
+    if (dbg) {
+      HIPCHK(h, hipEventRecord(lt1, sr));
+      HIPCHK(h, hipStreamSynchronize(sr));
+      float lms = 0, cms = 0, fms = 0;
+      (void)hipEventElapsedTime(&lms, lt0, lt1);
+      (void)hipEventElapsedTime(&fms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]);
+      (void)hipEventElapsedTime(&cms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k]);
+      int32_t r0 = 0;
+      (void)hipMemcpy(&r0, rv.state + bh::ST_RESUME, 4, hipMemcpyDeviceToHost);
+      fprintf(stderr, "[seg %d] coords %.2f ms (k_flow32 %.2f) | loop %.2f ms, rounds %d, iters %d, next resume at %d\n", k,
+              cms, fms, lms, st[bh::ST_ROUNDS], st[bh::ST_ITERS], r0);
+    }
+  }
+  if (lt0) (void)hipEventDestroy(lt0);
+  if (lt1) (void)hipEventDestroy(lt1);
+  (void)hipEventDestroy(sr_mark);
+  h->coords_for = (int)N;
+  float ms = 0;
+  h->sweep_ms = 0;
+  for (int k = 0; k < K; ++k)
+    if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
+  h->sweep_kernel = "k_flow32";
+  return rounds_tail(h, st);
+}
+
 int stage_rounds(bh_handle *h) {
   int rc;
+  if (h->group.empty()) {  // one shard: the segment pipeline when it applies
+    Dev &d = h->d;
+    d.N = (int64_t)h->h_creator.size();
+    int K = 1;
+    if (d.N > 0) {
+      if ((rc = upload(h))) return rc;
+      if ((rc = set_chain_tables(h))) return rc;
+      K = segments_for(h);
+    }
+    if (K > 1) {
+      d.rows = d.N;
+      d.e0 = 0;
+      d.seg_lo = h->seg_zero;
+      h->xchg_ms = 0;
+      return rounds_pipelined(h, K);
+    }
+  }
   if ((rc = run_local(h, rounds_coords))) return rc;
   if (h->world > 1 && h->shard_cols && use_flow(h->d)) {
     // LA columns: shard r computed columns [col0, col0 + ncol), each a
@@ -773,7 +974,29 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
     bh::configure_fame_kernels();
     bh::configure_order_kernels();
   }
-  if (rc == BH_OK && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = BH_ERR_DEVICE;
+  {  // the round loop's stream gets the higher priority: its kernels sit on
+     // the critical path while the coordinate pipeline streams beside it
+    int lo_pri = 0, hi_pri = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi_pri) != hipSuccess)
+      rc = BH_ERR_DEVICE;
+    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
+      rc = BH_ERR_DEVICE;
+  }
+  if (rc == BH_OK) rc = dalloc(h, &h->seg_zero, (size_t)n);
+  if (rc == BH_OK) rc = dalloc(h, &h->segbuf, (size_t)4 * n);
+  if (rc == BH_OK && hipMemset(h->seg_zero, 0, (size_t)n * 4) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipHostMalloc((void **)&h->seg_stage, (size_t)4 * n * 4, hipHostMallocDefault) != hipSuccess)
+    rc = BH_ERR_DEVICE;
+  d.seg_lo = h->seg_zero;
+  d.e0 = 0;
+  d.rows = 0;
+  d.tile_list = nullptr;
+  d.ntiles = 0;
+  h->tlist_cap = C / 64 + n + 64;
+  if (rc == BH_OK) rc = dalloc(h, &h->tlist, (size_t)2 * h->tlist_cap);
+  if (rc == BH_OK && hipHostMalloc((void **)&h->tlist_stage, (size_t)2 * h->tlist_cap * 4, hipHostMallocDefault) != hipSuccess)
+    rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipHostMalloc((void **)&h->pinned_state, 2 * bh::ST_COUNT * 4, hipHostMallocMapped) != hipSuccess)
     rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipHostGetDevicePointer((void **)&d.hdone, h->pinned_state, 0) != hipSuccess)
@@ -966,8 +1189,11 @@ int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id) {
   if (world > 1) {
     ncclUniqueId u;
     memcpy(u.internal, id, sizeof u.internal);
-    if (ncclCommInitRank(&h->comm, world, u, rank) != ncclSuccess)
-      return h->fail(BH_ERR_DEVICE, "ncclCommInitRank(%d of %d) failed", rank, world);
+    const ncclResult_t nr = ncclCommInitRank(&h->comm, world, u, rank);
+    if (nr != ncclSuccess) {
+      h->comm = nullptr;
+      return h->fail(BH_ERR_DEVICE, "ncclCommInitRank(%d of %d): %s", rank, world, ncclGetErrorString(nr));
+    }
   }
   h->rank = rank;
   h->world = world;
@@ -1130,6 +1356,9 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     int rc;
     if ((rc = upload(h))) return rc;
     d.N = N;
+    d.rows = N;
+    d.e0 = 0;
+    d.seg_lo = h->seg_zero;
     if ((rc = set_chain_tables(h))) return rc;
     bh::launch_prep(d, h->stream);
     const bool walked = use_flow(d);

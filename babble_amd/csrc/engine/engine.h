@@ -40,6 +40,7 @@ enum StateSlot {
   ST_FLAGGED = 8,  // candidates that needed the exact witness resolution
   ST_NBLOCKS = 9,
   ST_FLOWOVF = 10,  // k_flow32: a Lamport timestamp reached 2^21 (LT recomputed by k_flow)
+  ST_RESUME = 11,   // k_resume_point: the last round whose boundaries B[r][*] a prefix run fixed
   ST_COUNT = 16
 };
 
@@ -73,6 +74,15 @@ struct Dev {
   int32_t *la_col;  // [n][la_rows+64] column-major LA, chain-major rows (aliases la_ev)
   int32_t *lt_row;  // [la_rows+64] LT by chain-major row
   int32_t col0, ncol;  // k_flow / k_flow32: this shard's LA columns [col0, col0 + ncol) (+ the LT workgroup)
+  // Segments (insertion-order prefixes of the DAG):
+  // the coordinate kernels compute chain c's events [seg_lo[c], chain_len[c])
+  // (chain_len = the prefix's lengths); rows of the chain-major layout
+  // (chain_start) are those of all `rows` events; descriptors are built for
+  // event ids [e0, N).  One segment = seg_lo all 0, e0 0, rows N.
+  int32_t *seg_lo;
+  int64_t e0, rows;
+  const int32_t *tile_list;  // k_flow_transpose: the segment's 64-row tiles (null: every tile)
+  int64_t ntiles;
   int32_t *hdone;  // mapped pinned host word: set when the round loop is done
   int32_t flow_ltclamp;  // k_flow32 LT limit (2^21 - 256; BH_FLOW_LTCLAMP lowers it to test the fallback)
   uint8_t *depth, *chunk_maxd;
@@ -159,6 +169,14 @@ void launch_chunk_depth(const Dev &d, hipStream_t s);
 void launch_la_sweep(const Dev &d, hipStream_t s);
 void launch_permute(const Dev &d, hipStream_t s);  // sweep slabs -> chain-major LA rows
 void launch_round_init(const Dev &d, hipStream_t s);  // hand-off buffers for round 0
+// resume the round loop at round ST_RESUME (boundaries B[r0] kept from a
+// prefix run): hand-off buffers and loop state for iteration r0
+void launch_round_resume(const Dev &d, hipStream_t s);
+// ST_RESUME = the last round r whose B[r][q] all lie inside the prefix
+// (chain_len), so they hold for every longer prefix
+void launch_resume_point(const Dev &d, int32_t R, hipStream_t s);
+// FD entries of a segment's new rows for chains with no event in the segment
+void launch_fd_idle(const Dev &d, hipStream_t s);
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
 void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wcnt/wrow
 // per-event round / witness; events >= n_prev (inserted since the last

@@ -24,10 +24,32 @@
 // (after its vmcnt(0)) that the value is in HBM.
 #include "engine.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
 namespace bh {
+
+// Stores of the transpose's outputs (LA rows, FDT).  BH_XPOSE_NT builds use
+// non-temporal stores: streamed once, read rounds later, they need not
+// displace the round loop's working set from L2 / the Infinity Cache while
+// the segment pipeline runs both at once.
+__device__ __forceinline__ void xstore(int32_t *p, int32_t v) {
+#ifdef BH_XPOSE_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void xstore(int4 *p, int4 v) {
+#ifdef BH_XPOSE_NT
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<v4i *>(p));
+#else
+  *p = v;
+#endif
+}
 
 constexpr int FL_R = 64;     // value ring slots per chain (int2 {value, index})
 constexpr int FL_DR = 128;   // descriptor ring entries per chain
@@ -148,12 +170,13 @@ __device__ __forceinline__ void flow_body(const Dev &d, FlowLds &L, int col) {
     // column-major LA; `stored` (slot reusable) bounds how far the compute
     // lanes may run ahead, `pub` (store complete: after vmcnt(0)) tells far
     // readers the value is in HBM.
-    int32_t sp[2] = {0, 0}, len[2], cs[2];
+    int32_t sp[2], len[2], cs[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = lane + 64 * h;
       len[h] = c < n ? d.chain_len[c] : 0;
       cs[h] = c < n ? d.chain_start[c] : 0;
+      sp[h] = c < n ? d.seg_lo[c] : 0;
     }
     for (int pass = 1;; ++pass) {
       bool left = false;
@@ -314,7 +337,7 @@ __host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 21) 
 // before it}; the .y of a chain's first row holds the previous chain's last
 // own slot (the chain reads it as entry len)
 __global__ void k_flow_desc32(Dev d) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.N) return;
   int2 *opw = reinterpret_cast<int2 *>(d.opdesc);
   const int32_t o = d.op[e], p = d.epos[e];
@@ -336,11 +359,16 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   const int col = d.col0 + (int)blockIdx.x;  // this shard's columns; the LT workgroup is the last
   const int64_t stride = d.la_rows + 64;
   int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
+  // a segment resumes chain c at seg_lo[c]: its earlier events are in HBM
+  // (published, read back like any parent older than its ring), and a slot
+  // still holding GINIT (newer than every real generation) sends a lookup
+  // of one of them there
   for (int c = t; c < n; c += blockDim.x) {
-    L.filled[c] = 0;
-    L.consumed[c] = 0;
-    L.pub[c] = 0;
-    L.stored[c] = 0;
+    const int32_t lo = d.seg_lo[c];
+    L.filled[c] = lo;
+    L.consumed[c] = lo;
+    L.pub[c] = lo;
+    L.stored[c] = lo;
     L.cs[c] = d.chain_start[c];
     for (int s = 0; s < F2_R; ++s) L.vring[c][s] = F2_GINIT << 21;  // matches no real event
   }
@@ -352,12 +380,16 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
 
   if (wave == nw) {
     // ---------------- prefetch wave: descriptor rings, 32 entries per DMA ----------------
-    int32_t f[2] = {0, 0}, tot[2], cs[2];
+    int32_t f[2], tot[2], cs[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = lane + 64 * h;
       const int32_t len = c < n ? d.chain_len[c] : 0;
-      tot[h] = len > 0 ? len + 1 : 0;  // entry len carries the last event's own slot
+      const int32_t lo = c < n ? d.seg_lo[c] : 0;
+      // a DMA fills 32 ring entries at f & (F2_DR - 1): f stays a multiple of
+      // 32 so it never runs past the ring row (entries below lo go unused)
+      f[h] = lo & ~31;
+      tot[h] = len > lo ? len + 1 : 0;  // entry len carries the last event's own slot
       cs[h] = c < n ? d.chain_start[c] : 0;
     }
     for (;;) {
@@ -393,12 +425,13 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   }
   if (wave == nw + 1) {
     // ---------------- store wave: rings -> HBM ----------------
-    int32_t sp[2] = {0, 0}, len[2], cs[2];
+    int32_t sp[2], len[2], cs[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = lane + 64 * h;
       len[h] = c < n ? d.chain_len[c] : 0;
       cs[h] = c < n ? d.chain_start[c] : 0;
+      sp[h] = c < n ? d.seg_lo[c] : 0;
     }
     for (int pass = 1;; ++pass) {
       bool left = false;
@@ -439,7 +472,10 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   const uint32_t WAIT = f2_wait(n);
   char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
   const int2 *dring_c = &L.dring[cc][0];
-  int32_t k = 0, cur = 0, lim = 0;  // cur: value of event k-1 + 1
+  // cur: value of event k-1 + 1 (0: no self-parent); a resumed segment
+  // starts from the value its chain's previous event left in HBM
+  int32_t k = valid ? d.seg_lo[c] : 0, cur = 0, lim = 0;
+  if (k > 0) cur = out[d.chain_start[c] + k - 1] + 1;
   uint32_t dsc = WAIT;
   const int32_t ltclamp = min(d.flow_ltclamp, F2_LTCLAMP);
   const bool dg = d.diag != nullptr && col == 0 && wave == 0;
@@ -521,23 +557,14 @@ __global__ __launch_bounds__(256) void k_flow32(Dev d) {
 // chain boundaries; each run of rows of one chain is a walk segment whose
 // column c owns FD entries j in (LA[row before][c], LA[last row][c]].
 template <int TR, int BT>
-__global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
-  extern __shared__ int32_t tile[];  // [npad][TR + 1], then prev[npad]
-  __shared__ int32_t rc[TR], rj[TR];
-  __shared__ uint64_t segmask;
-  __shared__ int32_t cstart[FL_MAXN + 16], clen[FL_MAXN + 16];
+__device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int32_t *tile, int32_t *rc, int32_t *rj,
+                                           uint64_t &segmask, uint64_t &insmask, int32_t *cstart, int32_t *clen) {
   constexpr int IPP = BT / TR;  // columns per load pass
   constexpr int LU = 16;        // load passes in flight
   const int t = threadIdx.x;
-  // XCD-aware tile order: workgroup b runs on XCD b % 8, so give each XCD a
-  // contiguous range of tiles -- a tile's "row before" (the previous tile's
-  // last row) is then usually already in that XCD's L2
-  // (the grid is rounded up to a multiple of 8 workgroups)
-  const uint32_t per = gridDim.x / 8;
-  const int64_t tix = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (tix * TR >= d.N) return;
+  if (tix * TR >= d.rows) return;
   const int64_t row0 = tix * TR;
-  const int64_t N = d.N;
+  const int64_t N = d.rows;  // rows of the layout; the segment's are those with seg_lo <= index < chain_len
   const int n = d.n, npad = d.npad;
   const int64_t stride = d.la_rows + 64;
   const int ro = t % TR;
@@ -546,10 +573,17 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
   int32_t *prev = tile + npad * (TR + 1);
   if (t < TR) {
     const int32_t e = d.chain_ids[row];
-    if (t < rows) d.lt[e] = d.lt_row[row0 + t];
-    rc[t] = d.creator[e];
-    rj[t] = d.index[e];
+    const int32_t c = d.creator[e], k = d.index[e];
+    const bool ins = t < rows && k >= d.seg_lo[c] && k < d.chain_len[c];
+    if (ins) d.lt[e] = d.lt_row[row0 + t];
+    rc[t] = c;
+    rj[t] = k;
+    const uint64_t m = __ballot(ins);
+    if (t == 0) insmask = m;
   }
+  __syncthreads();
+  const uint64_t insm = insmask;
+  if (!insm) return;  // no row of this segment in the tile
   for (int i = t; i < n; i += BT) prev[i] = row0 > 0 ? d.la_col[(int64_t)i * stride + row0 - 1] : -1;
   for (int i = t; i < n; i += BT) {
     cstart[i] = d.chain_start[i];
@@ -579,10 +613,11 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
       const int r0 = t / q4, i4 = (t - r0 * q4) * 4;
       int4 *dst = reinterpret_cast<int4 *>(d.la + row0 * npad + i4);
       for (int r = r0; r < rows; r += rpp) {
+        if (!((insm >> r) & 1)) continue;  // rows of other segments are not (yet / any longer) ours
         int32_t o[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) o[u] = i4 + u < n ? tile[(i4 + u) * (TR + 1) + r] : -1;
-        dst[(int64_t)r * q4] = make_int4(o[0], o[1], o[2], o[3]);
+        xstore(dst + (int64_t)r * q4, make_int4(o[0], o[1], o[2], o[3]));
       }
     }
   }
@@ -592,12 +627,17 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
   for (uint64_t m = segs; m; m &= m - 1) {
     const int ra = __builtin_ctzll(m);
     const uint64_t rest = m & (m - 1);
-    const int rb = rest ? __builtin_ctzll(rest) : rows;  // segment rows [ra, rb)
-    const int32_t i = rc[ra], ka = rj[ra];
-    if (ka + (rb - ra) == clen[i] && d.fd_cols)  // chain i ends here: rows it never sees
+    const int rb0 = rest ? __builtin_ctzll(rest) : rows;  // rows [ra, rb0) of one chain
+    const int32_t i = rc[ra];
+    // its rows inside the segment: [ra1, rb)
+    const int32_t ka0 = rj[ra], lo_i = d.seg_lo[i];
+    const int ra1 = ra + max(0, lo_i - ka0), rb = ra + min(rb0 - ra, clen[i] - ka0);
+    if (ra1 >= rb) continue;
+    const int32_t ka = ka0 + (ra1 - ra);
+    if (ka + (rb - ra1) == clen[i] && d.fd_cols)  // chain i's last event (of the prefix): rows it never sees
       for (int c = wave; c < n; c += BT / 64) {
         const int32_t hi = tile[c * (TR + 1) + rb - 1];
-        for (int32_t j = hi + 1 + lane; j < clen[c]; j += 64) d.fdt[fdt_pos(cstart[c] + j, i, npad)] = FD_NONE;
+        for (int32_t j = hi + 1 + lane; j < clen[c]; j += 64) xstore(d.fdt + fdt_pos(cstart[c] + j, i, npad), FD_NONE);
       }
     // four columns per pass: their binary searches (at most 6 halvings of
     // a <= 64-row segment) interleave, so LDS latency is paid once per
@@ -609,9 +649,9 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
       for (int u = 0; u < 4; ++u) {
         const int c = min(c0 + u, n - 1);
         const int32_t *col = tile + c * (TR + 1);
-        lo[u] = ka == 0 ? -1 : (ra == 0 ? prev[c] : col[ra - 1]);
+        lo[u] = ka == 0 ? -1 : (ra1 == 0 ? prev[c] : col[ra1 - 1]);
         hi[u] = c0 + u < n ? col[rb - 1] : lo[u];
-        a[u] = ra;
+        a[u] = ra1;
         z[u] = rb - 1;
       }
 #pragma unroll
@@ -628,7 +668,7 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int32_t j = lo[u] + 1 + lane;
-        if (j <= hi[u]) d.fdt[fdt_pos(cstart[c0 + u] + j, i, npad)] = ka + a[u] - ra;
+        if (j <= hi[u]) xstore(d.fdt + fdt_pos(cstart[c0 + u] + j, i, npad), ka + a[u] - ra1);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -637,18 +677,46 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
         for (int32_t j0 = lo[u] + 65; j0 <= hi[u]; j0 += 64) {
           const int32_t j = j0 + lane;
           if (j <= hi[u]) {
-            int aa = ra, zz = rb - 1;
+            int aa = ra1, zz = rb - 1;
             while (aa < zz) {
               const int mm = (aa + zz) >> 1;
               if (col[mm] >= j) zz = mm;
               else aa = mm + 1;
             }
-            d.fdt[fdt_pos(cstart[c0 + u] + j, i, npad)] = ka + aa - ra;
+            xstore(d.fdt + fdt_pos(cstart[c0 + u] + j, i, npad), ka + aa - ra1);
           }
         }
       }
     }
   }
+}
+
+template <int TR, int BT>
+__global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
+  extern __shared__ int32_t tile[];  // [npad][TR + 1], then prev[npad]
+  __shared__ int32_t rc[TR], rj[TR];
+  __shared__ uint64_t segmask, insmask;
+  __shared__ int32_t cstart[FL_MAXN + 16], clen[FL_MAXN + 16];
+  if (d.tile_list) {
+    // a segment's tiles, a contiguous share per
+    // workgroup: few workgroups, so the round loop running beside them
+    // keeps its compute units; consecutive tiles keep the "row before" in
+    // the workgroup's XCD L2
+    const int64_t per = (d.ntiles + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * per, i1 = min<int64_t>(d.ntiles, i0 + per);
+    for (int64_t i = i0; i < i1; ++i) {
+      __syncthreads();
+      xpose_tile<TR, BT>(d, d.tile_list[i], tile, rc, rj, segmask, insmask, cstart, clen);
+    }
+    return;
+  }
+  // XCD-aware tile order: workgroup b runs on XCD b % 8, so give each XCD a
+  // contiguous range of tiles -- a tile's "row before" (the previous tile's
+  // last row) is then usually already in that XCD's L2
+  // (the grid is rounded up to a multiple of 8 workgroups)
+  const uint32_t per = gridDim.x / 8;
+  const int64_t tix = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  xpose_tile<TR, BT>(d, tix, tile, rc, rj, segmask, insmask, cstart, clen);
 }
 
 // 128 chains (one LDS ring row each + the sentinel row within a 17-bit
@@ -665,8 +733,8 @@ bool flow32_eligible(const Dev &d) {
 }
 
 void launch_flow_desc(const Dev &d, hipStream_t s) {
-  if (d.N == 0) return;
-  if (flow32_eligible(d)) k_flow_desc32<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
+  if (d.N <= d.e0) return;
+  if (flow32_eligible(d)) k_flow_desc32<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
   else k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
 }
 
@@ -688,8 +756,15 @@ void launch_flow_lt_fallback(const Dev &d, hipStream_t s) {
 }
 
 void launch_flow_transpose(const Dev &d, hipStream_t s) {
-  if (d.N == 0) return;
-  const unsigned tiles = (unsigned)((d.N + 63) / 64);
+  if (d.rows == 0) return;
+  if (d.tile_list) {
+    if (d.ntiles == 0) return;
+    const char *e = getenv("BH_XPOSE_WG");
+    const int64_t wg = std::min<int64_t>(d.ntiles, e ? std::max(1, atoi(e)) : 512);
+    k_flow_transpose<64, 512><<<(unsigned)wg, 512, (size_t)d.npad * 66 * 4, s>>>(d);
+    return;
+  }
+  const unsigned tiles = (unsigned)((d.rows + 63) / 64);
   k_flow_transpose<64, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 66 * 4, s>>>(d);
 }
 

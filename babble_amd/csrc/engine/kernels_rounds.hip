@@ -28,6 +28,8 @@
 // involvement and every load of an iteration depends only on B[r].
 #include "engine.h"
 
+#include <algorithm>
+
 namespace bh {
 
 // the round loop's end, told to the host through mapped pinned memory (a
@@ -368,9 +370,13 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
-  const int nwq = HW * q4;  // int4 per handed-over window (<= 1024)
   int4 *win = sm4;              // [HW][q4]: LA rows k0 .. k0 + 31
-  int32_t *fdw = reinterpret_cast<int32_t *>(sm4 + nwq);  // [npad][FDS]: FD rows rb .. rb + 31 by column
+  // [npad][FDS]: FD rows rb .. rb + 31 by column, for the hand-off after the
+  // search -- the window's space (every read of it is behind the search's
+  // last barrier), so the workgroup's LDS (18 KiB at n = 128) fits beside a
+  // k_flow32 workgroup (133 KiB) on one compute unit: the segment pipeline
+  // runs both at once
+  int32_t *fdw = reinterpret_cast<int32_t *>(sm4);
   constexpr int FDS = HW + 4;
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   const bool dg = d.diag != nullptr && t == 0;
@@ -546,6 +552,77 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
 }
 
+// Resuming the loop after a prefix run (segments).  A
+// prefix of the DAG in insertion order is closed under ancestry, so its
+// rows' lastAncestors are final; a candidate beyond the prefix cannot be
+// strongly seen by a prefix row, and an FD entry beyond the prefix compares
+// false against a prefix row's LA either way.  So every boundary the prefix
+// run finds INSIDE the prefix (B[r][q] < prefix length) holds for the whole
+// DAG, and the loop can resume at the last round whose boundaries all lie
+// inside: r0 = min over q of (first r with B[r][q] >= len_q) - 1.
+__global__ __launch_bounds__(1024) void k_resume_point(Dev d, int32_t R) {
+  __shared__ int32_t m;
+  if (threadIdx.x == 0) m = R;
+  __syncthreads();
+  for (int q = threadIdx.x; q < d.n; q += blockDim.x) {
+    const int32_t len = d.chain_len[q];
+    int lo = 0, hi = R;  // B[R][q] = len_q (the last iteration's output)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (d.B[(int64_t)mid * d.n + q] >= len) hi = mid;
+      else lo = mid + 1;
+    }
+    atomicMin(&m, lo);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) d.state[ST_RESUME] = max(0, m - 1);
+}
+
+void launch_resume_point(const Dev &d, int32_t R, hipStream_t s) { k_resume_point<<<1, 1024, 0, s>>>(d, R); }
+
+// iteration r0's inputs, parity 0: B[r0] and the candidates' FD rows (from
+// FDT, which now covers the longer prefix); the loop state
+__global__ __launch_bounds__(256) void k_round_resume(Dev d) {
+  const int c = blockIdx.x;
+  const int32_t r0 = d.state[ST_RESUME];
+  const int32_t b = d.B[(int64_t)r0 * d.n + c], len = d.chain_len[c], cs = d.chain_start[c];
+  if (threadIdx.x == 0) d.Bp[c] = b;
+  int32_t *cf = d.candfd + (int64_t)c * d.npad;
+  if (b < len)
+    for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs + b, i, d.npad)] : FD_NONE;
+  if (c == 0 && threadIdx.x == 0) {
+    d.state[ST_CUR0] = r0;
+    d.state[ST_CUR0 + 1] = 0;
+    d.state[ST_DONE] = 0;
+    d.state[ST_ROUNDS] = 0;
+    d.state[ST_ERR] = 0;
+    d.state[ST_ITERS] = r0;
+  }
+}
+
+void launch_round_resume(const Dev &d, hipStream_t s) { k_round_resume<<<d.n, 256, 0, s>>>(d); }
+
+// A chain with no event in the segment has no last-row tile to write
+// "never seen" (MaxInt32) into the new rows of the other chains: done here
+// from the LA row of its last event (or -1 everywhere if it has none)
+__global__ __launch_bounds__(256) void k_fd_idle(Dev d) {
+  const int i = blockIdx.x;
+  const int32_t hi_i = d.chain_len[i];
+  if (d.seg_lo[i] != hi_i) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t lrow = (int64_t)d.chain_start[i] + hi_i - 1;
+  for (int c = wave; c < d.n; c += 4) {
+    const int32_t seen = hi_i > 0 ? d.la[lrow * d.npad + c] : -1;
+    const int32_t cs = d.chain_start[c];
+    for (int32_t j = max(seen + 1, d.seg_lo[c]) + lane; j < d.chain_len[c]; j += 64)
+      d.fdt[fdt_pos(cs + j, i, d.npad)] = FD_NONE;
+  }
+}
+
+void launch_fd_idle(const Dev &d, hipStream_t s) {
+  if (d.fd_cols) k_fd_idle<<<d.n, 256, 0, s>>>(d);
+}
+
 bool round2_eligible(const Dev &d) { return d.fd_cols != 0; }
 
 void launch_round_init(const Dev &d, hipStream_t s) {
@@ -570,7 +647,7 @@ void configure_round_kernels() {
 // iteration parity p = round & 1 (ITER_BATCH is even, rounds start at 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
-    const size_t lds = (size_t)HW * (d.npad / 4) * 16 + (size_t)d.npad * (HW + 4) * 4;
+    const size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
     if (d.npad <= 64) k_round2<4><<<d.n, 1024, lds, s>>>(d, p);
     else k_round2<8><<<d.n, 1024, lds, s>>>(d, p);
     return;

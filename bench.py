@@ -118,11 +118,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # BH_BENCH_ONE_DEVICE=1: every rank on device 0, the barrier over gloo
+    # (rehearses the multi-process RCCL path on a one-GPU box)
+    one_dev = os.environ.get("BH_BENCH_ONE_DEVICE") == "1"
+    if one_dev:
+        local = 0
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if one_dev else "nccl")
 
     def log(*a):
         if not args.quiet and rank == 0:

@@ -455,3 +455,57 @@ def test_participant_lookup_rejects_unknown_ids():
     assert ei.value.kind == "OtherParent"
     hg.insert_event(int(ids[0]), 1, 0, int(ids[-1]), 0, bytes([77] * 32), bytes([77] * 32), 0)
     assert hg.stats().n_events == len(ids) + 1
+
+
+@pytest.mark.parametrize("K,n,N,seed,lag", [
+    (3, 4, 10_000, 0xBABB1E01, 0),
+    (5, 128, 60_000, 91, 0),
+    (7, 64, 50_000, 92, 21),
+    (2, 32, 40_000, 93, 0),
+    (13, 9, 30_000, 94, 3),
+])
+def test_segment_pipeline_parity(monkeypatch, K, n, N, seed, lag):
+    """Coordinates of prefix s + 1 overlapped with the round loop on prefix s,
+    the loop resuming at the last round the prefix fixed (BH_SEGMENTS=K;
+    full-size DAGs take 4 segments by default)."""
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    _random_parity(n, N, seed, lag)
+
+
+@pytest.mark.parametrize("K", [2, 6])
+def test_segment_pipeline_wild(monkeypatch, K):
+    """Other-parents far behind the segment start (read back from HBM by the
+    resumed dataflow) and chains idle for whole segments."""
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    _wild_parity(24, 40_000, 95, 30_000)
+    _wild_parity(128, 40_000, 96, 35_000)
+
+
+def test_segment_pipeline_lt_fallback(monkeypatch):
+    monkeypatch.setenv("BH_SEGMENTS", "4")
+    monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
+    hg = _random_parity(16, 20_000, 97, 2)
+    assert hg.results()["lamport"].max() > 300
+
+
+def test_segment_pipeline_schedule(monkeypatch):
+    """The per-sync schedule with every call through the segment pipeline."""
+    monkeypatch.setenv("BH_SEGMENTS", "3")
+    from babble_amd.dag import Dag
+    from babble_amd import Hashgraph
+    n, N, step = 9, 30_000, 5_000
+    d = Dag(n, N, 98, lagging=3, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi], opi[lo:hi],
+                         d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])
+        hg.run_consensus()
+        _compare(o, hg, f"segments, after [0, {hi})")
