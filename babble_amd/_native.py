@@ -21,7 +21,7 @@ ERRORS = {
 SYMBOLS = (
     "bh_create", "bh_destroy", "bh_last_error", "bh_insert_events", "bh_divide_rounds",
     "bh_decide_fame", "bh_decide_round_received", "bh_process_decided_rounds",
-    "bh_run_consensus", "bh_synchronize", "bh_get_stats", "bh_get_event_meta",
+    "bh_run_consensus", "bh_synchronize", "bh_reset_consensus", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_round_info", "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
     "bh_hash_bodies", "bh_verify_signatures", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
@@ -74,7 +74,7 @@ def load():
     L.bh_last_error.restype = C.c_char_p
     L.bh_insert_events.argtypes = [P, C.POINTER(Events), VP, C.POINTER(I64)]
     for f in ("bh_divide_rounds", "bh_decide_fame", "bh_decide_round_received",
-              "bh_process_decided_rounds", "bh_run_consensus", "bh_synchronize"):
+              "bh_process_decided_rounds", "bh_run_consensus", "bh_synchronize", "bh_reset_consensus"):
         getattr(L, f).argtypes = [P]
         getattr(L, f).restype = C.c_int
     L.bh_get_stats.argtypes = [P, C.POINTER(Stats)]

@@ -113,6 +113,17 @@ struct bh_handle {
   int32_t *tlist = nullptr, *tlist_stage = nullptr;  // [2 parities][tlist_cap] segment tile lists
   int64_t tlist_cap = 0;
   std::vector<int32_t> cstart_h;  // chain_start as uploaded
+  std::vector<int32_t> cap_h;     // rows of each chain's region
+  std::vector<int32_t> lens_h;    // chain lengths as uploaded
+  int64_t layout_rows = 0;        // rows of the layout (regions included)
+  bool layout_changed = true;
+  // incremental calls (a call that only appended events runs them as one
+  // more segment): coordinates and round loop hold the first n_coord events
+  // of the current layout; lens_coord their chain lengths
+  bool inc_valid = false;
+  int64_t n_coord = 0;
+  int64_t inc_calls = 0;  // DivideRounds calls that resumed (statistics)
+  std::vector<int32_t> lens_coord;
   // sharding
   int32_t rank = 0, world = 1;
   std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
@@ -200,20 +211,47 @@ int upload(bh_handle *h) {
   return BH_OK;
 }
 
+// Chain-major layout: chain c's events occupy rows [chain_start[c],
+// chain_start[c] + len_c) of a region of cap_c rows.  The regions are kept
+// while every chain fits (appended events extend a region in place, so the
+// rows already computed stay valid); when one outgrows its region they are
+// laid out again with fresh slack (max(BH_LAYOUT_SLACK or 1024, len / 8)
+// rows each, if the allocation has room; none otherwise) and layout_changed
+// is set.  Rows past a chain's events are gaps (chain_ids -1).
 int set_chain_tables(bh_handle *h) {
   const int n = h->d.n;
-  std::vector<int32_t> start(n), len(n);
-  int32_t acc = 0, mx = 0;
+  std::vector<int32_t> len((size_t)n);
+  int32_t mx = 0;
+  int64_t tot = 0;
   for (int c = 0; c < n; ++c) {
-    start[c] = acc;
-    len[c] = (int32_t)h->chain[c].size();
-    acc += len[c];
-    mx = std::max(mx, len[c]);
+    len[(size_t)c] = (int32_t)h->chain[(size_t)c].size();
+    mx = std::max(mx, len[(size_t)c]);
+    tot += len[(size_t)c];
   }
+  bool fits = (int)h->cap_h.size() == n;
+  for (int c = 0; fits && c < n; ++c) fits = len[(size_t)c] <= h->cap_h[(size_t)c];
+  h->layout_changed = !fits;
+  if (!fits) {
+    static const int64_t min_slack = getenv("BH_LAYOUT_SLACK") ? atoll(getenv("BH_LAYOUT_SLACK")) : 1024;
+    const bool slack = h->d.la_rows > h->cap;  // the allocation reserved room for it
+    int64_t need = 0;
+    for (int c = 0; c < n; ++c) need += len[(size_t)c] + std::max<int64_t>(min_slack, len[(size_t)c] / 8);
+    const bool use = slack && need <= h->d.la_rows;
+    h->cap_h.resize((size_t)n);
+    h->cstart_h.resize((size_t)n);
+    int64_t acc = 0;
+    for (int c = 0; c < n; ++c) {
+      h->cstart_h[(size_t)c] = (int32_t)acc;
+      h->cap_h[(size_t)c] = (int32_t)(len[(size_t)c] + (use ? std::max<int64_t>(min_slack, len[(size_t)c] / 8) : 0));
+      acc += h->cap_h[(size_t)c];
+    }
+    h->layout_rows = acc;
+    HIPCHK(h, hipMemcpyAsync(h->d.chain_start, h->cstart_h.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+  }
+  (void)tot;
   h->d.max_chain_len = mx;
-  h->cstart_h = start;
-  HIPCHK(h, hipMemcpyAsync(h->d.chain_start, start.data(), n * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemcpyAsync(h->d.chain_len, len.data(), n * 4, hipMemcpyHostToDevice, h->stream));
+  h->lens_h = len;
+  HIPCHK(h, hipMemcpyAsync(h->d.chain_len, h->lens_h.data(), n * 4, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return BH_OK;
 }
@@ -376,13 +414,16 @@ int exchange(bh_handle *h, Sel sel, const std::vector<size_t> &off, const std::v
   return BH_OK;
 }
 
-// per-shard ranges of a table of `items` entries of `esz` bytes each
+// per-shard ranges of items [base, base + items) of a table of `esz`-byte
+// entries (with ofs: item i spans entries [ofs[i], ofs[i + 1]))
 std::vector<size_t> range_bytes(const bh_handle *h, int64_t items, size_t esz, bool lengths,
-                                const std::vector<int32_t> *ofs = nullptr) {
+                                const std::vector<int32_t> *ofs = nullptr, int64_t base = 0) {
   std::vector<size_t> v((size_t)h->world);
   for (int r = 0; r < h->world; ++r) {
     int64_t lo, hi;
     shard_range(items, h->world, r, &lo, &hi);
+    lo += base;
+    hi += base;
     if (ofs) { lo = (*ofs)[(size_t)lo]; hi = (*ofs)[(size_t)hi]; }  // item ranges -> entry ranges
     v[(size_t)r] = lengths ? (size_t)(hi - lo) * esz : (size_t)lo * esz;
   }
@@ -398,12 +439,13 @@ int rounds_coords(bh_handle *h) {
   if ((rc = upload(h))) return rc;
   Dev &d = h->d;
   d.N = (int64_t)h->h_creator.size();
-  d.rows = d.N;
   d.e0 = 0;
   d.seg_lo = h->seg_zero;
   h->xchg_ms = 0;
   h->segments_used = 1;
+  h->inc_valid = false;
   if ((rc = set_chain_tables(h))) return rc;
+  d.rows = h->layout_rows;
   hipStream_t s = h->stream;
   HIPCHK(h, hipEventRecord(h->ev[0], s));
   bh::launch_prep(d, s);
@@ -426,7 +468,7 @@ int rounds_coords(bh_handle *h) {
 }
 
 // the rest: LA rows + firstDescendants, the round loop, witness tables
-int rounds_tail(bh_handle *h, const int32_t *st);
+int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin);
 
 int rounds_loop(bh_handle *h) {
   int rc;
@@ -449,18 +491,20 @@ int rounds_loop(bh_handle *h) {
   bh::launch_round_init(d, s);
   int32_t st[bh::ST_COUNT];
   if ((rc = run_round_loop(h, d, &h->graph, &h->graph_dev, st))) return rc;
-  return rounds_tail(h, st);
+  return rounds_tail(h, st, 0);
 }
 
-// after the loop: witness tables, per-event rounds, PendingRounds
-int rounds_tail(bh_handle *h, const int32_t *st) {
+// after the loop: witness tables, per-event rounds, PendingRounds.  Rounds
+// and witness flags of events [0, e_begin) are unchanged (an incremental
+// call appended events only)
+int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
   Dev &d = h->d;
   hipStream_t s = h->stream;
   h->R = st[bh::ST_ROUNDS];
   h->iters = st[bh::ST_ITERS];
   if (st[bh::ST_FLOWOVF]) bh::launch_flow_lt_fallback(d, s);  // LT only feeds the frame order
   bh::launch_witness_tables(d, h->R, s);
-  bh::launch_assign_rounds(d, h->n_div, h->P, s);
+  bh::launch_assign_rounds(d, e_begin, h->n_div, h->P, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[2], s));
   h->wofs_h.resize((size_t)h->R + 1);
@@ -479,17 +523,22 @@ int rounds_tail(bh_handle *h, const int32_t *st) {
 // the round loop runs prefix s on `stream`, resuming at the last round the
 // previous prefix fixed (k_resume_point).  Single shard, chain dataflow
 // path (k_flow32, n <= 128) only.
-int segments_for(const bh_handle *h) {
+bool segments_eligible(const bh_handle *h) {
   const Dev &d = h->d;
-  if (h->world > 1 || !use_flow(d) || !bh::flow32_eligible(d) || !d.fd_cols) return 1;
-  // measured at C3 (10M events): 4 segments 73.4 ms, 8 segments 72.4 ms,
-  // one 84.3 ms (profiles/r2_segments.log)
-  int K = d.N >= 4000000 ? 8 : d.N >= 1000000 ? 4 : 1;
-  if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(K, d.N / 4096 + 1));
+  return h->group.empty() && h->world == 1 && use_flow(d) && bh::flow32_eligible(d) && d.fd_cols;
 }
 
-int rounds_pipelined(bh_handle *h, int K) {
+// segments for `events` new events: measured at C3 (10M events): 4
+// segments 73.4 ms, 8 segments 72.4 ms, one 84.3 ms (profiles/r2_segments.log)
+int segments_for(int64_t events) {
+  int K = events >= 4000000 ? 8 : events >= 1000000 ? 4 : 1;
+  if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
+}
+
+// base > 0: an incremental call -- events [0, base) hold coordinates and
+// the round loop left its resume point (ST_RESUME) for that prefix
+int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   int rc;
   Dev &d = h->d;  // the whole prefix: every segment's view derives from it
   const int n = d.n;
@@ -505,10 +554,15 @@ int rounds_pipelined(bh_handle *h, int K) {
   // the coordinate stream starts after everything queued on the main one
   HIPCHK(h, hipEventRecord(h->ev[0], sr));
   HIPCHK(h, hipStreamWaitEvent(sc, h->ev[0], 0));
-  bh::launch_prep(d, sc);
+  if (base == 0) {
+    bh::launch_prep(d, sc);
+  } else {  // only the new events' chain-table entries; loop state kept
+    bh::launch_chain_scatter(d, base, sc);
+    HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, sc));
+  }
   const int64_t N = d.N;
-  std::vector<int64_t> Ns((size_t)K + 1, 0);
-  for (int k = 1; k <= K; ++k) Ns[(size_t)k] = N * k / K;
+  std::vector<int64_t> Ns((size_t)K + 1, base);
+  for (int k = 1; k <= K; ++k) Ns[(size_t)k] = base + (N - base) * k / K;
   // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
   auto lens_at = [&](int64_t bound, int32_t *out) {
     for (int c = 0; c < n; ++c) {
@@ -522,7 +576,7 @@ int rounds_pipelined(bh_handle *h, int K) {
     v.chain_len = v.seg_lo + n;
     v.N = Ns[(size_t)k + 1];
     v.e0 = Ns[(size_t)k];
-    v.rows = N;
+    v.rows = h->layout_rows;
     return v;
   };
   auto coords = [&](int k) -> int {
@@ -581,13 +635,14 @@ int rounds_pipelined(bh_handle *h, int K) {
     rv.chain_len = view(k).chain_len;
     if (serial) HIPCHK(h, hipStreamSynchronize(sc));
     if (dbg) HIPCHK(h, hipEventRecord(lt0, sr));
-    if (k == 0) bh::launch_round_init(rv, sr);
+    if (k == 0 && base == 0) bh::launch_round_init(rv, sr);
     else bh::launch_round_resume(rv, sr);
     if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], st))) {
       (void)hipEventDestroy(sr_mark);
       return rc;
     }
-    if (k + 1 < K) bh::launch_resume_point(rv, st[bh::ST_ROUNDS], sr);
+    // where the next segment -- or the next call's new events -- resume
+    bh::launch_resume_point(rv, st[bh::ST_ROUNDS], sr);
     if (dbg) {
       HIPCHK(h, hipEventRecord(lt1, sr));
       HIPCHK(h, hipStreamSynchronize(sr));
@@ -610,7 +665,11 @@ int rounds_pipelined(bh_handle *h, int K) {
   for (int k = 0; k < K; ++k)
     if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
   h->sweep_kernel = "k_flow32";
-  return rounds_tail(h, st);
+  if ((rc = rounds_tail(h, st, base))) return rc;
+  h->n_coord = N;
+  h->lens_coord = h->lens_h;
+  h->inc_valid = true;
+  return BH_OK;
 }
 
 int stage_rounds(bh_handle *h) {
@@ -618,18 +677,24 @@ int stage_rounds(bh_handle *h) {
   if (h->group.empty()) {  // one shard: the segment pipeline when it applies
     Dev &d = h->d;
     d.N = (int64_t)h->h_creator.size();
-    int K = 1;
     if (d.N > 0) {
       if ((rc = upload(h))) return rc;
       if ((rc = set_chain_tables(h))) return rc;
-      K = segments_for(h);
-    }
-    if (K > 1) {
-      d.rows = d.N;
-      d.e0 = 0;
-      d.seg_lo = h->seg_zero;
-      h->xchg_ms = 0;
-      return rounds_pipelined(h, K);
+      if (segments_eligible(h)) {
+        d.rows = h->layout_rows;
+        d.e0 = 0;
+        d.seg_lo = h->seg_zero;
+        h->xchg_ms = 0;
+        // a call that only appended events resumes from the last one
+        // (cost follows the new events)
+        const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
+        if (base == d.N) {  // nothing new to divide: DivideRounds changes nothing
+          h->stage = std::max(h->stage, 1);
+          return BH_OK;
+        }
+        h->inc_calls += base > 0;
+        return rounds_pipelined(h, segments_for(d.N - base), base);
+      }
     }
   }
   if ((rc = run_local(h, rounds_coords))) return rc;
@@ -646,17 +711,19 @@ int stage_rounds(bh_handle *h) {
 // ---------------------------------------------------------------------------
 // stage 2: DecideFame -- this shard's rounds, then exchanged
 
+// only PendingRounds' rounds [P, R): a processed round's witnesses are
+// decided for good (or trapped), DecideFame never visits it again
 int fame_local(bh_handle *h) {
   if (h->stage < 1) return h->fail(BH_ERR_STATE, "DecideFame before DivideRounds");
   int64_t r0, r1;
-  shard_range(h->R, h->world, h->rank, &r0, &r1);
-  bh::launch_fame(h->d, h->R, (int32_t)r0, (int32_t)r1, h->stream);
+  shard_range(h->R - h->P, h->world, h->rank, &r0, &r1);
+  bh::launch_fame(h->d, h->R, (int32_t)(h->P + r0), (int32_t)(h->P + r1), h->stream);
   HIPCHK(h, hipGetLastError());
   return BH_OK;
 }
 
 int fame_finish(bh_handle *h) {
-  bh::launch_fame_scatter(h->d, h->wofs_h[(size_t)h->R], h->stream);
+  bh::launch_fame_scatter_range(h->d, h->wofs_h[(size_t)h->P], h->wofs_h[(size_t)h->R], h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
   h->decided_h.assign((size_t)h->R, 0);
@@ -677,7 +744,7 @@ int stage_fame(bh_handle *h) {
   int rc;
   if ((rc = run_local(h, fame_local))) return rc;
   if (h->world > 1) {
-    const int64_t R = h->R;
+    const int64_t R = h->R - h->P, P = h->P;
     const int npad = h->d.npad;
     struct {
       void *(*sel)(bh_handle *);
@@ -691,7 +758,7 @@ int stage_fame(bh_handle *h) {
     };
     for (auto &pt : parts) {
       const std::vector<int32_t> *ofs = pt.by_witness ? &h->wofs_h : nullptr;
-      if ((rc = exchange(h, pt.sel, range_bytes(h, R, pt.esz, false, ofs), range_bytes(h, R, pt.esz, true, ofs))))
+      if ((rc = exchange(h, pt.sel, range_bytes(h, R, pt.esz, false, ofs, P), range_bytes(h, R, pt.esz, true, ofs, P))))
         return rc;
     }
   }
@@ -736,10 +803,11 @@ int order_local(bh_handle *h) {
   const int32_t P1 = next_prefix(h);
   h->pinned_state[bh::ST_COUNT] = P1;  // pinned staging word (the first ST_COUNT hold the loop's done flag)
   HIPCHK(h, hipMemcpyAsync(d.state + bh::ST_P, h->pinned_state + bh::ST_COUNT, 4, hipMemcpyHostToDevice, s));
-  bh::launch_order_buckets(d, h->R, s);
+  // frames [P, P1): rounds this call processes (earlier frames are final)
+  bh::launch_order_buckets(d, h->R, h->P, s);
   int64_t f0, f1;
-  shard_range(P1, h->world, h->rank, &f0, &f1);
-  bh::launch_order_sort(d, (int32_t)f0, (int32_t)f1, s);
+  shard_range(P1 - h->P, h->world, h->rank, &f0, &f1);
+  bh::launch_order_sort(d, (int32_t)(h->P + f0), (int32_t)(h->P + f1), s);
   HIPCHK(h, hipGetLastError());
   if (h->world > 1) {  // frame offsets: the order exchange's ranges
     h->fofs_h.resize((size_t)P1 + 1);
@@ -754,7 +822,8 @@ int order_finish(bh_handle *h) {
   Dev &d = h->d;
   hipStream_t s = h->stream;
   const int32_t P1 = next_prefix(h);
-  if (h->world > 1) bh::launch_cons_pos(d, h->fofs_h[(size_t)P1], s);  // frames sorted elsewhere arrived
+  if (h->world > 1)  // frames sorted by other shards arrived
+    bh::launch_cons_pos(d, h->fofs_h[(size_t)h->P], h->fofs_h[(size_t)P1], s);
   bh::launch_trap_processed(d, h->P, P1, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[5], s));
@@ -813,16 +882,16 @@ int stage_order(bh_handle *h) {
   int rc;
   if ((rc = run_local(h, order_local))) return rc;
   if (h->world > 1) {
-    const int32_t P1 = next_prefix(h);
+    const int32_t P0 = h->P, F = next_prefix(h) - h->P;
     // order: frame f's sorted events at [frame_ofs[f], frame_ofs[f + 1])
     if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.order; },
-                       range_bytes(h, P1, 4, false, &h->fofs_h), range_bytes(h, P1, 4, true, &h->fofs_h))))
+                       range_bytes(h, F, 4, false, &h->fofs_h, P0), range_bytes(h, F, 4, true, &h->fofs_h, P0))))
       return rc;
-    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.frame_ntx; }, range_bytes(h, P1, 8, false),
-                       range_bytes(h, P1, 8, true))))
+    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.frame_ntx; }, range_bytes(h, F, 8, false, nullptr, P0),
+                       range_bytes(h, F, 8, true, nullptr, P0))))
       return rc;
-    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.frame_loaded; }, range_bytes(h, P1, 4, false),
-                       range_bytes(h, P1, 4, true))))
+    if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.frame_loaded; },
+                       range_bytes(h, F, 4, false, nullptr, P0), range_bytes(h, F, 4, true, nullptr, P0))))
       return rc;
   }
   return run_local(h, order_finish);
@@ -935,19 +1004,23 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   };
   A(&d.creator, C); A(&d.index, C); A(&d.sp, C); A(&d.op, C); A(&d.ntx, C);
   A(&d.coin, C); A(&d.sigw, (size_t)C * 8);
-  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, C); A(&d.epos, C);
-  d.la_rows = C;
-  A(&d.la, (size_t)(C + 64) * d.npad);
+  // chain-major rows: with n <= 128 each chain's region keeps slack rows
+  // (set_chain_tables) so appended events extend it in place and a call can
+  // resume where the last one stopped; room for C/8 + 1024 per chain of it
+  const int64_t L = n <= bh::FL_MAXN ? C + C / 8 + (int64_t)n * 1024 : C;
+  A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, (size_t)L); A(&d.epos, C);
+  d.la_rows = L;
+  A(&d.la, (size_t)(L + 64) * d.npad);
   // the chunked sweep's slabs (la_ev) are dead once permuted into la; the
   // firstDescendants walk output (fdt) reuses the same allocation.  The
   // flow path's column-major LA (la_col) is read while FDT is written
   // (k_flow_transpose walks as it transposes): its own allocation
-  A(&d.fdt, (size_t)(C + 128) * d.npad);  // whole 64-row tiles (fdt_pos)
+  A(&d.fdt, (size_t)(L + 128) * d.npad);  // whole 64-row tiles (fdt_pos)
   d.la_ev = d.fdt;
-  if (n <= bh::FL_MAXN) A(&d.la_col, (size_t)(C + 64) * d.npad);
+  if (n <= bh::FL_MAXN) A(&d.la_col, (size_t)(L + 64) * d.npad);
   else d.la_col = d.fdt;
-  A(&d.opdesc, (size_t)2 * (C + 128));  // k_flow32: int2 entries
-  A(&d.lt_row, (size_t)C + 64);
+  A(&d.opdesc, (size_t)2 * (L + 128));  // k_flow32: int2 entries
+  A(&d.lt_row, (size_t)L + 64);
   d.fd_cols = d.npad <= 128;
   if (d.fd_cols) {
     A(&d.ssm, R1 * n * 16);
@@ -993,7 +1066,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.rows = 0;
   d.tile_list = nullptr;
   d.ntiles = 0;
-  h->tlist_cap = C / 64 + n + 64;
+  h->tlist_cap = L / 64 + n + 64;
   if (rc == BH_OK) rc = dalloc(h, &h->tlist, (size_t)2 * h->tlist_cap);
   if (rc == BH_OK && hipHostMalloc((void **)&h->tlist_stage, (size_t)2 * h->tlist_cap * 4, hipHostMallocDefault) != hipSuccess)
     rc = BH_ERR_DEVICE;
@@ -1168,6 +1241,28 @@ int bh_synchronize(bh_handle *h) {
   for (bh_handle *x : local_shards(h)) {
     HIPCHK(h, hipSetDevice(x->device));
     HIPCHK(h, hipStreamSynchronize(x->stream));
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  return BH_OK;
+}
+
+int bh_reset_consensus(bh_handle *h) {
+  if (!h) return BH_ERR_INVALID;
+  for (bh_handle *x : local_shards(h)) {
+    HIPCHK(h, hipSetDevice(x->device));
+    HIPCHK(h, hipStreamSynchronize(x->stream));
+    HIPCHK(h, hipMemset(x->d.blocked, 0, ((size_t)x->d.R_cap + 1) * 4));
+    x->stage = 0;
+    x->coords_for = -1;
+    x->n_div = x->n_rr = 0;
+    x->R = x->P = x->R_rr = 0;
+    x->pend_dec.clear();
+    x->decided_h.clear();
+    x->nundet = 0;
+    x->ncons = x->cons_txs = x->cons_loaded = 0;
+    x->blocks.clear();
+    x->inc_valid = false;
+    x->n_coord = 0;
   }
   HIPCHK(h, hipSetDevice(h->device));
   return BH_OK;
@@ -1356,10 +1451,10 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     int rc;
     if ((rc = upload(h))) return rc;
     d.N = N;
-    d.rows = N;
     d.e0 = 0;
     d.seg_lo = h->seg_zero;
     if ((rc = set_chain_tables(h))) return rc;
+    d.rows = h->layout_rows;
     bh::launch_prep(d, h->stream);
     const bool walked = use_flow(d);
     Dev full = d;  // every LA column, whatever this shard's share of the dataflow
@@ -1368,14 +1463,13 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     if (walked) bh::launch_flow_coordinates(full, h->stream);
     else bh::launch_coordinates(full, h->stream);
     bh::launch_first_descendants(full, h->stream, walked);
+    h->inc_valid = false;  // the loop state no longer matches the layout / prefix
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
     h->stage = 0;
   }
-  int64_t row = 0;
   const int32_t c = h->h_creator[(size_t)id];
-  for (int32_t q = 0; q < c; ++q) row += (int64_t)h->chain[q].size();
-  row += h->h_index[(size_t)id];
+  const int64_t row = (int64_t)h->cstart_h[(size_t)c] + h->h_index[(size_t)id];  // chain-major layout
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (last_ancestors)
     HIPCHK(h, hipMemcpy(last_ancestors, d.la + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));

@@ -163,7 +163,8 @@ void launch_sha256(const uint8_t *data, const int64_t *off, const int32_t *len, 
 void launch_ecdsa_verify(const uint8_t *hash, const uint8_t *r, const uint8_t *s, const int32_t *key,
                          const uint8_t *pub, int64_t count, uint8_t *ok, hipStream_t st);  // kernels_ecdsa.hip
 void launch_flow_transpose(const Dev &d, hipStream_t s);
-void launch_prep(const Dev &d, hipStream_t s);
+void launch_prep(const Dev &d, hipStream_t s);  // every event: chain table (gap rows -1), loop state
+void launch_chain_scatter(const Dev &d, int64_t e_begin, hipStream_t s);  // events [e_begin, N)
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep
 void launch_chunk_depth(const Dev &d, hipStream_t s);
 void launch_la_sweep(const Dev &d, hipStream_t s);
@@ -182,11 +183,13 @@ void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wc
 // per-event round / witness; events >= n_prev (inserted since the last
 // division) also get their initial fame / rr / consensus position, and are
 // marked trapped when they are witnesses of a round < P (already processed)
-void launch_assign_rounds(const Dev &d, int64_t n_prev, int32_t P, hipStream_t s);
+void launch_assign_rounds(const Dev &d, int64_t e_begin, int64_t n_prev, int32_t P, hipStream_t s);
 // DecideFame of rounds [r0, r1) into wfame / decided / nfam / minla
 void launch_fame(const Dev &d, int32_t R, int32_t r0, int32_t r1, hipStream_t s);
 // wfame -> per-event fame (trapped witnesses stay Undefined); W witnesses
 void launch_fame_scatter(const Dev &d, int32_t W, hipStream_t s);
+// DecideFame of the rounds [r0, r1): wfame entries [wofs[r0], wofs[r1]) to fame
+void launch_fame_scatter_range(const Dev &d, int32_t w0, int32_t w1, hipStream_t s);
 // rr of events still undetermined (rr already set is kept); rounds < P are
 // live-decided iff no trapped witness; counters[3] = undetermined after it;
 // frame_cnt[r] = events received in r (every r < R)
@@ -195,10 +198,11 @@ void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s);
 // launch_order_buckets: frame offsets and unsorted frame buckets of every
 // frame; launch_order_sort: sort frames [f0, f1), their tx / loaded counts
 // and consensus positions
-void launch_order_buckets(const Dev &d, int32_t R, hipStream_t s);
+// (frames < P0 were processed by earlier calls: their order stays)
+void launch_order_buckets(const Dev &d, int32_t R, int32_t P0, hipStream_t s);
 void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s);
-// cons_pos[order[i]] = i for i < ncons (after frames sorted elsewhere arrive)
-void launch_cons_pos(const Dev &d, int64_t ncons, hipStream_t s);
+// cons_pos[order[i]] = i for i in [i0, i1) (after frames sorted elsewhere arrive)
+void launch_cons_pos(const Dev &d, int64_t i0, int64_t i1, hipStream_t s);
 // witnesses of rounds [P0, P1) still Undefined when those rounds were processed
 void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s);
 void configure_fd_kernels();

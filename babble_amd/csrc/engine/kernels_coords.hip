@@ -23,8 +23,8 @@ namespace bh {
 // ---------------------------------------------------------------------------
 // prep: chain-major id table (ParticipantEventsCache, caches.go:34-129) and
 // round-loop state.
-__global__ void k_chain_scatter(Dev d) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_chain_scatter(Dev d, int64_t e_begin) {
+  int64_t e = e_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.N) return;
   const int32_t p = d.chain_start[d.creator[e]] + d.index[e];
   d.chain_ids[p] = (int32_t)e;
@@ -42,10 +42,13 @@ __global__ void k_state_init(Dev d) {
 }
 
 void launch_prep(const Dev &d, hipStream_t s) {
-  if (d.N > 0) {
-    k_chain_scatter<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
-  }
+  if (d.rows > 0) (void)hipMemsetAsync(d.chain_ids, 0xFF, (size_t)d.rows * 4, s);  // gap rows: -1
+  launch_chain_scatter(d, 0, s);
   k_state_init<<<1, 256, 0, s>>>(d);
+}
+
+void launch_chain_scatter(const Dev &d, int64_t e_begin, hipStream_t s) {
+  if (d.N > e_begin) k_chain_scatter<<<(unsigned)((d.N - e_begin + 255) / 256), 256, 0, s>>>(d, e_begin);
 }
 
 // ---------------------------------------------------------------------------

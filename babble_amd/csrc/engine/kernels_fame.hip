@@ -385,16 +385,18 @@ void launch_fame(const Dev &d, int32_t R, int32_t r0, int32_t r1, hipStream_t s)
 
 // per-event fame from the witness-ordered results; a trapped witness
 //  stays Undefined whatever the votes say
-__global__ void k_fame_scatter(Dev d, int32_t W) {
-  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (i >= W) return;
+__global__ void k_fame_scatter(Dev d, int32_t w0, int32_t w1) {
+  const int32_t i = w0 + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= w1) return;
   const int32_t e = d.wids[i];
   d.fame[e] = d.trapped[e] ? 0 : d.wfame[i];
 }
 
-void launch_fame_scatter(const Dev &d, int32_t W, hipStream_t s) {
-  if (W <= 0) return;
-  k_fame_scatter<<<(unsigned)((W + 255) / 256), 256, 0, s>>>(d, W);
+void launch_fame_scatter(const Dev &d, int32_t W, hipStream_t s) { launch_fame_scatter_range(d, 0, W, s); }
+
+void launch_fame_scatter_range(const Dev &d, int32_t w0, int32_t w1, hipStream_t s) {
+  if (w1 <= w0) return;
+  k_fame_scatter<<<(unsigned)((w1 - w0 + 255) / 256), 256, 0, s>>>(d, w0, w1);
 }
 
 }  // namespace bh

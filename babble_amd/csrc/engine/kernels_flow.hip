@@ -572,9 +572,9 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
   const int64_t row = min(row0 + ro, N - 1);
   int32_t *prev = tile + npad * (TR + 1);
   if (t < TR) {
-    const int32_t e = d.chain_ids[row];
-    const int32_t c = d.creator[e], k = d.index[e];
-    const bool ins = t < rows && k >= d.seg_lo[c] && k < d.chain_len[c];
+    const int32_t e = d.chain_ids[row];  // -1: a gap row of a chain's region
+    const int32_t c = e >= 0 ? d.creator[e] : -1, k = e >= 0 ? d.index[e] : 0;
+    const bool ins = t < rows && e >= 0 && k >= d.seg_lo[c] && k < d.chain_len[c];
     if (ins) d.lt[e] = d.lt_row[row0 + t];
     rc[t] = c;
     rj[t] = k;
@@ -629,6 +629,7 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
     const uint64_t rest = m & (m - 1);
     const int rb0 = rest ? __builtin_ctzll(rest) : rows;  // rows [ra, rb0) of one chain
     const int32_t i = rc[ra];
+    if (i < 0) continue;  // gap rows
     // its rows inside the segment: [ra1, rb)
     const int32_t ka0 = rj[ra], lo_i = d.seg_lo[i];
     const int ra1 = ra + max(0, lo_i - ka0), rb = ra + min(rb0 - ra, clen[i] - ka0);

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(1024) void k_frame_scan(Dev d) {
   if (t == 1023) { d.state[ST_NCONS] = part[1023]; d.state[ST_NBLOCKS] = partb[1023]; }
 }
 
-__global__ __launch_bounds__(256) void k_frame_scatter(Dev d) {
+__global__ __launch_bounds__(256) void k_frame_scatter(Dev d, int32_t P0) {
   __shared__ int32_t hist[HB], basev[HB], rmin_s;
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * OB;
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void k_frame_scatter(Dev d) {
   for (int u = 0; u < 4; ++u) {
     const int64_t x = base + u * 256 + t;
     rr[u] = x < d.N ? d.rr[x] : UNSET;
-    if (rr[u] == UNSET || rr[u] >= P) rr[u] = -1;
+    if (rr[u] == UNSET || rr[u] >= P || rr[u] < P0) rr[u] = -1;  // frames < P0: ordered by earlier calls
     else lo = min(lo, rr[u]);
   }
   __syncthreads();
@@ -316,12 +316,12 @@ void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s) {
   if (R > 0) k_frame_count<<<(unsigned)((d.N + OB - 1) / OB), 256, 0, s>>>(d);
 }
 
-void launch_order_buckets(const Dev &d, int32_t R, hipStream_t s) {
+void launch_order_buckets(const Dev &d, int32_t R, int32_t P0, hipStream_t s) {
   if (R <= 0) return;
   k_order_init<<<1, 1024, 0, s>>>(d, R);
   const unsigned g = (unsigned)((d.N + OB - 1) / OB);
   k_frame_scan<<<1, 1024, 0, s>>>(d);
-  k_frame_scatter<<<g, 256, 0, s>>>(d);
+  k_frame_scatter<<<g, 256, 0, s>>>(d, P0);
 }
 
 void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s) {
@@ -329,14 +329,14 @@ void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s) {
   k_frame_sort<<<f1 - f0, 1024, FRAME_LDS_MAX * 12, s>>>(d, f0);
 }
 
-__global__ void k_cons_pos(Dev d, int64_t ncons) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < ncons) d.cons_pos[d.order[i]] = i;
+__global__ void k_cons_pos(Dev d, int64_t i0, int64_t i1) {
+  const int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < i1) d.cons_pos[d.order[i]] = i;
 }
 
-void launch_cons_pos(const Dev &d, int64_t ncons, hipStream_t s) {
-  if (ncons <= 0) return;
-  k_cons_pos<<<(unsigned)((ncons + 255) / 256), 256, 0, s>>>(d, ncons);
+void launch_cons_pos(const Dev &d, int64_t i0, int64_t i1, hipStream_t s) {
+  if (i1 <= i0) return;
+  k_cons_pos<<<(unsigned)((i1 - i0 + 255) / 256), 256, 0, s>>>(d, i0, i1);
 }
 
 }  // namespace bh

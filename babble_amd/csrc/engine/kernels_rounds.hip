@@ -741,8 +741,8 @@ void launch_witness_tables(const Dev &d, int R, hipStream_t s) {
 // received (nil) and consensus position.  A new witness of a round that is
 // already processed (r < P) is never queued again (hashgraph.go:809-815) and
 // so never decided: it is trapped.
-__global__ void k_assign(Dev d, int64_t n_prev, int32_t P) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_assign(Dev d, int64_t e_begin, int64_t n_prev, int32_t P) {
+  const int64_t e = e_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.N) return;
   const int32_t R = d.state[ST_ROUNDS];
   const int32_t c = d.creator[e], k = d.index[e];
@@ -766,9 +766,9 @@ __global__ void k_assign(Dev d, int64_t n_prev, int32_t P) {
   }
 }
 
-void launch_assign_rounds(const Dev &d, int64_t n_prev, int32_t P, hipStream_t s) {
-  if (d.N == 0) return;
-  k_assign<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d, n_prev, P);
+void launch_assign_rounds(const Dev &d, int64_t e_begin, int64_t n_prev, int32_t P, hipStream_t s) {
+  if (d.N <= e_begin) return;
+  k_assign<<<(unsigned)((d.N - e_begin + 255) / 256), 256, 0, s>>>(d, e_begin, n_prev, P);
 }
 
 // witnesses of the rounds just processed, [P0, P1), that were still

@@ -159,6 +159,11 @@ class Hashgraph:
     def synchronize(self):
         self._check(self._L.bh_synchronize(self._h))
 
+    def reset_consensus(self):
+        """Forget every pass's results, keep the events (bh_reset_consensus):
+        the next run_consensus recomputes the whole DAG."""
+        self._check(self._L.bh_reset_consensus(self._h))
+
     # ---- state ----
     def stats(self):
         s = _native.Stats()

@@ -165,7 +165,12 @@ def main():
         except ImportError:
             pass
 
+    # a step = one consensus pass over the whole resident DAG: the engine keeps
+    # its results between calls (a call only processes what was inserted
+    # since), so every step starts from reset_consensus -- the state of a
+    # Hashgraph that has just had the DAG inserted (BenchmarkConsensus)
     for w in range(args.warmup):
+        hg.reset_consensus()
         hg.run_consensus()
         log(f"warmup {w}: stages_ms={['%.2f' % x for x in hg.stage_ms()]}")
     sweep_ms, stage_tot = [], np.zeros(6)
@@ -173,6 +178,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        hg.reset_consensus()
         hg.run_consensus()
         sweep_ms.append(hg.profile()[1])
         stage_tot += np.array(hg.stage_ms())

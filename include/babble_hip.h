@@ -77,14 +77,24 @@ const char *bh_last_error(const bh_handle *h);
  * Returns BH_OK if all were accepted, else the first error code. */
 int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted);
 
-/* The consensus passes (node/core.go:335-377).  Batch schedule: each pass
- * computes its stage over every inserted event. */
+/* The consensus passes (node/core.go:335-377), with the Go Hashgraph's
+ * state kept between calls: a call after more events were inserted
+ * continues from the previous one (coordinates, rounds and fame of the new
+ * events and still-pending rounds; frames of newly decided rounds), and the
+ * result depends on the call schedule exactly as the reference's does
+ * (RoundInfo.queued, PendingRounds' sticky decided flags). */
 int bh_divide_rounds(bh_handle *h);           /* hashgraph.go:767-849 (+ coordinates) */
 int bh_decide_fame(bh_handle *h);             /* hashgraph.go:852-947 */
 int bh_decide_round_received(bh_handle *h);   /* hashgraph.go:951-1036 */
 int bh_process_decided_rounds(bh_handle *h);  /* hashgraph.go:1041-1231 */
 int bh_run_consensus(bh_handle *h);           /* all four, queued on one stream */
 int bh_synchronize(bh_handle *h);             /* wait for queued device work */
+/* Forget every pass's results, keep the inserted events: the state of a
+ * Hashgraph into which the same events were just inserted
+ * (hashgraph_test.go's createHashgraph; what BenchmarkConsensus re-runs).
+ * The next RunConsensus recomputes everything; without this call a pass
+ * only processes what was inserted since the previous one. */
+int bh_reset_consensus(bh_handle *h);
 
 typedef struct {
   int64_t n_events;
