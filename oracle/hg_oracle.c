@@ -14,6 +14,8 @@
 #include "hg_oracle.h"
 
 #include <limits.h>
+#include <openssl/sha.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -84,6 +86,31 @@ struct hgo {
   int64_t *frame_first, *frame_len;
   int32_t *frame_ev;
   int64_t frame_ev_len;
+  /* Frame roots (GetFrame, hashgraph.go:1150-1218), per frame round */
+  struct frame_roots **roots;
+  /* InmemStore.lastConsensusEvents (inmem_store.go:178-183): per slot, -1 = none */
+  int32_t *last_cons;
+  /* event bytes for Frame.Marshal (frame.go:17-26): Go-JSON body (no
+   * trailing newline) and the Signature string, per event; optional */
+  uint8_t **body, **sig;
+  int32_t *body_len, *sig_len;
+  /* FrameHash of each block (NewBlockFromFrame, block.go:100-110) */
+  uint8_t *blk_fhash;
+  int8_t *blk_has_fhash;
+};
+
+/* Root (root.go:88-96) of one participant in one frame: NextRound, the
+ * SelfParent RootEvent (an event id, or -1 for the base root event
+ * "Root<id>", root.go:75-84) and Others: key event -> RootEvent of value
+ * event, sorted by key hash (Go's encoding/json sorts map keys) */
+typedef struct {
+  int32_t next_round, sp;
+  int32_t n_others, cap_others;
+  int32_t *oth_key, *oth_val;
+} root_t;
+
+struct frame_roots {
+  root_t *r; /* [n] in participant order (Participants.ToPeerSlice) */
 };
 
 static void *xcalloc(size_t n, size_t s) {
@@ -130,6 +157,12 @@ hgo *hgo_create(int32_t n, const int64_t *participant_ids, int64_t capacity) {
   h->chain = (int32_t **)xcalloc(n, sizeof(int32_t *));
   h->chain_len = (int32_t *)xcalloc(n, 4);
   h->chain_cap = (int32_t *)xcalloc(n, 4);
+  h->last_cons = (int32_t *)xcalloc(n, 4);
+  for (int32_t i = 0; i < n; i++) h->last_cons[i] = -1;
+  h->body = (uint8_t **)xcalloc(C, sizeof(uint8_t *));
+  h->sig = (uint8_t **)xcalloc(C, sizeof(uint8_t *));
+  h->body_len = (int32_t *)xcalloc(C, 4);
+  h->sig_len = (int32_t *)xcalloc(C, 4);
   h->last_round = -1; /* inmem_store.go:45 */
   h->lcr = -1;
   return h;
@@ -151,6 +184,17 @@ void hgo_destroy(hgo *h) {
   free(h->rounds);
   free(h->blk_rr); free(h->blk_first); free(h->blk_count); free(h->blk_ntx);
   free(h->frame_done); free(h->frame_first); free(h->frame_len);
+  for (int32_t r = 0; r < h->rounds_cap; r++) {
+    if (!h->roots || !h->roots[r]) continue;
+    for (int32_t i = 0; i < h->n; i++) { free(h->roots[r]->r[i].oth_key); free(h->roots[r]->r[i].oth_val); }
+    free(h->roots[r]->r);
+    free(h->roots[r]);
+  }
+  free(h->roots);
+  free(h->last_cons);
+  for (int64_t e = 0; e < h->cap; e++) { free(h->body[e]); free(h->sig[e]); }
+  free(h->body); free(h->sig); free(h->body_len); free(h->sig_len);
+  free(h->blk_fhash); free(h->blk_has_fhash);
   free(h);
 }
 
@@ -167,6 +211,8 @@ static void ensure_round_cap(hgo *h, int32_t r) {
   memset(h->frame_done + h->rounds_cap, 0, (size_t)(nc - h->rounds_cap));
   h->frame_first = (int64_t *)xrealloc(h->frame_first, (size_t)nc * 8);
   h->frame_len = (int64_t *)xrealloc(h->frame_len, (size_t)nc * 8);
+  h->roots = (struct frame_roots **)xrealloc(h->roots, (size_t)nc * sizeof(struct frame_roots *));
+  memset(h->roots + h->rounds_cap, 0, (size_t)(nc - h->rounds_cap) * sizeof(struct frame_roots *));
   h->rounds_cap = nc;
 }
 
@@ -566,6 +612,247 @@ static int get_frame(hgo *h, int32_t rr, int64_t *first, int64_t *len) {
   return HGO_OK;
 }
 
+/* ------------------------------------------------------------------------ */
+/* Frame roots (GetFrame hashgraph.go:1150-1218, createRoot :546-640)         */
+
+static void root_add_other(root_t *r, int32_t key, int32_t val) {
+  if (r->n_others == r->cap_others) {
+    r->cap_others = r->cap_others ? 2 * r->cap_others : 4;
+    r->oth_key = (int32_t *)xrealloc(r->oth_key, (size_t)r->cap_others * 4);
+    r->oth_val = (int32_t *)xrealloc(r->oth_val, (size_t)r->cap_others * 4);
+  }
+  r->oth_key[r->n_others] = key;
+  r->oth_val[r->n_others] = val;
+  r->n_others++;
+}
+
+/* createRoot(ev) (hashgraph.go:602-640): NextRound = round(ev); SelfParent =
+ * the RootEvent of ev's self-parent (for a first event, its creator's base
+ * Root event "Root<id>" with Index / LamportTimestamp / Round -1:
+ * createSelfParentRootEvent :546-566 reads them from the Root, root.go:73-84);
+ * Others[ev] = the RootEvent of its other-parent (createOtherParentRootEvent
+ * :568-600 -- a base Root has no Others to take it from) */
+static void create_root(hgo *h, int32_t ev, root_t *r) {
+  r->next_round = round_of(h, ev);
+  r->sp = h->sp[ev];
+  if (h->op[ev] >= 0) root_add_other(r, ev, h->op[ev]);
+}
+
+static int cmp_hash_of(const hgo *hh, int32_t a, int32_t b) {
+  return memcmp(hh->hash + (size_t)a * 32, hh->hash + (size_t)b * 32, 32);
+}
+
+/* the roots of frame rr, whose sorted events are frame_ev[f .. f + l);
+ * lastConsensusEvents as they stand before the frame's events are added */
+static void frame_roots(hgo *h, int32_t rr, int64_t f, int64_t l) {
+  ensure_round_cap(h, rr);
+  if (h->roots[rr]) return; /* GetFrame is cached by the Store (inmem_store.go:254-270) */
+  const int32_t n = h->n;
+  struct frame_roots *fr = (struct frame_roots *)xcalloc(1, sizeof *fr);
+  fr->r = (root_t *)xcalloc((size_t)n, sizeof(root_t));
+  int8_t *has = (int8_t *)xcalloc((size_t)n, 1);
+  /* "Each time we run into the first Event of a participant, we create a
+   * Root for it" (:1161-1172) */
+  for (int64_t k = 0; k < l; k++) {
+    const int32_t ev = h->frame_ev[f + k], p = h->creator[ev];
+    if (!has[p]) { has[p] = 1; create_root(h, ev, &fr->r[p]); }
+  }
+  /* participants with no event in the frame: createRoot(last consensus
+   * event) or, with none, their Root -- a base Root here (:1174-1197) */
+  for (int32_t p = 0; p < n; p++) {
+    if (has[p]) continue;
+    if (h->last_cons[p] >= 0) create_root(h, h->last_cons[p], &fr->r[p]);
+    else { fr->r[p].next_round = 0; fr->r[p].sp = -1; }
+  }
+  /* other-parents outside the frame (:1199-1218): `treated` holds the
+   * frame's events met so far in sorted order; an event whose other-parent
+   * is not among them, and which is not the event its creator's root was
+   * made from (same self-parent), adds its other-parent to that root */
+  int8_t *treated = (int8_t *)xcalloc((size_t)(h->N ? h->N : 1), 1);
+  for (int64_t k = 0; k < l; k++) {
+    const int32_t ev = h->frame_ev[f + k];
+    treated[ev] = 1;
+    const int32_t op = h->op[ev];
+    if (op >= 0 && !treated[op] && h->sp[ev] != fr->r[h->creator[ev]].sp)
+      root_add_other(&fr->r[h->creator[ev]], ev, op);
+  }
+  free(treated);
+  free(has);
+  /* Go's encoding/json writes map keys sorted ("0x" + uppercase hex: the
+   * string order is the hash byte order) */
+  for (int32_t p = 0; p < n; p++) {
+    root_t *r = &fr->r[p];
+    for (int32_t a = 1; a < r->n_others; a++) {
+      const int32_t kk = r->oth_key[a], vv = r->oth_val[a];
+      int32_t b = a - 1;
+      while (b >= 0 && cmp_hash_of(h, kk, r->oth_key[b]) < 0) {
+        r->oth_key[b + 1] = r->oth_key[b];
+        r->oth_val[b + 1] = r->oth_val[b];
+        b--;
+      }
+      r->oth_key[b + 1] = kk;
+      r->oth_val[b + 1] = vv;
+    }
+  }
+  h->roots[rr] = fr;
+}
+
+/* ---- Go encoding/json (json.NewEncoder(..).Encode) of Frame / Block ---- */
+typedef struct { uint8_t *p; int64_t len, cap; } jbuf;
+static void jput(jbuf *b, const void *src, int64_t n) {
+  if (b->len + n > b->cap) {
+    while (b->len + n > b->cap) b->cap = b->cap ? 2 * b->cap : 4096;
+    b->p = (uint8_t *)xrealloc(b->p, (size_t)b->cap);
+  }
+  memcpy(b->p + b->len, src, (size_t)n);
+  b->len += n;
+}
+static void jstr(jbuf *b, const char *s) { jput(b, s, (int64_t)strlen(s)); }
+static void jint(jbuf *b, long long v) {
+  char t[32];
+  jput(b, t, snprintf(t, sizeof t, "%lld", v));
+}
+/* Event.Hex() = fmt.Sprintf("0x%X", hash) (event.go:239-245) */
+static void jhex(jbuf *b, const hgo *h, int32_t ev) {
+  static const char HX[] = "0123456789ABCDEF";
+  char t[66];
+  const uint8_t *x = h->hash + (size_t)ev * 32;
+  t[0] = '0'; t[1] = 'x';
+  for (int i = 0; i < 32; i++) { t[2 + 2 * i] = HX[x[i] >> 4]; t[3 + 2 * i] = HX[x[i] & 15]; }
+  jput(b, t, 66);
+}
+/* []byte encodes as a base64 (StdEncoding, padded) string */
+static void jb64(jbuf *b, const uint8_t *x, int n) {
+  static const char A[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  char t[4];
+  for (int i = 0; i < n; i += 3) {
+    const uint32_t v = (uint32_t)x[i] << 16 | (i + 1 < n ? (uint32_t)x[i + 1] << 8 : 0) | (i + 2 < n ? x[i + 2] : 0);
+    t[0] = A[v >> 18]; t[1] = A[(v >> 12) & 63];
+    t[2] = i + 1 < n ? A[(v >> 6) & 63] : '=';
+    t[3] = i + 2 < n ? A[v & 63] : '=';
+    jput(b, t, 4);
+  }
+}
+/* RootEvent (root.go:65-71); ev < 0: the base root event of slot p */
+static void jroot_event(jbuf *b, hgo *h, int32_t ev, int32_t p) {
+  jstr(b, "{\"Hash\":\"");
+  if (ev < 0) { jstr(b, "Root"); jint(b, h->pids[p]); }
+  else jhex(b, h, ev);
+  jstr(b, "\",\"CreatorID\":");
+  jint(b, h->pids[ev < 0 ? p : h->creator[ev]]);
+  jstr(b, ",\"Index\":");
+  jint(b, ev < 0 ? -1 : h->index[ev]);
+  jstr(b, ",\"LamportTimestamp\":");
+  jint(b, ev < 0 ? -1 : lamport_of(h, ev));
+  jstr(b, ",\"Round\":");
+  jint(b, ev < 0 ? -1 : round_of(h, ev));
+  jstr(b, "}");
+}
+
+static int frame_has_bytes(const hgo *h, int64_t f, int64_t l) {
+  for (int64_t k = 0; k < l; k++)
+    if (!h->body[h->frame_ev[f + k]] || !h->sig[h->frame_ev[f + k]]) return 0;
+  return 1;
+}
+
+/* Frame.Marshal (frame.go:17-26): {"Round":..,"Roots":[..],"Events":[..]}
+ * + "\n"; an Event encodes its exported fields Body and Signature
+ * (event.go:102-106).  Returns 0, or -1 if unavailable. */
+static int frame_json(hgo *h, int32_t rr, jbuf *b) {
+  if (rr < 0 || rr >= h->rounds_cap || !h->roots[rr] || !h->frame_done[rr]) return -1;
+  const int64_t f = h->frame_first[rr], l = h->frame_len[rr];
+  if (!frame_has_bytes(h, f, l)) return -1;
+  b->len = 0;
+  jstr(b, "{\"Round\":");
+  jint(b, rr);
+  jstr(b, ",\"Roots\":[");
+  for (int32_t p = 0; p < h->n; p++) {
+    const root_t *r = &h->roots[rr]->r[p];
+    if (p) jstr(b, ",");
+    jstr(b, "{\"NextRound\":");
+    jint(b, r->next_round);
+    jstr(b, ",\"SelfParent\":");
+    jroot_event(b, h, r->sp, p);
+    jstr(b, ",\"Others\":{");
+    for (int32_t k = 0; k < r->n_others; k++) {
+      if (k) jstr(b, ",");
+      jstr(b, "\"");
+      jhex(b, h, r->oth_key[k]);
+      jstr(b, "\":");
+      jroot_event(b, h, r->oth_val[k], p);
+    }
+    jstr(b, "}}");
+  }
+  jstr(b, "],\"Events\":[");
+  for (int64_t k = 0; k < l; k++) {
+    const int32_t ev = h->frame_ev[f + k];
+    if (k) jstr(b, ",");
+    jstr(b, "{\"Body\":");
+    jput(b, h->body[ev], h->body_len[ev]);
+    jstr(b, ",\"Signature\":\"");
+    jput(b, h->sig[ev], h->sig_len[ev]);
+    jstr(b, "\"}");
+  }
+  jstr(b, "]}\n");
+  return 0;
+}
+
+/* the base64 transaction strings of an event body's JSON: the text between
+ * the brackets of its leading "Transactions" array (EventBody field order,
+ * event.go:16-21; null when nil); *len 0 when there are none */
+static const uint8_t *body_txs(const hgo *h, int32_t ev, int32_t *len) {
+  static const char P[] = "{\"Transactions\":[";
+  const uint8_t *x = h->body[ev];
+  *len = 0;
+  if (h->body_len[ev] < (int32_t)sizeof P || memcmp(x, P, sizeof P - 1)) return NULL;
+  int32_t k = sizeof P - 1;
+  while (k < h->body_len[ev] && x[k] != ']') k++;
+  *len = k - (int32_t)(sizeof P - 1);
+  return x + sizeof P - 1;
+}
+
+/* Block.Marshal with no signatures yet (block.go:92-97, 178-185):
+ * {"Body":{"Index":..,"RoundReceived":..,"StateHash":null,"FrameHash":"b64",
+ * "Transactions":[..]},"Signatures":{}} + "\n"; the Body alone (with its own
+ * newline) when body_only */
+static void block_json(hgo *h, int64_t blk, int body_only, jbuf *b) {
+  const int32_t rr = h->blk_rr[blk];
+  b->len = 0;
+  if (!body_only) jstr(b, "{\"Body\":");
+  jstr(b, "{\"Index\":");
+  jint(b, blk);
+  jstr(b, ",\"RoundReceived\":");
+  jint(b, rr);
+  jstr(b, ",\"StateHash\":null,\"FrameHash\":\"");
+  jb64(b, h->blk_fhash + (size_t)blk * 32, 32);
+  jstr(b, "\",\"Transactions\":[");
+  int first = 1;
+  for (int64_t k = 0; k < h->blk_count[blk]; k++) {
+    int32_t tl;
+    const uint8_t *t = body_txs(h, h->cons[h->blk_first[blk] + k], &tl);
+    if (!tl) continue;
+    if (!first) jstr(b, ",");
+    jput(b, t, tl);
+    first = 0;
+  }
+  jstr(b, body_only ? "]}\n" : "]},\"Signatures\":{}}\n");
+}
+
+int hgo_set_event_bytes(hgo *h, int32_t e, const uint8_t *body, int32_t body_len, const uint8_t *sig,
+                        int32_t sig_len) {
+  if (e < 0 || e >= h->N || body_len < 0 || sig_len < 0) return HGO_ERR_STATE;
+  if (body_len > 0 && body[body_len - 1] == '\n') body_len--; /* the Encoder's newline is not part of the Event's JSON */
+  free(h->body[e]);
+  free(h->sig[e]);
+  h->body[e] = (uint8_t *)xcalloc((size_t)body_len + 1, 1);
+  memcpy(h->body[e], body, (size_t)body_len);
+  h->body_len[e] = body_len;
+  h->sig[e] = (uint8_t *)xcalloc((size_t)sig_len + 1, 1);
+  memcpy(h->sig[e], sig, (size_t)sig_len);
+  h->sig_len[e] = sig_len;
+  return HGO_OK;
+}
+
 int hgo_process_decided_rounds(hgo *h) {
   int32_t processed = 0;
   for (int32_t p = 0; p < h->pend_len; p++) {
@@ -574,6 +861,7 @@ int hgo_process_decided_rounds(hgo *h) {
     if (h->has_lcr && pr->index == h->lcr) continue;
     int64_t f, l;
     if (get_frame(h, pr->index, &f, &l) != HGO_OK) return HGO_ERR_STATE;
+    frame_roots(h, pr->index, f, l); /* before the frame's events become consensus events */
     if (l > 0) {
       int64_t first = h->ncons, txs = 0;
       for (int64_t k = 0; k < l; k++) {
@@ -583,6 +871,7 @@ int hgo_process_decided_rounds(hgo *h) {
         h->consensus_txs += h->ntx[e];
         txs += h->ntx[e];
         if (h->index[e] == 0 || h->ntx[e] > 0) h->pending_loaded--;
+        h->last_cons[h->creator[e]] = e; /* InmemStore.AddConsensusEvent (inmem_store.go:178-183) */
       }
       /* NewBlockFromFrame(LastBlockIndex()+1, frame) (block.go:100-110) */
       if (h->nblocks == h->blk_cap) {
@@ -591,6 +880,14 @@ int hgo_process_decided_rounds(hgo *h) {
         h->blk_first = (int64_t *)xrealloc(h->blk_first, (size_t)h->blk_cap * 8);
         h->blk_count = (int64_t *)xrealloc(h->blk_count, (size_t)h->blk_cap * 8);
         h->blk_ntx = (int64_t *)xrealloc(h->blk_ntx, (size_t)h->blk_cap * 8);
+        h->blk_fhash = (uint8_t *)xrealloc(h->blk_fhash, (size_t)h->blk_cap * 32);
+        h->blk_has_fhash = (int8_t *)xrealloc(h->blk_has_fhash, (size_t)h->blk_cap);
+      }
+      { /* FrameHash = SHA-256 of the frame's JSON (frame.go:35-41), when the event bytes are known */
+        jbuf b = {0};
+        h->blk_has_fhash[h->nblocks] = frame_json(h, pr->index, &b) == 0;
+        if (h->blk_has_fhash[h->nblocks]) SHA256(b.p, (size_t)b.len, h->blk_fhash + (size_t)h->nblocks * 32);
+        free(b.p);
       }
       h->blk_rr[h->nblocks] = pr->index;
       h->blk_first[h->nblocks] = first;
@@ -679,6 +976,50 @@ int64_t hgo_undetermined(const hgo *h, int32_t *ids, int64_t cap) {
   int64_t k = h->und_len < cap ? h->und_len : cap;
   if (ids) memcpy(ids, h->und, (size_t)k * 4);
   return h->und_len;
+}
+
+int32_t hgo_frame_roots(const hgo *h, int32_t rr, int32_t *next_round, int32_t *sp, int32_t *n_others,
+                        int32_t *oth_key, int32_t *oth_val, int32_t cap) {
+  if (rr < 0 || rr >= h->rounds_cap || !h->roots[rr]) return -1;
+  int32_t k = 0;
+  for (int32_t p = 0; p < h->n; p++) {
+    const root_t *r = &h->roots[rr]->r[p];
+    if (next_round) next_round[p] = r->next_round;
+    if (sp) sp[p] = r->sp;
+    if (n_others) n_others[p] = r->n_others;
+    for (int32_t q = 0; q < r->n_others; q++, k++)
+      if (k < cap) {
+        if (oth_key) oth_key[k] = r->oth_key[q];
+        if (oth_val) oth_val[k] = r->oth_val[q];
+      }
+  }
+  return k;
+}
+
+static int64_t jbuf_out(jbuf *b, uint8_t *buf, int64_t cap) {
+  if (buf) memcpy(buf, b->p, (size_t)(b->len < cap ? b->len : cap));
+  const int64_t len = b->len;
+  free(b->p);
+  return len;
+}
+
+int64_t hgo_frame_json(hgo *h, int32_t rr, uint8_t *buf, int64_t cap) {
+  jbuf b = {0};
+  if (frame_json(h, rr, &b) != 0) { free(b.p); return -1; }
+  return jbuf_out(&b, buf, cap);
+}
+
+int hgo_block_frame_hash(const hgo *h, int64_t blk, uint8_t *out32) {
+  if (blk < 0 || blk >= h->nblocks || !h->blk_has_fhash[blk]) return -1;
+  memcpy(out32, h->blk_fhash + (size_t)blk * 32, 32);
+  return 0;
+}
+
+int64_t hgo_block_json(hgo *h, int64_t blk, int body_only, uint8_t *buf, int64_t cap) {
+  if (blk < 0 || blk >= h->nblocks || !h->blk_has_fhash[blk]) return -1;
+  jbuf b = {0};
+  block_json(h, blk, body_only, &b);
+  return jbuf_out(&b, buf, cap);
 }
 
 int hgo_see(hgo *h, int32_t x, int32_t y) { return see(h, x, y); }

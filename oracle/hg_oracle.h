@@ -90,6 +90,27 @@ int32_t hgo_pending_rounds(const hgo *h, int32_t *index, int8_t *decided, int32_
 void hgo_coordinates(const hgo *h, int32_t id, int32_t *la, int32_t *fd);
 /* UndeterminedEvents queue, in order */
 int64_t hgo_undetermined(const hgo *h, int32_t *ids, int64_t cap);
+/* ---- frames and blocks (GetFrame hashgraph.go:1125-1231, frame.go,
+ * root.go, block.go) ---- */
+/* The bytes Frame.Marshal needs of event e: its Go-JSON body
+ * (EventBody.Marshal, event.go:32-39; the trailing newline is dropped) and
+ * its Signature string.  Optional: without them no FrameHash is computed. */
+int hgo_set_event_bytes(hgo *h, int32_t e, const uint8_t *body, int32_t body_len, const uint8_t *sig,
+                        int32_t sig_len);
+/* Roots of frame rr (a processed round), participant order: NextRound,
+ * SelfParent (event id, -1 = the base root event), number of Others; then
+ * the Others (key event -> RootEvent of the value event) of all roots in
+ * order, each root's sorted by key hash.  Returns the total number of
+ * Others, -1 if the frame has no roots. */
+int32_t hgo_frame_roots(const hgo *h, int32_t rr, int32_t *next_round, int32_t *sp, int32_t *n_others,
+                        int32_t *oth_key, int32_t *oth_val, int32_t cap);
+/* Frame.Marshal of frame rr (with the Encoder's newline): returns its
+ * length and copies up to cap bytes; -1 if unavailable */
+int64_t hgo_frame_json(hgo *h, int32_t rr, uint8_t *buf, int64_t cap);
+/* FrameHash of block blk (SHA-256 of its frame's JSON); -1 if unavailable */
+int hgo_block_frame_hash(const hgo *h, int64_t blk, uint8_t *out32);
+/* Block.Marshal (no signatures) or, body_only, BlockBody.Marshal of block blk */
+int64_t hgo_block_json(hgo *h, int64_t blk, int body_only, uint8_t *buf, int64_t cap);
 /* primitives, exposed for the ancestry known-answer tests */
 int hgo_see(hgo *h, int32_t x, int32_t y);
 int hgo_strongly_see(hgo *h, int32_t x, int32_t y);

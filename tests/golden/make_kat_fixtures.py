@@ -27,6 +27,17 @@ def play(to, index, sp, op, name, txs=None):
     return [to, index, sp or None, op or None, name, txs]
 
 
+# Root / RootEvent (root.go:65-96) by name: a RootEvent is [event name or
+# "Root" (the base root event NewBaseRootEvent, root.go:73-84), creator slot,
+# Index, LamportTimestamp, Round]; next_round None = not asserted
+def root(next_round, self_parent, others):
+    return {"next_round": next_round, "self_parent": self_parent, "others": others}
+
+
+def base_root(slot, next_round=0):
+    return root(next_round, ["Root", slot, -1, -1, -1], {})
+
+
 FIXTURES = {}
 
 # --- initHashgraph, hashgraph_test.go:161-202 ------------------------------
@@ -198,6 +209,14 @@ FIXTURES["kat_consensus"] = {
             "2": ["f1", "f1b", "f0", "f2", "f10", "f0x", "f21", "f02", "f02b"]},
         # TestKnown hashgraph_test.go:1536-1553
         "known": [10, 9, 9],
+        # TestGetFrame hashgraph_test.go:1565-1670: the roots of frames 1 and
+        # 2 (SelfParent and Others; the test does not compare NextRound)
+        "frame_roots": {
+            "1": [base_root(0, None), base_root(1, None), base_root(2, None)],
+            "2": [root(None, ["e02", 0, 1, 4, 0],
+                       {"f0": ["f1b", 1, 3, 6, 1], "f0x": ["e21", 2, 1, 2, 0]}),
+                  root(None, ["e10", 1, 1, 1, 0], {"f1": ["e02", 0, 1, 4, 0]}),
+                  root(None, ["e21b", 2, 2, 3, 0], {"f2": ["f1b", 1, 3, 6, 1]})]},
     },
 }
 
@@ -296,6 +315,17 @@ FIXTURES["kat_sparse"] = {
             "1": ["w00", "w01", "w02", "w03", "e10", "e21", "e32"],
             "2": ["w10", "w11", "f01", "w12", "w13"],
             "3": ["w21", "w22", "w23", "g13"]},
+        # the roots it asserts with reflect.DeepEqual (hashgraph_test.go:2568-2653)
+        "frame_roots": {
+            "1": [base_root(0), base_root(1), base_root(2), base_root(3)],
+            "2": [root(1, ["w00", 0, 0, 0, 0], {"w10": ["e32", 3, 1, 3, 0]}),
+                  root(1, ["e10", 1, 1, 1, 0], {"w11": ["w10", 0, 1, 4, 1]}),
+                  root(1, ["e21", 2, 1, 2, 0], {"w12": ["f01", 0, 2, 6, 1]}),
+                  root(1, ["e32", 3, 1, 3, 0], {"w13": ["w12", 2, 2, 7, 1]})],
+            "3": [root(1, ["w10", 0, 1, 4, 1], {"f01": ["w11", 1, 2, 5, 1]}),
+                  root(2, ["w11", 1, 2, 5, 1], {"w21": ["w13", 3, 2, 8, 1]}),
+                  root(2, ["w12", 2, 2, 7, 1], {"w22": ["w21", 1, 3, 9, 2]}),
+                  root(2, ["w13", 3, 2, 8, 1], {"w23": ["w22", 2, 3, 10, 2]})]},
     },
 }
 

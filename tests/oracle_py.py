@@ -52,6 +52,14 @@ def lib():
         L.hgo_round_of.argtypes = [P, I32]
         L.hgo_lamport_of.restype = I32
         L.hgo_lamport_of.argtypes = [P, I32]
+        L.hgo_set_event_bytes.argtypes = [P, I32, C.c_char_p, I32, C.c_char_p, I32]
+        L.hgo_frame_roots.restype = I32
+        L.hgo_frame_roots.argtypes = [P, I32, VP, VP, VP, VP, VP, I32]
+        L.hgo_frame_json.restype = I64
+        L.hgo_frame_json.argtypes = [P, I32, VP, I64]
+        L.hgo_block_frame_hash.argtypes = [P, I64, VP]
+        L.hgo_block_json.restype = I64
+        L.hgo_block_json.argtypes = [P, I64, C.c_int, VP, I64]
         _LIB = L
     return _LIB
 
@@ -184,3 +192,48 @@ class Oracle:
 
     def witness(self, x):
         return bool(self.L.hgo_witness_of(self.h, x))
+
+    # ---- frames and blocks ----
+    def set_event_bytes(self, e, body, sig):
+        if self.L.hgo_set_event_bytes(self.h, int(e), bytes(body), len(body), bytes(sig), len(sig)):
+            raise ValueError(f"event {e} out of range")
+
+    def frame_roots(self, rr):
+        """Roots of frame rr, participant order: [(next_round, self_parent
+        event or -1 for the base root, [(key event, value event), ...])]."""
+        n = self.n
+        nr, sp, no = (np.empty(n, np.int32) for _ in range(3))
+        k = self.L.hgo_frame_roots(self.h, rr, _p(nr), _p(sp), _p(no), None, None, 0)
+        if k < 0:
+            return None
+        key = np.empty(max(k, 1), np.int32)
+        val = np.empty(max(k, 1), np.int32)
+        self.L.hgo_frame_roots(self.h, rr, None, None, None, _p(key), _p(val), k)
+        out, o = [], 0
+        for p in range(n):
+            out.append((int(nr[p]), int(sp[p]),
+                        [(int(key[o + j]), int(val[o + j])) for j in range(no[p])]))
+            o += int(no[p])
+        return out
+
+    def frame_json(self, rr):
+        k = self.L.hgo_frame_json(self.h, rr, None, 0)
+        if k < 0:
+            return None
+        buf = np.empty(k, np.uint8)
+        self.L.hgo_frame_json(self.h, rr, _p(buf), k)
+        return buf.tobytes()
+
+    def block_frame_hash(self, b):
+        out = np.empty(32, np.uint8)
+        if self.L.hgo_block_frame_hash(self.h, b, _p(out)):
+            return None
+        return out.tobytes()
+
+    def block_json(self, b, body_only=False):
+        k = self.L.hgo_block_json(self.h, b, int(body_only), None, 0)
+        if k < 0:
+            return None
+        buf = np.empty(k, np.uint8)
+        self.L.hgo_block_json(self.h, b, int(body_only), _p(buf), k)
+        return buf.tobytes()
