@@ -24,14 +24,16 @@ SYMBOLS = (
     "bh_run_consensus", "bh_synchronize", "bh_reset_consensus", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_round_info", "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
-    "bh_hash_bodies", "bh_verify_signatures", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
+    "bh_hash_bodies", "bh_verify_signatures", "bh_set_event_bytes", "bh_get_frame_roots",
+    "bh_get_frame_json", "bh_get_block_hashes", "bh_get_block_json", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
 )
 
 
 class Config(C.Structure):
     _fields_ = [("n_participants", C.c_int32), ("participant_ids", C.POINTER(C.c_int64)),
                 ("max_events", C.c_int64), ("device", C.c_int32),
-                ("n_devices", C.c_int32), ("device_ids", C.POINTER(C.c_int32))]
+                ("n_devices", C.c_int32), ("device_ids", C.POINTER(C.c_int32)),
+                ("frames", C.c_int32)]
 
 
 class Events(C.Structure):
@@ -97,6 +99,16 @@ def load():
     L.bh_hash_bodies.restype = C.c_int
     L.bh_verify_signatures.argtypes = [P, VP, VP, VP, VP, I64, VP, I32, VP]
     L.bh_verify_signatures.restype = C.c_int
+    L.bh_set_event_bytes.argtypes = [P, I64, I64, VP, VP, VP, VP]
+    L.bh_set_event_bytes.restype = C.c_int
+    L.bh_get_frame_roots.argtypes = [P, I32, VP, VP, VP, VP, VP, I32]
+    L.bh_get_frame_roots.restype = I32
+    L.bh_get_frame_json.argtypes = [P, I32, VP, I64]
+    L.bh_get_frame_json.restype = I64
+    L.bh_get_block_hashes.argtypes = [P, I64, I64, VP, VP, VP]
+    L.bh_get_block_hashes.restype = C.c_int
+    L.bh_get_block_json.argtypes = [P, I64, I32, VP, I64]
+    L.bh_get_block_json.restype = I64
     L.bh_comm_unique_id.argtypes = [VP]
     L.bh_comm_unique_id.restype = C.c_int
     L.bh_comm_init.argtypes = [P, I32, I32, VP]

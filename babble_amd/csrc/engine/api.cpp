@@ -28,139 +28,12 @@
 
 #include "babble_hip.h"
 #include "engine.h"
-
-using bh::Dev;
-
-namespace {
-
-constexpr int ITER_BATCH = 32;  // round-loop iterations per graph replay
-constexpr int NSTAGE = 5;
-
-struct Block {
-  int32_t rr;
-  int64_t first, count, ntx;
-};
-
-}  // namespace
-
-struct bh_handle {
-  Dev d{};
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  int64_t cap = 0;
-  // host mirrors (insert bookkeeping: ParticipantEventsCache + checks)
-  std::vector<int64_t> pids;
-  // participant ID -> slot: open addressing, power-of-two table >= 4n,
-  // linear probing (one or two probes per lookup on the insert loop)
-  std::vector<int64_t> slot_key;
-  std::vector<int32_t> slot_val;
-  uint64_t slot_mask = 0;
-  int32_t slot_find(int64_t id) const {
-    for (uint64_t i = ((uint64_t)id * 0x9E3779B97F4A7C15ull) >> 32 & slot_mask;; i = (i + 1) & slot_mask) {
-      if (slot_val[i] < 0) return -1;
-      if (slot_key[i] == id) return slot_val[i];
-    }
-  }
-  std::vector<std::vector<int32_t>> chain;  // ids by creator, by index
-  std::vector<int32_t> h_creator, h_index, h_sp, h_op, h_ntx;
-  std::vector<uint8_t> h_coin;
-  std::vector<uint32_t> h_sigw;
-  int64_t uploaded = 0;  // events already on the device
-  int64_t loaded_total = 0;
-  // The Go Hashgraph's state persists across calls: InsertEvent appends to
-  // UndeterminedEvents and changes nothing else; each pass updates its own
-  // part (hashgraph.go:714-1122).  The engine keeps the same split.
-  //   n_div   events covered by the last DivideRounds (round / witness / LT)
-  //   n_rr    events covered by the last DecideRoundReceived
-  //   R       rounds (Store.LastRound() + 1)
-  //   P       processed prefix: LastConsensusRound + 1
-  //   pend_dec  PendingRounds' decided flags for rounds [P, R): sticky, as
-  //             updatePendingRounds only ever sets them (hashgraph.go:689-695)
-  int stage = 0;  // last pass run: 0 none, 1 rounds, 2 fame, 3 rr, 4 processed
-  int coords_for = -1;  // N the device coordinates were computed for
-  int64_t n_div = 0, n_rr = 0;
-  int32_t R = 0, P = 0;
-  std::vector<int8_t> pend_dec;     // indexed by round, meaningful for [P, R)
-  std::vector<int8_t> decided_h;    // last fame pass: round r's witnesses all decided
-  int64_t nundet = 0;               // undetermined among [0, n_rr) after the last rr pass
-  int32_t R_rr = 0;                 // R at the last rr pass (frame_cnt covers [0, R_rr))
-  int64_t ncons = 0, cons_txs = 0, cons_loaded = 0;
-  std::vector<Block> blocks;
-  // round-loop graph
-  hipGraphExec_t graph = nullptr;
-  Dev graph_dev{};
-  int32_t *pinned_state = nullptr;
-  uint8_t *sha_buf = nullptr;  // bh_hash_bodies scratch
-  size_t sha_cap = 0;
-  hipEvent_t ev[NSTAGE + 1]{};
-  hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)
-  float sweep_ms = 0;
-  const char *sweep_kernel = "";
-  float stage_ms[NSTAGE]{};
-  int64_t iters = 0;
-  int64_t *d_counters_host = nullptr;
-  // segment pipeline: coordinates of prefix s + 1 on
-  // stream2 while the round loop runs prefix s on `stream`
-  hipStream_t stream2 = nullptr;
-  int32_t *seg_zero = nullptr;   // [n] zeros: seg_lo of a one-segment view
-  int32_t *segbuf = nullptr;     // [2 parities][lo, len][n]
-  int32_t *seg_stage = nullptr;  // pinned staging of segbuf, same layout
-  hipGraphExec_t seg_graph[2] = {nullptr, nullptr};
-  Dev seg_graph_dev[2]{};
-  std::vector<hipEvent_t> seg_ev;  // per segment: coordinates done, k_flow32 start / end
-  int32_t segments_used = 1;
-  int32_t *tlist = nullptr, *tlist_stage = nullptr;  // [2 parities][tlist_cap] segment tile lists
-  int64_t tlist_cap = 0;
-  std::vector<int32_t> cstart_h;  // chain_start as uploaded
-  std::vector<int32_t> cap_h;     // rows of each chain's region
-  std::vector<int32_t> lens_h;    // chain lengths as uploaded
-  int64_t layout_rows = 0;        // rows of the layout (regions included)
-  bool layout_changed = true;
-  // incremental calls (a call that only appended events runs them as one
-  // more segment): coordinates and round loop hold the first n_coord events
-  // of the current layout; lens_coord their chain lengths
-  bool inc_valid = false;
-  int64_t n_coord = 0;
-  int64_t inc_calls = 0;  // DivideRounds calls that resumed (statistics)
-  std::vector<int32_t> lens_coord;
-  // sharding
-  int32_t rank = 0, world = 1;
-  std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
-  ncclComm_t comm = nullptr;       // multi-process group (bh_comm_init)
-  bool shard_cols = false;         // split the coordinate dataflow's LA columns (else every shard computes all)
-  float xchg_ms = 0;               // exchange time of the last pass sequence (host wall, incl. waits)
-  std::vector<int32_t> wofs_h;     // [R + 1] witness offsets (fame exchange ranges; launch size)
-  std::vector<int32_t> fofs_h;     // [P + 1] frame offsets (order exchange ranges)
-
-  int fail(int code, const char *fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    err = buf;
-    return code;
-  }
-};
-
-#define HIPCHK(h, call)                                                              \
-  do {                                                                               \
-    hipError_t e_ = (call);                                                          \
-    if (e_ != hipSuccess)                                                            \
-      return (h)->fail(BH_ERR_DEVICE, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
-                       __FILE__, __LINE__);                                          \
-  } while (0)
+#include "handle.h"
 
 namespace {
-
-template <class T>
-int dalloc(bh_handle *h, T **p, size_t count) {
-  HIPCHK(h, hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T)));
-  return BH_OK;
-}
 
 void free_all(bh_handle *h) {
+  frames_free(h);
   Dev &d = h->d;
   void *ptrs[] = {d.creator, d.index, d.sp, d.op, d.ntx, d.coin, d.sigw, d.chain_start,
                   d.chain_len, d.chain_ids, d.epos, d.la, d.lt, d.depth, d.chunk_maxd, d.desc, d.B,
@@ -206,7 +79,10 @@ int upload(bh_handle *h) {
   HIPCHK(h, hipMemcpyAsync(d.ntx + a, h->h_ntx.data() + a, k * 4, hipMemcpyHostToDevice, s));
   HIPCHK(h, hipMemcpyAsync(d.coin + a, h->h_coin.data() + a, k, hipMemcpyHostToDevice, s));
   HIPCHK(h, hipMemcpyAsync(d.sigw + a * 8, h->h_sigw.data() + a * 8, k * 32, hipMemcpyHostToDevice, s));
+  if (h->frames_on)  // h_hash holds the events [a, b)
+    HIPCHK(h, hipMemcpyAsync(h->fr.hash + a * 32, h->h_hash.data(), k * 32, hipMemcpyHostToDevice, s));
   HIPCHK(h, hipStreamSynchronize(s));
+  h->h_hash.clear();
   h->uploaded = b;
   return BH_OK;
 }
@@ -830,6 +706,8 @@ int order_finish(bh_handle *h) {
   HIPCHK(h, hipStreamSynchronize(s));
   int32_t st[bh::ST_COUNT];
   HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
+  const int32_t P0 = h->P;
+  const int64_t ncons0 = h->ncons;
   h->P = P1;
   h->ncons = st[bh::ST_NCONS];
   h->cons_txs = h->cons_loaded = 0;
@@ -846,6 +724,10 @@ int order_finish(bh_handle *h) {
       h->cons_txs += ntx[r];
       h->cons_loaded += ld[r];
     }
+  }
+  if (h->frames_on && P1 > P0) {
+    const int rc = frames_project(h, P0, P1, ncons0, h->ncons);
+    if (rc != BH_OK) return rc;
   }
   h->stage = 4;
   for (int i = 0; i < NSTAGE; ++i) {
@@ -1081,6 +963,10 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   if (rc == BH_OK && hipMemset(d.state, 0, bh::ST_COUNT * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.counters, 0, 4 * 8) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.blocked, 0, R1 * 4) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && cfg->frames) {
+    h->frames_on = true;
+    rc = frames_alloc(h);
+  }
   if (rc == BH_OK && getenv("BH_DIAG") && atoi(getenv("BH_DIAG"))) {
     rc = dalloc(h, &d.diag, bh::DG_COUNT);
     if (rc == BH_OK && hipMemset(d.diag, 0, bh::DG_COUNT * 8) != hipSuccess) rc = BH_ERR_DEVICE;
@@ -1190,6 +1076,7 @@ static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_
     h->h_op.push_back(op);
     h->h_ntx.push_back(ev->n_transactions[i]);
     h->h_coin.push_back(ev->hash[i * 32 + 16] != 0 ? 1 : 0);
+    if (h->frames_on) h->h_hash.insert(h->h_hash.end(), ev->hash + i * 32, ev->hash + i * 32 + 32);
     const uint8_t *rb = ev->sig_r + i * 32;
     uint32_t w[8];  // big-endian words of r
     memcpy(w, rb, 32);
@@ -1263,6 +1150,7 @@ int bh_reset_consensus(bh_handle *h) {
     x->blocks.clear();
     x->inc_valid = false;
     x->n_coord = 0;
+    if (x->frames_on) frames_reset(x);
   }
   HIPCHK(h, hipSetDevice(h->device));
   return BH_OK;

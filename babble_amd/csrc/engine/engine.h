@@ -135,6 +135,50 @@ struct Dev {
   unsigned long long *diag;
 };
 
+// Block projection (kernels_frames.hip, frames.cpp): the
+// roots GetFrame gives each frame (hashgraph.go:1125-1231, createRoot
+// :546-640), Frame.Marshal -> FrameHash (frame.go:17-41) and Block.Marshal
+// -> the block's hash (block.go:100-123, 178-205).  Allocated when
+// bh_config.frames is set.  Frames are indexed by round received f; a
+// root is (f, p) = f * n + p.
+struct Frames {
+  uint8_t *hash;                 // [C][32] event hashes (Event.Hex keys, RootEvent.Hash)
+  int64_t *pids;                 // [n] participant IDs (RootEvent.CreatorID)
+  uint8_t *arena;                // event bytes: Go-JSON bodies (no newline) and Signature strings
+  int64_t *body_off, *sig_off;   // [C] offsets into arena
+  int32_t *body_len, *sig_len;   // [C], -1 = not given
+  int32_t *root_src;             // [R1][n] the event createRoot made root (f, p) from; -1 = base Root
+  int32_t *last_pos;             // [n] consensus position of each creator's last consensus event, -1 none
+  int32_t *first_pos, *last_in;  // [R1][n] scratch: first / last position of creator p in frame f
+  int64_t *oofs;                 // [R1 * n + 1] Others of root g: okey / oval [oofs[g], oofs[g + 1])
+  int32_t *okey, *oval;          // Others: key event -> RootEvent of value event, sorted by key hash
+  int32_t *ocur;                 // [R1][n] scratch fill cursors
+  int64_t *sz, *sz2;             // [max(R1 * n, C) + 1] scratch sizes -> exclusive scans
+  int64_t *part;                 // scan partials
+  int8_t *missing;               // [R1] scratch: some event of the frame has no bytes
+  int64_t *jofs, *bofs;          // [R1 + 1] frame / block JSON offsets (scratch)
+  int32_t *jlen, *blen;          // [R1] their lengths
+  uint8_t *fhash, *bhash;        // [R1][32] FrameHash / block hash of frame f's block
+  int8_t *fvalid;                // [R1] fhash / bhash computed
+  uint8_t *dig;                  // [R1][32] scratch digests
+  uint8_t *json, *bjson;         // materialized Frame / Block JSON of the last projection
+};
+constexpr int32_t NO_FIRST = 0x7f7f7f7f;  // first_pos of a creator absent from the frame (memset 0x7f)
+
+// frames [f0, f0 + F), whose consensus positions are [i0, i1) (frames.cpp)
+void launch_frame_roots(const Dev &d, const Frames &fr, int32_t f0, int32_t F, int64_t i0, int64_t i1,
+                        int64_t obase, hipStream_t s);
+void launch_frame_json_size(const Dev &d, const Frames &fr, int32_t f0, int32_t F, int64_t i0, int64_t i1,
+                            hipStream_t s);  // -> jofs[F] = bytes
+void launch_frame_json_write(const Dev &d, const Frames &fr, int32_t f0, int32_t F, int64_t i0, int64_t i1,
+                             bool store, hipStream_t s);  // -> json, fhash (store)
+void launch_block_json_size(const Dev &d, const Frames &fr, int32_t f0, int32_t F, int64_t i0, int64_t i1,
+                            hipStream_t s);  // -> bofs[F]
+void launch_block_json_write(const Dev &d, const Frames &fr, int32_t f0, int32_t F, int64_t i0, int64_t i1,
+                             bool store, hipStream_t s);  // -> bjson, bhash (store)
+// root (f, p) for every p: out[3p] NextRound, out[3p+1] SelfParent event (-1 base), out[3p+2] #Others
+void launch_root_query(const Dev &d, const Frames &fr, int32_t f, int32_t *out, hipStream_t s);
+
 enum DiagSlot {
   DG_SW_TOTAL = 0, DG_SW_WAIT_DESC, DG_SW_WAIT_RING, DG_SW_SUBSTEPS, DG_SW_FAR, DG_SW_CHUNKS,
   DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,

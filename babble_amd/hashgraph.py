@@ -56,10 +56,12 @@ def shard_range(items, world, rank):
 
 
 class Hashgraph:
-    def __init__(self, participant_ids, max_events, device=0, devices=None):
+    def __init__(self, participant_ids, max_events, device=0, devices=None, frames=False):
         """devices: a list of HIP ordinals to shard the passes over in this
         process (repeats allowed: shards sharing one device); None = one
-        device, `device`."""
+        device, `device`.  frames: keep event hashes / bytes on the device
+        and project frames and blocks (GetFrame roots, FrameHash, block
+        hashes) at every ProcessDecidedRounds."""
         self._L = _native.load()
         ids = np.ascontiguousarray(participant_ids, dtype=np.int64)
         if np.any(np.diff(ids) <= 0):
@@ -70,10 +72,10 @@ class Hashgraph:
             self._devs = np.ascontiguousarray(devices, dtype=np.int32)
             cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
                                  int(self._devs[0]), len(self._devs),
-                                 self._devs.ctypes.data_as(C.POINTER(C.c_int32)))
+                                 self._devs.ctypes.data_as(C.POINTER(C.c_int32)), int(bool(frames)))
         else:
             cfg = _native.Config(self.n, ids.ctypes.data_as(C.POINTER(C.c_int64)), int(max_events),
-                                 int(device), 0, None)
+                                 int(device), 0, None, int(bool(frames)))
         h = C.c_void_p()
         rc = self._L.bh_create(C.byref(cfg), C.byref(h))
         if rc != _native.BH_OK:
@@ -267,6 +269,73 @@ class Hashgraph:
     def profile_kernel(self):
         """Name of the coordinate kernel the last run timed."""
         return self._L.bh_get_profile_kernel(self._h).decode()
+
+    # ---- block projection (bh_config.frames; SURVEY 8(f) row 1) ----
+    def set_event_bytes(self, first, bodies, sigs):
+        """EventBody.Marshal() bytes and Signature strings of the inserted
+        events [first, first + len(bodies)) (bh_set_event_bytes)."""
+        if len(bodies) != len(sigs):
+            raise ValueError("one signature per body")
+        if not len(bodies):
+            return
+
+        def blob(items):
+            lens = np.fromiter((len(b) for b in items), np.int64, len(items))
+            offs = np.zeros(len(items) + 1, np.int64)
+            np.cumsum(lens, out=offs[1:])
+            data = np.frombuffer(b"".join(bytes(b) for b in items) or b"\0", np.uint8)
+            return data, offs
+        bd, bo = blob(bodies)
+        sd, so = blob(sigs)
+        self._check(self._L.bh_set_event_bytes(self._h, int(first), len(bodies), _ptr(bd), _ptr(bo),
+                                               _ptr(sd), _ptr(so)))
+
+    def _neg(self, rc):
+        if rc < 0:
+            raise HashgraphError(int(-rc), self._L.bh_last_error(self._h).decode())
+        return rc
+
+    def frame_roots(self, round_received):
+        """GetFrame(r).Roots (hashgraph.go:1125-1231): [(next_round,
+        self_parent event or -1 for the base root event, [(key event, value
+        event), ...] sorted by key hash)] in peer order."""
+        n = self.n
+        nr, sp, no = (np.empty(n, np.int32) for _ in range(3))
+        k = self._neg(self._L.bh_get_frame_roots(self._h, int(round_received), _ptr(nr), _ptr(sp), _ptr(no),
+                                                 None, None, 0))
+        key = np.empty(max(k, 1), np.int32)
+        val = np.empty(max(k, 1), np.int32)
+        self._neg(self._L.bh_get_frame_roots(self._h, int(round_received), None, None, None, _ptr(key),
+                                             _ptr(val), k))
+        out, o = [], 0
+        for p in range(n):
+            out.append((int(nr[p]), int(sp[p]), [(int(key[o + j]), int(val[o + j])) for j in range(no[p])]))
+            o += int(no[p])
+        return out
+
+    def frame_json(self, round_received):
+        """Frame.Marshal() of a processed round (frame.go:17-26)."""
+        k = self._neg(self._L.bh_get_frame_json(self._h, int(round_received), None, 0))
+        buf = np.empty(max(k, 1), np.uint8)
+        self._neg(self._L.bh_get_frame_json(self._h, int(round_received), _ptr(buf), k))
+        return buf[:k].tobytes()
+
+    def block_hashes(self, first=0, count=None):
+        """(frame_hash [m, 32], block_hash [m, 32], valid [m]) of blocks."""
+        b = self.stats().blocks
+        count = b - first if count is None else count
+        fh = np.zeros((max(count, 1), 32), np.uint8)
+        bh = np.zeros((max(count, 1), 32), np.uint8)
+        ok = np.zeros(max(count, 1), np.int8)
+        self._check(self._L.bh_get_block_hashes(self._h, int(first), int(count), _ptr(fh), _ptr(bh), _ptr(ok)))
+        return fh[:count], bh[:count], ok[:count].astype(bool)
+
+    def block_json(self, b, body_only=False):
+        """Block.Marshal() (or BlockBody.Marshal() with body_only) of block b."""
+        k = self._neg(self._L.bh_get_block_json(self._h, int(b), int(bool(body_only)), None, 0))
+        buf = np.empty(max(k, 1), np.uint8)
+        self._neg(self._L.bh_get_block_json(self._h, int(b), int(bool(body_only)), _ptr(buf), k))
+        return buf[:k].tobytes()
 
     def hash_bodies(self, bodies):
         """Event.Hash() (event.go:50-56) of each body on the device: SHA-256

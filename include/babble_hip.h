@@ -47,6 +47,12 @@ typedef struct {
    * one device, `device`.  Ordinals may repeat (shards sharing a device). */
   int32_t n_devices;
   const int32_t *device_ids;
+  /* Block projection: nonzero keeps every event's hash
+   * on the device and accepts its bytes (bh_set_event_bytes); each
+   * ProcessDecidedRounds then computes the roots of its frames (GetFrame),
+   * and, for frames whose events' bytes are all known, the FrameHash and
+   * the hash of the block made from it (NewBlockFromFrame). */
+  int32_t frames;
 } bh_config;
 
 /* A batch of events in topological order, in the reference's compact wire
@@ -176,6 +182,44 @@ int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, i
 int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig_r, const uint8_t *sig_s,
                          const int32_t *keys, int64_t count, const uint8_t *pubkeys, int32_t n_keys,
                          uint8_t *ok);
+
+/* ---- Block projection (bh_config.frames) ----
+ * The bytes Frame.Marshal (frame.go:17-26) needs of events [first, first +
+ * count) (already inserted): body i = bodies[body_offsets[i] ..
+ * body_offsets[i+1]) is EventBody.Marshal() (event.go:32-39; the Encoder's
+ * trailing newline may be included), signature i = sigs[sig_offsets[i] ..
+ * sig_offsets[i+1]) is Event.Signature (crypto.EncodeSignature, "r|s" in
+ * base 36).  Offsets: count + 1 ascending entries.  Set them before the
+ * ProcessDecidedRounds that emits their frame: a frame with an event whose
+ * bytes are missing gets roots but no FrameHash. */
+int bh_set_event_bytes(bh_handle *h, int64_t first, int64_t count, const uint8_t *bodies,
+                       const int64_t *body_offsets, const uint8_t *sigs, const int64_t *sig_offsets);
+/* Hashgraph.GetFrame(round_received).Roots (hashgraph.go:1125-1231) of a
+ * processed round: per participant (peer order) NextRound, SelfParent (an
+ * event id; -1 = the base root event "Root<id>", root.go:73-84) and the
+ * number of Others; then the Others of all roots in order, each root's
+ * sorted by key hash (Go's JSON map order): key event id -> RootEvent of the
+ * value event id (its CreatorID / Index / LamportTimestamp / Round are the
+ * event's).  Arrays nullable; up to cap Others.  Returns the total number of
+ * Others, or a negative status (-BH_ERR_KEY_NOT_FOUND: not a processed round). */
+int32_t bh_get_frame_roots(bh_handle *h, int32_t round_received, int32_t *next_round, int32_t *self_parent,
+                           int32_t *n_others, int32_t *other_key, int32_t *other_value, int32_t cap);
+/* Frame.Marshal() of a processed round (its Go-JSON bytes, newline
+ * included): returns the length and copies up to cap bytes (buf nullable);
+ * negative status when unavailable (-BH_ERR_STATE: some event's bytes are
+ * missing). */
+int64_t bh_get_frame_json(bh_handle *h, int32_t round_received, uint8_t *buf, int64_t cap);
+/* Blocks [first, first + count): FrameHash (Block.FrameHash(), block.go:100-
+ * 110) and the block's hash (Block.Hash(), block.go:196-205: SHA-256 of
+ * Block.Marshal() before any signature is added), 32 bytes each; valid[i]
+ * = 0 when the frame's bytes were incomplete (the hashes are then zero).
+ * Arrays nullable. */
+int bh_get_block_hashes(bh_handle *h, int64_t first, int64_t count, uint8_t *frame_hash, uint8_t *block_hash,
+                        int8_t *valid);
+/* Block.Marshal() (body_only = 0) or BlockBody.Marshal() (body_only = 1,
+ * block.go:21-29 -- what checkGossip compares) of block b: length, up to
+ * cap bytes copied; negative status when unavailable. */
+int64_t bh_get_block_json(bh_handle *h, int64_t b, int32_t body_only, uint8_t *buf, int64_t cap);
 
 /* Sharding across processes: one shard per process,
  * each holding the whole DAG, joined by an RCCL communicator.  Rank 0 makes
