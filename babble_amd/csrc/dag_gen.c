@@ -122,6 +122,77 @@ int32_t bg_body_json(const bg_dag *d, int64_t e, char *buf) {
   return o;
 }
 
+/* big.Int.Text(36) of a 32-byte big-endian value */
+static int base36(const uint8_t *be, char *out) {
+  uint8_t v[32];
+  memcpy(v, be, 32);
+  char t[64];
+  int k = 0, nz = 1;
+  while (nz) {
+    uint32_t rem = 0;
+    nz = 0;
+    for (int i = 0; i < 32; i++) {
+      const uint32_t cur = rem << 8 | v[i];
+      v[i] = (uint8_t)(cur / 36);
+      rem = cur % 36;
+      nz |= v[i];
+    }
+    t[k++] = "0123456789abcdefghijklmnopqrstuvwxyz"[rem];
+  }
+  for (int i = 0; i < k; i++) out[i] = t[k - 1 - i];
+  return k;
+}
+
+int32_t bg_sig_string(const bg_dag *d, int64_t e, char *buf) {
+  int o = base36(d->sig_r + (size_t)e * 32, buf);
+  buf[o++] = '|';
+  return o + base36(d->sig_s + (size_t)e * 32, buf + o);
+}
+
+typedef struct {
+  const bg_dag *d;
+  int64_t first, lo, hi;
+  uint8_t *bodies, *sigs;
+  int64_t *bo, *so;  /* per-event lengths first, offsets after the scan */
+  int pass;
+} bytes_job;
+
+static void *bytes_worker(void *arg) {
+  bytes_job *j = (bytes_job *)arg;
+  char jb[1024];
+  for (int64_t i = j->lo; i < j->hi; i++) {
+    const int64_t e = j->first + i;
+    if (j->pass == 0) {
+      j->bo[i + 1] = bg_body_json(j->d, e, jb);
+      j->so[i + 1] = bg_sig_string(j->d, e, jb);
+    } else {  /* through jb: sprintf's terminator must not land in the next body */
+      memcpy(j->bodies + j->bo[i], jb, (size_t)bg_body_json(j->d, e, jb));
+      memcpy(j->sigs + j->so[i], jb, (size_t)bg_sig_string(j->d, e, jb));
+    }
+  }
+  return NULL;
+}
+
+void bg_event_bytes(const bg_dag *d, int64_t first, int64_t count, uint8_t *bodies, int64_t *body_offsets,
+                    uint8_t *sigs, int64_t *sig_offsets) {
+  enum { T = 16 };
+  pthread_t th[T];
+  bytes_job jobs[T];
+  body_offsets[0] = sig_offsets[0] = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    for (int t = 0; t < T; t++) {
+      jobs[t] = (bytes_job){d, first, count * t / T, count * (t + 1) / T, bodies, sigs, body_offsets, sig_offsets, pass};
+      pthread_create(&th[t], NULL, bytes_worker, &jobs[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    if (pass == 0)
+      for (int64_t i = 0; i < count; i++) {
+        body_offsets[i + 1] += body_offsets[i];
+        sig_offsets[i + 1] += sig_offsets[i];
+      }
+  }
+}
+
 /* ---- ECDSA (P-256) ---- */
 typedef struct {
   const bg_dag *d;

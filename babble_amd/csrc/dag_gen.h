@@ -61,6 +61,15 @@ int32_t bg_tx_bytes(const bg_dag *d, int64_t e, uint8_t *buf64);
 /* Go-JSON body of event e (for tests), returns length; buf must hold 1024 B */
 int32_t bg_body_json(const bg_dag *d, int64_t e, char *buf);
 /* FNV-1a-32 (common/hash32.go) */
+/* Event.Signature of event e: crypto.EncodeSignature(r, s) = r and s in
+ * base 36, lower case, joined by '|' (crypto/utils.go:39-41); returns the
+ * length (at most 101) */
+int32_t bg_sig_string(const bg_dag *d, int64_t e, char *buf);
+/* bodies (EventBody.Marshal, with its newline) and signature strings of
+ * events [first, first + count), concatenated; offsets get count + 1
+ * entries each.  Buffers: at least 1024 * count and 104 * count bytes. */
+void bg_event_bytes(const bg_dag *d, int64_t first, int64_t count, uint8_t *bodies, int64_t *body_offsets,
+                    uint8_t *sigs, int64_t *sig_offsets);
 uint32_t bg_fnv1a32(const uint8_t *data, int64_t len);
 
 #ifdef __cplusplus

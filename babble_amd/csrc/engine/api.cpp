@@ -1374,7 +1374,8 @@ int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap) {
   if (!h) return 0;
   for (int i = 0; i < NSTAGE && i < cap; ++i) ms[i] = h->stage_ms[i];
   if (cap > NSTAGE) ms[NSTAGE] = h->xchg_ms;
-  return NSTAGE + 1;
+  if (cap > NSTAGE + 1) ms[NSTAGE + 1] = h->frames_ms;
+  return NSTAGE + 2;
 }
 
 int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {

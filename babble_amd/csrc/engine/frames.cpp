@@ -99,6 +99,8 @@ int frames_alloc(bh_handle *h) {
   A(&fr.missing, R1); A(&fr.jofs, R1 + 1); A(&fr.bofs, R1 + 1); A(&fr.jlen, R1); A(&fr.blen, R1);
   A(&fr.fhash, R1 * 32); A(&fr.bhash, R1 * 32); A(&fr.fvalid, R1); A(&fr.dig, R1 * 32);
   if (rc != BH_OK) return rc;
+  HIPCHK(h, hipEventCreate(&h->ev_fr[0]));
+  HIPCHK(h, hipEventCreate(&h->ev_fr[1]));
   HIPCHK(h, hipMemcpy(fr.pids, h->pids.data(), (size_t)n * 8, hipMemcpyHostToDevice));
   HIPCHK(h, hipMemset(fr.body_len, 0xff, (size_t)C * 4));
   HIPCHK(h, hipMemset(fr.sig_len, 0xff, (size_t)C * 4));
@@ -116,6 +118,8 @@ void frames_free(bh_handle *h) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   fr = bh::Frames{};
+  for (auto &e : h->ev_fr)
+    if (e) (void)hipEventDestroy(e);
 }
 
 // RunConsensus from scratch (bh_reset_consensus): no frame processed yet;
@@ -133,10 +137,15 @@ void frames_reset(bh_handle *h) {
 
 int frames_project(bh_handle *h, int32_t P0, int32_t P1, int64_t i0, int64_t i1) {
   const int32_t F = P1 - P0;
+  HIPCHK(h, hipEventRecord(h->ev_fr[0], h->stream));
   bh::launch_frame_roots(h->d, h->fr, P0, F, i0, i1, h->others_total, h->stream);
   HIPCHK(h, hipGetLastError());
   if (int rc = read_i64(h, h->fr.oofs + (int64_t)P1 * h->d.n, &h->others_total)) return rc;
-  return project_json(h, P0, F, i0, i1, true, true);
+  if (int rc = project_json(h, P0, F, i0, i1, true, true)) return rc;
+  HIPCHK(h, hipEventRecord(h->ev_fr[1], h->stream));
+  HIPCHK(h, hipEventSynchronize(h->ev_fr[1]));
+  HIPCHK(h, hipEventElapsedTime(&h->frames_ms, h->ev_fr[0], h->ev_fr[1]));
+  return BH_OK;
 }
 
 extern "C" {

@@ -127,6 +127,8 @@ struct bh_handle {
   int64_t arena_cap = 0, arena_len = 0;
   int64_t others_total = 0;        // Others of the processed frames (oofs[P * n])
   size_t json_cap = 0, bjson_cap = 0;
+  hipEvent_t ev_fr[2]{};           // around the last projection
+  float frames_ms = 0;
 
   int fail(int code, const char *fmt, ...) {
     char buf[512];

@@ -49,6 +49,10 @@ def _lib():
         L.bg_body_json.restype = C.c_int32
         L.bg_tx_bytes.argtypes = [C.POINTER(_Dag), C.c_int64, C.c_void_p]
         L.bg_tx_bytes.restype = C.c_int32
+        L.bg_sig_string.argtypes = [C.POINTER(_Dag), C.c_int64, C.c_char_p]
+        L.bg_sig_string.restype = C.c_int32
+        L.bg_event_bytes.argtypes = [C.POINTER(_Dag), C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -94,6 +98,24 @@ class Dag:
         buf = C.create_string_buffer(1024)
         k = _lib().bg_body_json(C.byref(self._d), e, buf)
         return buf.raw[:k]
+
+    def sig_string(self, e):
+        """Event.Signature: r|s in base 36 (crypto/utils.go:39-41)"""
+        buf = C.create_string_buffer(128)
+        k = _lib().bg_sig_string(C.byref(self._d), e, buf)
+        return buf.raw[:k]
+
+    def event_bytes(self, first=0, count=None):
+        """(bodies u8, body_offsets [count+1], sigs u8, sig_offsets) of events
+        [first, first + count): the blobs bh_set_event_bytes takes"""
+        count = self.N - first if count is None else count
+        bodies = np.empty(max(1024 * count, 1), np.uint8)
+        sigs = np.empty(max(104 * count, 1), np.uint8)
+        bo = np.zeros(count + 1, np.int64)
+        so = np.zeros(count + 1, np.int64)
+        _lib().bg_event_bytes(C.byref(self._d), first, count, bodies.ctypes.data, bo.ctypes.data,
+                              sigs.ctypes.data, so.ctypes.data)
+        return bodies[:bo[-1]], bo, sigs[:so[-1]], so
 
     def tx_bytes(self, e):
         buf = (C.c_uint8 * 64)()

@@ -173,7 +173,7 @@ def main():
         hg.reset_consensus()
         hg.run_consensus()
         log(f"warmup {w}: stages_ms={['%.2f' % x for x in hg.stage_ms()]}")
-    sweep_ms, stage_tot = [], np.zeros(6)
+    sweep_ms, stage_tot = [], np.zeros(7)
     barrier()
     sync()
     t0 = time.perf_counter()

@@ -157,7 +157,8 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors,
 /* device milliseconds of the last run, per stage:
  * [0] coordinates+lamport, [1] rounds+witnesses, [2] fame, [3] round received,
  * [4] frames/order/blocks, [5] shard exchanges (host wall time, 0 for one
- * shard); returns the number of entries */
+ * shard), [6] block projection (bh_config.frames: roots, Frame / Block JSON
+ * and their hashes; 0 without); returns the number of entries */
 int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap);
 /* kernel statistics of the last run for the roofline report: number of
  * round-loop iterations, coordinate sweep launches' average ms */
