@@ -23,7 +23,7 @@ SYMBOLS = (
     "bh_decide_fame", "bh_decide_round_received", "bh_process_decided_rounds",
     "bh_run_consensus", "bh_synchronize", "bh_reset_consensus", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
-    "bh_get_round_info", "bh_get_coordinates", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
+    "bh_get_round_info", "bh_get_coordinates", "bh_query_events", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
     "bh_hash_bodies", "bh_verify_signatures", "bh_set_event_bytes", "bh_get_frame_roots",
     "bh_get_frame_json", "bh_get_block_hashes", "bh_get_block_json", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
 )
@@ -90,6 +90,8 @@ def load():
     L.bh_get_round_info.argtypes = [P, I32, C.POINTER(RoundInfo), VP, VP, I32]
     L.bh_get_round_info.restype = C.c_int
     L.bh_get_coordinates.argtypes = [P, I64, VP, VP]
+    L.bh_query_events.argtypes = [P, I32, I64, VP, VP, VP]
+    L.bh_query_events.restype = C.c_int
     L.bh_get_stage_ms.argtypes = [P, C.POINTER(C.c_float), I32]
     L.bh_get_stage_ms.restype = I32
     L.bh_get_profile.argtypes = [P, C.POINTER(I64), C.POINTER(C.c_float)]

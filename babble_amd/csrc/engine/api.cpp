@@ -46,6 +46,7 @@ void free_all(bh_handle *h) {
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
   if (h->sha_buf) (void)hipFree(h->sha_buf);
+  if (h->q_buf) (void)hipFree(h->q_buf);
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
   for (auto &e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1330,12 +1331,13 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
   return BH_OK;
 }
 
-int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_t *first_descendants) {
-  if (!h || id < 0 || id >= (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
-  (void)hipSetDevice(h->device);
+// the coordinates of every inserted event on the device (they are produced
+// lazily by the first pass; a query between an insert and the next
+// DivideRounds computes them here)
+static int ensure_coords(bh_handle *h) {
   Dev &d = h->d;
   const int64_t N = (int64_t)h->h_creator.size();
-  if (h->coords_for != N) {  // coordinates are produced lazily by the first pass
+  if (h->coords_for != N) {
     int rc;
     if ((rc = upload(h))) return rc;
     d.N = N;
@@ -1356,6 +1358,15 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
     h->coords_for = (int)N;
     h->stage = 0;
   }
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
+
+int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_t *first_descendants) {
+  if (!h || id < 0 || id >= (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
+  (void)hipSetDevice(h->device);
+  Dev &d = h->d;
+  if (int rc = ensure_coords(h)) return rc;
   const int32_t c = h->h_creator[(size_t)id];
   const int64_t row = (int64_t)h->cstart_h[(size_t)c] + h->h_index[(size_t)id];  // chain-major layout
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1367,6 +1378,40 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
   } else if (first_descendants) {
     HIPCHK(h, hipMemcpy(first_descendants, d.fd + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
   }
+  return BH_OK;
+}
+
+int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x, const int64_t *y, int32_t *out) {
+  if (!h) return BH_ERR_INVALID;
+  if (kind < BH_Q_ANCESTOR || kind > BH_Q_ROUND_DIFF || count < 0 || (count > 0 && (!x || !y || !out)))
+    return h->fail(BH_ERR_INVALID, "bh_query_events: bad kind or buffers");
+  const int64_t N = (int64_t)h->h_creator.size();
+  for (int64_t i = 0; i < count; ++i)
+    if (x[i] < 0 || x[i] >= N || y[i] < 0 || y[i] >= N)
+      return h->fail(BH_ERR_KEY_NOT_FOUND, "bh_query_events: event %lld / %lld not inserted", (long long)x[i],
+                     (long long)y[i]);
+  if (count == 0) return BH_OK;
+  if (kind == BH_Q_ROUND_DIFF && h->n_div < N)
+    return h->fail(BH_ERR_STATE, "roundDiff before DivideRounds covered every event");
+  (void)hipSetDevice(h->device);
+  if (int rc = ensure_coords(h)) return rc;
+  const size_t need = (size_t)count * 20;
+  if (need > h->q_cap) {
+    if (h->q_buf) (void)hipFree(h->q_buf);
+    h->q_buf = nullptr;
+    h->q_cap = 0;
+    HIPCHK(h, hipMalloc((void **)&h->q_buf, need));
+    h->q_cap = need;
+  }
+  int64_t *dx = reinterpret_cast<int64_t *>(h->q_buf), *dy = dx + count;
+  int32_t *dout = reinterpret_cast<int32_t *>(dy + count);
+  hipStream_t s = h->stream;
+  HIPCHK(h, hipMemcpyAsync(dx, x, (size_t)count * 8, hipMemcpyHostToDevice, s));
+  HIPCHK(h, hipMemcpyAsync(dy, y, (size_t)count * 8, hipMemcpyHostToDevice, s));
+  bh::launch_query(h->d, kind, count, dx, dy, dout, s);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemcpyAsync(out, dout, (size_t)count * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(h, hipStreamSynchronize(s));
   return BH_OK;
 }
 
@@ -1409,6 +1454,7 @@ int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, i
   const size_t need = nb + (size_t)count * (8 + 4 + 32);
   if (need > h->sha_cap) {
     if (h->sha_buf) (void)hipFree(h->sha_buf);
+  if (h->q_buf) (void)hipFree(h->q_buf);
     h->sha_buf = nullptr;
     h->sha_cap = 0;
     HIPCHK(h, hipMalloc((void **)&h->sha_buf, need));
@@ -1441,6 +1487,7 @@ int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig
   const size_t need = (size_t)count * (3 * 32 + 4 + 1) + (size_t)n_keys * 64 + 64;
   if (need > h->sha_cap) {  // shares the hashing scratch buffer
     if (h->sha_buf) (void)hipFree(h->sha_buf);
+  if (h->q_buf) (void)hipFree(h->q_buf);
     h->sha_buf = nullptr;
     h->sha_cap = 0;
     HIPCHK(h, hipMalloc((void **)&h->sha_buf, need));

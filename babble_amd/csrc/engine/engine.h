@@ -249,6 +249,10 @@ void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s);
 void launch_cons_pos(const Dev &d, int64_t i0, int64_t i1, hipStream_t s);
 // witnesses of rounds [P0, P1) still Undefined when those rounds were processed
 void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s);
+// pair predicates for bh_query_events (kernels_query.hip): kind 0 ancestor,
+// 1 selfAncestor, 2 see, 3 stronglySee, 4 roundDiff
+void launch_query(const Dev &d, int32_t kind, int64_t count, const int64_t *x, const int64_t *y, int32_t *out,
+                  hipStream_t s);
 void configure_fd_kernels();
 void launch_first_descendants(const Dev &d, hipStream_t s, bool walked);  // fd from la (FDT already written by k_flow_transpose when walked)
 

@@ -80,6 +80,8 @@ struct bh_handle {
   Dev graph_dev{};
   int32_t *pinned_state = nullptr;
   uint8_t *sha_buf = nullptr;  // bh_hash_bodies scratch
+  uint8_t *q_buf = nullptr;    // bh_query_events scratch
+  size_t q_cap = 0;
   size_t sha_cap = 0;
   hipEvent_t ev[NSTAGE + 1]{};
   hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)

@@ -253,6 +253,19 @@ class Hashgraph:
         self._check(self._L.bh_get_coordinates(self._h, int(event_id), _ptr(la), _ptr(fd)))
         return la, fd
 
+    QUERY = {"ancestor": 0, "self_ancestor": 1, "see": 2, "strongly_see": 3, "round_diff": 4}
+
+    def query(self, kind, x, y):
+        """ancestor / self_ancestor / see / strongly_see (bool arrays) or
+        round_diff (int32) of the event pairs (x[i], y[i]) (bh_query_events)."""
+        xs = np.ascontiguousarray(np.atleast_1d(x), np.int64)
+        ys = np.ascontiguousarray(np.atleast_1d(y), np.int64)
+        if xs.shape != ys.shape:
+            raise ValueError("x and y must pair up")
+        out = np.empty(len(xs), np.int32)
+        self._check(self._L.bh_query_events(self._h, self.QUERY[kind], len(xs), _ptr(xs), _ptr(ys), _ptr(out)))
+        return out if kind == "round_diff" else out.astype(bool)
+
     def stage_ms(self):
         """[coordinates, rounds, fame, round_received, order, exchange,
         projection] ms of the last run (device events; exchange: host wall

@@ -154,6 +154,15 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
 /* lastAncestors / firstDescendants indexes of one event (event.go:115-116) */
 int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors,
                        int32_t *first_descendants);
+/* The Hashgraph's private predicates over event pairs (x[i], y[i]) (event
+ * ids), for tests and tools that call them on the Go Hashgraph:
+ * BH_Q_ANCESTOR ancestor(x, y) (hashgraph.go:80-118), BH_Q_SELF_ANCESTOR
+ * selfAncestor (:120-149), BH_Q_SEE see (:152-157), BH_Q_STRONGLY_SEE
+ * stronglySee (:159-191) -> out 1 / 0; BH_Q_ROUND_DIFF roundDiff (:382-395)
+ * -> round(x) - round(y) (BH_ERR_STATE before DivideRounds covered the
+ * events).  Coordinates are those of every inserted event. */
+enum { BH_Q_ANCESTOR = 0, BH_Q_SELF_ANCESTOR = 1, BH_Q_SEE = 2, BH_Q_STRONGLY_SEE = 3, BH_Q_ROUND_DIFF = 4 };
+int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x, const int64_t *y, int32_t *out);
 /* device milliseconds of the last run, per stage:
  * [0] coordinates+lamport, [1] rounds+witnesses, [2] fame, [3] round received,
  * [4] frames/order/blocks, [5] shard exchanges (host wall time, 0 for one
