@@ -103,6 +103,9 @@ struct Dev {
   // q * LPC / 64 = candidate (c, B[r][c]) strongly sees (q, B[r-1][q])
   unsigned long long *ssm;
   int32_t round_lpc;  // LPC of k_round2 (4 or 8)
+  // [n][R_cap + 1][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
+  // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])
+  unsigned long long *ssw;
   int32_t *last_la; // [n][npad] LA row of each chain's last event
   int32_t max_chain_len;
   // round-loop hand-off (k_round2, npad <= 128), by round parity

@@ -12,7 +12,8 @@
 // r keeps the votes of all x in W(r) as bitsets over the voters (n/64 words),
 // and tallies with popcount(S_j[y] & V_{j-1}[x]), where S_j[y] is the bitset
 // of the W(j-1) witnesses y strongly sees.  For n <= 128 S_j comes from the
-// round loop's ballots (k_fame_masks, below); for larger n it is an
+// round loop's ballots (k_fame_masks, below), for n <= 512 from the wide
+// loop's chain masks (same kernel, 512-bit masks); for larger n it is an
 // n x n x n integer compare-and-count, register-tiled 8x8 per thread over
 // LA rows (voters) and firstDescendants rows (voted) (k_fame).  The
 // workgroup then publishes the round's decided flag, its famous count and
@@ -228,111 +229,130 @@ __device__ __forceinline__ uint32_t fame_ballot_word(const unsigned long long *b
   return word;
 }
 
-__global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R, int32_t r0) {
-  __shared__ uint32_t V[2][128][4];  // votes: [cur][x chain][word over W(j-1) chains]
-  __shared__ uint32_t S[128][4];     // ssm rows of W(j), restricted to W(j-1)
-  __shared__ uint32_t wx[4], wp[4], wc[4];  // W(r), W(j-1), W(j)
-  __shared__ int32_t dec[128], nd[128], yev[128], xev[128], xk[128];
-  __shared__ int32_t misc[2];  // [0] undecided, [1] conflicting decisions
-  __shared__ int32_t frow[128];  // LA rows of famous witnesses
-  __shared__ int32_t nfam_s;
+// Chain masks of NW 32-bit words (MAXN = 32 NW chains): NW = 4 for the
+// k_round2 path (ballots in its raw LPC-strided layout, ssm), NW = 16 for
+// the k_round_wide path (n <= 512; packed chain masks, ssw).  2 MAXN
+// threads: thread (x, h) owns vote words [h NW/2, (h+1) NW/2) of witness x,
+// i.e. the voters y of that half of the chains.
+template <int NW>
+struct FameLds {
+  static constexpr int MAXN = 32 * NW;
+  uint32_t V[2][MAXN][NW];  // votes: [cur][x chain][word over W(j-1) chains]
+  uint32_t S[MAXN][NW];     // stronglySee rows of W(j), restricted to W(j-1)
+  uint32_t wx[NW], wp[NW], wc[NW];  // W(r), W(j-1), W(j)
+  int32_t dec[MAXN], nd[MAXN], yev[MAXN], xev[MAXN], xk[MAXN];
+  int32_t frow[MAXN];  // LA rows of famous witnesses
+  int32_t misc[2];     // [0] undecided, [1] conflicting decisions
+  int32_t nfam_s;
+};
+
+// S_j[y] word w: the W(j-1) chains y = (chain, B[j]) strongly sees
+template <int NW>
+__device__ __forceinline__ uint32_t fame_ss_word(const Dev &d, int y, int j, int w) {
+  if (NW == 4) return fame_ballot_word(d.ssm + ((int64_t)y * (d.R_cap + 1) + j) * 16, d.round_lpc, w);
+  const unsigned long long m = d.ssw[((int64_t)y * (d.R_cap + 1) + j) * 8 + (w >> 1)];
+  return (uint32_t)(m >> (32 * (w & 1)));
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_t r0) {
+  constexpr int MAXN = 32 * NW, HW_ = NW / 2, HY = MAXN / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm_[];
+  FameLds<NW> &L = *reinterpret_cast<FameLds<NW> *>(fsm_);
   const int r = r0 + (int)blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const int n = d.n, npad = d.npad, sm = d.sm;
-  if (t < 4) wx[t] = fame_wmask_word(d, r, t);
-  for (int q = t; q < 128; q += nt) {
-    dec[q] = 0;
-    nd[q] = 0;
-    xev[q] = -1;
-    xk[q] = 0;
-    yev[q] = 0;  // j = r+1: LA row of y
+  if (t < NW) L.wx[t] = fame_wmask_word(d, r, t);
+  for (int q = t; q < MAXN; q += nt) {
+    L.dec[q] = 0;
+    L.nd[q] = 0;
+    L.xev[q] = -1;
+    L.xk[q] = 0;
+    L.yev[q] = 0;  // j = r+1: LA row of y
     if (q < n) {
       const int32_t b0 = d.B[(int64_t)r * n + q];
-      if (b0 < d.chain_len[q]) xev[q] = d.chain_ids[d.chain_start[q] + b0];
-      xk[q] = b0;
-      if (r + 1 < R) yev[q] = d.chain_start[q] + min(d.B[(int64_t)(r + 1) * n + q], d.chain_len[q] - 1);
+      if (b0 < d.chain_len[q]) L.xev[q] = d.chain_ids[d.chain_start[q] + b0];
+      L.xk[q] = b0;
+      if (r + 1 < R) L.yev[q] = d.chain_start[q] + min(d.B[(int64_t)(r + 1) * n + q], d.chain_len[q] - 1);
     }
   }
   __syncthreads();
   if (t == 0) {
-    misc[0] = __popc(wx[0]) + __popc(wx[1]) + __popc(wx[2]) + __popc(wx[3]);
-    misc[1] = 0;
+    int u = 0;
+    for (int w = 0; w < NW; ++w) u += __popc(L.wx[w]);
+    L.misc[0] = u;
+    L.misc[1] = 0;
   }
-  const int x = t & 127, h = t >> 7;  // vote words 2h, 2h+1 of witness x
-  const bool isx = (wx[x >> 5] >> (x & 31)) & 1u;
+  const int x = t % MAXN, h = t / MAXN;  // vote words h*HW_ .. +HW_ of witness x
+  const bool isx = (L.wx[x >> 5] >> (x & 31)) & 1u;
   int cur = 0;
   if (r + 1 < R) {
     // ---- j = r+1: vote(y, x) = see(y, x) ----
-    if (t < 4) wc[t] = fame_wmask_word(d, r + 1, t);
+    if (t < NW) L.wc[t] = fame_wmask_word(d, r + 1, t);
     __syncthreads();
     {
-      uint32_t v0 = 0, v1 = 0;
       const int xc = min(x, n - 1);
-      for (int b = 0; b < 64; ++b) {
-        const int y = h * 64 + b;
-        if (y >= n || !((wc[y >> 5] >> (y & 31)) & 1u)) continue;
-        if (d.la[(int64_t)yev[y] * npad + xc] >= xk[xc]) {
-          if (b < 32) v0 |= 1u << b;
-          else v1 |= 1u << (b - 32);
+      for (int k = 0; k < HW_; ++k) {
+        uint32_t v = 0;
+        for (int b = 0; b < 32; ++b) {
+          const int y = h * HY + k * 32 + b;
+          if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
+          if (d.la[(int64_t)L.yev[y] * npad + xc] >= L.xk[xc]) v |= 1u << b;
         }
+        L.V[0][x][h * HW_ + k] = v;
       }
-      V[0][x][2 * h] = v0;
-      V[0][x][2 * h + 1] = v1;
     }
     __syncthreads();
     // ---- j >= r+2 ----
     for (int j = r + 2; j < R; ++j) {
-      if (misc[0] == 0) break;
-      if (t < 4) {
-        wp[t] = wc[t];
-        wc[t] = fame_wmask_word(d, j, t);
+      if (L.misc[0] == 0) break;
+      if (t < NW) {
+        L.wp[t] = L.wc[t];
+        L.wc[t] = fame_wmask_word(d, j, t);
       }
       __syncthreads();
       for (int y = t; y < n; y += nt) {
-        const bool isy = (wc[y >> 5] >> (y & 31)) & 1u;
-        yev[y] = isy ? d.chain_ids[d.chain_start[y] + d.B[(int64_t)j * n + y]] : -1;
-        const unsigned long long *b = d.ssm + ((int64_t)y * (d.R_cap + 1) + j) * 16;
+        const bool isy = (L.wc[y >> 5] >> (y & 31)) & 1u;
+        L.yev[y] = isy ? d.chain_ids[d.chain_start[y] + d.B[(int64_t)j * n + y]] : -1;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) S[y][w] = isy ? fame_ballot_word(b, d.round_lpc, w) & wp[w] : 0u;
+        for (int w = 0; w < NW; ++w) L.S[y][w] = isy ? fame_ss_word<NW>(d, y, j, w) & L.wp[w] : 0u;
       }
       __syncthreads();
       const int diff = j - r;
       const bool normal = (diff % n) != 0;
-      if (isx && !dec[x]) {
-        uint32_t v0 = 0, v1 = 0;
+      if (isx && !L.dec[x]) {
         int decide = 0;
-        for (int b = 0; b < 64; ++b) {
-          const int y = h * 64 + b;
-          if (y >= n || !((wc[y >> 5] >> (y & 31)) & 1u)) continue;
-          int yays = 0, tot = 0;
+        for (int k = 0; k < HW_; ++k) {
+          uint32_t v = 0;
+          for (int b = 0; b < 32; ++b) {
+            const int y = h * HY + k * 32 + b;
+            if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
+            int yays = 0, tot = 0;
 #pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            yays += __popc(S[y][w] & V[cur][x][w]);
-            tot += __popc(S[y][w]);
+            for (int w = 0; w < NW; ++w) {
+              yays += __popc(L.S[y][w] & L.V[cur][x][w]);
+              tot += __popc(L.S[y][w]);
+            }
+            const int nays = tot - yays;
+            const bool vv = yays >= nays;
+            const int tt = vv ? yays : nays;
+            bool vote;
+            if (normal) {
+              if (tt >= sm) decide |= vv ? 1 : 2;
+              vote = vv;
+            } else {
+              vote = tt >= sm ? vv : d.coin[L.yev[y]] != 0;
+            }
+            if (vote) v |= 1u << b;
           }
-          const int nays = tot - yays;
-          const bool v = yays >= nays;
-          const int tt = v ? yays : nays;
-          bool vote;
-          if (normal) {
-            if (tt >= sm) decide |= v ? 1 : 2;
-            vote = v;
-          } else {
-            vote = tt >= sm ? v : d.coin[yev[y]] != 0;
-          }
-          if (vote) {
-            if (b < 32) v0 |= 1u << b;
-            else v1 |= 1u << (b - 32);
-          }
+          L.V[cur ^ 1][x][h * HW_ + k] = v;
         }
-        V[cur ^ 1][x][2 * h] = v0;
-        V[cur ^ 1][x][2 * h + 1] = v1;
-        if (decide) atomicOr(&nd[x], decide);
+        if (decide) atomicOr(&L.nd[x], decide);
       }
       __syncthreads();
-      if (t < 128 && isx && dec[x] == 0 && nd[x]) {
-        if (nd[x] == 3) misc[1] = 1;  // conflicting decisions: impossible without forks
-        dec[x] = nd[x] == 1 ? 1 : 2;
-        atomicSub(&misc[0], 1);
+      if (t < MAXN && isx && L.dec[x] == 0 && L.nd[x]) {
+        if (L.nd[x] == 3) L.misc[1] = 1;  // conflicting decisions: impossible without forks
+        L.dec[x] = L.nd[x] == 1 ? 1 : 2;
+        atomicSub(&L.misc[0], 1);
       }
       __syncthreads();
       cur ^= 1;
@@ -340,26 +360,26 @@ __global__ __launch_bounds__(256) void k_fame_masks(Dev d, int32_t R, int32_t r0
   }
   // ---- publish ----
   __syncthreads();
-  if (t < 128 && isx) {  // witness x's position in W(r): the witnesses of lower chains before it
+  if (t < MAXN && isx) {  // witness x's position in W(r): the witnesses of lower chains before it
     int rank = 0;
-    for (int w = 0; w < (x >> 5); ++w) rank += __popc(wx[w]);
-    rank += __popc(wx[x >> 5] & ((1u << (x & 31)) - 1u));
-    d.wfame[d.wofs[r] + rank] = (int8_t)dec[x];
+    for (int w = 0; w < (x >> 5); ++w) rank += __popc(L.wx[w]);
+    rank += __popc(L.wx[x >> 5] & ((1u << (x & 31)) - 1u));
+    d.wfame[d.wofs[r] + rank] = (int8_t)L.dec[x];
   }
   if (t == 0) {
-    d.decided[r] = misc[0] == 0 ? 1 : 0;
-    if (misc[1]) d.state[ST_ERR] = 2;
+    d.decided[r] = L.misc[0] == 0 ? 1 : 0;
+    if (L.misc[1]) d.state[ST_ERR] = 2;
     int m = 0;
     for (int q = 0; q < n; ++q)
-      if (((wx[q >> 5] >> (q & 31)) & 1u) && dec[q] == 1) frow[m++] = d.chain_start[q] + d.B[(int64_t)r * n + q];
-    nfam_s = m;
+      if (((L.wx[q >> 5] >> (q & 31)) & 1u) && L.dec[q] == 1) L.frow[m++] = d.chain_start[q] + d.B[(int64_t)r * n + q];
+    L.nfam_s = m;
   }
   __syncthreads();
   // famous count and min LA over famous witnesses (roundReceived)
-  const int nf = nfam_s;
+  const int nf = L.nfam_s;
   for (int c = t; c < npad; c += nt) {
     int32_t m = INT32_MAX;
-    for (int i = 0; i < nf; ++i) m = min(m, d.la[(int64_t)frow[i] * npad + c]);
+    for (int i = 0; i < nf; ++i) m = min(m, d.la[(int64_t)L.frow[i] * npad + c]);
     d.minla[(int64_t)r * npad + c] = m;
     if (c == 0) d.nfam[r] = nf;
   }
@@ -372,12 +392,18 @@ size_t fame_lds_bytes(int n) {
 
 void configure_fame_kernels() {
   (void)hipFuncSetAttribute((const void *)k_fame, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  (void)hipFuncSetAttribute((const void *)k_fame_masks<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(FameLds<16>));
 }
 
 void launch_fame(const Dev &d, int32_t R, int32_t r0, int32_t r1, hipStream_t s) {
   if (r1 <= r0) return;
   if (d.fd_cols) {  // masks from the k_round2 loop
-    k_fame_masks<<<r1 - r0, 256, 0, s>>>(d, R, r0);
+    k_fame_masks<4><<<r1 - r0, 256, sizeof(FameLds<4>), s>>>(d, R, r0);
+    return;
+  }
+  if (d.ssw) {  // masks from the k_round_wide loop (n <= 512)
+    k_fame_masks<16><<<r1 - r0, 1024, sizeof(FameLds<16>), s>>>(d, R, r0);
     return;
   }
   k_fame<<<r1 - r0, 256, fame_lds_bytes(d.n), s>>>(d, R, r0);

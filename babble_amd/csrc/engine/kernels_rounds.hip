@@ -219,6 +219,7 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
   __shared__ int32_t hist[WROWS + 1];
   __shared__ int32_t sh_res, sh_nc;
+  __shared__ int8_t tq_s[512];  // T_q of every candidate in the current window (ssw, n <= 512)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, rs = npad + SCAN_PAD, q4 = npad / 4;
@@ -289,6 +290,7 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
         tw = lo;
       }
       if (act && part == 0 && tw < WROWS) atomicAdd(&hist[tw], 1);
+      if (d.ssw && part == 0 && q < n) tq_s[q] = (int8_t)(act ? tw : WROWS);
     }
     __syncthreads();
     if (sh_nc == 0) break;
@@ -305,6 +307,17 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
     __syncthreads();
     if (sh_res >= 0) { result = wk0 + sh_res; break; }
     wk0 += wrows;
+  }
+  // fame's input for the new candidate y = (c, result): the candidates of
+  // round r it strongly sees are those whose T_q in the final window is at
+  // most y's row (stronglySee is monotone along the chain)
+  if (d.ssw && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
+    const int res = sh_res;
+    for (int q0 = 0; q0 < 512; q0 += 256) {
+      const int q = q0 + t;
+      const unsigned long long m = __ballot(q < n && tq_s[q] <= res);
+      if (lane == 0) d.ssw[((int64_t)c * (d.R_cap + 1) + r + 1) * 8 + (q0 >> 6) + wave] = m;
+    }
   }
   if (t == 0) {
     if (sh_nc == 0) {
