@@ -332,6 +332,11 @@ int rounds_coords(bh_handle *h) {
     bh::launch_flow(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
     h->sweep_kernel = bh::flow32_eligible(d) ? "k_flow32" : "k_flow";
+  } else if (bh::floww_eligible(d)) {
+    HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
+    bh::launch_floww(d, s);
+    HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
+    h->sweep_kernel = "k_floww";
   } else {
     bh::launch_chunk_depth(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
@@ -352,8 +357,24 @@ int rounds_loop(bh_handle *h) {
   Dev &d = h->d;
   hipStream_t s = h->stream;
   const bool walked = use_flow(d);
-  if (walked) bh::launch_flow_transpose(d, s);
-  bh::launch_first_descendants(d, s, walked);
+  bool wide_flow = bh::floww_eligible(d);
+  if (wide_flow) {  // k_floww's watchdog (ST_FLOWOVF = 2): the chunked sweep instead
+    int32_t ovf = 0;
+    HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    if (ovf == 2) {
+      HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
+      bh::launch_chunk_depth(d, s);
+      bh::launch_la_sweep(d, s);
+      bh::launch_permute(d, s);
+      h->sweep_kernel = "k_la_sweep";
+      wide_flow = false;
+    }
+  }
+  // LA rows and the firstDescendants walk (FDT) from the dataflow's
+  // column-major LA; n > 128 then transposes FDT into chain-major FD rows
+  if (walked || wide_flow) bh::launch_flow_transpose(d, s);
+  bh::launch_first_descendants(d, s, walked || wide_flow);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
   h->coords_for = (int)d.N;
@@ -379,7 +400,15 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
   hipStream_t s = h->stream;
   h->R = st[bh::ST_ROUNDS];
   h->iters = st[bh::ST_ITERS];
-  if (st[bh::ST_FLOWOVF]) bh::launch_flow_lt_fallback(d, s);  // LT only feeds the frame order
+  if (st[bh::ST_FLOWOVF]) {  // LT reached the one-dword limit; LT only feeds the frame order
+    if (bh::floww_eligible(d)) {  // the chunked sweep recomputes LA (same values) and LT
+      bh::launch_chunk_depth(d, s);
+      bh::launch_la_sweep(d, s);
+      bh::launch_permute(d, s);
+    } else {
+      bh::launch_flow_lt_fallback(d, s);
+    }
+  }
   bh::launch_witness_tables(d, h->R, s);
   bh::launch_assign_rounds(d, e_begin, h->n_div, h->P, s);
   HIPCHK(h, hipGetLastError());
@@ -900,7 +929,10 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   // (k_flow_transpose walks as it transposes): its own allocation
   A(&d.fdt, (size_t)(L + 128) * d.npad);  // whole 64-row tiles (fdt_pos)
   d.la_ev = d.fdt;
-  if (n <= bh::FL_MAXN) A(&d.la_col, (size_t)(L + 64) * d.npad);
+  // the dataflow's column-major LA has its own allocation: the transpose
+  // reads it while the firstDescendants walk writes FDT (n <= 512; wider
+  // groups take the chunked sweep, whose slabs may share FDT's memory)
+  if (n <= 512) A(&d.la_col, (size_t)(L + 64) * d.npad);
   else d.la_col = d.fdt;
   A(&d.opdesc, (size_t)2 * (L + 128));  // k_flow32: int2 entries
   A(&d.lt_row, (size_t)L + 64);

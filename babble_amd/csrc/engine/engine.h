@@ -210,6 +210,10 @@ void launch_sha256(const uint8_t *data, const int64_t *off, const int32_t *len, 
 void launch_ecdsa_verify(const uint8_t *hash, const uint8_t *r, const uint8_t *s, const int32_t *key,
                          const uint8_t *pub, int64_t count, uint8_t *ok, hipStream_t st);  // kernels_ecdsa.hip
 void launch_flow_transpose(const Dev &d, hipStream_t s);
+// the chain dataflow for 128 < n <= 512 (kernels_flow_wide.hip): column-major
+// LA + LT rows; LA rows come from launch_flow_transpose, FD from kernels_fd
+bool floww_eligible(const Dev &d);
+void launch_floww(const Dev &d, hipStream_t s);
 void launch_prep(const Dev &d, hipStream_t s);  // every event: chain table (gap rows -1), loop state
 void launch_chain_scatter(const Dev &d, int64_t e_begin, hipStream_t s);  // events [e_begin, N)
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep

@@ -635,7 +635,7 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
     const int ra1 = ra + max(0, lo_i - ka0), rb = ra + min(rb0 - ra, clen[i] - ka0);
     if (ra1 >= rb) continue;
     const int32_t ka = ka0 + (ra1 - ra);
-    if (ka + (rb - ra1) == clen[i] && d.fd_cols)  // chain i's last event (of the prefix): rows it never sees
+    if (ka + (rb - ra1) == clen[i])  // chain i's last event (of the prefix): rows it never sees
       for (int c = wave; c < n; c += BT / 64) {
         const int32_t hi = tile[c * (TR + 1) + rb - 1];
         for (int32_t j = hi + 1 + lane; j < clen[c]; j += 64) xstore(d.fdt + fdt_pos(cstart[c] + j, i, npad), FD_NONE);
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(BT) void k_flow_transpose(Dev d) {
   extern __shared__ int32_t tile[];  // [npad][TR + 1], then prev[npad]
   __shared__ int32_t rc[TR], rj[TR];
   __shared__ uint64_t segmask, insmask;
-  __shared__ int32_t cstart[FL_MAXN + 16], clen[FL_MAXN + 16];
+  __shared__ int32_t cstart[512 + 16], clen[512 + 16];  // up to the wide dataflow's 512 chains
   if (d.tile_list) {
     // a segment's tiles, a contiguous share per
     // workgroup: few workgroups, so the round loop running beside them

@@ -1,0 +1,266 @@
+// kernels_flow_wide.hip -- the chain dataflow of kernels_flow.hip for wide
+// groups (128 < n <= 512): initEventCoordinates (hashgraph.go:439-507) and
+// _lamportTimestamp (:325-379) as one workgroup per LA column (plus one for
+// LT), one lane per creator chain, 8 compute waves.
+//
+// What changes against k_flow32 (n <= 128) is the LDS budget: 512 chains'
+// rings must fit one compute unit, so
+//   * value rings hold 32 events per chain (one dword: generation (k / 32,
+//     11 bits) << 21 | value + 1), 66 KiB;
+//   * descriptor rings hold 32 other-parent descriptors per chain (one dword:
+//     generation << 21 | LDS byte address of the parent's slot), 66 KiB; the
+//     lane forms its own slot's address and generation from k (two VALU ops
+//     more per step than k_flow32, whose descriptor entries carry it);
+//   * there is no store wave: a compute lane stores each value to
+//     column-major LA as it computes it, and publishes (for consumers whose
+//     parent has left its 32-slot ring) the events whose stores an
+//     `s_waitcnt vmcnt(16)` at its header proves complete -- the stores of
+//     two headers ago.
+// Two prefetch waves keep the descriptor rings filled, 16 entries per
+// refill, loading for all their chains at once (one LDS-DMA per chain
+// refill, as k_flow32 does, made the prefetch the bottleneck at 512 chains).  Chains shorter than 0x7FE * 32 = 65,472 events;
+// Lamport timestamps at 2^21 are clamped and flagged (ST_FLOWOVF), and the
+// host then recomputes the coordinates with the chunked sweep.
+#include "engine.h"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace bh {
+
+constexpr int FW_MAXN = 512;
+constexpr int FW_R = 32, FW_RS = FW_R + 1;    // value-ring slots per chain (+1 pad)
+constexpr int FW_DR = 32, FW_DRS = FW_DR + 1;  // descriptor-ring entries per chain
+constexpr int FW_REFILL = 16;                  // entries per descriptor refill
+constexpr int FW_PW = 2;                       // prefetch waves
+constexpr uint32_t FW_VMASK = 0x1FFFFFu, FW_GMASK = 0xFFE00000u;
+constexpr uint32_t FW_GNOOP = 0x7FF, FW_GWAIT = 0x7FE, FW_GINIT = 0x7FF;
+constexpr int32_t FW_MAXLEN = 0x7FE * FW_R;
+constexpr int32_t FW_LTCLAMP = (1 << 21) - 256;
+
+__host__ __device__ constexpr uint32_t fw_desc(int32_t dch, int32_t j) {
+  return ((uint32_t)(j >> 5) << 21) | (uint32_t)((dch * FW_RS + (j & (FW_R - 1))) * 4);
+}
+// sentinel row n: slot R-1 = "no other-parent" (value -1), slot R-2 never matches
+__host__ __device__ constexpr uint32_t fw_noop(int n) { return (FW_GNOOP << 21) | (uint32_t)((n * FW_RS + FW_R - 1) * 4); }
+__host__ __device__ constexpr uint32_t fw_wait(int n) { return (FW_GWAIT << 21) | (uint32_t)((n * FW_RS + FW_R - 2) * 4); }
+
+// opdesc[row] = descriptor of the row's other-parent
+__global__ void k_flow_descw(Dev d) {
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  const int32_t o = d.op[e];
+  d.opdesc[d.epos[e]] = (int32_t)(o < 0 ? fw_noop(d.n) : fw_desc(d.creator[o], d.index[o]));
+}
+
+struct FlowLdsW {
+  uint32_t vring[FW_MAXN + 1][FW_RS];  // 66 KiB, LDS offset 0
+  int32_t dring[FW_MAXN][FW_DRS];      // 66 KiB
+  int32_t filled[FW_MAXN], consumed[FW_MAXN], pub[FW_MAXN], cs[FW_MAXN];
+  int32_t abort_;  // set by a compute wave whose watchdog fired: every wave leaves
+};
+// a compute wave none of whose lanes advanced for this many headers (~0.6 s;
+// a run takes tens of ms) leaves, the workgroup with it, and flags
+// ST_FLOWOVF = 2: the host recomputes the coordinates with the chunked sweep
+constexpr int32_t FW_WATCHDOG = 1 << 20;
+
+typedef __attribute__((address_space(3))) volatile int lds_vint_w;
+
+template <bool LT>
+__device__ __forceinline__ void floww_body(const Dev &d, FlowLdsW &L) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = d.n;
+  const int nw = (n + 63) >> 6;
+  const int col = d.col0 + (int)blockIdx.x;
+  const int64_t stride = d.la_rows + 64;
+  int32_t *out = LT ? d.lt_row : d.la_col + (int64_t)col * stride;
+  for (int c = t; c < n; c += blockDim.x) {
+    const int32_t lo = d.seg_lo[c];
+    L.filled[c] = lo;
+    L.consumed[c] = lo;
+    L.pub[c] = lo;
+    L.cs[c] = d.chain_start[c];
+    for (int s = 0; s < FW_R; ++s) L.vring[c][s] = FW_GINIT << 21;  // matches no real event
+  }
+  for (int s = t; s < FW_R; s += blockDim.x) L.vring[n][s] = s == FW_R - 1 ? (FW_GNOOP << 21) : 0u;
+  if (t == 0) L.abort_ = 0;
+  __syncthreads();
+  lds_vint_w *filled = (lds_vint_w *)L.filled, *consumed = (lds_vint_w *)L.consumed, *pub = (lds_vint_w *)L.pub;
+  lds_vint_w *abort_ = (lds_vint_w *)&L.abort_;
+
+  if (wave >= nw) {
+    // ---------------- prefetch waves: descriptor rings ----------------
+    // FW_PW waves, each owning chains lane + 64 h for its share of h; a
+    // pass loads the next 16 descriptors of every chain that has room, for
+    // all its chains at once (one memory latency per pass), then writes them
+    // to the rings and publishes `filled`
+    constexpr int H = FW_MAXN / 64 / FW_PW;
+    const int h0 = (wave - nw) * H;
+    if (h0 >= (n + 63) / 64) return;
+    int32_t f[H], len[H], cs[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int c = lane + 64 * (h0 + h);
+      len[h] = c < n ? d.chain_len[c] : 0;
+      const int32_t lo = c < n ? d.seg_lo[c] : 0;
+      f[h] = lo & ~(FW_REFILL - 1);  // refills stay aligned to the ring
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (;;) {
+      bool left = false;
+      bool need[H];
+      int32_t v[H][FW_REFILL];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int c = lane + 64 * (h0 + h);
+        const int32_t cons = c < n ? consumed[c] : 0;
+        need[h] = f[h] < len[h] && f[h] - cons <= FW_DR - FW_REFILL;
+        left |= f[h] < len[h];
+        const int32_t *src = d.opdesc + cs[h] + f[h];
+#pragma unroll
+        for (int i = 0; i < FW_REFILL; ++i) v[h][i] = need[h] ? __builtin_nontemporal_load(src + i) : 0;
+      }
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int c = lane + 64 * (h0 + h);
+        if (need[h]) {
+          int32_t *dst = &L.dring[c][f[h] & (FW_DR - 1)];
+#pragma unroll
+          for (int i = 0; i < FW_REFILL; ++i) dst[i] = v[h][i];
+          f[h] += FW_REFILL;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int c = lane + 64 * (h0 + h);
+        if (c < n) filled[c] = min(f[h], len[h]);
+      }
+      if (!__any(left) || *abort_) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return;
+  }
+  if (wave > nw) return;
+  int32_t stall = 0;
+
+  // ---------------- compute waves: one chain per lane ----------------
+  const int c = wave * 64 + lane;
+  const bool valid = c < n;
+  const int32_t len = valid ? d.chain_len[c] : 0;
+  const int cc = valid ? c : 0;
+  const int32_t inc = LT ? 1 : (c == col ? 1 : 0);  // LT + 1; LA[e][creator] = index
+  const uint32_t ring_c = (uint32_t)(cc * FW_RS * 4);
+  const uint32_t wscratch = (uint32_t)((n * FW_RS + (lane & 15)) * 4);
+  const uint32_t WAIT = fw_wait(n);
+  char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
+  const int32_t *dring_c = &L.dring[cc][0];
+  int32_t *const outc = out + (valid ? d.chain_start[c] : 0);
+  int32_t k = valid ? d.seg_lo[c] : 0, cur = 0, lim = 0;
+  if (k > 0) cur = outc[k - 1] + 1;
+  int32_t k1 = k, k2 = k;  // k at the previous two headers: the stores before k2 are complete
+  const bool dg = d.diag != nullptr && col == 0 && wave == 0;
+  const unsigned long long t_start = dg ? stamp() : 0;
+  int32_t step = 0;
+  uint32_t dsc = WAIT;
+  const int32_t ltclamp = min(d.flow_ltclamp, FW_LTCLAMP);
+  // one step: the other-parent's slot, the next descriptor, the value
+  // written to the ring and (by the lanes that advance) to HBM; a lane that
+  // does not advance writes the sentinel row
+#define FW_STEP()                                                                     \
+  do {                                                                                \
+    const uint32_t slot_ = *reinterpret_cast<const uint32_t *>(lds + (dsc & 0x1FFFFu)); \
+    const int32_t kn_ = k + 1;                                                        \
+    const uint32_t dn_ = (uint32_t)dring_c[kn_ & (FW_DR - 1)];                        \
+    const bool ready_ = (slot_ ^ dsc) < (1u << 21);                                   \
+    const int32_t v_ = max(cur, (int32_t)(slot_ & FW_VMASK)) + inc;                   \
+    const uint32_t wa_ = ready_ ? ring_c + ((uint32_t)(k & (FW_R - 1)) << 2) : wscratch; \
+    *reinterpret_cast<uint32_t *>(lds + wa_) = ((uint32_t)(k >> 5) << 21) | (uint32_t)v_; \
+    if (ready_) outc[k] = v_ - 1;                                                     \
+    cur = ready_ ? v_ : cur;                                                          \
+    dsc = ready_ ? (kn_ < lim ? dn_ : WAIT) : dsc;                                    \
+    k = ready_ ? kn_ : k;                                                             \
+  } while (0)
+  for (;;) {
+    // header: publish, limits, stalled descriptors, LT clamp, read-backs, exit
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if (valid) {
+      pub[c] = k2;
+      consumed[c] = k;
+    }
+    k2 = k1;
+    k1 = k;
+    lim = valid ? filled[cc] : 0;
+    if (dsc == WAIT && k < lim) dsc = (uint32_t)dring_c[k & (FW_DR - 1)];
+    if (LT && __builtin_expect(__any(cur > ltclamp), 0)) {
+      if (cur > ltclamp) {
+        cur = ltclamp;
+        atomicMax(&d.state[ST_FLOWOVF], 1);
+      }
+    }
+    if (!__any(k < len)) break;
+    stall = __any(k != k2) ? 0 : stall + 1;
+    if (stall > FW_WATCHDOG || *abort_) {
+      if (lane == 0) {
+        *abort_ = 1;
+        atomicMax(&d.state[ST_FLOWOVF], 2);
+      }
+      break;
+    }
+    {
+      // a parent its ring has moved past: read it back once published
+      const uint32_t sa = dsc & 0x1FFFFu;
+      const uint32_t slot = *reinterpret_cast<const uint32_t *>(lds + sa);
+      const int32_t si = (int32_t)(sa >> 2), dd = si / FW_RS;
+      const int32_t jj = (int32_t)((dsc >> 21) << 5) | (si - dd * FW_RS);
+      const bool far = (slot & FW_GMASK) > (dsc & FW_GMASK) && dd < n && pub[dd] > jj;
+      if (__builtin_expect(__any(far), 0)) {
+        if (far) {
+          const int32_t *fp = out + L.cs[dd] + jj;
+          int32_t val;
+          asm volatile("global_load_dword %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(val) : "v"(fp) : "memory");
+          const int32_t v = max(cur, val + 1) + inc;
+          *reinterpret_cast<uint32_t *>(lds + ring_c + ((uint32_t)(k & (FW_R - 1)) << 2)) =
+              ((uint32_t)(k >> 5) << 21) | (uint32_t)v;
+          outc[k] = v - 1;
+          cur = v;
+          ++k;
+          dsc = k < lim ? (uint32_t)dring_c[k & (FW_DR - 1)] : WAIT;
+        }
+      }
+    }
+    FW_STEP(); FW_STEP(); FW_STEP(); FW_STEP();
+    FW_STEP(); FW_STEP(); FW_STEP(); FW_STEP();
+    step += 8;
+  }
+#undef FW_STEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (valid) {
+    pub[c] = len;
+    consumed[c] = len;
+  }
+  if (dg && lane == 0) {
+    d.diag[DG_FL_STEPS] = step;
+    d.diag[DG_FL_CYC] = stamp() - t_start;
+  }
+}
+
+__global__ __launch_bounds__(64 * (FW_MAXN / 64 + FW_PW)) void k_floww(Dev d) {
+  __shared__ FlowLdsW L;  // static: the ring's LDS base is the constant 0
+  if ((int)blockIdx.x == d.ncol) floww_body<true>(d, L);
+  else floww_body<false>(d, L);
+}
+
+bool floww_eligible(const Dev &d) {
+  const char *e = getenv("BH_SWEEP");
+  return d.n > FL_MAXN && d.n <= FW_MAXN && d.max_chain_len <= FW_MAXLEN && !(e && !strcmp(e, "chunk"));
+}
+
+void launch_floww(const Dev &d, hipStream_t s) {
+  if (d.N == 0) return;
+  if (d.N > d.e0) k_flow_descw<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+  const int nw = (d.n + 63) / 64;
+  k_floww<<<d.ncol + 1, (nw + FW_PW) * 64, 0, s>>>(d);
+}
+
+}  // namespace bh

@@ -235,9 +235,20 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
   const int qpl = (q4 + LPC - 1) / LPC;
   if (t == 0) sh_nc = 0;
   __syncthreads();
+  {
+    // candidates of round r: counted before any window, since a chain whose
+    // boundary already reached its end has no window at all and must still
+    // write B[r + 1] = len (and not read as "no candidates anywhere")
+    int nc = 0;
+    for (int q = t; q < n; q += blockDim.x) nc += Bp[q] < d.chain_len[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nc += __shfl_xor(nc, off);
+    if (lane == 0 && nc) atomicAdd(&sh_nc, nc);
+  }
+  __syncthreads();
   int32_t wk0 = Bp[c];
   int32_t result = len;
-  for (int w = 0;; ++w) {
+  for (;;) {
     const int wrows = min(WROWS, len - wk0);
     if (wrows <= 0) break;
     __syncthreads();
@@ -256,10 +267,6 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
       int32_t bq = 0, lq = 0, sq = 0;
       if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
       const bool act = q < n && bq < lq;
-      if (w == 0) {
-        const unsigned long long m = __ballot(act && part == 0);
-        if (lane == 0) atomicAdd(&sh_nc, __popcll(m));
-      }
       const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad);
       int4 f[PIECES];
 #pragma unroll

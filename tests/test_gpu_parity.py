@@ -404,6 +404,20 @@ def test_flow32_lt_fallback(monkeypatch):
     assert hg.results()["lamport"].max() > 300
 
 
+def test_floww_parity_and_lt_fallback(monkeypatch):
+    """The wide dataflow (k_floww, 128 < n <= 512): parity on random and
+    lagging DAGs against the oracle and against the chunked sweep, then with
+    a lowered LT limit that sends the timestamps to the sweep fallback."""
+    hg = _random_parity(200, 30_000, 74, 0)
+    assert hg.profile_kernel() == "k_floww"  # not its watchdog's sweep fallback
+    hg = _random_parity(512, 25_000, 75, 3)
+    assert hg.profile_kernel() == "k_floww"
+    _wild_parity(150, 30_000, 76, 20_000)
+    monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
+    hg = _random_parity(160, 20_000, 77, 2)
+    assert hg.results()["lamport"].max() > 300
+
+
 def test_flow64_parity(monkeypatch):
     """The two-dword dataflow kernel (chains of 2^17 .. 2^21 events) forced
     on DAGs the one-dword kernel would take."""
