@@ -63,6 +63,25 @@ __device__ __forceinline__ int ge4(int4 a, int4 b) {
   return (a.x >= b.x) + (a.y >= b.y) + (a.z >= b.z) + (a.w >= b.w);
 }
 
+// #{a < b} over 4 lanes of LA (>= -1) against FD (>= 0 or FD_NONE): a - b
+// never overflows, so its sign bit is the comparison
+__device__ __forceinline__ int lt4(int4 a, int4 b) {
+  const uint32_t dx = (uint32_t)a.x - (uint32_t)b.x, dy = (uint32_t)a.y - (uint32_t)b.y;
+  const uint32_t dz = (uint32_t)a.z - (uint32_t)b.z, dw = (uint32_t)a.w - (uint32_t)b.w;
+  return (int)((dx >> 31) + (dy >> 31) + (dz >> 31) + (dw >> 31));
+}
+
+// sum over an aligned group of LPC lanes, every lane gets the total (DPP for
+// groups within a row of 16 lanes)
+template <int LPC>
+__device__ __forceinline__ int group_total(int v) {
+  if (LPC >= 2) v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  if (LPC >= 4) v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  if (LPC >= 8) v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+  if (LPC >= 16) v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, true); // row_mirror
+  return v;
+}
+
 template <int LPC>
 __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
@@ -212,27 +231,31 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 
 // n > 256/LPC candidates (wide configurations): T_q per candidate pass
 // accumulated in one histogram over the whole window, windows advanced
-// until SM is reached.  Same arithmetic as k_round, candidate rows reloaded
-// per pass.
+// until SM is reached.  Lane `part` of a candidate's group owns the PIECES
+// consecutive 16-B pieces part*PIECES .. +PIECES of the row: its FD pieces
+// sit in registers, its LA pieces of a window row in LDS at a fixed offset
+// (row * WRS4 + part * (PIECES + 1), skewed by one piece per lane so the
+// group's reads fall in distinct banks), so a probe is PIECES ds_read_b128
+// with immediate offsets, issued back to back, and 4 * PIECES compares.
+// Pieces past the row (pc >= q4) are -1 in LDS and FD_NONE in registers.
 template <int LPC>
-__global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
-  extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
+__global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU
+  extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
+  constexpr int WRS4 = LPC * (PIECES + 1);
   __shared__ int32_t hist[WROWS + 1];
   __shared__ int32_t sh_res, sh_nc;
   __shared__ int8_t tq_s[512];  // T_q of every candidate in the current window (ssw, n <= 512)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
-  const int n = d.n, npad = d.npad, sm = d.sm, rs = npad + SCAN_PAD, q4 = npad / 4;
+  const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   const int done = d.state[ST_DONE];
   const int r = d.state[ST_CUR0 + p];
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
   if (done) return;
-  int32_t *win = ssm;
   constexpr int CPP = 256 / LPC;
   const int part = t % LPC;
   const int npass = (n + CPP - 1) / CPP;
-  const int qpl = (q4 + LPC - 1) / LPC;
   if (t == 0) sh_nc = 0;
   __syncthreads();
   {
@@ -253,11 +276,11 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
     if (wrows <= 0) break;
     __syncthreads();
     {
-      const int tot = wrows * q4;
+      constexpr int RP = LPC * PIECES;  // pieces per padded row
       const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-      for (int i = t; i < tot; i += 256) {
-        const int row = i / q4;
-        reinterpret_cast<int4 *>(win + row * rs)[i - row * q4] = src[i];
+      for (int i = t; i < wrows * RP; i += 256) {
+        const int row = i / RP, pc = i - row * RP;
+        win4[row * WRS4 + pc + pc / PIECES] = pc < q4 ? src[row * q4 + pc] : make_int4(-1, -1, -1, -1);
       }
     }
     if (t <= WROWS) hist[t] = 0;
@@ -267,22 +290,24 @@ __global__ __launch_bounds__(256) void k_round_wide(Dev d, int p) {
       int32_t bq = 0, lq = 0, sq = 0;
       if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
       const bool act = q < n && bq < lq;
-      const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad);
+      const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad) + part * PIECES;
+      const int nvalid = q4 - part * PIECES;  // this lane's pieces inside the row
       int4 f[PIECES];
 #pragma unroll
       for (int u = 0; u < PIECES; ++u) {
-        const int pc = u * LPC + part;
-        f[u] = (u < qpl && pc < q4) ? fr[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+        const int4 v = fr[min(u, max(nvalid - 1, 0))];
+        f[u] = u < nvalid ? v : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
       }
+      const int4 *xb = win4 + part * (PIECES + 1);
       auto ss = [&](int row) -> bool {
-        const int4 *x4 = reinterpret_cast<const int4 *>(win + row * rs);
-        int cnt = 0;
+        const int4 *x4 = xb + row * WRS4;
+        int4 x[PIECES];
 #pragma unroll
-        for (int u = 0; u < PIECES; ++u)
-          if (u < qpl) cnt += ge4(x4[min(u * LPC + part, q4 - 1)], f[u]);
+        for (int u = 0; u < PIECES; ++u) x[u] = x4[u];
+        int lt = 0;
 #pragma unroll
-        for (int o = 1; o < LPC; o <<= 1) cnt += __shfl_xor(cnt, o);
-        return cnt >= sm;
+        for (int u = 0; u < PIECES; ++u) lt += lt4(x[u], f[u]);
+        return LPC * PIECES * 4 - group_total<LPC>(lt) >= sm;
       };
       int tw = WROWS;
       if (ss(wrows - 1)) {
@@ -436,10 +461,13 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const unsigned long long ts1 = dg ? stamp() : 0;
   // count(row) into slot: groups whose candidate `row` strongly sees
   auto probe = [&](const int4 *x4, int slot) {
-    int s = 0;
+    int4 x[PPL];  // all reads first: one LDS round trip per probe
 #pragma unroll
-    for (int u = 0; u < PPL; ++u) s += ge4(x4[min(part + LPC * u, q4 - 1)], f[u]);
-    s = group_sum<LPC>(s);
+    for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * u, q4 - 1)];
+    int lt = 0;
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
+    const int s = LPC * PPL * 4 - group_sum<LPC>(lt);
     const unsigned long long m = __ballot(act && part == 0 && s >= sm);
     if (lane == 0 && m) atomicAdd(&cntk[slot], __popcll(m));
     return m;  // this wave's candidates the row strongly sees (fame's S_j)
@@ -672,9 +700,9 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
     else k_round2<8><<<d.n, 1024, lds, s>>>(d, p);
     return;
   }
-  const size_t wbytes = (size_t)WROWS * (d.npad + SCAN_PAD) * 4;
   const int lpc = lanes_per_candidate(d.npad);
   const bool wide = d.n > 256 / lpc;
+  const size_t wbytes = wide ? (size_t)WROWS * lpc * (PIECES + 1) * 16 : (size_t)WROWS * (d.npad + SCAN_PAD) * 4;
 #define L(K) K<<<d.n, 256, wbytes, s>>>(d, p)
   switch (lpc) {
     case 1: if (wide) L(k_round_wide<1>); else L(k_round<1>); break;
