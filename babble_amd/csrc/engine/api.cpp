@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fd16, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -943,6 +943,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   } else {
     A(&d.fd, (size_t)(C + 64) * d.npad);
     if (n <= 512) A(&d.ssw, R1 * n * 8);  // k_round_wide's masks for k_fame_masks<16>
+    if (n <= 512) A(&d.fd16, (size_t)(C + 64) * ((d.npad + 7) / 8 * 4));
   }
   A(&d.last_la, (size_t)(n + 1) * d.npad);
   A(&d.candfd, (size_t)2 * n * d.npad);

@@ -25,6 +25,7 @@ namespace bh {
 
 constexpr int32_t UNSET = INT32_MIN;    // Go nil
 constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
+constexpr int32_t P16_MAXLEN = 65000;  // longest chain the 16-bit round loop takes
 constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 8192;     // frames sorted in LDS up to this size (96 KiB)
 constexpr int FL_MAXN = 128;            // participants the dataflow sweep (k_flow) handles
@@ -93,6 +94,8 @@ struct Dev {
   int32_t *Bp;     // [2][n] B[r] / B[r+1] by round parity
   // firstDescendants of every event (updateAncestorFirstDescendant)
   int32_t *fd;      // [la_rows + 64][npad] chain-major rows
+  uint32_t *fd16;   // [la_rows + 64][(npad + 7) / 8 * 4] the same rows as 16-bit FD + 1 (0xFFFF: none),
+                    // two per dword, for k_round_wide<*, true> (n <= 512, chains <= P16_MAXLEN)
   int32_t *fdt;     // walk output, tiled by 64 chain-major rows (fdt_pos; shares la_ev's allocation)
   // fd_cols (npad <= 128): FDT is complete (the walks write MaxInt32 where
   // no event of a chain sees a row) and is the only per-event FD table; the

@@ -162,6 +162,12 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
       o[u] = x;
     }
     *reinterpret_cast<int4 *>(d.fd + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
+    if (d.fd16) {  // FD + 1 as 16 bits, FD_NONE -> 0xFFFF (its + 1 wraps to 2^31)
+      auto h16 = [](int32_t v) { return min((uint32_t)v + 1u, 0xFFFFu); };
+      const int64_t w0 = (row0 + r) * ((npad + 7) / 8 * 4) + i4 / 2;
+      *reinterpret_cast<uint2 *>(d.fd16 + w0) = make_uint2(h16(o[0]) | h16(o[1]) << 16, h16(o[2]) | h16(o[3]) << 16);
+      if ((npad & 4) && i4 + 4 == npad) *reinterpret_cast<uint2 *>(d.fd16 + w0 + 2) = make_uint2(~0u, ~0u);
+    }
   }
 }
 

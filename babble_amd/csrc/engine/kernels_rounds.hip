@@ -82,6 +82,23 @@ __device__ __forceinline__ int group_total(int v) {
   return v;
 }
 
+// 16-bit rows (chains <= P16_MAXLEN events): LA + 1 in [0, len] against
+// FD + 1 in [1, len] or 0xFFFF (none), two columns per dword.  Per dword:
+// saturating f - x (non-zero iff x < f), min 1, accumulate -- three packed
+// ops for two columns.  Inline asm: the compiler would split the packed
+// compare back into per-half compares.
+__device__ __forceinline__ uint32_t lt16x2_acc(uint32_t acc, uint32_t x, uint32_t f, uint32_t one) {
+  uint32_t dd;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(dd) : "v"(f), "v"(x));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(dd) : "v"(dd), "v"(one));
+  asm("v_pk_add_u16 %0, %1, %2" : "=v"(dd) : "v"(acc), "v"(dd));
+  return dd;
+}
+
+__device__ __forceinline__ uint32_t pack_la16(int32_t a, int32_t b) {
+  return (uint32_t)(a + 1) | ((uint32_t)(b + 1) << 16);
+}
+
 template <int LPC>
 __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
@@ -238,10 +255,15 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // group's reads fall in distinct banks), so a probe is PIECES ds_read_b128
 // with immediate offsets, issued back to back, and 4 * PIECES compares.
 // Pieces past the row (pc >= q4) are -1 in LDS and FD_NONE in registers.
-template <int LPC>
+//
+// P16: the same search over 16-bit rows (fd16, LA converted while staged):
+// lane `part` owns 8 pieces of 8 columns, half the LDS reads and 3/5 of the
+// compare work per probe.
+template <int LPC, bool P16>
 __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU
   extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
-  constexpr int WRS4 = LPC * (PIECES + 1);
+  constexpr int PP = P16 ? 8 : PIECES;  // 16-B pieces per lane
+  constexpr int WRS4 = LPC * (PP + 1);
   __shared__ int32_t hist[WROWS + 1];
   __shared__ int32_t sh_res, sh_nc;
   __shared__ int8_t tq_s[512];  // T_q of every candidate in the current window (ssw, n <= 512)
@@ -276,11 +298,20 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     if (wrows <= 0) break;
     __syncthreads();
     {
-      constexpr int RP = LPC * PIECES;  // pieces per padded row
+      constexpr int RP = LPC * PP;  // pieces per padded row
       const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
       for (int i = t; i < wrows * RP; i += 256) {
         const int row = i / RP, pc = i - row * RP;
-        win4[row * WRS4 + pc + pc / PIECES] = pc < q4 ? src[row * q4 + pc] : make_int4(-1, -1, -1, -1);
+        if constexpr (P16) {  // columns 8pc .. 8pc + 7 (npad is a multiple of 4)
+          const int4 a = src[row * q4 + min(2 * pc, q4 - 1)];
+          const int4 b = src[row * q4 + min(2 * pc + 1, q4 - 1)];
+          const bool va = 8 * pc < npad, vb = 8 * pc + 4 < npad;  // else -1 (packs to 0)
+          win4[row * WRS4 + pc + pc / PP] =
+              make_int4(va ? (int)pack_la16(a.x, a.y) : 0, va ? (int)pack_la16(a.z, a.w) : 0,
+                        vb ? (int)pack_la16(b.x, b.y) : 0, vb ? (int)pack_la16(b.z, b.w) : 0);
+        } else {
+          win4[row * WRS4 + pc + pc / PP] = pc < q4 ? src[row * q4 + pc] : make_int4(-1, -1, -1, -1);
+        }
       }
     }
     if (t <= WROWS) hist[t] = 0;
@@ -290,24 +321,52 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       int32_t bq = 0, lq = 0, sq = 0;
       if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
       const bool act = q < n && bq < lq;
-      const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad) + part * PIECES;
-      const int nvalid = q4 - part * PIECES;  // this lane's pieces inside the row
-      int4 f[PIECES];
+      int4 f[PP];
+      if constexpr (P16) {
+        const int f16q = (npad + 7) / 8;  // 16-B pieces per fd16 row
+        const int4 *fr = reinterpret_cast<const int4 *>(d.fd16) + (int64_t)(act ? sq + bq : 0) * f16q + part * PP;
+        const int nvalid = f16q - part * PP;
 #pragma unroll
-      for (int u = 0; u < PIECES; ++u) {
-        const int4 v = fr[min(u, max(nvalid - 1, 0))];
-        f[u] = u < nvalid ? v : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+        for (int u = 0; u < PP; ++u) {
+          const int4 v = fr[min(u, max(nvalid - 1, 0))];
+          f[u] = u < nvalid ? v : make_int4(-1, -1, -1, -1);  // 0xFFFF: never reached
+        }
+      } else {
+        // every lane holds PIECES pieces; those past the row (pc >= q4) are
+        // FD_NONE, which no LA value reaches, so the probe needs no per-piece
+        // branch and its LDS reads issue back to back
+        const int4 *fr = reinterpret_cast<const int4 *>(d.fd + (int64_t)(act ? sq + bq : 0) * npad) + part * PP;
+        const int nvalid = q4 - part * PP;  // this lane's pieces inside the row
+#pragma unroll
+        for (int u = 0; u < PP; ++u) {
+          const int4 v = fr[min(u, max(nvalid - 1, 0))];
+          f[u] = u < nvalid ? v : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+        }
       }
-      const int4 *xb = win4 + part * (PIECES + 1);
+      const int4 *xb = win4 + part * (PP + 1);
       auto ss = [&](int row) -> bool {
         const int4 *x4 = xb + row * WRS4;
-        int4 x[PIECES];
+        int4 x[PP];
 #pragma unroll
-        for (int u = 0; u < PIECES; ++u) x[u] = x4[u];
+        for (int u = 0; u < PP; ++u) x[u] = x4[u];
         int lt = 0;
+        if constexpr (P16) {
+          const uint32_t one = 0x00010001u;
+          uint32_t acc = 0;
 #pragma unroll
-        for (int u = 0; u < PIECES; ++u) lt += lt4(x[u], f[u]);
-        return LPC * PIECES * 4 - group_total<LPC>(lt) >= sm;
+          for (int u = 0; u < PP; ++u) {
+            acc = lt16x2_acc(acc, (uint32_t)x[u].x, (uint32_t)f[u].x, one);
+            acc = lt16x2_acc(acc, (uint32_t)x[u].y, (uint32_t)f[u].y, one);
+            acc = lt16x2_acc(acc, (uint32_t)x[u].z, (uint32_t)f[u].z, one);
+            acc = lt16x2_acc(acc, (uint32_t)x[u].w, (uint32_t)f[u].w, one);
+          }
+          lt = (int)((acc & 0xFFFFu) + (acc >> 16));
+        } else {
+#pragma unroll
+          for (int u = 0; u < PP; ++u) lt += lt4(x[u], f[u]);
+        }
+        constexpr int COLS = LPC * PP * (P16 ? 8 : 4);  // columns per group, padding included
+        return COLS - group_total<LPC>(lt) >= sm;
       };
       int tw = WROWS;
       if (ss(wrows - 1)) {
@@ -673,6 +732,10 @@ void launch_fd_idle(const Dev &d, hipStream_t s) {
 
 bool round2_eligible(const Dev &d) { return d.fd_cols != 0; }
 
+// the 16-bit wide loop: fd16 rows exist (k_fd_transpose wrote them) and
+// every LA / FD value + 1 fits below 0xFFFF
+bool round_p16(const Dev &d) { return d.fd16 != nullptr && d.max_chain_len <= P16_MAXLEN && !getenv("BH_NO_P16"); }
+
 void launch_round_init(const Dev &d, hipStream_t s) {
   if (round2_eligible(d)) k_round2_init<<<d.n, 256, 0, s>>>(d);
 }
@@ -687,7 +750,9 @@ static int lanes_per_candidate(int npad) {
 void configure_round_kernels() {
 #define CFG(K) (void)hipFuncSetAttribute((const void *)K, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024)
   CFG(k_round<1>); CFG(k_round<2>); CFG(k_round<4>); CFG(k_round<8>); CFG(k_round<16>);
-  CFG(k_round_wide<1>); CFG(k_round_wide<2>); CFG(k_round_wide<4>); CFG(k_round_wide<8>); CFG(k_round_wide<16>);
+  CFG((k_round_wide<1, false>)); CFG((k_round_wide<2, false>)); CFG((k_round_wide<4, false>));
+  CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
+  CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
   CFG(k_round2<4>); CFG(k_round2<8>);
 #undef CFG
 }
@@ -702,16 +767,24 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   }
   const int lpc = lanes_per_candidate(d.npad);
   const bool wide = d.n > 256 / lpc;
+  if (wide && round_p16(d) && (lpc == 4 || lpc == 8)) {
+    const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
+    if (lpc == 4) k_round_wide<4, true><<<d.n, 256, wb16, s>>>(d, p);
+    else k_round_wide<8, true><<<d.n, 256, wb16, s>>>(d, p);
+    return;
+  }
   const size_t wbytes = wide ? (size_t)WROWS * lpc * (PIECES + 1) * 16 : (size_t)WROWS * (d.npad + SCAN_PAD) * 4;
 #define L(K) K<<<d.n, 256, wbytes, s>>>(d, p)
+#define LW(W) (k_round_wide<W, false>)<<<d.n, 256, wbytes, s>>>(d, p)
   switch (lpc) {
-    case 1: if (wide) L(k_round_wide<1>); else L(k_round<1>); break;
-    case 2: if (wide) L(k_round_wide<2>); else L(k_round<2>); break;
-    case 4: if (wide) L(k_round_wide<4>); else L(k_round<4>); break;
-    case 8: if (wide) L(k_round_wide<8>); else L(k_round<8>); break;
-    default: if (wide) L(k_round_wide<16>); else L(k_round<16>); break;
+    case 1: if (wide) LW(1); else L(k_round<1>); break;
+    case 2: if (wide) LW(2); else L(k_round<2>); break;
+    case 4: if (wide) LW(4); else L(k_round<4>); break;
+    case 8: if (wide) LW(8); else L(k_round<8>); break;
+    default: if (wide) LW(16); else L(k_round<16>); break;
   }
 #undef L
+#undef LW
 }
 
 // ---------------------------------------------------------------------------

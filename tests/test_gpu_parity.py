@@ -358,10 +358,14 @@ def test_chunk_sweep_wild(monkeypatch):
     _wild_parity(8, 30_000, 41, 25_000)
 
 
+@pytest.mark.parametrize("p16", [True, False])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
-def test_wide_parity(n, N, seed):
-    """More participants than the dataflow sweep / k_round2 / LDS fame
-    support: chunked sweep, k_round_wide, fame from HBM rows."""
+def test_wide_parity(monkeypatch, n, N, seed, p16):
+    """More participants than k_round2 / LDS fame support: k_round_wide
+    over 16-bit rows (fd16; n = 300 has a half-filled last piece) and over
+    the 32-bit rows (BH_NO_P16, the path for chains beyond P16_MAXLEN)."""
+    if not p16:
+        monkeypatch.setenv("BH_NO_P16", "1")
     _random_parity(n, N, seed)
 
 
