@@ -12,8 +12,15 @@ all: babble_amd/libbabble_gen.so babble_amd/libbabble_hip.so oracle/liboracle.so
 babble_amd/libbabble_gen.so: babble_amd/csrc/dag_gen.c babble_amd/csrc/dag_gen.h
 	$(CC) -O2 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
 
-babble_amd/libbabble_hip.so: $(ENGINE_SRC) $(ENGINE_HDR)
-	$(HIPCC) $(HIPFLAGS) -Iinclude -shared -o $@ $(ENGINE_SRC) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+# one object per source (build/engine/*.o), so an edit rebuilds one file
+ENGINE_OBJ := $(patsubst babble_amd/csrc/engine/%,build/engine/%.o,$(ENGINE_SRC))
+
+build/engine/%.o: babble_amd/csrc/engine/% $(ENGINE_HDR)
+	@mkdir -p build/engine
+	$(HIPCC) $(HIPFLAGS) -Iinclude -c -o $@ $<
+
+babble_amd/libbabble_hip.so: $(ENGINE_OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(ENGINE_OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle/liboracle.so: oracle/hg_oracle.c oracle/hg_oracle.h
 	$(MAKE) -C oracle
@@ -23,6 +30,6 @@ tests/cpp/hg_replay: tests/cpp/hg_replay.cpp include/babble_hashgraph.hpp includ
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lbabble_amd -lbabble_hip -Wl,-rpath,'$$ORIGIN/../../babble_amd'
 
 clean:
-	rm -f babble_amd/*.so oracle/*.so tests/cpp/hg_replay
+	rm -rf babble_amd/*.so oracle/*.so tests/cpp/hg_replay build/engine
 
 .PHONY: all clean

@@ -466,11 +466,20 @@ __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
   for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs, i, d.npad)] : FD_NONE;
 }
 
-template <int LPC>
+// TQ (default): every lane group binary-searches its own T_q (the first
+// window row strongly seeing candidate q) with no barrier between probes; one
+// 33-bin histogram + prefix then gives B[r+1][c] = the first row where
+// #{q : T_q <= row} reaches SM.  !TQ (BH_ROUND_ROWS=1, A/B): the row-probe
+// search -- the workgroup binary-searches count(row) together, one barrier
+// per probe.  Same compares per probe; the groups of a wave read different
+// rows, so each group starts its four 128-B chunks at chunk (q & 3): the
+// four groups of a ds_read_b128 lane set then hit distinct banks.
+template <int LPC, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   constexpr int PPL = 4;  // pieces per lane: LPC * PPL >= npad / 4
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
   __shared__ int32_t cntk[16];
+  __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
@@ -492,6 +501,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
   const int32_t k0 = Bp[c];
   const int q = t / LPC, part = t % LPC;
+  const int rot = TQ ? (q & (PPL - 1)) : 0;  // piece order of this group (bank spread)
   int32_t bq = 0, lq = 0;
   if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; }
   int4 f[PPL];
@@ -499,7 +509,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     const int4 *cf = reinterpret_cast<const int4 *>(d.candfd) + ((int64_t)p * n + min(q, n - 1)) * q4;
 #pragma unroll
     for (int u = 0; u < PPL; ++u) {
-      const int pc = part + LPC * u;
+      const int pc = part + LPC * ((u + rot) & (PPL - 1));
       f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
     }
   }
@@ -516,18 +526,24 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int4 fv = *reinterpret_cast<const int4 *>(d.fdt + fdt_pos(rb + fp, fi, npad));
   if (t < rows * q4) win[t] = wv;
   if (t < 16) cntk[t] = 0;
+  if (TQ && t <= HW) hist[t] = 0;
   __syncthreads();
   const unsigned long long ts1 = dg ? stamp() : 0;
+  const unsigned long long rt1 = dg ? __builtin_amdgcn_s_memrealtime() : 0;  // loads landed
   // count(row) into slot: groups whose candidate `row` strongly sees
-  auto probe = [&](const int4 *x4, int slot) {
+  // does window row x4 strongly see this group's candidate?
+  auto ss_row = [&](const int4 *x4) {
     int4 x[PPL];  // all reads first: one LDS round trip per probe
 #pragma unroll
-    for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * u, q4 - 1)];
+    for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * ((u + rot) & (PPL - 1)), q4 - 1)];
     int lt = 0;
 #pragma unroll
     for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
-    const int s = LPC * PPL * 4 - group_sum<LPC>(lt);
-    const unsigned long long m = __ballot(act && part == 0 && s >= sm);
+    return LPC * PPL * 4 - group_sum<LPC>(lt) >= sm;
+  };
+  auto probe = [&](const int4 *x4, int slot) {
+    const bool s = ss_row(x4);
+    const unsigned long long m = __ballot(act && part == 0 && s);
     if (lane == 0 && m) atomicAdd(&cntk[slot], __popcll(m));
     return m;  // this wave's candidates the row strongly sees (fame's S_j)
   };
@@ -538,7 +554,34 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   int slot = 1;
   int32_t res = -1;  // window row of B[r+1][c], or -1
   unsigned long long ssb = 0;  // this wave's ballot of the probe that verified the answer row
-  if (rows > 0) {
+  if (TQ && rows > 0) {
+    // T_q by a per-group binary search over [0, rows] (rows = none in the window)
+    int lo = 0, hi = rows;
+    while (__any(lo < hi)) {
+      const int mid = (lo + hi) >> 1;
+      const bool s = ss_row(win + min(mid, rows - 1) * q4);
+      if (lo < hi) {
+        hi = s ? mid : hi;
+        lo = s ? lo : mid + 1;
+      }
+    }
+    if (act && part == 0 && lo < rows) atomicAdd(&hist[lo], 1);
+    __syncthreads();
+    if (wave == 0) {
+      int h = lane < rows ? hist[lane] : 0;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(h, off);
+        h += lane >= off ? o : 0;
+      }
+      const unsigned long long hit = __ballot(lane < rows && h >= sm);
+      if (lane == 0) hist[HW] = hit ? (int)__builtin_ctzll(hit) : -1;
+    }
+    __syncthreads();
+    res = hist[HW];
+    // fame's S_j for the new candidate: the candidates whose T_q is at most its row
+    ssb = __ballot(act && part == 0 && res >= 0 && lo <= res);
+  } else if (rows > 0) {
     // binary search assuming the window's last row reaches SM (count is
     // monotone); that row is probed only if the search ends on it unverified
     int lo = 0, hi = rows - 1;
@@ -604,7 +647,6 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     __syncthreads();
   }
   // ---- hand-off for the next iteration ----
-  unsigned long long rthb = 0;
   if (nc > 0 && r + 1 < d.R_cap && result < len) {
     const int32_t off = result - k0;
     int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
@@ -612,7 +654,6 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     if (off < HW && frel < HW) {  // both from the rows staged during the search
       if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
       __syncthreads();
-      if (dg) rthb = __builtin_amdgcn_s_memrealtime();
       if (t < npad) cf[t] = t < n ? fdw[t * FDS + frel] : FD_NONE;
     } else {
       if (t < npad) cf[t] = t < n ? d.fdt[fdt_pos(cs + result, t, npad)] : FD_NONE;
@@ -630,7 +671,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
       const unsigned long long fl = (unsigned long long)(min(result - k0, 255) & 255) |
                                     (unsigned long long)(res < 0) << 8 | (unsigned long long)(nc > 0) << 9;
-      tl[0] = rt0 | fl << 52; tl[1] = rt2; tl[2] = rthb; tl[3] = __builtin_amdgcn_s_memrealtime();
+      tl[0] = rt0 | fl << 52; tl[1] = rt2; tl[2] = rt1; tl[3] = __builtin_amdgcn_s_memrealtime();
     } else if (r < TL_R0 - 64 || r >= TL_R0 + TL_NR + 64) {
       // phase counters (device-scope atomics from every workgroup: they
       // stretch the round by several us, so none near the timeline window)
@@ -753,7 +794,7 @@ void configure_round_kernels() {
   CFG((k_round_wide<1, false>)); CFG((k_round_wide<2, false>)); CFG((k_round_wide<4, false>));
   CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
-  CFG(k_round2<4>); CFG(k_round2<8>);
+  CFG((k_round2<4, true>)); CFG((k_round2<8, true>)); CFG((k_round2<4, false>)); CFG((k_round2<8, false>));
 #undef CFG
 }
 
@@ -761,8 +802,14 @@ void configure_round_kernels() {
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
     const size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
-    if (d.npad <= 64) k_round2<4><<<d.n, 1024, lds, s>>>(d, p);
-    else k_round2<8><<<d.n, 1024, lds, s>>>(d, p);
+    static const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));
+    if (rows_search) {
+      if (d.npad <= 64) k_round2<4, false><<<d.n, 1024, lds, s>>>(d, p);
+      else k_round2<8, false><<<d.n, 1024, lds, s>>>(d, p);
+    } else {
+      if (d.npad <= 64) k_round2<4, true><<<d.n, 1024, lds, s>>>(d, p);
+      else k_round2<8, true><<<d.n, 1024, lds, s>>>(d, p);
+    }
     return;
   }
   const int lpc = lanes_per_candidate(d.npad);

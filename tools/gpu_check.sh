@@ -23,7 +23,13 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench2) step bench_c2 600 python bench.py --cfg 2 --steps 3 --warmup 1 ;;
     bench3) step bench_c3 900 python bench.py --cfg 3 --steps 3 --warmup 1 ;;
+    serial) step serial 600 env BH_SEG_SERIAL=1 BH_SEG_DEBUG=1 python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    serialrows) step serial_rows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_SEG_DEBUG=1 python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    tl) step tl 600 env BH_DIAG=1 BH_TIMELINE=gpurun_out/tl.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    tlser) step tlser 600 env BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlser.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    tlrows) step tlrows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlrows.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench) step bench 900 python bench.py ;;
+    benchrows) step bench_rows 900 env BH_ROUND_ROWS=1 python bench.py --cpu-sample 0 ;;
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;

@@ -1,0 +1,50 @@
+"""Summarise the round loop's realtime stamps (BH_DIAG=1 BH_TIMELINE=file).
+
+Per round r (TL_R0 .. TL_R0 + TL_NR) and chain c the kernel stores four
+s_memrealtime stamps (100 MHz): workgroup start (low 52 bits), search end,
+hand-off barrier, workgroup end.  Prints medians over rounds of
+  launch spread  (last start - first start of the round's workgroups),
+  loads          (first barrier - start, per workgroup),
+  search         (search end - first barrier),
+  hand-off       (end - search end),
+  round span     (last end - first start),
+  boundary       (first start of round r+1 - last end of round r).
+"""
+import sys
+
+import numpy as np
+
+TL_NR, NC = 64, 128
+
+
+def main(path):
+    a = np.fromfile(path, dtype=np.uint64)[: TL_NR * NC * 4].reshape(TL_NR, NC, 4)
+    start = (a[:, :, 0] & ((1 << 52) - 1)).astype(np.int64)
+    srch, end = a[:, :, 1].astype(np.int64), a[:, :, 3].astype(np.int64)
+    ld = a[:, :, 2].astype(np.int64)
+    live = (start > 0) & (end > 0)
+    rows = []
+    for r in range(TL_NR):
+        m = live[r]
+        if m.sum() < 2:
+            continue
+        s, e, q = start[r, m], end[r, m], srch[r, m]
+        nxt = None
+        if r + 1 < TL_NR and live[r + 1].sum() > 1:
+            nxt = start[r + 1, live[r + 1]].min() - e.max()
+        l = ld[r, m]
+        rows.append((s.max() - s.min(), np.median(l - s), np.median(q - l), np.median(e - q), e.max() - s.min(), nxt))
+    if not rows:
+        print("no stamps")
+        return
+    ns = 10.0  # s_memrealtime ticks at 100 MHz
+    cols = ["launch spread", "loads", "search", "hand-off", "round span", "boundary"]
+    for i, name in enumerate(cols):
+        v = [x[i] for x in rows if x[i] is not None]
+        print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
+    per_round = np.diff(np.array([start[r, live[r]].min() for r in range(TL_NR) if live[r].sum() > 1]))
+    print(f"{'round period':14s} median {np.median(per_round) * ns / 1000:6.2f} us")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
