@@ -97,6 +97,21 @@ struct hgo {
   /* FrameHash of each block (NewBlockFromFrame, block.go:100-110) */
   uint8_t *blk_fhash;
   int8_t *blk_has_fhash;
+  /* the Store's Roots (inmem_store.go:221-227): base roots (root.go:98-106)
+   * unless hgo_reset installed a Frame's roots (Hashgraph.Reset,
+   * hashgraph.go:1324-1369).  Per participant slot: NextRound and the
+   * SelfParent RootEvent's Index / LamportTimestamp / Round; chain positions
+   * start at base = SelfParent.Index + 1 (the first event's Index) */
+  int is_reset;
+  int32_t *r_next, *r_sp_index, *r_sp_lt, *r_sp_round;
+  /* Root.Others: entry k belongs to the root of slot oth_root[k], keyed by
+   * the hash of the event whose other-parent it describes (oth_key) */
+  int32_t n_oth;
+  int32_t *oth_root, *oth_creator, *oth_index, *oth_lt, *oth_round;
+  uint8_t *oth_key, *oth_hash;
+  /* per event: the Others entry its other-parent resolved to (op == -2) */
+  int32_t *ext;
+  int64_t blk_index0; /* LastBlockIndex()+1 of the first block (Reset: block.Index()+1) */
 };
 
 /* Root (root.go:88-96) of one participant in one frame: NextRound, the
@@ -165,6 +180,15 @@ hgo *hgo_create(int32_t n, const int64_t *participant_ids, int64_t capacity) {
   h->sig_len = (int32_t *)xcalloc(C, 4);
   h->last_round = -1; /* inmem_store.go:45 */
   h->lcr = -1;
+  h->ext = (int32_t *)xcalloc(C, 4);
+  h->r_next = (int32_t *)xcalloc(n, 4);
+  h->r_sp_index = (int32_t *)xcalloc(n, 4);
+  h->r_sp_lt = (int32_t *)xcalloc(n, 4);
+  h->r_sp_round = (int32_t *)xcalloc(n, 4);
+  for (int32_t i = 0; i < n; i++) { /* NewBaseRoot (root.go:75-106) */
+    h->r_next[i] = 0;
+    h->r_sp_index[i] = h->r_sp_lt[i] = h->r_sp_round[i] = -1;
+  }
   return h;
 }
 
@@ -195,6 +219,9 @@ void hgo_destroy(hgo *h) {
   for (int64_t e = 0; e < h->cap; e++) { free(h->body[e]); free(h->sig[e]); }
   free(h->body); free(h->sig); free(h->body_len); free(h->sig_len);
   free(h->blk_fhash); free(h->blk_has_fhash);
+  free(h->ext); free(h->r_next); free(h->r_sp_index); free(h->r_sp_lt); free(h->r_sp_round);
+  free(h->oth_root); free(h->oth_creator); free(h->oth_index); free(h->oth_lt); free(h->oth_round);
+  free(h->oth_key); free(h->oth_hash);
   free(h);
 }
 
@@ -297,19 +324,50 @@ static int strongly_see(const hgo *h, int32_t x, int32_t y) {
   return c >= h->sm;
 }
 
-/* round / _round (hashgraph.go:193-278) for base roots (root.go:75-106):
- * the Root's SelfParent has Round -1 and NextRound is 0, Others is empty. */
+/* round / _round (hashgraph.go:193-278) with the Store's Roots (root.go):
+ * sp < 0 is the creator's Root SelfParent (rootsBySelfParent, :211-214);
+ * op == -2 is an other-parent known only through Root.Others. */
 static int32_t round_of(hgo *h, int32_t x);
 
 static int32_t *g_wbuf;
 static int32_t g_wcap;
 
+/* Root.Others[ev.Hex()] of ev's creator's Root: the entry index, or -1 */
+static int32_t others_key(const hgo *h, int32_t x) {
+  for (int32_t k = 0; k < h->n_oth; k++)
+    if (h->oth_root[k] == h->creator[x] && !memcmp(h->oth_key + (size_t)k * 32, h->hash + (size_t)x * 32, 32))
+      return k;
+  return -1;
+}
+
+/* the hash of x's other-parent (a store event, or the Root.Others entry it
+ * resolved to at insert) */
+static const uint8_t *op_hash(const hgo *h, int32_t x) {
+  return h->op[x] >= 0 ? h->hash + (size_t)h->op[x] * 32 : h->oth_hash + (size_t)h->ext[x] * 32;
+}
+
+/* `other, ok := root.Others[ex.Hex()]; ok && other.Hash == ex.OtherParent()` */
+static int32_t others_match(const hgo *h, int32_t x) {
+  if (h->op[x] == -1) return -1;
+  const int32_t k = others_key(h, x);
+  return k >= 0 && !memcmp(h->oth_hash + (size_t)k * 32, op_hash(h, x), 32) ? k : -1;
+}
+
+/* round of x's self-parent: the Root's SelfParent.Round for a first event */
+static int32_t sp_round_of(hgo *h, int32_t x) {
+  return h->sp[x] < 0 ? h->r_sp_round[h->creator[x]] : round_of(h, h->sp[x]);
+}
+
 static int32_t round_impl(hgo *h, int32_t x) {
   int32_t sp = h->sp[x], op = h->op[x];
-  if (sp < 0 && op < 0) return 0; /* directly attached to the Root: NextRound */
-  int32_t pr = sp < 0 ? -1 : round_of(h, sp);
-  if (op >= 0) {
-    int32_t opr = round_of(h, op);
+  const int32_t cr = h->creator[x];
+  /* directly attached to the Root: authoritative unless the other-parent is
+   * a real event outside Root.Others (:229-236) */
+  if (sp < 0 && (op == -1 || others_match(h, x) >= 0)) return h->r_next[cr];
+  int32_t pr = sp_round_of(h, x);
+  if (op != -1) {
+    /* an other-parent in Root.Others takes Root.NextRound (:246-256) */
+    int32_t opr = others_match(h, x) >= 0 ? h->r_next[cr] : round_of(h, op);
     if (opr > pr) pr = opr;
   }
   /* count the parentRound witnesses that x strongly sees */
@@ -321,7 +379,6 @@ static int32_t round_impl(hgo *h, int32_t x) {
 }
 
 static int32_t round_of(hgo *h, int32_t x) {
-  if (x < 0) return -1; /* x is the Root: Root.SelfParent.Round */
   if (h->round_memo[x] != UNSET) return h->round_memo[x];
   int32_t r = round_impl(h, x);
   h->round_memo[x] = r;
@@ -329,15 +386,23 @@ static int32_t round_of(hgo *h, int32_t x) {
 }
 
 /* witness (hashgraph.go:281-296) */
-static int witness_of(hgo *h, int32_t x) { return round_of(h, x) > round_of(h, h->sp[x]); }
+static int witness_of(hgo *h, int32_t x) { return round_of(h, x) > sp_round_of(h, x); }
 
-/* lamportTimestamp / _lamportTimestamp (hashgraph.go:313-379) */
+/* lamportTimestamp / _lamportTimestamp (hashgraph.go:313-379): a first
+ * event's self-parent is the Root's SelfParent (:347-349); an other-parent
+ * not in the Store takes the LamportTimestamp of its Root.Others entry
+ * (:358-375) */
 static int32_t lamport_of(hgo *h, int32_t x) {
-  if (x < 0) return -1; /* Root.SelfParent.LamportTimestamp */
   if (h->lt_memo[x] != UNSET) return h->lt_memo[x];
-  int32_t plt = lamport_of(h, h->sp[x]);
-  if (h->op[x] >= 0) {
-    int32_t o = lamport_of(h, h->op[x]);
+  int32_t plt = h->sp[x] < 0 ? h->r_sp_lt[h->creator[x]] : lamport_of(h, h->sp[x]);
+  if (h->op[x] != -1) {
+    int32_t o = INT32_MIN;
+    if (h->op[x] >= 0) {
+      o = lamport_of(h, h->op[x]);
+    } else {
+      const int32_t k = others_match(h, x);
+      if (k >= 0) o = h->oth_lt[k];
+    }
     if (o > plt) plt = o;
   }
   h->lt_memo[x] = plt + 1;
@@ -357,6 +422,11 @@ static void chain_push(hgo *h, int32_t c, int32_t id) {
 
 int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
                const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx) {
+  return hgo_insert_ext(h, creator, index, sp, op, -1, -1, hash32, sig_r32, ntx);
+}
+
+int hgo_insert_ext(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op, int32_t op_creator,
+                   int32_t op_index, const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx) {
   if (creator < 0 || creator >= h->n) return HGO_ERR_BAD_CREATOR;
   if (h->N >= h->cap) return HGO_ERR_CAPACITY;
   /* checkSelfParent: self-parent must be the creator's last known event,
@@ -364,14 +434,32 @@ int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
   int32_t clen = h->chain_len[creator];
   int32_t last = clen ? h->chain[creator][clen - 1] : -1;
   if (sp != last) return HGO_ERR_SELF_PARENT;
-  /* checkOtherParent (hashgraph.go:417-436) */
-  if (op >= h->N || op < -1) return HGO_ERR_OTHER_PARENT;
+  /* checkOtherParent (hashgraph.go:417-436); an other-parent the Store does
+   * not hold is looked up in the creator's Root.Others: by (creator, index)
+   * as ReadWireInfo resolves it (:1431-1457), then keyed by the event's own
+   * hash with the same Hash (:424-431) */
+  int32_t ext = -1;
+  if (op == -2) {
+    int32_t k = -1;
+    for (int32_t q = 0; q < h->n_oth && k < 0; q++)
+      if (h->oth_root[q] == creator && h->oth_creator[q] == op_creator && h->oth_index[q] == op_index) k = q;
+    if (k < 0) return HGO_ERR_OTHER_PARENT;
+    int32_t k2 = -1;
+    for (int32_t q = 0; q < h->n_oth && k2 < 0; q++)
+      if (h->oth_root[q] == creator && !memcmp(h->oth_key + (size_t)q * 32, hash32, 32)) k2 = q;
+    if (k2 < 0 || memcmp(h->oth_hash + (size_t)k2 * 32, h->oth_hash + (size_t)k * 32, 32)) return HGO_ERR_OTHER_PARENT;
+    ext = k2;
+  } else if (op >= h->N || op < -1) {
+    return HGO_ERR_OTHER_PARENT;
+  }
   /* Index continuity: ParticipantEventsCache.Set rejects skipped/passed
-   * indexes (caches.go / common/rolling_index.go:58-96) */
-  if (index != clen) return HGO_ERR_SELF_PARENT;
+   * indexes (caches.go / common/rolling_index.go:58-96); chains start at the
+   * Root's SelfParent.Index + 1 */
+  if (index != h->r_sp_index[creator] + 1 + clen) return HGO_ERR_SELF_PARENT;
 
   int32_t x = (int32_t)h->N++;
   h->creator[x] = creator; h->index[x] = index; h->sp[x] = sp; h->op[x] = op;
+  h->ext[x] = ext;
   h->ntx[x] = ntx;
   memcpy(h->hash + (size_t)x * 32, hash32, 32);
   memcpy(h->sigr + (size_t)x * 32, sig_r32, 32);
@@ -384,6 +472,7 @@ int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
   int32_t n = h->n;
   int32_t *la = LA(h, x), *fd = FD(h, x);
   for (int32_t i = 0; i < n; i++) fd[i] = FD_NONE;
+  /* parents the Store does not hold (Roots, Root.Others) contribute nothing */
   if (sp < 0 && op < 0) {
     for (int32_t i = 0; i < n; i++) la[i] = -1;
   } else if (sp < 0) {
@@ -401,9 +490,10 @@ int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
   /* updateAncestorFirstDescendant (hashgraph.go:510-544): walk each last
    * ancestor's self-parent chain while its firstDescendant is unset */
   for (int32_t i = 0; i < n; i++) {
+    const int32_t base = h->r_sp_index[i] + 1; /* Index of chain i's first event */
     int32_t k = la[i];
-    while (k >= 0) {
-      int32_t a = h->chain[i][k];
+    while (k >= base) {
+      int32_t a = h->chain[i][k - base];
       int32_t *fa = FD(h, a);
       if (fa[creator] != FD_NONE) break;
       fa[creator] = index;
@@ -424,6 +514,65 @@ int64_t hgo_insert_batch(hgo *h, int64_t count, const int32_t *creator, const in
     bad += hgo_insert(h, creator[e], index[e], sp[e], op[e], hash32 + (size_t)e * 32,
                       sig_r32 + (size_t)e * 32, ntx[e]) != HGO_OK;
   return bad;
+}
+
+int64_t hgo_insert_batch_ext(hgo *h, int64_t count, const int32_t *creator, const int32_t *index,
+                             const int32_t *sp, const int32_t *op, const int32_t *op_creator,
+                             const int32_t *op_index, const uint8_t *hash32, const uint8_t *sig_r32,
+                             const int32_t *ntx, int32_t *status) {
+  int64_t bad = 0;
+  for (int64_t e = 0; e < count; e++) {
+    const int rc = hgo_insert_ext(h, creator[e], index[e], sp[e], op[e], op_creator[e], op_index[e],
+                                  hash32 + (size_t)e * 32, sig_r32 + (size_t)e * 32, ntx[e]);
+    if (status) status[e] = rc;
+    bad += rc != HGO_OK;
+  }
+  return bad;
+}
+
+/* Hashgraph.Reset(block, frame) (hashgraph.go:1324-1369) minus the frame's
+ * events (the caller inserts them next, as Reset does): Store.Reset(roots)
+ * (inmem_store.go:272-282), SetBlock(block) (LastBlockIndex = its Index),
+ * setLastConsensusRound(block.RoundReceived()).  Fresh hashgraphs only. */
+int hgo_reset(hgo *h, int32_t round_received, int64_t block_index, const int32_t *next_round,
+              const int32_t *sp_index, const int32_t *sp_lt, const int32_t *sp_round, int32_t n_others,
+              const int32_t *oth_root, const uint8_t *oth_key32, const int32_t *oth_creator,
+              const int32_t *oth_index, const int32_t *oth_lt, const int32_t *oth_round,
+              const uint8_t *oth_hash32) {
+  if (h->N || h->is_reset || n_others < 0) return HGO_ERR_STATE;
+  for (int32_t i = 0; i < h->n; i++) {
+    h->r_next[i] = next_round[i];
+    h->r_sp_index[i] = sp_index[i];
+    h->r_sp_lt[i] = sp_lt[i];
+    h->r_sp_round[i] = sp_round[i];
+  }
+  const size_t K = (size_t)n_others;
+  h->n_oth = n_others;
+  h->oth_root = (int32_t *)xcalloc(K, 4);
+  h->oth_creator = (int32_t *)xcalloc(K, 4);
+  h->oth_index = (int32_t *)xcalloc(K, 4);
+  h->oth_lt = (int32_t *)xcalloc(K, 4);
+  h->oth_round = (int32_t *)xcalloc(K, 4);
+  h->oth_key = (uint8_t *)xcalloc(K, 32);
+  h->oth_hash = (uint8_t *)xcalloc(K, 32);
+  if (K) {
+    memcpy(h->oth_root, oth_root, K * 4);
+    memcpy(h->oth_creator, oth_creator, K * 4);
+    memcpy(h->oth_index, oth_index, K * 4);
+    memcpy(h->oth_lt, oth_lt, K * 4);
+    memcpy(h->oth_round, oth_round, K * 4);
+    memcpy(h->oth_key, oth_key32, K * 32);
+    memcpy(h->oth_hash, oth_hash32, K * 32);
+  }
+  h->is_reset = 1;
+  h->blk_index0 = block_index + 1;
+  h->has_lcr = 1;
+  h->lcr = round_received;
+  return HGO_OK;
+}
+
+void hgo_known(const hgo *h, int32_t *known) { /* InmemStore.KnownEvents (inmem_store.go:152-163) */
+  for (int32_t i = 0; i < h->n; i++) known[i] = h->r_sp_index[i] + h->chain_len[i];
 }
 
 /* ------------------------------------------------------------------------ */
@@ -861,7 +1010,9 @@ int hgo_process_decided_rounds(hgo *h) {
     if (h->has_lcr && pr->index == h->lcr) continue;
     int64_t f, l;
     if (get_frame(h, pr->index, &f, &l) != HGO_OK) return HGO_ERR_STATE;
-    frame_roots(h, pr->index, f, l); /* before the frame's events become consensus events */
+    /* roots before the frame's events become consensus events (not restated
+     * for a Reset hashgraph, whose roots would start from the Reset roots) */
+    if (!h->is_reset) frame_roots(h, pr->index, f, l);
     if (l > 0) {
       int64_t first = h->ncons, txs = 0;
       for (int64_t k = 0; k < l; k++) {

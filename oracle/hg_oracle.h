@@ -16,8 +16,10 @@
  * src/hashgraph/hashgraph_test.go transcribed as tests/golden/kat_*.json and
  * checked by tests/test_oracle_kat.py.
  *
- * Scope: fresh hashgraphs (base roots, hashgraph/root.go:75-106); Reset
- * roots (root.Others) are a later row.
+ * Roots: base roots (hashgraph/root.go:75-106) for a fresh hashgraph, or a
+ * Frame's roots installed by hgo_reset (Hashgraph.Reset, hashgraph.go:
+ * 1324-1369; the Root cases A-F of docs/fastsync.rst:140-175).  Frames and
+ * FrameHashes are restated for fresh hashgraphs only.
  */
 #ifndef HG_ORACLE_H
 #define HG_ORACLE_H
@@ -51,6 +53,31 @@ void hgo_destroy(hgo *h);
  * Returns HGO_OK (the event gets the next global id) or an error (rejected). */
 int hgo_insert(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op,
                const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx);
+
+/* the same with an other-parent the Store may not hold: op == -2 names it by
+ * (op_creator slot, op_index), resolved through the creator's Root.Others as
+ * ReadWireInfo + checkOtherParent do (hashgraph.go:1431-1457, 417-436) */
+int hgo_insert_ext(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t op, int32_t op_creator,
+                   int32_t op_index, const uint8_t *hash32, const uint8_t *sig_r32, int32_t ntx);
+int64_t hgo_insert_batch_ext(hgo *h, int64_t count, const int32_t *creator, const int32_t *index,
+                             const int32_t *sp, const int32_t *op, const int32_t *op_creator,
+                             const int32_t *op_index, const uint8_t *hash32, const uint8_t *sig_r32,
+                             const int32_t *ntx, int32_t *status);
+
+/* Hashgraph.Reset(block, frame) before the frame's events are inserted
+ * (fresh hashgraph only): per participant slot the Root's NextRound and
+ * SelfParent Index / LamportTimestamp / Round; the Others entries (owning
+ * root slot, key event hash, value RootEvent creator slot / Index /
+ * LamportTimestamp / Round / Hash); LastConsensusRound = round_received,
+ * LastBlockIndex = block_index. */
+int hgo_reset(hgo *h, int32_t round_received, int64_t block_index, const int32_t *next_round,
+              const int32_t *sp_index, const int32_t *sp_lt, const int32_t *sp_round, int32_t n_others,
+              const int32_t *oth_root, const uint8_t *oth_key32, const int32_t *oth_creator,
+              const int32_t *oth_index, const int32_t *oth_lt, const int32_t *oth_round,
+              const uint8_t *oth_hash32);
+/* Store.KnownEvents: last Index per participant slot (the Root's
+ * SelfParent.Index when it has no event) */
+void hgo_known(const hgo *h, int32_t *known);
 
 /* hgo_insert over arrays (test/bench harness convenience); returns the
  * number of rejected events */

@@ -29,6 +29,10 @@ def lib():
         L.hgo_insert.argtypes = [P, I32, I32, I32, I32, VP, VP, I32]
         L.hgo_insert_batch.restype = I64
         L.hgo_insert_batch.argtypes = [P, I64, VP, VP, VP, VP, VP, VP, VP]
+        L.hgo_insert_batch_ext.restype = I64
+        L.hgo_insert_batch_ext.argtypes = [P, I64, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]
+        L.hgo_reset.argtypes = [P, I32, I64, VP, VP, VP, VP, I32, VP, VP, VP, VP, VP, VP, VP]
+        L.hgo_known.argtypes = [P, VP]
         for f in ("hgo_divide_rounds", "hgo_decide_fame", "hgo_decide_round_received",
                   "hgo_process_decided_rounds", "hgo_run_consensus"):
             getattr(L, f).argtypes = [P]
@@ -100,6 +104,35 @@ class Oracle:
                                       _p(hashes), _p(sig_r), _p(a[4]))
         if bad:
             raise RuntimeError(f"oracle rejected {bad} events")
+
+    def reset(self, rs):
+        """Hashgraph.Reset's Store.Reset + SetBlock + LastConsensusRound
+        (the frame's events are inserted next); rs: a ResetInputs"""
+        a = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in rs.root_arrays().items()}
+        kh = np.ascontiguousarray(rs.oth_key, dtype=np.uint8).reshape(-1, 32)
+        vh = np.ascontiguousarray(rs.oth_hash, dtype=np.uint8).reshape(-1, 32)
+        rc = self.L.hgo_reset(self.h, rs.round_received, rs.block_index, _p(a["next_round"]),
+                              _p(a["sp_index"]), _p(a["sp_lt"]), _p(a["sp_round"]), len(a["oth_root"]),
+                              _p(a["oth_root"]), _p(kh), _p(a["oth_creator"]), _p(a["oth_index"]),
+                              _p(a["oth_lt"]), _p(a["oth_round"]), _p(vh))
+        if rc:
+            raise RuntimeError(f"hgo_reset: {rc}")
+
+    def insert_ext(self, creator, index, sp, op, op_creator, op_index, hashes, sig_r, ntx):
+        """insert with other-parents possibly known only through Root.Others
+        (op == -2, named by (op_creator, op_index)); returns per-event status"""
+        a = [np.ascontiguousarray(x, dtype=np.int32) for x in (creator, index, sp, op, op_creator, op_index, ntx)]
+        hashes = np.ascontiguousarray(hashes, dtype=np.uint8).reshape(-1, 32)
+        sig_r = np.ascontiguousarray(sig_r, dtype=np.uint8).reshape(-1, 32)
+        st = np.zeros(len(a[0]), np.int32)
+        self.L.hgo_insert_batch_ext(self.h, len(a[0]), _p(a[0]), _p(a[1]), _p(a[2]), _p(a[3]), _p(a[4]),
+                                    _p(a[5]), _p(hashes), _p(sig_r), _p(a[6]), _p(st))
+        return st
+
+    def known(self):
+        k = np.empty(self.n, np.int32)
+        self.L.hgo_known(self.h, _p(k))
+        return k
 
     def divide_rounds(self):
         return self.L.hgo_divide_rounds(self.h)

@@ -1,0 +1,130 @@
+"""Pins the oracle's Reset / FastSync roots to the
+reference's own Reset tests:
+
+- TestResetFromFrame (hashgraph_test.go:1711-1907): reset from block 1 of
+  initConsensusHashgraph; the frame's events keep their Round and
+  LamportTimestamp, round 1 has the same witnesses, LastBlockIndex and
+  LastConsensusRound come from the block, and after inserting the events of
+  rounds 2-4 rounds 1-4 have the same witnesses;
+- TestFunkyHashgraphReset / TestSparseHashgraphReset (:2344-2417,
+  :2656-2738): reset from blocks 0-2, insert the diff, run consensus, rounds
+  bi..5 have the same witnesses (compareRoundWitnesses, :2740-2774).
+
+Plus, on generated gossip DAGs, the Lamport timestamps the roots carry and
+Go's rejection of diff events whose other-parent predates the frame."""
+import numpy as np
+import pytest
+
+from babble_amd.dag import Dag
+from kat import KatDag
+from oracle_py import Oracle
+from reset import DagArrays, ResetInputs, oracle_insert
+
+
+def _run(d):
+    o = Oracle(d.n, d.participant_ids, capacity=len(d.creator) + 64)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    o.run_consensus()
+    return o
+
+
+def _witnesses(o, r):
+    res = o.results()
+    return set(np.nonzero((res["round"] == r) & (res["witness"] == 1))[0].tolist())
+
+
+def _reset(o, d, block, extra=None):
+    rs = ResetInputs(o, d, block)
+    o2 = Oracle(d.n, d.participant_ids, capacity=len(d.creator) + 64)
+    o2.reset(rs)
+    st = oracle_insert(o2, rs, rs.frame)
+    assert not st.any(), st
+    return rs, o2
+
+
+def _mapped_witnesses(rs, o2, r):
+    inv = {v: k for k, v in rs.new_id.items()}
+    return {inv[x] for x in _witnesses(o2, r)}
+
+
+def test_reset_from_frame_kat():
+    d = KatDag("kat_consensus")
+    o = _run(d)
+    rs, o2 = _reset(o, d, 1)
+    # Known: the frame's last Index per creator (expectedKnown {0: 5, 1: 4, 2: 4}
+    # -- participants sorted by ID, as the KAT slots are)
+    assert o2.known().tolist() == [5, 4, 4]
+    o2.divide_rounds()
+    assert _mapped_witnesses(rs, o2, 1) == _witnesses(o, 1)
+    res, res2 = o.results(), o2.results()
+    for e in rs.frame:
+        assert res2["round"][rs.new_id[e]] == res["round"][e], d.names[e]
+        assert res2["lamport"][rs.new_id[e]] == res["lamport"][e], d.names[e]
+    o2.decide_fame()
+    o2.decide_round_received()
+    o2.process_decided_rounds()
+    assert o2.last_consensus_round() == rs.round_received
+    assert o2.L.hgo_num_blocks(o2.h) == 0  # LastBlockIndex stays the reset block's
+    # continue: the events of rounds 2..4, topologically
+    later = [e for e in range(len(d)) if 2 <= res["round"][e] <= 4 and e not in rs.new_id]
+    st = oracle_insert(o2, rs, later)
+    assert not st.any(), st
+    o2.run_consensus()
+    for r in range(1, 5):
+        assert _mapped_witnesses(rs, o2, r) == _witnesses(o, r), r
+
+
+@pytest.mark.parametrize("name", ["kat_funky_full", "kat_sparse"])
+@pytest.mark.parametrize("block", [0, 1, 2])
+def test_reset_kat_diff(name, block):
+    d = KatDag(name)
+    o = _run(d)
+    rs, o2 = _reset(o, d, block)
+    st = oracle_insert(o2, rs, rs.diff)
+    assert not st.any(), st
+    o2.run_consensus()
+    for r in range(block, 6):
+        assert _mapped_witnesses(rs, o2, r) == _witnesses(o, r), (r, block)
+
+
+def reset_generated(n, N, seed, lag, block):
+    """a gossip DAG, its consensus, and a reset from `block` with the whole
+    diff inserted and consensus run (oracle only)"""
+    g = Dag(n, N, seed, lagging=lag)
+    d = DagArrays(g)
+    o = Oracle(n, d.participant_ids, capacity=N + 64)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    o.run_consensus()
+    rs, o2 = _reset(o, d, block)
+    st = oracle_insert(o2, rs, rs.diff)
+    o2.run_consensus()
+    return d, o, rs, o2, st
+
+
+def lamport_preserved(o, rs, o2, st):
+    """The Root SelfParents and Root.Others carry the exact Lamport timestamps
+    of the events the reset hashgraph lacks, so every event it accepted has
+    the original's LamportTimestamp (_lamportTimestamp, hashgraph.go:325-379).
+    Rounds carry no such guarantee: witnesses received before the frame are
+    missing from the reset hashgraph's low rounds (they are not re-inserted),
+    so rounds and fame can differ from the original's there -- Go's result,
+    which the GPU parity tests compare the engine against."""
+    res, res2 = o.results(), o2.results()
+    old = np.array(sorted(rs.new_id, key=rs.new_id.get))
+    assert len(old) == o2.num_events()
+    assert np.array_equal(res2["lamport"], res["lamport"][old])
+
+
+@pytest.mark.parametrize("n,N,seed,lag,block", [(4, 3000, 0xBA0, 0, 3), (7, 4000, 0xBA1, 0, 5),
+                                                 (16, 8000, 0xBA2, 0, 4), (16, 8000, 0xBA3, 5, 2)])
+def test_reset_generated(n, N, seed, lag, block):
+    d, o, rs, o2, st = reset_generated(n, N, seed, lag, block)
+    if lag == 0:
+        assert (st == 0).all()
+        assert o2.blocks()["round_received"].size > 0
+    else:
+        # lagging peers: diff events whose other-parent is a pre-frame event
+        # outside Root.Others are rejected (checkOtherParent), and so are
+        # their descendants, as in Go
+        assert (st != 0).any()
+    lamport_preserved(o, rs, o2, st)
