@@ -21,7 +21,7 @@ ERRORS = {
 SYMBOLS = (
     "bh_create", "bh_destroy", "bh_last_error", "bh_insert_events", "bh_divide_rounds",
     "bh_decide_fame", "bh_decide_round_received", "bh_process_decided_rounds",
-    "bh_run_consensus", "bh_synchronize", "bh_reset_consensus", "bh_get_stats", "bh_get_event_meta",
+    "bh_run_consensus", "bh_synchronize", "bh_reset_consensus", "bh_reset", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_round_info", "bh_get_coordinates", "bh_query_events", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
     "bh_hash_bodies", "bh_verify_signatures", "bh_set_event_bytes", "bh_get_frame_roots",
@@ -41,6 +41,15 @@ class Events(C.Structure):
                 ("self_parent_index", C.c_void_p), ("other_parent_creator_id", C.c_void_p),
                 ("other_parent_index", C.c_void_p), ("hash", C.c_void_p), ("sig_r", C.c_void_p),
                 ("n_transactions", C.c_void_p)]
+
+
+class Roots(C.Structure):
+    _fields_ = [("round_received", C.c_int32), ("block_index", C.c_int64),
+                ("next_round", C.c_void_p), ("self_parent_index", C.c_void_p),
+                ("self_parent_lamport", C.c_void_p), ("self_parent_round", C.c_void_p),
+                ("n_others", C.c_int32), ("other_root", C.c_void_p), ("other_key", C.c_void_p),
+                ("other_creator_id", C.c_void_p), ("other_index", C.c_void_p),
+                ("other_lamport", C.c_void_p), ("other_round", C.c_void_p), ("other_hash", C.c_void_p)]
 
 
 class Stats(C.Structure):
@@ -80,6 +89,7 @@ def load():
         getattr(L, f).argtypes = [P]
         getattr(L, f).restype = C.c_int
     L.bh_get_stats.argtypes = [P, C.POINTER(Stats)]
+    L.bh_reset.argtypes = [P, C.POINTER(Roots)]
     L.bh_get_event_meta.argtypes = [P, I64, I64, VP, VP, VP, VP, VP, VP]
     L.bh_get_consensus_order.argtypes = [P, I64, I64, VP]
     L.bh_get_blocks.argtypes = [P, I64, I64, VP, VP, VP, VP]

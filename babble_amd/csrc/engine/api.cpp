@@ -41,7 +41,8 @@ void free_all(bh_handle *h) {
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
                   d.wfame, d.frame_loaded, d.Bp, d.fd, d.fd16, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
-                  d.la_col != d.fdt ? d.la_col : nullptr};  // la_ev aliases fdt
+                  d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
+                  d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -82,6 +83,10 @@ int upload(bh_handle *h) {
   HIPCHK(h, hipMemcpyAsync(d.sigw + a * 8, h->h_sigw.data() + a * 8, k * 32, hipMemcpyHostToDevice, s));
   if (h->frames_on)  // h_hash holds the events [a, b)
     HIPCHK(h, hipMemcpyAsync(h->fr.hash + a * 32, h->h_hash.data(), k * 32, hipMemcpyHostToDevice, s));
+  if (h->reset_on) {
+    HIPCHK(h, hipMemcpyAsync(d.rflag + a, h->h_rflag.data() + a, k, hipMemcpyHostToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(d.ext_lt + a, h->h_ext_lt.data() + a, k * 4, hipMemcpyHostToDevice, s));
+  }
   HIPCHK(h, hipStreamSynchronize(s));
   h->h_hash.clear();
   h->uploaded = b;
@@ -310,6 +315,59 @@ std::vector<size_t> range_bytes(const bh_handle *h, int64_t items, size_t esz, b
 // ---------------------------------------------------------------------------
 // stage 1: coordinates, Lamport timestamps, rounds, witnesses
 
+// A Reset hashgraph's coordinates (kernels_reset.hip): the events [0, E0)
+// -- every event whose other-parent only Root.Others knows lies in it --
+// one at a time, then the chain dataflow resumes every chain after them as
+// a segment does (Root LamportTimestamps seed the chains, lt_seed); each
+// part is transposed and walked for firstDescendants like a segment
+int reset_coords(bh_handle *h, hipStream_t s) {
+  Dev &d = h->d;
+  const int n = d.n;
+  if (!(bh::flow32_eligible(d) && use_flow(d)) && !bh::floww_eligible(d))
+    return h->fail(BH_ERR_STATE, "Reset hashgraphs need the chain dataflow (n <= 512, chains within its limits)");
+  const int64_t N = d.N, E0 = std::min<int64_t>(h->E0, N);
+  int32_t *stg = h->seg_stage;  // [lo, len] of part A, then of part B
+  for (int c = 0; c < n; ++c) {
+    const auto &ch = h->chain[(size_t)c];
+    const int32_t a = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)E0) - ch.begin());
+    stg[c] = 0;
+    stg[n + c] = a;
+    stg[2 * n + c] = a;
+    stg[3 * n + c] = (int32_t)ch.size();
+  }
+  HIPCHK(h, hipMemcpyAsync(h->segbuf, stg, (size_t)4 * n * 4, hipMemcpyHostToDevice, s));
+  Dev va = d, vb = d;
+  va.seg_lo = h->segbuf;
+  va.chain_len = h->segbuf + n;
+  va.N = E0;
+  va.e0 = 0;
+  va.tile_list = nullptr;
+  vb.seg_lo = h->segbuf + 2 * n;
+  vb.chain_len = h->segbuf + 3 * n;
+  vb.e0 = E0;
+  vb.tile_list = nullptr;
+  if (E0 > 0) {
+    bh::launch_reset_coords(va, s);
+    bh::launch_flow_transpose(va, s);
+    bh::launch_fd_idle(va, s);
+  }
+  HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
+  if (N > E0) {
+    if (bh::flow32_eligible(d) && use_flow(d)) {
+      bh::launch_flow_desc(vb, s);
+      bh::launch_flow(vb, s);
+      h->sweep_kernel = "k_flow32";
+    } else {
+      bh::launch_floww(vb, s);
+      h->sweep_kernel = "k_floww";
+    }
+    bh::launch_flow_transpose(vb, s);
+    bh::launch_fd_idle(vb, s);
+  }
+  HIPCHK(h, hipGetLastError());
+  return BH_OK;
+}
+
 // coordinates up to the dataflow kernel (this shard's LA columns when split)
 int rounds_coords(bh_handle *h) {
   int rc;
@@ -326,7 +384,10 @@ int rounds_coords(bh_handle *h) {
   hipStream_t s = h->stream;
   HIPCHK(h, hipEventRecord(h->ev[0], s));
   bh::launch_prep(d, s);
-  if (use_flow(d)) {
+  if (h->reset_on) {
+    int rc2 = reset_coords(h, s);
+    if (rc2) return rc2;
+  } else if (use_flow(d)) {
     bh::launch_flow_desc(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
     bh::launch_flow(d, s);
@@ -362,6 +423,8 @@ int rounds_loop(bh_handle *h) {
     int32_t ovf = 0;
     HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
+    if (ovf && h->reset_on)
+      return h->fail(BH_ERR_CAPACITY, "the wide dataflow gave up on a Reset hashgraph (no sweep fallback with roots)");
     if (ovf == 2) {
       HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
       bh::launch_chunk_depth(d, s);
@@ -373,7 +436,7 @@ int rounds_loop(bh_handle *h) {
   }
   // LA rows and the firstDescendants walk (FDT) from the dataflow's
   // column-major LA; n > 128 then transposes FDT into chain-major FD rows
-  if (walked || wide_flow) bh::launch_flow_transpose(d, s);
+  if ((walked || wide_flow) && !h->reset_on) bh::launch_flow_transpose(d, s);  // (reset_coords transposed already)
   bh::launch_first_descendants(d, s, walked || wide_flow);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
@@ -386,8 +449,19 @@ int rounds_loop(bh_handle *h) {
     h->stage = 1;
     return BH_OK;
   }
-  bh::launch_round_init(d, s);
   int32_t st[bh::ST_COUNT];
+  if (h->reset_on) {
+    // rounds below r0 event by event, then the loop from B[r0]
+    HIPCHK(h, hipMemsetAsync(d.rexists, 0, (size_t)d.R_cap + 1, s));
+    HIPCHK(h, hipMemsetAsync(d.fw, 0xFF, (size_t)(d.r0 - d.rlo) * d.n * 4, s));
+    HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FIATMAX, 0xFF, 4, s));
+    bh::launch_fiat(d, s);
+    bh::launch_round_resume(d, s);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(&h->fiat_max, d.state + bh::ST_FIATMAX, 4, hipMemcpyDeviceToHost, s));
+  } else {
+    bh::launch_round_init(d, s);
+  }
   if ((rc = run_round_loop(h, d, &h->graph, &h->graph_dev, st))) return rc;
   return rounds_tail(h, st, 0);
 }
@@ -400,6 +474,10 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
   hipStream_t s = h->stream;
   h->R = st[bh::ST_ROUNDS];
   h->iters = st[bh::ST_ITERS];
+  // a Reset hashgraph with no event at round r0 yet: the last round is the fiat pass's
+  if (h->reset_on && h->R <= d.r0) h->R = h->fiat_max + 1;
+  if (h->reset_on && st[bh::ST_FLOWOVF])  // the fallbacks know no Root LamportTimestamps
+    return h->fail(BH_ERR_CAPACITY, "Lamport timestamps beyond the dataflow kernel's range after Reset");
   if (st[bh::ST_FLOWOVF]) {  // LT reached the one-dword limit; LT only feeds the frame order
     if (bh::floww_eligible(d)) {  // the chunked sweep recomputes LA (same values) and LT
       bh::launch_chunk_depth(d, s);
@@ -431,7 +509,7 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
 // path (k_flow32, n <= 128) only.
 bool segments_eligible(const bh_handle *h) {
   const Dev &d = h->d;
-  return h->group.empty() && h->world == 1 && use_flow(d) && bh::flow32_eligible(d) && d.fd_cols;
+  return h->group.empty() && h->world == 1 && use_flow(d) && bh::flow32_eligible(d) && d.fd_cols && !h->reset_on;
 }
 
 // segments for `events` new events: measured at C3 (10M events): 4
@@ -622,14 +700,15 @@ int stage_rounds(bh_handle *h) {
 int fame_local(bh_handle *h) {
   if (h->stage < 1) return h->fail(BH_ERR_STATE, "DecideFame before DivideRounds");
   int64_t r0, r1;
-  shard_range(h->R - h->P, h->world, h->rank, &r0, &r1);
-  bh::launch_fame(h->d, h->R, (int32_t)(h->P + r0), (int32_t)(h->P + r1), h->stream);
+  shard_range(std::max(0, h->R - h->P), h->world, h->rank, &r0, &r1);
+  if (r1 > r0) bh::launch_fame(h->d, h->R, (int32_t)(h->P + r0), (int32_t)(h->P + r1), h->stream);
   HIPCHK(h, hipGetLastError());
   return BH_OK;
 }
 
 int fame_finish(bh_handle *h) {
-  bh::launch_fame_scatter_range(h->d, h->wofs_h[(size_t)h->P], h->wofs_h[(size_t)h->R], h->stream);
+  if (h->R > h->P)  // (a Reset hashgraph starts with P = LastConsensusRound, possibly above R)
+    bh::launch_fame_scatter_range(h->d, h->wofs_h[(size_t)h->P], h->wofs_h[(size_t)h->R], h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
   h->decided_h.assign((size_t)h->R, 0);
@@ -674,9 +753,20 @@ int stage_fame(bh_handle *h) {
 // ---------------------------------------------------------------------------
 // stage 3: DecideRoundReceived (every shard, every event)
 
+// Hashgraph.LastConsensusRound (-1 = nil): the last processed round, or the
+// Reset block's round until a later one is processed
+int32_t last_consensus_round(const bh_handle *h) {
+  return h->reset_on ? std::max(h->P - 1, h->reset_lcr) : h->P - 1;
+}
+
+// PendingRounds: after a Reset, the entry of LastConsensusRound stays at the
+// head of the queue once processed -- ProcessDecidedRounds skips it without
+// counting it (hashgraph.go:1063-1065, 1043-1047) -- then rounds [P, R)
+int32_t stale_head(const bh_handle *h) { return h->reset_on && h->P > h->reset_lcr ? 1 : 0; }
+
 int stage_rr_local(bh_handle *h) {
   if (h->stage < 2) return h->fail(BH_ERR_STATE, "DecideRoundReceived before DecideFame");
-  bh::launch_round_received(h->d, h->R, h->P, h->stream);
+  bh::launch_round_received(h->d, h->R, h->P, last_consensus_round(h), h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[4], h->stream));
   int64_t und = 0;
@@ -1067,11 +1157,15 @@ static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_
   for (int64_t i = 0; i < ev->count; ++i) {
     int code = BH_OK;
     int32_t c = h->slot_find(ev->creator_id[i]), op = -1;
+    int32_t oth = -1;    // the Root.Others entry keyed by this event that names its other-parent
+    bool ext = false;    // ... and the Store does not hold that other-parent
     if (c < 0) {
       code = BH_ERR_UNKNOWN_PARTICIPANT;
     } else {
       const auto &ch = h->chain[c];
-      const int32_t last = (int32_t)ch.size() - 1;  // base Root index is -1
+      // chains start after their Root's SelfParent (Index -1 for a base Root)
+      const int32_t base = h->reset_on ? h->base_h[(size_t)c] : 0;
+      const int32_t last = base + (int32_t)ch.size() - 1;
       // checkSelfParent (hashgraph.go:398-414): self-parent must be the
       // creator's last known event (its Root when it has none)
       if (ev->self_parent_index[i] != last) code = BH_ERR_SELF_PARENT;
@@ -1083,9 +1177,35 @@ static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_
         if (oslot < 0) code = BH_ERR_OTHER_PARENT;
         else {
           const auto &oc = h->chain[oslot];
-          const int32_t k = ev->other_parent_index[i];
-          if (k < 0 || k >= (int32_t)oc.size()) code = BH_ERR_OTHER_PARENT;
-          else op = oc[k];
+          const int32_t k = ev->other_parent_index[i] - (h->reset_on ? h->base_h[(size_t)oslot] : 0);
+          if (k >= 0 && k < (int32_t)oc.size()) op = oc[k];
+          if (h->reset_on) {
+            // Root.Others[ev.Hex()] (hashgraph.go:229-256, 358-375, 424-431)
+            std::string key((const char *)&c, 4);
+            key.append((const char *)ev->hash + i * 32, 32);
+            const auto it = h->oth_by_key.find(key);
+            const int32_t e2 = it == h->oth_by_key.end() ? -1 : it->second;
+            if (op >= 0) {  // held by the Store; Others may still name the same event
+              if (e2 >= 0 && !memcmp(h->others[(size_t)e2].hash, h->h_hashes.data() + (size_t)op * 32, 32)) oth = e2;
+            } else {
+              // ReadWireInfo: the creator's Root.Others entry with this
+              // (CreatorID, Index) (:1435-1456), then checkOtherParent: the
+              // entry keyed by the event's own hash must name the same hash
+              int32_t e1 = -1;
+              for (size_t q = 0; q < h->others.size() && e1 < 0; ++q) {
+                const auto &o = h->others[q];
+                if (o.root == c && o.creator == oslot && o.index == ev->other_parent_index[i]) e1 = (int32_t)q;
+              }
+              if (e1 >= 0 && e2 >= 0 && !memcmp(h->others[(size_t)e1].hash, h->others[(size_t)e2].hash, 32)) {
+                oth = e2;
+                ext = true;
+              } else {
+                code = BH_ERR_OTHER_PARENT;
+              }
+            }
+          } else if (op < 0) {
+            code = BH_ERR_OTHER_PARENT;
+          }
         }
       }
       if (code == BH_OK && (int64_t)h->h_creator.size() >= h->cap) code = BH_ERR_CAPACITY;
@@ -1106,7 +1226,13 @@ static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_
     const int32_t id = (int32_t)h->h_creator.size();
     auto &ch = h->chain[c];
     h->h_creator.push_back(c);
-    h->h_index.push_back(ev->index[i]);
+    h->h_index.push_back((int32_t)ch.size());  // chain position (Index - the chain's base)
+    if (h->reset_on) {
+      h->h_hashes.insert(h->h_hashes.end(), ev->hash + i * 32, ev->hash + i * 32 + 32);
+      h->h_rflag.push_back((int8_t)((oth >= 0 ? 1 : 0) | (ext ? 2 : 0)));
+      h->h_ext_lt.push_back(ext ? h->others[(size_t)oth].lt : bh::UNSET);
+      if (ext) h->E0 = id + 1;
+    }
     h->h_sp.push_back(ch.empty() ? -1 : ch.back());
     h->h_op.push_back(op);
     h->h_ntx.push_back(ev->n_transactions[i]);
@@ -1177,7 +1303,8 @@ int bh_reset_consensus(bh_handle *h) {
     x->stage = 0;
     x->coords_for = -1;
     x->n_div = x->n_rr = 0;
-    x->R = x->P = x->R_rr = 0;
+    x->R = x->R_rr = 0;
+    x->P = x->reset_on ? x->reset_lcr : 0;
     x->pend_dec.clear();
     x->decided_h.clear();
     x->nundet = 0;
@@ -1188,6 +1315,115 @@ int bh_reset_consensus(bh_handle *h) {
     if (x->frames_on) frames_reset(x);
   }
   HIPCHK(h, hipSetDevice(h->device));
+  return BH_OK;
+}
+
+// the per-round tables for R_cap rounds (a Reset hashgraph starts at the
+// frame's round, so its tables must reach past it); contents start zeroed
+static int realloc_round_tables(bh_handle *h, int32_t R_cap) {
+  Dev &d = h->d;
+  void **pp[] = {(void **)&d.ssm, (void **)&d.ssw, (void **)&d.B, (void **)&d.wofs, (void **)&d.wcnt,
+                 (void **)&d.blocked, (void **)&d.frame_loaded, (void **)&d.decided, (void **)&d.nfam,
+                 (void **)&d.minla, (void **)&d.frame_cnt, (void **)&d.frame_ofs, (void **)&d.frame_cur,
+                 (void **)&d.blk_of_frame, (void **)&d.frame_ntx, (void **)&d.rexists};
+  const bool had_ssm = d.ssm != nullptr, had_ssw = d.ssw != nullptr;
+  for (void **p : pp)
+    if (*p) {
+      (void)hipFree(*p);
+      *p = nullptr;
+    }
+  d.R_cap = R_cap;
+  const size_t R1 = (size_t)R_cap + 1;
+  const int n = d.n;
+  int rc = BH_OK;
+  auto A = [&](auto **p, size_t cnt, size_t esz) {
+    if (rc == BH_OK) rc = dalloc(h, p, cnt);
+    if (rc == BH_OK && hipMemset(*p, 0, std::max<size_t>(cnt, 1) * esz) != hipSuccess) rc = BH_ERR_DEVICE;
+  };
+  if (had_ssm) A(&d.ssm, R1 * n * 16, 8);
+  if (had_ssw) A(&d.ssw, R1 * n * 8, 8);
+  A(&d.B, R1 * n, 4); A(&d.wofs, R1, 4); A(&d.wcnt, R1, 4); A(&d.blocked, R1, 4); A(&d.frame_loaded, R1, 4);
+  A(&d.decided, R1, 1); A(&d.nfam, R1, 4); A(&d.minla, R1 * d.npad, 4); A(&d.frame_cnt, R1, 4);
+  A(&d.frame_ofs, R1, 4); A(&d.frame_cur, R1, 4); A(&d.blk_of_frame, R1, 4); A(&d.frame_ntx, R1, 8);
+  A(&d.rexists, R1, 1);
+  return rc == BH_OK ? BH_OK : h->fail(rc, "round tables for %d rounds", R_cap);
+}
+
+int bh_reset(bh_handle *h, const bh_roots *rt) {
+  if (!h || !rt || !rt->next_round || !rt->self_parent_index || !rt->self_parent_lamport || !rt->self_parent_round ||
+      rt->n_others < 0 || (rt->n_others > 0 && (!rt->other_root || !rt->other_key || !rt->other_creator_id ||
+                                                 !rt->other_index || !rt->other_lamport || !rt->other_round ||
+                                                 !rt->other_hash)))
+    return BH_ERR_INVALID;
+  if (!h->h_creator.empty() || h->reset_on || h->stage != 0)
+    return h->fail(BH_ERR_STATE, "bh_reset: a fresh handle only (no events inserted, no pass run)");
+  if (!h->group.empty() || h->world > 1 || h->frames_on)
+    return h->fail(BH_ERR_STATE, "bh_reset: one shard, block projection off");
+  if (rt->round_received < 0 || rt->block_index < -1) return h->fail(BH_ERR_INVALID, "bh_reset: bad block");
+  (void)hipSetDevice(h->device);
+  Dev &d = h->d;
+  const int n = d.n;
+  int32_t F = -1, lo = INT32_MAX;
+  for (int c = 0; c < n; ++c) {
+    if (rt->self_parent_index[c] < -1 || rt->next_round[c] < 0)
+      return h->fail(BH_ERR_INVALID, "bh_reset: root %d: bad SelfParent index / NextRound", c);
+    F = std::max(F, std::max(rt->next_round[c], rt->self_parent_round[c]));
+    lo = std::min(lo, std::min(rt->next_round[c], rt->self_parent_round[c]));
+  }
+  // rounds >= F + 1 follow the closed form; every
+  // pending round must be among them, as GetFrame's roots guarantee
+  if (F >= rt->round_received)
+    return h->fail(BH_ERR_INVALID, "bh_reset: a root's round %d is not below the block's round %d", F,
+                   rt->round_received);
+  h->base_h.resize((size_t)n);
+  h->next_h.assign(rt->next_round, rt->next_round + n);
+  h->sp_round_h.assign(rt->self_parent_round, rt->self_parent_round + n);
+  h->sp_lt_h.assign(rt->self_parent_lamport, rt->self_parent_lamport + n);
+  for (int c = 0; c < n; ++c) h->base_h[(size_t)c] = rt->self_parent_index[c] + 1;
+  h->others.clear();
+  h->oth_by_key.clear();
+  for (int32_t k = 0; k < rt->n_others; ++k) {
+    bh_handle::Other o{};
+    o.root = rt->other_root[k];
+    o.creator = h->slot_find(rt->other_creator_id[k]);
+    if (o.root < 0 || o.root >= n || o.creator < 0)
+      return h->fail(BH_ERR_INVALID, "bh_reset: Others entry %d: bad root / creator", k);
+    o.index = rt->other_index[k];
+    o.lt = rt->other_lamport[k];
+    o.round = rt->other_round[k];
+    memcpy(o.key, rt->other_key + (size_t)k * 32, 32);
+    memcpy(o.hash, rt->other_hash + (size_t)k * 32, 32);
+    std::string key((const char *)&o.root, 4);
+    key.append((const char *)o.key, 32);
+    h->oth_by_key.emplace(key, (int32_t)h->others.size());  // a Go map holds one entry per key
+    h->others.push_back(o);
+  }
+  // the round tables reach past the block's round
+  const int64_t C = std::max<int64_t>(h->cap, 1);
+  const int64_t need = (int64_t)rt->round_received + C / d.sm + 2;
+  if (need > INT32_MAX / 2) return h->fail(BH_ERR_CAPACITY, "bh_reset: round %d too large", rt->round_received);
+  int rc;
+  if ((rc = realloc_round_tables(h, (int32_t)std::max<int64_t>(d.R_cap, need)))) return rc;
+  d.r0 = F + 1;
+  d.rlo = std::max(0, lo);
+  d.frame_lo = rt->round_received + 1;  // round_received's frame is the block itself (hashgraph.go:1063-1065)
+  auto up = [&](int32_t **p, const std::vector<int32_t> &v) -> int {
+    if (dalloc(h, p, (size_t)n)) return BH_ERR_DEVICE;
+    HIPCHK(h, hipMemcpy(*p, v.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    return BH_OK;
+  };
+  if ((rc = up(&d.chain_base, h->base_h)) || (rc = up(&d.lt_seed, h->sp_lt_h)) || (rc = up(&d.root_next, h->next_h)) ||
+      (rc = up(&d.root_sp_round, h->sp_round_h)))
+    return rc;
+  if ((rc = dalloc(h, &d.rflag, (size_t)C)) || (rc = dalloc(h, &d.ext_lt, (size_t)C)) ||
+      (rc = dalloc(h, &d.fw, (size_t)(d.r0 - d.rlo) * n)))
+    return rc;
+  h->reset_on = true;
+  h->reset_lcr = rt->round_received;
+  h->reset_block = rt->block_index;
+  h->reset_F = F;
+  h->P = rt->round_received;  // rounds below LastConsensusRound are never queued (hashgraph.go:809-815)
+  h->inc_valid = false;
   return BH_OK;
 }
 
@@ -1236,14 +1472,14 @@ int bh_get_stats(bh_handle *h, bh_stats *o) {
   memset(o, 0, sizeof *o);
   o->n_events = (int64_t)h->h_creator.size();
   o->last_round = h->R - 1;
-  o->last_consensus_round = h->P - 1;
+  o->last_consensus_round = last_consensus_round(h);
   o->consensus_events = h->ncons;
   o->consensus_transactions = h->cons_txs;
   o->pending_loaded_events = h->loaded_total - h->cons_loaded;
   // received by the last DecideRoundReceived, plus everything inserted since
   o->undetermined_events = h->nundet + (o->n_events - h->n_rr);
-  o->blocks = (int64_t)h->blocks.size();
-  o->pending_rounds = h->R - h->P;
+  o->blocks = (int64_t)h->blocks.size() + (h->reset_on ? h->reset_block + 1 : 0);
+  o->pending_rounds = std::max(0, h->R - h->P) + stale_head(h);
   return BH_OK;
 }
 
@@ -1267,6 +1503,8 @@ int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round
   if (fame) { HIPCHK(h, get(fame, d.fame, 1)); std::fill(fame + k, fame + k + rest, -1); }
   if (round_received) {
     HIPCHK(h, get(round_received, d.rr, 4));
+    for (int64_t i = 0; i < k; ++i)  // left UndeterminedEvents without one (Reset): nil
+      if (round_received[i] == bh::RR_DROP) round_received[i] = INT32_MIN;
     std::fill(round_received + k, round_received + k + rest, INT32_MIN);
   }
   if (consensus_pos) {
@@ -1300,10 +1538,10 @@ int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_rec
 
 int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap) {
   if (!h) return 0;
-  const int32_t cnt = h->R - h->P;
+  const int32_t head = stale_head(h), cnt = std::max(0, h->R - h->P) + head;
   for (int32_t i = 0; i < cnt && i < cap; ++i) {
-    if (index) index[i] = h->P + i;
-    if (decided) decided[i] = h->pend_dec[(size_t)(h->P + i)];
+    if (index) index[i] = h->P - head + i;
+    if (decided) decided[i] = i < head ? 1 : h->pend_dec[(size_t)(h->P - head + i)];
   }
   return cnt;
 }
@@ -1334,13 +1572,22 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
   const int n = d.n;
   memset(info, 0, sizeof *info);
   info->round = r;
-  // round r on chain c = indexes [B[r][c], B[r+1][c]) (B[R][c] = chain length)
-  std::vector<int32_t> b((size_t)2 * n), len((size_t)n);
-  HIPCHK(h, hipMemcpy(b.data(), d.B + (int64_t)r * n, (size_t)2 * n * 4, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpy(len.data(), d.chain_len, (size_t)n * 4, hipMemcpyDeviceToHost));
-  int64_t ne = 0;
-  for (int c = 0; c < n; ++c) ne += std::min(b[(size_t)(n + c)], len[(size_t)c]) - std::min(b[(size_t)c], len[(size_t)c]);
-  info->n_events = (int32_t)ne;
+  if (r < d.r0) {  // below a Reset's closed form: k_fiat's rounds, which may be missing
+    int8_t ex = 0;
+    HIPCHK(h, hipMemcpy(&ex, d.rexists + r, 1, hipMemcpyDeviceToHost));
+    if (!ex) return h->fail(BH_ERR_KEY_NOT_FOUND, "GetRound %d: Not Found", r);
+    std::vector<int32_t> rd((size_t)h->n_div);
+    if (h->n_div) HIPCHK(h, hipMemcpy(rd.data(), d.round, (size_t)h->n_div * 4, hipMemcpyDeviceToHost));
+    info->n_events = (int32_t)std::count(rd.begin(), rd.end(), r);
+  } else {
+    // round r on chain c = indexes [B[r][c], B[r+1][c]) (B[R][c] = chain length)
+    std::vector<int32_t> b((size_t)2 * n), len((size_t)n);
+    HIPCHK(h, hipMemcpy(b.data(), d.B + (int64_t)r * n, (size_t)2 * n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(len.data(), d.chain_len, (size_t)n * 4, hipMemcpyDeviceToHost));
+    int64_t ne = 0;
+    for (int c = 0; c < n; ++c) ne += std::min(b[(size_t)(n + c)], len[(size_t)c]) - std::min(b[(size_t)c], len[(size_t)c]);
+    info->n_events = (int32_t)ne;
+  }
   int32_t wofs = 0, wcnt = 0;
   HIPCHK(h, hipMemcpy(&wofs, d.wofs + r, 4, hipMemcpyDeviceToHost));
   HIPCHK(h, hipMemcpy(&wcnt, d.wcnt + r, 4, hipMemcpyDeviceToHost));
@@ -1358,10 +1605,19 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
   }
   info->n_witnesses = wcnt;
   info->witnesses_decided = all ? 1 : 0;
-  if (r < h->R_rr) HIPCHK(h, hipMemcpy(&info->n_consensus, d.frame_cnt + r, 4, hipMemcpyDeviceToHost));
-  info->queued = 1;  // every round >= LastConsensusRound is queued when it first appears
-  info->pending = r >= h->P ? 1 : 0;
-  info->pending_decided = r >= h->P ? h->pend_dec[(size_t)r] : 0;
+  if (r < h->R_rr && r >= d.frame_lo) {
+    HIPCHK(h, hipMemcpy(&info->n_consensus, d.frame_cnt + r, 4, hipMemcpyDeviceToHost));
+  } else if (r < h->R_rr && h->n_rr) {  // a frame never emitted (Reset): count the events received in r
+    std::vector<int32_t> rr((size_t)h->n_rr);
+    HIPCHK(h, hipMemcpy(rr.data(), d.rr, (size_t)h->n_rr * 4, hipMemcpyDeviceToHost));
+    info->n_consensus = (int32_t)std::count(rr.begin(), rr.end(), r);
+  }
+  // every round >= LastConsensusRound is queued when it first appears; after
+  // a Reset the rounds below the block's are never queued
+  info->queued = !h->reset_on || r >= h->reset_lcr ? 1 : 0;
+  const bool head = stale_head(h) && r == h->P - 1;
+  info->pending = r >= h->P || head ? 1 : 0;
+  info->pending_decided = r >= h->P ? h->pend_dec[(size_t)r] : head ? 1 : 0;
   return BH_OK;
 }
 
@@ -1384,9 +1640,14 @@ static int ensure_coords(bh_handle *h) {
     Dev full = d;  // every LA column, whatever this shard's share of the dataflow
     full.col0 = 0;
     full.ncol = d.n;
-    if (walked) bh::launch_flow_coordinates(full, h->stream);
-    else bh::launch_coordinates(full, h->stream);
-    bh::launch_first_descendants(full, h->stream, walked);
+    if (h->reset_on) {
+      if ((rc = reset_coords(h, h->stream))) return rc;
+      bh::launch_first_descendants(full, h->stream, true);
+    } else {
+      if (walked) bh::launch_flow_coordinates(full, h->stream);
+      else bh::launch_coordinates(full, h->stream);
+      bh::launch_first_descendants(full, h->stream, walked);
+    }
     h->inc_valid = false;  // the loop state no longer matches the layout / prefix
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
@@ -1412,6 +1673,11 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
   } else if (first_descendants) {
     HIPCHK(h, hipMemcpy(first_descendants, d.fd + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
   }
+  if (h->reset_on)  // chain positions -> Index (chains start after their Root's SelfParent)
+    for (int i = 0; i < d.n; ++i) {
+      if (last_ancestors && last_ancestors[i] >= 0) last_ancestors[i] += h->base_h[(size_t)i];
+      if (first_descendants && first_descendants[i] != bh::FD_NONE) first_descendants[i] += h->base_h[(size_t)i];
+    }
   return BH_OK;
 }
 

@@ -42,6 +42,7 @@ enum StateSlot {
   ST_NBLOCKS = 9,
   ST_FLOWOVF = 10,  // k_flow32: a Lamport timestamp reached 2^21 (LT recomputed by k_flow)
   ST_RESUME = 11,   // k_resume_point: the last round whose boundaries B[r][*] a prefix run fixed
+  ST_FIATMAX = 12,  // k_fiat: the highest round of an event below the closed form's first round (-1: none)
   ST_COUNT = 16
 };
 
@@ -139,7 +140,27 @@ struct Dev {
   // diagnostic phase counters (BH_DIAG=1 builds the buffer; null otherwise).
   // Only a separate diagnostic run reads them; no result depends on them.
   unsigned long long *diag;
+  // Reset / FastSync roots (bh_reset; hashgraph.go:1324-1369, root.go,
+  // docs/fastsync.rst:140-175); all null / 0 for a fresh hashgraph.  Event
+  // indexes on the device are chain positions; chain c's first event has
+  // Index chain_base[c] (its Root's SelfParent.Index + 1).
+  int32_t *chain_base;     // [n]
+  int32_t *lt_seed;        // [n] Root.SelfParent.LamportTimestamp
+  int32_t *root_next;      // [n] Root.NextRound
+  int32_t *root_sp_round;  // [n] Root.SelfParent.Round
+  int8_t *rflag;           // [C] bit 0: the other-parent is the one Root.Others[event] names
+  int32_t *ext_lt;         // [C] LamportTimestamp of that Root.Others entry (INT32_MIN: none)
+  // The closed form of the round loop holds from round r0 = F + 1 on, F the
+  // highest NextRound / SelfParent.Round of a root;
+  // k_fiat computes rounds below it event by event.  fw[(r - rlo) * n + c]:
+  // chain c's witness of fiat round r (-1: none); rexists[r]: round r < r0
+  // has an event (RoundInfo exists, inmem_store.go:185-191).
+  int32_t r0, rlo;
+  int32_t *fw;
+  int8_t *rexists;
+  int32_t frame_lo;  // frames below it are never emitted (Reset: LastConsensusRound's, hashgraph.go:1063-1065)
 };
+constexpr int32_t RR_DROP = INT32_MIN + 1;  // left UndeterminedEvents with no round received (hashgraph.go:970-977)
 
 // Block projection (kernels_frames.hip, frames.cpp): the
 // roots GetFrame gives each frame (hashgraph.go:1125-1231, createRoot
@@ -233,6 +254,11 @@ void launch_resume_point(const Dev &d, int32_t R, hipStream_t s);
 // FD entries of a segment's new rows for chains with no event in the segment
 void launch_fd_idle(const Dev &d, hipStream_t s);
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
+// Reset hashgraphs: coordinates of events [0, d.N) one event at a time (the
+// batch whose other-parents only Root.Others knows), and the rounds below r0
+// in insertion order with B[r0] for the loop (kernels_reset.hip)
+void launch_reset_coords(const Dev &d, hipStream_t s);
+void launch_fiat(const Dev &d, hipStream_t s);
 void launch_witness_tables(const Dev &d, int R, hipStream_t s);  // wids/wofs/wcnt/wrow
 // per-event round / witness; events >= n_prev (inserted since the last
 // division) also get their initial fame / rr / consensus position, and are
@@ -247,7 +273,8 @@ void launch_fame_scatter_range(const Dev &d, int32_t w0, int32_t w1, hipStream_t
 // rr of events still undetermined (rr already set is kept); rounds < P are
 // live-decided iff no trapped witness; counters[3] = undetermined after it;
 // frame_cnt[r] = events received in r (every r < R)
-void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s);
+// (lcr: LastConsensusRound, for the rounds a Reset hashgraph lacks)
+void launch_round_received(const Dev &d, int32_t R, int32_t P, int32_t lcr, hipStream_t s);
 // frames / order / blocks of rounds [0, P): ST_P holds P (set by the host).
 // launch_order_buckets: frame offsets and unsorted frame buckets of every
 // frame; launch_order_sort: sort frames [f0, f1), their tx / loaded counts

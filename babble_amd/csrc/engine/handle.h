@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "babble_hip.h"
@@ -131,6 +132,26 @@ struct bh_handle {
   size_t json_cap = 0, bjson_cap = 0;
   hipEvent_t ev_fr[2]{};           // around the last projection
   float frames_ms = 0;
+
+  // Reset / FastSync roots (bh_reset; hashgraph.go:1324-1369).  Chains
+  // start at base_h[c] = Root.SelfParent.Index + 1; Root.Others entries are
+  // found by (root slot, key hash) and by (root slot, creator slot, Index)
+  bool reset_on = false;
+  int32_t reset_lcr = -1;      // block.RoundReceived(): LastConsensusRound after Reset
+  int64_t reset_block = -1;    // block.Index(): LastBlockIndex after Reset
+  int32_t reset_F = -1;        // highest NextRound / SelfParent.Round of a root
+  std::vector<int32_t> base_h, next_h, sp_round_h, sp_lt_h;
+  struct Other {
+    int32_t root, creator, index, lt, round;
+    uint8_t key[32], hash[32];
+  };
+  std::vector<Other> others;
+  std::unordered_map<std::string, int32_t> oth_by_key;  // root slot bytes + key hash -> entry
+  std::vector<uint8_t> h_hashes;                        // every event's hash (Others matching)
+  std::vector<int8_t> h_rflag;                          // Dev::rflag
+  std::vector<int32_t> h_ext_lt;                        // Dev::ext_lt
+  int64_t E0 = 0;  // events [0, E0) hold every other-parent only Root.Others knows
+  int32_t fiat_max = -1;
 
   int fail(int code, const char *fmt, ...) {
     char buf[512];

@@ -476,6 +476,7 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
   // starts from the value its chain's previous event left in HBM
   int32_t k = valid ? d.seg_lo[c] : 0, cur = 0, lim = 0;
   if (k > 0) cur = out[d.chain_start[c] + k - 1] + 1;
+  else if (LT && valid && d.lt_seed) cur = d.lt_seed[c] + 1;  // a Reset root's SelfParent LamportTimestamp
   uint32_t dsc = WAIT;
   const int32_t ltclamp = min(d.flow_ltclamp, F2_LTCLAMP);
   const bool dg = d.diag != nullptr && col == 0 && wave == 0;

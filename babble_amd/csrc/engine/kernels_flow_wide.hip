@@ -158,6 +158,7 @@ __device__ __forceinline__ void floww_body(const Dev &d, FlowLdsW &L) {
   int32_t *const outc = out + (valid ? d.chain_start[c] : 0);
   int32_t k = valid ? d.seg_lo[c] : 0, cur = 0, lim = 0;
   if (k > 0) cur = outc[k - 1] + 1;
+  else if (LT && valid && d.lt_seed) cur = d.lt_seed[c] + 1;  // a Reset root's SelfParent LamportTimestamp
   int32_t k1 = k, k2 = k;  // k at the previous two headers: the stores before k2 are complete
   const bool dg = d.diag != nullptr && col == 0 && wave == 0;
   const unsigned long long t_start = dg ? stamp() : 0;

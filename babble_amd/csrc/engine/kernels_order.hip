@@ -27,7 +27,7 @@ namespace bh {
 // round is "decided" here as DecideRoundReceived reads it, live:
 // RoundInfo.WitnessesDecided (roundInfo.go:78-85) -- for a processed round
 // (< P) that is "no trapped witness", for a pending one the fame pass's flag.
-__global__ __launch_bounds__(256) void k_round_received(Dev d, int32_t R, int32_t P) {
+__global__ __launch_bounds__(256) void k_round_received(Dev d, int32_t R, int32_t P, int32_t lcr) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int und = 0;
   if (x < d.N) {
@@ -35,6 +35,13 @@ __global__ __launch_bounds__(256) void k_round_received(Dev d, int32_t R, int32_
     if (res == UNSET) {
       const int32_t r = d.round[x], c = d.creator[x], k = d.index[x];
       for (int32_t i = r + 1; i < R; ++i) {
+        // a round below a Reset's r0 may not exist: GetRound fails, and an
+        // event below LastConsensusRound leaves UndeterminedEvents without a
+        // round received (hashgraph.go:970-977); at or above r0 every round exists
+        if (i < d.r0 && !d.rexists[i]) {
+          if (r < lcr) res = RR_DROP;
+          break;
+        }
         const bool live = i < P ? d.blocked[i] == 0 : d.decided[i] != 0;
         if (!live) break;
         if (d.nfam[i] > 0 && k <= d.minla[(int64_t)i * d.npad + c]) { res = i; break; }
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(256) void k_frame_count(Dev d) {
   for (int u = 0; u < 4; ++u) {
     const int64_t x = base + u * 256 + t;
     rr[u] = x < d.N ? d.rr[x] : UNSET;
-    if (rr[u] == UNSET) rr[u] = -1;
+    if (rr[u] < d.frame_lo) rr[u] = -1;  // none (UNSET, RR_DROP), or a frame never emitted (Reset)
     else lo = min(lo, rr[u]);
   }
   __syncthreads();
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(256) void k_frame_scatter(Dev d, int32_t P0) {
   for (int u = 0; u < 4; ++u) {
     const int64_t x = base + u * 256 + t;
     rr[u] = x < d.N ? d.rr[x] : UNSET;
-    if (rr[u] == UNSET || rr[u] >= P || rr[u] < P0) rr[u] = -1;  // frames < P0: ordered by earlier calls
+    if (rr[u] == UNSET || rr[u] >= P || rr[u] < P0 || rr[u] < d.frame_lo) rr[u] = -1;  // frames < P0: ordered by earlier calls
     else lo = min(lo, rr[u]);
   }
   __syncthreads();
@@ -285,7 +292,8 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
     d.cons_pos[e] = (int64_t)off + i;
     const int32_t tx = d.ntx[e];
     ntx += tx;
-    loaded += (d.index[e] == 0 || tx > 0);  // IsLoaded, event.go:169-178
+    const int32_t index = d.index[e] + (d.chain_base ? d.chain_base[d.creator[e]] : 0);
+    loaded += (index == 0 || tx > 0);  // IsLoaded, event.go:169-178
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -308,11 +316,11 @@ void configure_order_kernels() {
                             FRAME_LDS_MAX * 12);
 }
 
-void launch_round_received(const Dev &d, int32_t R, int32_t P, hipStream_t s) {
+void launch_round_received(const Dev &d, int32_t R, int32_t P, int32_t lcr, hipStream_t s) {
   (void)hipMemsetAsync(d.counters + 3, 0, 8, s);
   if (R > 0) (void)hipMemsetAsync(d.frame_cnt, 0, (size_t)R * 4, s);
   if (d.N == 0) return;
-  k_round_received<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d, R, P);
+  k_round_received<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d, R, P, lcr);
   if (R > 0) k_frame_count<<<(unsigned)((d.N + OB - 1) / OB), 256, 0, s>>>(d);
 }
 

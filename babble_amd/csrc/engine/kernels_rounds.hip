@@ -767,9 +767,7 @@ __global__ __launch_bounds__(256) void k_fd_idle(Dev d) {
   }
 }
 
-void launch_fd_idle(const Dev &d, hipStream_t s) {
-  if (d.fd_cols) k_fd_idle<<<d.n, 256, 0, s>>>(d);
-}
+void launch_fd_idle(const Dev &d, hipStream_t s) { k_fd_idle<<<d.n, 256, 0, s>>>(d); }
 
 bool round2_eligible(const Dev &d) { return d.fd_cols != 0; }
 
@@ -842,6 +840,10 @@ __global__ __launch_bounds__(64) void k_wcount(Dev d) {
   const int r = blockIdx.x, lane = threadIdx.x, n = d.n;
   int cnt = 0;
   for (int q = lane; q < n; q += 64) {
+    if (r < d.r0) {  // k_fiat's witnesses (Reset)
+      cnt += r >= d.rlo && d.fw[(int64_t)(r - d.rlo) * n + q] >= 0;
+      continue;
+    }
     const int32_t b0 = d.B[(int64_t)r * n + q], b1 = d.B[(int64_t)(r + 1) * n + q];
     cnt += (b0 < d.chain_len[q] && b1 > b0) ? 1 : 0;
   }
@@ -879,7 +881,11 @@ __global__ __launch_bounds__(64) void k_wfill(Dev d) {
     const int q = c0 + lane;
     int32_t b0 = 0;
     bool w = false;
-    if (q < n) {
+    if (q < n && r < d.r0) {  // k_fiat's witnesses (Reset)
+      const int32_t x = r >= d.rlo ? d.fw[(int64_t)(r - d.rlo) * n + q] : -1;
+      w = x >= 0;
+      b0 = w ? d.index[x] : 0;
+    } else if (q < n) {
       b0 = d.B[(int64_t)r * n + q];
       w = b0 < d.chain_len[q] && d.B[(int64_t)(r + 1) * n + q] > b0;
     }
@@ -915,15 +921,23 @@ __global__ void k_assign(Dev d, int64_t e_begin, int64_t n_prev, int32_t P) {
   const int32_t R = d.state[ST_ROUNDS];
   const int32_t c = d.creator[e], k = d.index[e];
   const int n = d.n;
-  int lo = 0, hi = R - 1;  // B[0][c] = 0 <= k
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (d.B[(int64_t)mid * n + c] <= k) lo = mid;
-    else hi = mid - 1;
+  int lo = d.r0;
+  bool w;
+  if (d.r0 > 0 && k < d.B[(int64_t)d.r0 * n + c]) {
+    // below the closed form's first round (Reset): k_fiat's round and witness
+    lo = d.round[e];
+    w = d.witness[e] != 0;
+  } else {
+    int hi = R - 1;  // B[r0][c] <= k
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (d.B[(int64_t)mid * n + c] <= k) lo = mid;
+      else hi = mid - 1;
+    }
+    d.round[e] = lo;
+    w = d.B[(int64_t)lo * n + c] == k;
+    d.witness[e] = w ? 1 : 0;
   }
-  d.round[e] = lo;
-  const bool w = d.B[(int64_t)lo * n + c] == k;
-  d.witness[e] = w ? 1 : 0;
   if (e >= n_prev) {
     d.fame[e] = w ? 0 : -1;
     d.rr[e] = UNSET;

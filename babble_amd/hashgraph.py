@@ -161,6 +161,31 @@ class Hashgraph:
     def synchronize(self):
         self._check(self._L.bh_synchronize(self._h))
 
+    def reset(self, round_received, block_index, next_round, self_parent_index, self_parent_lamport,
+              self_parent_round, other_root=(), other_key=(), other_creator_id=(), other_index=(),
+              other_lamport=(), other_round=(), other_hash=()):
+        """Hashgraph.Reset(block, frame) before the frame's events are
+        inserted (hashgraph.go:1324-1369): the frame's Roots in participant
+        order and their Others flattened (bh_reset).  Insert frame.Events next,
+        then later events, as wire events."""
+        n = len(self.participant_ids)
+        per = [np.ascontiguousarray(a, dtype=np.int32) for a in
+               (next_round, self_parent_index, self_parent_lamport, self_parent_round)]
+        if any(a.size != n for a in per):
+            raise ValueError("one root per participant")
+        k = len(other_root)
+        oth = [np.ascontiguousarray(a, dtype=dt) for a, dt in (
+            (other_root, np.int32), (other_key, np.uint8), (other_creator_id, np.int64),
+            (other_index, np.int32), (other_lamport, np.int32), (other_round, np.int32),
+            (other_hash, np.uint8))]
+        if oth[1].size != 32 * k or oth[6].size != 32 * k or any(oth[i].size != k for i in (0, 2, 3, 4, 5)):
+            raise ValueError("Others arrays disagree in length")
+        oth = [a if a.size else np.zeros(1, a.dtype) for a in oth]
+        rt = _native.Roots(int(round_received), int(block_index), *[_ptr(a) for a in per], k,
+                           *[_ptr(a) for a in oth])
+        self._keep_roots = (per, oth)
+        self._check(self._L.bh_reset(self._h, C.byref(rt)))
+
     def reset_consensus(self):
         """Forget every pass's results, keep the events (bh_reset_consensus):
         the next run_consensus recomputes the whole DAG."""

@@ -102,6 +102,37 @@ int bh_synchronize(bh_handle *h);             /* wait for queued device work */
  * only processes what was inserted since the previous one. */
 int bh_reset_consensus(bh_handle *h);
 
+/* Hashgraph.Reset(block, frame) (hashgraph.go:1324-1369; FastSync,
+ * node/core.go:240-283) on a fresh handle, before the frame's events are
+ * inserted: Store.Reset(frame.Roots), SetBlock(block), LastConsensusRound =
+ * block.RoundReceived().  The caller then inserts frame.Events (in frame
+ * order) and any later events with bh_insert_events, as Reset and the
+ * gossip after it do; an other-parent the engine does not hold is resolved
+ * through the creator's Root.Others like ReadWireInfo + checkOtherParent
+ * (:1431-1457, 417-436), and rounds / Lamport timestamps follow the Root
+ * cases A-F (docs/fastsync.rst:140-175).  Roots are given in participant
+ * (ID) order, as Frame.Roots; Others entries flattened, each naming the
+ * position of the Root that holds it.  Requires one shard, frames off, and
+ * every NextRound / SelfParent.Round below round_received (as GetFrame's
+ * roots are).  Blocks made afterwards have Index block_index + 1 + i. */
+typedef struct {
+  int32_t round_received;              /* block.RoundReceived() */
+  int64_t block_index;                 /* block.Index() */
+  const int32_t *next_round;           /* [n] Root.NextRound */
+  const int32_t *self_parent_index;    /* [n] Root.SelfParent.Index */
+  const int32_t *self_parent_lamport;  /* [n] Root.SelfParent.LamportTimestamp */
+  const int32_t *self_parent_round;    /* [n] Root.SelfParent.Round */
+  int32_t n_others;
+  const int32_t *other_root;           /* [n_others] position of the Root holding the entry */
+  const uint8_t *other_key;            /* [n_others][32] hash of the event keying it (Others[ev.Hex()]) */
+  const int64_t *other_creator_id;     /* RootEvent.CreatorID */
+  const int32_t *other_index;          /* RootEvent.Index */
+  const int32_t *other_lamport;        /* RootEvent.LamportTimestamp */
+  const int32_t *other_round;          /* RootEvent.Round */
+  const uint8_t *other_hash;           /* [n_others][32] RootEvent.Hash */
+} bh_roots;
+int bh_reset(bh_handle *h, const bh_roots *roots);
+
 typedef struct {
   int64_t n_events;
   int32_t last_round;             /* Store.LastRound() */
@@ -110,7 +141,7 @@ typedef struct {
   int64_t consensus_transactions; /* Hashgraph.ConsensusTransactions */
   int64_t pending_loaded_events;  /* Hashgraph.PendingLoadedEvents */
   int64_t undetermined_events;    /* len(Hashgraph.UndeterminedEvents) */
-  int64_t blocks;                 /* Store.LastBlockIndex()+1 */
+  int64_t blocks;                 /* Store.LastBlockIndex()+1 (after bh_reset: block_index + 1 + blocks made) */
   int32_t pending_rounds;         /* len(Hashgraph.PendingRounds) */
 } bh_stats;
 int bh_get_stats(bh_handle *h, bh_stats *out);

@@ -1,0 +1,139 @@
+"""Reset / FastSync roots through the engine (SURVEY 8(f) row 4;
+Hashgraph.Reset hashgraph.go:1324-1369, the Root cases of
+docs/fastsync.rst:140-175): a fresh handle is reset from block b of a
+hashgraph that ran consensus (its Frame's roots, tests/reset.py), the frame's
+events and then the rest of the DAG arrive as wire events, and every output
+-- rounds, witnesses, Lamport timestamps, fame, round received, consensus
+order, blocks, PendingRounds, UndeterminedEvents, LastConsensusRound,
+rejected inserts -- must equal the oracle's Reset restatement (pinned by the
+reference's Reset tests in tests/test_oracle_reset.py) on the same inputs.
+Covers the reference's Reset DAGs (kat_consensus block 1, the funky and
+sparse hashgraphs' blocks 0-2), generated gossip DAGs at n = 4 ... 128
+(chain dataflow k_flow32 + k_round2) and n = 160 (k_floww + k_round_wide),
+lagging peers (diff events Go rejects), and RunConsensus after every gossip
+batch."""
+import numpy as np
+import pytest
+
+from babble_amd.dag import Dag
+from kat import KatDag
+from oracle_py import Oracle
+from reset import DagArrays, ResetInputs, oracle_insert
+from test_gpu_parity import _compare
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_run(d):
+    o = Oracle(d.n, d.participant_ids, capacity=len(d.creator) + 64)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    o.run_consensus()
+    return o
+
+
+def _engine_reset(rs, d, cap):
+    from babble_amd import Hashgraph
+    pid = np.asarray(d.participant_ids, np.int64)
+    hg = Hashgraph(pid, cap)
+    hg.reset(rs.round_received, rs.block_index, rs.next_round, rs.sp_index, rs.sp_lt, rs.sp_round,
+             rs.oth_root, rs.oth_key, pid[np.asarray(rs.oth_creator, np.int64)] if rs.oth_creator else [],
+             rs.oth_index, rs.oth_lt, rs.oth_round, rs.oth_hash)
+    return hg
+
+
+def _wire(hg, d, ids):
+    """the original events `ids` as wire events (their WireBody never changes)"""
+    ids = np.asarray(ids, np.int64)
+    if ids.size == 0:
+        return np.zeros(0, np.int32)
+    pid = np.asarray(d.participant_ids, np.int64)
+    cr, ix, sp, op = d.creator[ids], d.index[ids], d.sp[ids], d.op[ids]
+    spi = ix - 1  # WireBody.SelfParentIndex (the Root SelfParent.Index for a chain after the Reset)
+    opc = np.where(op >= 0, pid[d.creator[np.maximum(op, 0)]], -1)
+    opi = np.where(op >= 0, d.index[np.maximum(op, 0)], -1)
+    return hg.insert_events(pid[cr], ix, spi, opc, opi, d.hashes[ids], d.sig_r[ids], d.ntx[ids],
+                            raise_on_error=False)
+
+
+def _coords_sample(o2, hg, k=12):
+    N = o2.num_events()
+    for e in np.unique(np.linspace(0, N - 1, min(N, k)).astype(int)):
+        la, fd = o2.coordinates(int(e))
+        gla, gfd = hg.coordinates(int(e))
+        assert np.array_equal(la, gla) and np.array_equal(fd, gfd), e
+
+
+def _run_pair(d, block, batches=1, cap_extra=64):
+    o = _oracle_run(d)
+    rs = ResetInputs(o, d, block)
+    o2 = Oracle(d.n, d.participant_ids, capacity=len(d.creator) + cap_extra)
+    o2.reset(rs)
+    hg = _engine_reset(rs, d, len(d.creator) + cap_extra)
+    st_o = oracle_insert(o2, rs, rs.frame)
+    st_g = _wire(hg, d, rs.frame)
+    assert np.array_equal(st_o != 0, st_g != 0), "frame inserts"
+    o2.run_consensus()
+    hg.run_consensus()
+    _compare(o2, hg, f"block {block} frame")
+    diff = rs.diff
+    for bi in range(batches):
+        part = diff[len(diff) * bi // batches: len(diff) * (bi + 1) // batches]
+        st_o = oracle_insert(o2, rs, part)
+        st_g = _wire(hg, d, part)
+        assert np.array_equal(st_o != 0, st_g != 0), f"diff inserts, batch {bi}"
+        o2.run_consensus()
+        hg.run_consensus()
+        _compare(o2, hg, f"block {block} batch {bi}")
+    st = hg.stats()
+    assert st.blocks == rs.block_index + 1 + len(o2.blocks()["round_received"])
+    _coords_sample(o2, hg)
+    return o2, hg, rs
+
+
+def test_reset_from_frame_kat():
+    """TestResetFromFrame (hashgraph_test.go:1711-1907) through the engine"""
+    d = KatDag("kat_consensus")
+    o2, hg, rs = _run_pair(d, 1)
+    assert hg.stats().last_consensus_round == rs.round_received
+
+
+@pytest.mark.parametrize("name", ["kat_funky_full", "kat_sparse"])
+@pytest.mark.parametrize("block", [0, 1, 2])
+def test_reset_kat(name, block):
+    """TestFunkyHashgraphReset / TestSparseHashgraphReset (:2344-2417, :2656-2738)"""
+    _run_pair(KatDag(name), block)
+
+
+@pytest.mark.parametrize("n,N,seed,lag,block,batches", [
+    (4, 3000, 0xBA0, 0, 3, 1), (7, 4000, 0xBA1, 0, 5, 4), (16, 8000, 0xBA2, 0, 4, 3),
+    (16, 8000, 0xBA3, 5, 2, 1), (32, 20000, 0xBA4, 0, 6, 5), (64, 30000, 0xBA5, 20, 3, 2),
+    (128, 40000, 0xBA6, 0, 4, 3), (160, 30000, 0xBA7, 0, 3, 2)])
+def test_reset_generated(n, N, seed, lag, block, batches):
+    d = DagArrays(Dag(n, N, seed, lagging=lag))
+    _run_pair(d, block, batches)
+
+
+def test_reset_round_info_and_errors():
+    """RoundInfo of the rounds a Reset hashgraph has (and lacks), and the
+    rejections bh_reset makes"""
+    from babble_amd import Hashgraph
+    from babble_amd.hashgraph import HashgraphError
+    d = DagArrays(Dag(8, 4000, 0xBA8))
+    o2, hg, rs = _run_pair(d, 4)
+    res = o2.results()
+    for r in range(0, hg.stats().last_round + 1):
+        present = bool((res["round"] == r).any())
+        if not present:
+            with pytest.raises(HashgraphError):
+                hg.round_info(r)
+            continue
+        info = hg.round_info(r)
+        want = set(np.nonzero((res["round"] == r) & (res["witness"] == 1))[0].tolist())
+        assert set(info["witnesses"].tolist()) == want, r
+        assert info["n_events"] == int((res["round"] == r).sum()), r
+        assert info["queued"] == (r >= rs.round_received), r
+    # a handle that already has events cannot be reset; a root above the block's round is refused
+    pid = np.asarray(d.participant_ids, np.int64)
+    h2 = Hashgraph(pid, 100)
+    with pytest.raises(HashgraphError):
+        h2.reset(1, 0, [5] * 8, [-1] * 8, [-1] * 8, [-1] * 8)
