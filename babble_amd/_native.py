@@ -57,7 +57,7 @@ class Stats(C.Structure):
                 ("last_consensus_round", C.c_int32), ("consensus_events", C.c_int64),
                 ("consensus_transactions", C.c_int64), ("pending_loaded_events", C.c_int64),
                 ("undetermined_events", C.c_int64), ("blocks", C.c_int64),
-                ("pending_rounds", C.c_int32)]
+                ("pending_rounds", C.c_int32), ("first_block", C.c_int64)]
 
 
 class RoundInfo(C.Structure):

@@ -1480,6 +1480,7 @@ int bh_get_stats(bh_handle *h, bh_stats *o) {
   o->undetermined_events = h->nundet + (o->n_events - h->n_rr);
   o->blocks = (int64_t)h->blocks.size() + (h->reset_on ? h->reset_block + 1 : 0);
   o->pending_rounds = std::max(0, h->R - h->P) + stale_head(h);
+  o->first_block = h->reset_on ? h->reset_block + 1 : 0;
   return BH_OK;
 }
 

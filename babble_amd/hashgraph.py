@@ -247,7 +247,8 @@ class Hashgraph:
         return ids
 
     def blocks(self):
-        b = self.stats().blocks
+        st = self.stats()
+        b = st.blocks - st.first_block  # blocks this handle made (a Reset starts after the block's Index)
         out = dict(round_received=np.empty(b, np.int32), first=np.empty(b, np.int64),
                    count=np.empty(b, np.int64), ntx=np.empty(b, np.int64))
         if b:

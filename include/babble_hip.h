@@ -143,6 +143,7 @@ typedef struct {
   int64_t undetermined_events;    /* len(Hashgraph.UndeterminedEvents) */
   int64_t blocks;                 /* Store.LastBlockIndex()+1 (after bh_reset: block_index + 1 + blocks made) */
   int32_t pending_rounds;         /* len(Hashgraph.PendingRounds) */
+  int64_t first_block;            /* Index of bh_get_blocks' block 0 (after bh_reset: block_index + 1) */
 } bh_stats;
 int bh_get_stats(bh_handle *h, bh_stats *out);
 
