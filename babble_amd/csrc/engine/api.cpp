@@ -437,6 +437,7 @@ int rounds_loop(bh_handle *h) {
   // LA rows and the firstDescendants walk (FDT) from the dataflow's
   // column-major LA; n > 128 then transposes FDT into chain-major FD rows
   if ((walked || wide_flow) && !h->reset_on) bh::launch_flow_transpose(d, s);  // (reset_coords transposed already)
+  d.fd_rows = !((walked || wide_flow) && bh::round_p16(d));  // 32-bit fd rows only where read
   bh::launch_first_descendants(d, s, walked || wide_flow);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
@@ -1643,10 +1644,12 @@ static int ensure_coords(bh_handle *h) {
     full.ncol = d.n;
     if (h->reset_on) {
       if ((rc = reset_coords(h, h->stream))) return rc;
+      d.fd_rows = full.fd_rows = !bh::round_p16(d);
       bh::launch_first_descendants(full, h->stream, true);
     } else {
       if (walked) bh::launch_flow_coordinates(full, h->stream);
       else bh::launch_coordinates(full, h->stream);
+      d.fd_rows = full.fd_rows = 1;  // (the chunked sweep's FDT is not complete)
       bh::launch_first_descendants(full, h->stream, walked);
     }
     h->inc_valid = false;  // the loop state no longer matches the layout / prefix
@@ -1668,7 +1671,7 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (last_ancestors)
     HIPCHK(h, hipMemcpy(last_ancestors, d.la + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
-  if (first_descendants && d.fd_cols) {  // one column of FDT
+  if (first_descendants && (d.fd_cols || !d.fd_rows)) {  // one column of FDT
     HIPCHK(h, hipMemcpy2D(first_descendants, 4, d.fdt + bh::fdt_pos(row, 0, d.npad), 64 * 4, 4, (size_t)d.n,
                           hipMemcpyDeviceToHost));
   } else if (first_descendants) {

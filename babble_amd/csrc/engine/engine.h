@@ -103,6 +103,10 @@ struct Dev {
   // round loop reads windows of it and hands fame its stronglySee results
   // as ballots (ssm); no fd
   int32_t fd_cols;
+  // fd_rows (npad > 128): k_fd_transpose writes the 32-bit fd rows; 0 when
+  // the 16-bit loop runs on a complete FDT (k_flow_transpose walked it), and
+  // FD readers then read FDT
+  int32_t fd_rows;
   // [n][R_cap + 1][16 waves] k_round2 ballots: lane (q * LPC) % 64 of wave
   // q * LPC / 64 = candidate (c, B[r][c]) strongly sees (q, B[r-1][q])
   unsigned long long *ssm;
@@ -291,6 +295,8 @@ void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s);
 void launch_query(const Dev &d, int32_t kind, int64_t count, const int64_t *x, const int64_t *y, int32_t *out,
                   hipStream_t s);
 void configure_fd_kernels();
-void launch_first_descendants(const Dev &d, hipStream_t s, bool walked);  // fd from la (FDT already written by k_flow_transpose when walked)
+void launch_first_descendants(const Dev &d, hipStream_t s, bool walked);
+// the 16-bit wide round loop applies (fd16 rows, chains <= P16_MAXLEN)
+bool round_p16(const Dev &d);  // fd from la (FDT already written by k_flow_transpose when walked)
 
 }  // namespace bh

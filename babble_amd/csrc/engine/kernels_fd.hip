@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
       if (ii < n && (fast || j <= d.last_la[(int64_t)ii * npad + c])) x = tile[ii * (TR_ROWS + 1) + r];
       o[u] = x;
     }
-    *reinterpret_cast<int4 *>(d.fd + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
+    if (d.fd_rows) *reinterpret_cast<int4 *>(d.fd + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
     if (d.fd16) {  // FD + 1 as 16 bits, FD_NONE -> 0xFFFF (its + 1 wraps to 2^31)
       auto h16 = [](int32_t v) { return min((uint32_t)v + 1u, 0xFFFFu); };
       const int64_t w0 = (row0 + r) * ((npad + 7) / 8 * 4) + i4 / 2;

@@ -590,9 +590,9 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
     cstart[i] = d.chain_start[i];
     clen[i] = d.chain_len[i];
   }
-  // column i of a load is uniform per wave (TR = 64): scalar base address,
-  // 32-bit lane offset
-  for (int i = __builtin_amdgcn_readfirstlane(t / TR); i < n; i += LU * IPP) {
+  // column i of a load is uniform per wave when TR = 64: scalar base
+  // address, 32-bit lane offset (TR = 32: two columns per wave)
+  for (int i = TR >= 64 ? __builtin_amdgcn_readfirstlane(t / TR) : t / TR; i < n; i += LU * IPP) {
     int32_t v[LU];
 #pragma unroll
     for (int u = 0; u < LU; ++u)
@@ -766,6 +766,13 @@ void launch_flow_transpose(const Dev &d, hipStream_t s) {
     k_flow_transpose<64, 512><<<(unsigned)wg, 512, (size_t)d.npad * 66 * 4, s>>>(d);
     return;
   }
+  if (d.npad > 128) {
+    // wide rows: 32-row tiles (70 KiB of LDS) so two workgroups share a
+    // compute unit -- the walk's LDS round trips are latency, not bandwidth
+    const unsigned tiles = (unsigned)((d.rows + 31) / 32);
+    k_flow_transpose<32, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 34 * 4, s>>>(d);
+    return;
+  }
   const unsigned tiles = (unsigned)((d.rows + 63) / 64);
   k_flow_transpose<64, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 66 * 4, s>>>(d);
 }
@@ -778,6 +785,8 @@ void launch_flow_coordinates(const Dev &d, hipStream_t s) {
 
 void configure_flow_kernels() {
   (void)hipFuncSetAttribute((const void *)k_flow_transpose<64, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            150 * 1024);
+  (void)hipFuncSetAttribute((const void *)k_flow_transpose<32, 512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             150 * 1024);
 }
 

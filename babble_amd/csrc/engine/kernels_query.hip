@@ -18,7 +18,7 @@ __device__ __forceinline__ int32_t la_at(const Dev &d, int32_t e, int i) {
 }
 __device__ __forceinline__ int32_t fd_at(const Dev &d, int32_t e, int i) {
   const int64_t row = d.epos[e];
-  return d.fd_cols ? d.fdt[fdt_pos(row, i, d.npad)] : d.fd[row * d.npad + i];
+  return d.fd_cols || !d.fd_rows ? d.fdt[fdt_pos(row, i, d.npad)] : d.fd[row * d.npad + i];
 }
 
 __global__ __launch_bounds__(256) void k_query(Dev d, int32_t kind, int64_t count, const int64_t *xs,

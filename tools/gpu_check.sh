@@ -37,5 +37,6 @@ for s in "$@"; do
     pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_" --cfg 3 ;;
     pmct) step pmc_t 900 bash tools/pmc.sh t "k_flow_transpose|k_fd_transpose" --cfg 3 ;;
     prof3) step prof_c3 900 bash tools/prof.sh c3 --cfg 3 --steps 3 --warmup 1 ;;
+    prof4) step prof_c4 1100 bash tools/prof.sh c4 --cfg 4 --steps 1 --warmup 1 ;;
   esac
 done
