@@ -35,6 +35,7 @@ for s in "$@"; do
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
     pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_" --cfg 3 ;;
+    pmc4) step pmc_c4 1100 bash tools/pmc.sh c4 "k_" --cfg 4 ;;
     pmct) step pmc_t 900 bash tools/pmc.sh t "k_flow_transpose|k_fd_transpose" --cfg 3 ;;
     prof3) step prof_c3 900 bash tools/prof.sh c3 --cfg 3 --steps 3 --warmup 1 ;;
     prof4) step prof_c4 1100 bash tools/prof.sh c4 --cfg 4 --steps 1 --warmup 1 ;;
