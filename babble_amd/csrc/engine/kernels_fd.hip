@@ -22,6 +22,7 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace bh {
 
@@ -180,10 +181,18 @@ void launch_first_descendants(const Dev &d, hipStream_t s, bool walked) {
   if (d.fd_cols) return;  // FDT complete; no chain-major rows
   k_last_la_init<<<1, 256, 0, s>>>(d);
   k_last_la<<<d.n, 256, 0, s>>>(d);
-  if (d.npad <= 512)
+  // tile rows: LDS is npad x (TR + 1) words, so wide groups take short
+  // tiles and several workgroups per compute unit (the kernel is bound by
+  // its loads' latency: n = 512 with 64-row tiles left one 4-wave workgroup
+  // per CU, 1.2 TB/s); BH_FDT_TR overrides (A/B)
+  static const int tr_env = getenv("BH_FDT_TR") ? atoi(getenv("BH_FDT_TR")) : 0;
+  const int tr = tr_env ? tr_env : d.npad <= 128 ? 64 : 16;
+  if (tr >= 64)
     k_fd_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
-  else
+  else if (tr >= 32)
     k_fd_transpose<32><<<(unsigned)((d.N + 31) / 32), 256, (size_t)d.npad * 33 * 4, s>>>(d);
+  else
+    k_fd_transpose<16><<<(unsigned)((d.N + 15) / 16), 256, (size_t)d.npad * 17 * 4, s>>>(d);
 }
 
 void configure_fd_kernels() {

@@ -767,10 +767,17 @@ void launch_flow_transpose(const Dev &d, hipStream_t s) {
     return;
   }
   if (d.npad > 128) {
-    // wide rows: 32-row tiles (70 KiB of LDS) so two workgroups share a
-    // compute unit -- the walk's LDS round trips are latency, not bandwidth
-    const unsigned tiles = (unsigned)((d.rows + 31) / 32);
-    k_flow_transpose<32, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 34 * 4, s>>>(d);
+    // wide rows: short tiles so several workgroups share a compute unit --
+    // the walk's LDS round trips are latency, not bandwidth (BH_XPOSE_TR:
+    // 16 or 32 rows, A/B)
+    static const int tr = getenv("BH_XPOSE_TR") ? atoi(getenv("BH_XPOSE_TR")) : 32;
+    if (tr <= 16) {
+      const unsigned tiles = (unsigned)((d.rows + 15) / 16);
+      k_flow_transpose<16, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 18 * 4, s>>>(d);
+    } else {
+      const unsigned tiles = (unsigned)((d.rows + 31) / 32);
+      k_flow_transpose<32, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 34 * 4, s>>>(d);
+    }
     return;
   }
   const unsigned tiles = (unsigned)((d.rows + 63) / 64);

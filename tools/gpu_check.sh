@@ -31,8 +31,12 @@ for s in "$@"; do
     tlrows) step tlrows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlrows.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench) step bench 900 python bench.py ;;
     benchrows) step bench_rows 900 env BH_ROUND_ROWS=1 python bench.py --cpu-sample 0 ;;
+    bench4tr32) step bench_c4_tr32 1100 env BH_FDT_TR=32 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    bench4x16) step bench_c4_x16 1100 env BH_XPOSE_TR=16 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    bench4tr64) step bench_c4_tr64 1100 env BH_FDT_TR=64 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
+    bench4q) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
     pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_" --cfg 3 ;;
     pmc4) step pmc_c4 1100 bash tools/pmc.sh c4 "k_" --cfg 4 ;;
