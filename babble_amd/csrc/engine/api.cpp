@@ -507,10 +507,15 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
 // (segments): the coordinate kernels of prefix s + 1 run on stream2 while
 // the round loop runs prefix s on `stream`, resuming at the last round the
 // previous prefix fixed (k_resume_point).  Single shard, chain dataflow
-// path (k_flow32, n <= 128) only.
+// path (k_flow32, n <= 128) only; a shard of a multi-process group too
+// (coordinates replicated).
 bool segments_eligible(const bh_handle *h) {
   const Dev &d = h->d;
-  return h->group.empty() && h->world == 1 && use_flow(d) && bh::flow32_eligible(d) && d.fd_cols && !h->reset_on;
+  // one shard per process replicates the coordinates and the round loop
+  // unless its LA columns are split (BH_SHARD_COORDS=columns): it runs the
+  // same pipeline as a lone handle, and only fame / frame sorts exchange
+  return h->group.empty() && (h->world == 1 || !h->shard_cols) && use_flow(d) && bh::flow32_eligible(d) &&
+         d.fd_cols && !h->reset_on;
 }
 
 // segments for `events` new events: measured at C3 (10M events): 4
