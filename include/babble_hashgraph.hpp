@@ -142,6 +142,38 @@ class Hashgraph {
     return st;
   }
 
+  // Reset(block, frame) (hashgraph.go:1324-1369) on a fresh Hashgraph,
+  // before frame.Events are inserted: the frame's roots in participant order
+  // and their Others flattened (bh_roots, include/babble_hip.h)
+  struct RootOther {
+    int32_t root;         // position of the Root holding the entry
+    uint8_t key[32];      // hash of the event keying it (Others[ev.Hex()])
+    int64_t creator_id;   // RootEvent.CreatorID
+    int32_t index, lamport_timestamp, round;
+    uint8_t hash[32];     // RootEvent.Hash
+  };
+  void Reset(int32_t round_received, int64_t block_index, const std::vector<int32_t> &next_round,
+             const std::vector<int32_t> &self_parent_index, const std::vector<int32_t> &self_parent_lamport,
+             const std::vector<int32_t> &self_parent_round, const std::vector<RootOther> &others) {
+    const size_t k = others.size();
+    std::vector<int32_t> root(k), idx(k), lt(k), rnd(k);
+    std::vector<int64_t> cre(k);
+    std::vector<uint8_t> key(k * 32), hash(k * 32);
+    for (size_t i = 0; i < k; ++i) {
+      root[i] = others[i].root;
+      cre[i] = others[i].creator_id;
+      idx[i] = others[i].index;
+      lt[i] = others[i].lamport_timestamp;
+      rnd[i] = others[i].round;
+      std::copy(others[i].key, others[i].key + 32, key.begin() + 32 * i);
+      std::copy(others[i].hash, others[i].hash + 32, hash.begin() + 32 * i);
+    }
+    bh_roots rt{round_received, block_index, next_round.data(), self_parent_index.data(),
+                self_parent_lamport.data(), self_parent_round.data(), (int32_t)k, root.data(), key.data(),
+                cre.data(), idx.data(), lt.data(), rnd.data(), hash.data()};
+    check(bh_reset(h_, &rt));
+  }
+
   void DivideRounds() { check(bh_divide_rounds(h_)); }
   void DecideFame() { check(bh_decide_fame(h_)); }
   void DecideRoundReceived() { check(bh_decide_round_received(h_)); }
