@@ -57,50 +57,95 @@ void launch_reset_coords(const Dev &d, hipStream_t s) {
 }
 
 constexpr int FI_MAXN = 512;
+constexpr int FI_CACHE_N = 128;  // witness FD rows of one round cached in LDS up to this many chains
+
+struct FiatLds {
+  int32_t done[FI_MAXN], bfirst[FI_MAXN];
+  // the chunk's events (1024 ids from `base`) and the previous chunk's
+  // (slot (id - base + 1024) of 2048): creator, index (chain position) and
+  // the rounds this pass gave them; parents and flags of the current chunk
+  int32_t list[1024], wcnt[16];
+  int32_t cc[2048], ck[2048], crd[2048];
+  int32_t csp[1024], cop[1024];
+  int8_t cfl[1024];
+  // FD rows of round cache_r's witnesses (n <= FI_CACHE_N): fdc[j][i] for
+  // the j-th witness in chain order
+  int32_t fdc[FI_CACHE_N][FI_CACHE_N];
+  int32_t wl[FI_CACHE_N];  // those witnesses' ids
+  int32_t cache_r, cache_nw;
+  int32_t cnt, ndone, pr, ss, stop, fmax;
+};
 
 __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
-  __shared__ int32_t done[FI_MAXN], bfirst[FI_MAXN];
-  __shared__ int32_t list[1024], wcnt[16];
-  __shared__ int32_t sh_cnt, sh_ndone, sh_pr, sh_ss, sh_stop;
+  __shared__ FiatLds L;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, n = d.n, npad = d.npad;
   const int32_t r0 = d.r0, rlo = d.rlo;
+  const bool cached = n <= FI_CACHE_N;
   for (int c = t; c < n; c += 1024) {
-    done[c] = 0;
-    bfirst[c] = d.chain_len[c];
+    L.done[c] = 0;
+    L.bfirst[c] = d.chain_len[c];
   }
-  if (t == 0) { sh_ndone = 0; sh_stop = 0; }
+  if (t == 0) { L.ndone = 0; L.stop = 0; L.cache_r = -1; L.cache_nw = 0; L.fmax = -1; }
+  for (int i = t; i < 1024; i += 1024) L.cc[i] = -1;
   __syncthreads();
-  // round of an event processed before x: its stored round, or "at least
-  // r0" if its chain was done at or before it
-  auto round_of = [&](int32_t y) -> int32_t {
-    const int32_t cy = d.creator[y];
-    return (done[cy] && d.index[y] >= bfirst[cy]) ? r0 : d.round[y];
-  };
   for (int64_t base = 0; base < d.N; base += 1024) {
-    // the chunk's events on chains not done yet, in order
+    // the chunk's events, staged (the previous chunk's move down); those on
+    // chains not done yet listed in order
     const int64_t e = base + t;
-    const bool need = e < d.N && !done[d.creator[e]];
-    const unsigned long long m = __ballot(need);
-    if (lane == 0) wcnt[wave] = __popcll(m);
-    __syncthreads();
-    int32_t pos = __popcll(m & ((1ull << lane) - 1ull));
-    for (int w = 0; w < wave; ++w) pos += wcnt[w];
-    if (need) list[pos] = (int32_t)e;
-    if (t == 0) {
-      int32_t tot = 0;
-      for (int w = 0; w < 16; ++w) tot += wcnt[w];
-      sh_cnt = tot;
+    bool need = false;
+    if (base > 0) {
+      L.cc[t] = L.cc[1024 + t];
+      L.ck[t] = L.ck[1024 + t];
+      L.crd[t] = L.crd[1024 + t];
     }
     __syncthreads();
-    const int32_t cnt = sh_cnt;
+    if (e < d.N) {
+      const int32_t c = d.creator[e];
+      L.cc[1024 + t] = c;
+      L.ck[1024 + t] = d.index[e];
+      L.csp[t] = d.sp[e];
+      L.cop[t] = d.op[e];
+      L.cfl[t] = d.rflag[e];
+      L.crd[1024 + t] = UNSET;
+      need = !L.done[c];
+    }
+    const unsigned long long m = __ballot(need);
+    if (lane == 0) L.wcnt[wave] = __popcll(m);
     __syncthreads();
+    int32_t pos = __popcll(m & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wave; ++w) pos += L.wcnt[w];
+    if (need) L.list[pos] = t;
+    if (t == 0) {
+      int32_t tot = 0;
+      for (int w = 0; w < 16; ++w) tot += L.wcnt[w];
+      L.cnt = tot;
+    }
+    __syncthreads();
+    const int32_t cnt = L.cnt;
     for (int32_t j = 0; j < cnt; ++j) {
-      const int32_t x = list[j], c = d.creator[x];
-      if (done[c]) continue;  // uniform: done[] only changes behind barriers
+      const int32_t xi = L.list[j];
+      const int32_t x = (int32_t)(base + xi), c = L.cc[1024 + xi];
+      if (L.done[c]) continue;  // uniform: done[] only changes behind barriers
+      // x's lastAncestors, loaded while lane 0 works out its parent round
+      const int64_t rx = d.epos[x];
+      const int32_t la0 = lane < n ? d.la[rx * npad + lane] : -1;
+      const int32_t la1 = lane + 64 < n ? d.la[rx * npad + lane + 64] : -1;
       if (t == 0) {
-        const int32_t sp = d.sp[x], op = d.op[x];
-        const bool oth = d.rflag[x] & 1;               // Root.Others[x] names x's other-parent
-        const bool op_empty = op < 0 && !(d.rflag[x] & 2);  // no other-parent at all
+        // round of an event before x: "at least r0" if its chain was done at
+        // or before it, else the round this pass gave it
+        auto round_of = [&](int32_t y) -> int32_t {
+          int32_t cy, ky, ry;
+          if (y >= base - (base > 0 ? 1024 : 0)) {
+            const int32_t sl = (int32_t)(y - base + 1024);
+            cy = L.cc[sl]; ky = L.ck[sl]; ry = L.crd[sl];
+          } else {
+            cy = d.creator[y]; ky = d.index[y]; ry = d.round[y];
+          }
+          return (L.done[cy] && ky >= L.bfirst[cy]) ? r0 : ry;
+        };
+        const int32_t sp = L.csp[xi], op = L.cop[xi];
+        const bool oth = L.cfl[xi] & 1;                 // Root.Others[x] names x's other-parent
+        const bool op_empty = op < 0 && !(L.cfl[xi] & 2);  // no other-parent at all
         int32_t pr;
         if (sp < 0 && (oth || op_empty)) {
           pr = -1 - d.root_next[c];  // attached to the Root: NextRound by fiat (encoded < 0)
@@ -109,52 +154,89 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
           if (oth) pr = max(pr, d.root_next[c]);
           else if (op >= 0) pr = max(pr, round_of(op));
         }
-        sh_pr = pr;
-        sh_ss = 0;
+        L.pr = pr;
+        L.ss = 0;
       }
       __syncthreads();
-      const int32_t pr = sh_pr;
-      if (pr >= 0 && pr < r0) {
+      const int32_t pr = L.pr;
+      if (pr >= 0 && pr < r0 && pr >= rlo) {
         // #witnesses of round pr that x strongly sees (_stronglySee :172-191)
-        const int64_t rx = d.epos[x];
-        for (int q = wave; q < n; q += 16) {
-          const int32_t w = pr >= rlo ? d.fw[(int64_t)(pr - rlo) * n + q] : -1;
-          if (w < 0) continue;
-          const int64_t rw = d.epos[w];
-          int cntc = 0;
-          for (int i = lane; i < n; i += 64) cntc += d.la[rx * npad + i] >= d.fdt[fdt_pos(rw, i, npad)];
+        const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
+        if (cached) {
+          if (L.cache_r != pr) {  // stage round pr's witness FD rows
+            __syncthreads();
+            if (t == 0) {
+              int32_t k = 0;
+              for (int q = 0; q < n; ++q)
+                if (wrow[q] >= 0) L.wl[k++] = wrow[q];
+              L.cache_nw = k;
+            }
+            __syncthreads();
+            const int32_t nw = L.cache_nw;
+            for (int p = t; p < nw * n; p += 1024) {
+              const int32_t jw = p / n, i = p - jw * n;
+              L.fdc[jw][i] = d.fdt[fdt_pos(d.epos[L.wl[jw]], i, npad)];
+            }
+            __syncthreads();
+            if (t == 0) L.cache_r = pr;
+            __syncthreads();
+          }
+          const int32_t nw = L.cache_nw;
+          for (int jw = wave; jw < nw; jw += 16) {
+            int cntc = (lane < n && la0 >= L.fdc[jw][lane]) + (lane + 64 < n && la1 >= L.fdc[jw][lane + 64]);
 #pragma unroll
-          for (int off = 32; off > 0; off >>= 1) cntc += __shfl_xor(cntc, off);
-          if (lane == 0 && cntc >= d.sm) atomicAdd(&sh_ss, 1);
+            for (int off = 32; off > 0; off >>= 1) cntc += __shfl_xor(cntc, off);
+            if (lane == 0 && cntc >= d.sm) atomicAdd(&L.ss, 1);
+          }
+        } else {
+          for (int q = wave; q < n; q += 16) {
+            const int32_t w = wrow[q];
+            if (w < 0) continue;
+            const int64_t rw = d.epos[w];
+            int cntc = 0;
+            for (int i = lane; i < n; i += 64) cntc += d.la[rx * npad + i] >= d.fdt[fdt_pos(rw, i, npad)];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) cntc += __shfl_xor(cntc, off);
+            if (lane == 0 && cntc >= d.sm) atomicAdd(&L.ss, 1);
+          }
         }
       }
       __syncthreads();
       if (t == 0) {
         int32_t r;
         if (pr < 0) r = -1 - pr;
-        else r = pr < r0 && sh_ss >= d.sm ? pr + 1 : pr;
-        const int32_t k = d.index[x];
+        else r = pr < r0 && L.ss >= d.sm ? pr + 1 : pr;
+        const int32_t k = L.ck[1024 + xi];
         if (r >= r0) {  // x opens round >= r0 on its chain: the closed form's candidate
-          done[c] = 1;
-          bfirst[c] = k;
-          if (++sh_ndone == n) sh_stop = 1;
+          L.done[c] = 1;
+          L.bfirst[c] = k;
+          if (++L.ndone == n) L.stop = 1;
         } else {
-          const int32_t spr = d.sp[x] < 0 ? d.root_sp_round[c] : d.round[d.sp[x]];
+          const int32_t sp = L.csp[xi];
+          const int32_t spr = sp < 0 ? d.root_sp_round[c]
+                            : sp >= base - (base > 0 ? 1024 : 0) ? L.crd[sp - base + 1024] : d.round[sp];
           const bool w = r > spr;  // witness (hashgraph.go:281-296)
           d.round[x] = r;
           d.witness[x] = w ? 1 : 0;
+          L.crd[1024 + xi] = r;
           d.rexists[r] = 1;
-          if (w) d.fw[(int64_t)(r - rlo) * n + c] = x;
-          if (r > d.state[ST_FIATMAX]) d.state[ST_FIATMAX] = r;
+          if (w) {
+            d.fw[(int64_t)(r - rlo) * n + c] = x;
+            if (r == L.cache_r) L.cache_r = -1;  // the cached round gained a witness
+          }
+          L.fmax = max(L.fmax, r);
         }
       }
       __syncthreads();
     }
-    if (sh_stop) break;
+    if (L.stop) break;
   }
   __syncthreads();
-  for (int c = t; c < n; c += 1024) d.B[(int64_t)r0 * n + c] = bfirst[c];
-  if (t == 0) d.state[ST_RESUME] = r0;
+  for (int c = t; c < n; c += 1024) d.B[(int64_t)r0 * n + c] = L.bfirst[c];
+  if (t == 0) {
+    d.state[ST_RESUME] = r0;
+    d.state[ST_FIATMAX] = L.fmax;
+  }
 }
 
 void launch_fiat(const Dev &d, hipStream_t s) {
