@@ -42,7 +42,7 @@ void free_all(bh_handle *h) {
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
                   d.wfame, d.frame_loaded, d.Bp, d.fd, d.fd16, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
-                  d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
+                  d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.wfd, d.rexists};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -460,6 +460,21 @@ int rounds_loop(bh_handle *h) {
     bh::launch_round_resume(d, s);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemcpyAsync(&h->fiat_max, d.state + bh::ST_FIATMAX, 4, hipMemcpyDeviceToHost, s));
+    if (getenv("BH_FIAT_DEBUG")) {
+      int32_t fs[4] = {0, 0, 0, 0};
+      HIPCHK(h, hipMemcpyAsync(fs, d.state + bh::ST_FIATMAX, 16, hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      fprintf(stderr, "[k_fiat] max round %d, chains done %d of %d, events visited %d, chunks %d (r0 %d)\n", fs[0], fs[1],
+              d.n, fs[2], fs[3], d.r0);
+      if (d.diag) {
+        unsigned long long g[5] = {0, 0, 0, 0, 0};
+        HIPCHK(h, hipMemcpy(g, d.diag + 24, sizeof g, hipMemcpyDeviceToHost));
+        const double e = (double)(g[4] ? g[4] : 1);
+        fprintf(stderr, "[k_fiat] cycles per event: pr %.0f, counts %.0f, results %.0f, witness rows %.0f (%llu events)\n",
+                g[0] / e, g[1] / e, g[2] / e, g[3] / e, g[4]);
+        HIPCHK(h, hipMemset(d.diag + 24, 0, sizeof g));
+      }
+    }
   } else {
     bh::launch_round_init(d, s);
   }
@@ -1422,7 +1437,8 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
       (rc = up(&d.root_sp_round, h->sp_round_h)))
     return rc;
   if ((rc = dalloc(h, &d.rflag, (size_t)C)) || (rc = dalloc(h, &d.ext_lt, (size_t)C)) ||
-      (rc = dalloc(h, &d.fw, (size_t)(d.r0 - d.rlo) * n)))
+      (rc = dalloc(h, &d.fw, (size_t)(d.r0 - d.rlo) * n)) ||
+      (rc = dalloc(h, &d.wfd, (size_t)(d.r0 - d.rlo) * n * d.npad)))
     return rc;
   h->reset_on = true;
   h->reset_lcr = rt->round_received;

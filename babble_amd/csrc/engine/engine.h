@@ -43,6 +43,7 @@ enum StateSlot {
   ST_FLOWOVF = 10,  // k_flow32: a Lamport timestamp reached 2^21 (LT recomputed by k_flow)
   ST_RESUME = 11,   // k_resume_point: the last round whose boundaries B[r][*] a prefix run fixed
   ST_FIATMAX = 12,  // k_fiat: the highest round of an event below the closed form's first round (-1: none)
+  ST_FIATDONE = 13, ST_FIATEV = 14, ST_FIATCH = 15,  // k_fiat: chains done, events visited, chunks scanned
   ST_COUNT = 16
 };
 
@@ -161,6 +162,7 @@ struct Dev {
   // has an event (RoundInfo exists, inmem_store.go:185-191).
   int32_t r0, rlo;
   int32_t *fw;
+  int32_t *wfd;  // [(r0 - rlo) * n][npad]: FD row of fw's witness (k_fiat's stronglySee counts)
   int8_t *rexists;
   int32_t frame_lo;  // frames below it are never emitted (Reset: LastConsensusRound's, hashgraph.go:1063-1065)
 };

@@ -57,7 +57,13 @@ void launch_reset_coords(const Dev &d, hipStream_t s) {
 }
 
 constexpr int FI_MAXN = 512;
-constexpr int FI_CACHE_N = 128;  // witness FD rows of one round cached in LDS up to this many chains
+
+// a workgroup barrier that waits for LDS traffic only: the per-event
+// hand-offs of k_fiat go through LDS, so loads in flight (the next event's
+// lastAncestors) and stores (its results) keep going across it.  Where global
+// data one wave stored is read by another (fw / wfd) a full __syncthreads
+// stays.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 struct FiatLds {
   int32_t done[FI_MAXN], bfirst[FI_MAXN];
@@ -66,26 +72,23 @@ struct FiatLds {
   // the rounds this pass gave them; parents and flags of the current chunk
   int32_t list[1024], wcnt[16];
   int32_t cc[2048], ck[2048], crd[2048];
-  int32_t csp[1024], cop[1024];
+  int32_t csp[1024], cop[1024], cep[1024];
   int8_t cfl[1024];
-  // FD rows of round cache_r's witnesses (n <= FI_CACHE_N): fdc[j][i] for
-  // the j-th witness in chain order
-  int32_t fdc[FI_CACHE_N][FI_CACHE_N];
-  int32_t wl[FI_CACHE_N];  // those witnesses' ids
-  int32_t cache_r, cache_nw;
-  int32_t cnt, ndone, pr, ss, stop, fmax;
+  int32_t rnext[FI_MAXN], rspr[FI_MAXN];  // Root.NextRound / SelfParent.Round
+  int32_t cnt, ndone, pr, ss, stop, fmax, nvis, nch, neww, newslot;
 };
 
 __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
   __shared__ FiatLds L;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, n = d.n, npad = d.npad;
   const int32_t r0 = d.r0, rlo = d.rlo;
-  const bool cached = n <= FI_CACHE_N;
   for (int c = t; c < n; c += 1024) {
     L.done[c] = 0;
     L.bfirst[c] = d.chain_len[c];
+    L.rnext[c] = d.root_next[c];
+    L.rspr[c] = d.root_sp_round[c];
   }
-  if (t == 0) { L.ndone = 0; L.stop = 0; L.cache_r = -1; L.cache_nw = 0; L.fmax = -1; }
+  if (t == 0) { L.ndone = 0; L.stop = 0; L.fmax = -1; L.nvis = 0; L.nch = 0; L.neww = -1; }
   for (int i = t; i < 1024; i += 1024) L.cc[i] = -1;
   __syncthreads();
   for (int64_t base = 0; base < d.N; base += 1024) {
@@ -106,6 +109,7 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
       L.csp[t] = d.sp[e];
       L.cop[t] = d.op[e];
       L.cfl[t] = d.rflag[e];
+      L.cep[t] = d.epos[e];
       L.crd[1024 + t] = UNSET;
       need = !L.done[c];
     }
@@ -119,17 +123,30 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
       int32_t tot = 0;
       for (int w = 0; w < 16; ++w) tot += L.wcnt[w];
       L.cnt = tot;
+      L.nch++;
     }
     __syncthreads();
     const int32_t cnt = L.cnt;
+    // lastAncestors of the next listed event, loaded one event ahead
+    int32_t nla0 = -1, nla1 = -1;
+    if (cnt > 0) {
+      const int64_t rx = L.cep[L.list[0]];
+      if (lane < n) nla0 = d.la[rx * npad + lane];
+      if (lane + 64 < n) nla1 = d.la[rx * npad + lane + 64];
+    }
     for (int32_t j = 0; j < cnt; ++j) {
       const int32_t xi = L.list[j];
       const int32_t x = (int32_t)(base + xi), c = L.cc[1024 + xi];
+      const int32_t la0 = nla0, la1 = nla1;
+      if (j + 1 < cnt) {
+        const int64_t rn = L.cep[L.list[j + 1]];
+        if (lane < n) nla0 = d.la[rn * npad + lane];
+        if (lane + 64 < n) nla1 = d.la[rn * npad + lane + 64];
+      }
       if (L.done[c]) continue;  // uniform: done[] only changes behind barriers
-      // x's lastAncestors, loaded while lane 0 works out its parent round
-      const int64_t rx = d.epos[x];
-      const int32_t la0 = lane < n ? d.la[rx * npad + lane] : -1;
-      const int32_t la1 = lane + 64 < n ? d.la[rx * npad + lane + 64] : -1;
+      const int64_t rx = L.cep[xi];
+      const bool dg = d.diag != nullptr && t == 0;
+      const unsigned long long q0t = dg ? __builtin_amdgcn_s_memtime() : 0;
       if (t == 0) {
         // round of an event before x: "at least r0" if its chain was done at
         // or before it, else the round this pass gave it
@@ -139,7 +156,7 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
             const int32_t sl = (int32_t)(y - base + 1024);
             cy = L.cc[sl]; ky = L.ck[sl]; ry = L.crd[sl];
           } else {
-            cy = d.creator[y]; ky = d.index[y]; ry = d.round[y];
+            cy = d.creator[y]; ky = d.index[y]; ry = __builtin_nontemporal_load(d.round + y);
           }
           return (L.done[cy] && ky >= L.bfirst[cy]) ? r0 : ry;
         };
@@ -148,60 +165,61 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
         const bool op_empty = op < 0 && !(L.cfl[xi] & 2);  // no other-parent at all
         int32_t pr;
         if (sp < 0 && (oth || op_empty)) {
-          pr = -1 - d.root_next[c];  // attached to the Root: NextRound by fiat (encoded < 0)
+          pr = -1 - L.rnext[c];  // attached to the Root: NextRound by fiat (encoded < 0)
         } else {
-          pr = sp < 0 ? d.root_sp_round[c] : round_of(sp);
-          if (oth) pr = max(pr, d.root_next[c]);
+          pr = sp < 0 ? L.rspr[c] : round_of(sp);
+          if (oth) pr = max(pr, L.rnext[c]);
           else if (op >= 0) pr = max(pr, round_of(op));
         }
         L.pr = pr;
         L.ss = 0;
+        L.nvis++;
       }
-      __syncthreads();
+      lds_barrier();
+      const unsigned long long q1t = dg ? __builtin_amdgcn_s_memtime() : 0;
       const int32_t pr = L.pr;
       if (pr >= 0 && pr < r0 && pr >= rlo) {
         // #witnesses of round pr that x strongly sees (_stronglySee :172-191)
+        // the round's witnesses' FD rows, chain-major (wfd, written as each
+        // witness is found): a wave takes every 16th chain, loads all its
+        // rows' columns first, then counts columns by ballot
         const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
-        if (cached) {
-          if (L.cache_r != pr) {  // stage round pr's witness FD rows
-            __syncthreads();
-            if (t == 0) {
-              int32_t k = 0;
-              for (int q = 0; q < n; ++q)
-                if (wrow[q] >= 0) L.wl[k++] = wrow[q];
-              L.cache_nw = k;
-            }
-            __syncthreads();
-            const int32_t nw = L.cache_nw;
-            for (int p = t; p < nw * n; p += 1024) {
-              const int32_t jw = p / n, i = p - jw * n;
-              L.fdc[jw][i] = d.fdt[fdt_pos(d.epos[L.wl[jw]], i, npad)];
-            }
-            __syncthreads();
-            if (t == 0) L.cache_r = pr;
-            __syncthreads();
-          }
-          const int32_t nw = L.cache_nw;
-          for (int jw = wave; jw < nw; jw += 16) {
-            int cntc = (lane < n && la0 >= L.fdc[jw][lane]) + (lane + 64 < n && la1 >= L.fdc[jw][lane + 64]);
+        const int32_t *frow = d.wfd + (int64_t)(pr - rlo) * n * npad;
+        int ssw = 0;
+        for (int q0 = wave; q0 < n; q0 += 16 * 8) {
+          int32_t f0[8], f1[8];
+          bool has[8];
+          // every load of the batch issued at once (one L2 round trip): rows of
+          // absent witnesses are read too and masked after.  L2-served loads:
+          // this workgroup stored fw / wfd moments ago
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) cntc += __shfl_xor(cntc, off);
-            if (lane == 0 && cntc >= d.sm) atomicAdd(&L.ss, 1);
+          for (int u = 0; u < 8; ++u) {
+            const int q = min(q0 + 16 * u, n - 1);
+            const int32_t *fr = frow + (int64_t)q * npad;
+            has[u] = __builtin_nontemporal_load(wrow + q) >= 0 && q0 + 16 * u < n;
+            f0[u] = __builtin_nontemporal_load(fr + min(lane, npad - 1));
+            f1[u] = __builtin_nontemporal_load(fr + min(lane + 64, npad - 1));
           }
-        } else {
-          for (int q = wave; q < n; q += 16) {
-            const int32_t w = wrow[q];
-            if (w < 0) continue;
-            const int64_t rw = d.epos[w];
-            int cntc = 0;
-            for (int i = lane; i < n; i += 64) cntc += d.la[rx * npad + i] >= d.fdt[fdt_pos(rw, i, npad)];
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) cntc += __shfl_xor(cntc, off);
-            if (lane == 0 && cntc >= d.sm) atomicAdd(&L.ss, 1);
+          for (int u = 0; u < 8; ++u) {
+            if (!has[u] || lane >= n) f0[u] = FD_NONE;
+            if (!has[u] || lane + 64 >= n) f1[u] = FD_NONE;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            int cntc = __popcll(__ballot(la0 >= f0[u])) + __popcll(__ballot(la1 >= f1[u]));
+            for (int i0 = 128; i0 < n; i0 += 64) {  // chains beyond 128 (n <= 512)
+              const int i = i0 + lane;
+              cntc += __popcll(__ballot(has[u] && i < n &&
+                                        d.la[rx * npad + i] >= __builtin_nontemporal_load(frow + (int64_t)(q0 + 16 * u) * npad + i)));
+            }
+            ssw += has[u] && cntc >= d.sm;
           }
         }
+        if (lane == 0 && ssw) atomicAdd(&L.ss, ssw);
       }
-      __syncthreads();
+      lds_barrier();
+      const unsigned long long q2t = dg ? __builtin_amdgcn_s_memtime() : 0;
       if (t == 0) {
         int32_t r;
         if (pr < 0) r = -1 - pr;
@@ -213,8 +231,9 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
           if (++L.ndone == n) L.stop = 1;
         } else {
           const int32_t sp = L.csp[xi];
-          const int32_t spr = sp < 0 ? d.root_sp_round[c]
-                            : sp >= base - (base > 0 ? 1024 : 0) ? L.crd[sp - base + 1024] : d.round[sp];
+          const int32_t spr = sp < 0 ? L.rspr[c]
+                            : sp >= base - (base > 0 ? 1024 : 0) ? L.crd[sp - base + 1024]
+                                                                  : __builtin_nontemporal_load(d.round + sp);
           const bool w = r > spr;  // witness (hashgraph.go:281-296)
           d.round[x] = r;
           d.witness[x] = w ? 1 : 0;
@@ -222,12 +241,30 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
           d.rexists[r] = 1;
           if (w) {
             d.fw[(int64_t)(r - rlo) * n + c] = x;
-            if (r == L.cache_r) L.cache_r = -1;  // the cached round gained a witness
+            L.neww = x;
+            L.newslot = (r - rlo) * n + c;
           }
           L.fmax = max(L.fmax, r);
         }
       }
-      __syncthreads();
+      lds_barrier();
+      const unsigned long long q3t = dg ? __builtin_amdgcn_s_memtime() : 0;
+      if (L.neww >= 0) {  // a new witness: its FD row, chain-major, for the counts
+        const int64_t rw = L.cep[L.neww - base];
+        for (int i = t; i < npad; i += 1024)
+          d.wfd[(int64_t)L.newslot * npad + i] = i < n ? d.fdt[fdt_pos(rw, i, npad)] : FD_NONE;
+        __syncthreads();  // (stores then loads within the workgroup: one compute unit's cache)
+        if (t == 0) L.neww = -1;
+        __syncthreads();
+      }
+      if (dg) {  // phase cycles (BH_DIAG): pr, counts, results, witness rows
+        const unsigned long long q4t = __builtin_amdgcn_s_memtime();
+        d.diag[24] += q1t - q0t;
+        d.diag[25] += q2t - q1t;
+        d.diag[26] += q3t - q2t;
+        d.diag[27] += q4t - q3t;
+        d.diag[28] += 1;
+      }
     }
     if (L.stop) break;
   }
@@ -236,6 +273,9 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
   if (t == 0) {
     d.state[ST_RESUME] = r0;
     d.state[ST_FIATMAX] = L.fmax;
+    d.state[ST_FIATDONE] = L.ndone;
+    d.state[ST_FIATEV] = L.nvis;
+    d.state[ST_FIATCH] = L.nch;
   }
 }
 

@@ -40,6 +40,8 @@ for s in "$@"; do
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
     pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_" --cfg 3 ;;
     pmc4) step pmc_c4 1100 bash tools/pmc.sh c4 "k_" --cfg 4 ;;
+    bresetdiag) step bench_reset_diag 600 env BH_DIAG=1 BH_FIAT_DEBUG=1 python tools/bench_reset.py --n 128 --N 1000000 --block 2 --steps 1 ;;
+    bresetdbg) step bench_reset_dbg 600 env BH_FIAT_DEBUG=1 python tools/bench_reset.py --n 128 --N 1000000 --block 2 --steps 1 ;;
     breset) step bench_reset 600 python tools/bench_reset.py --n 128 --N 1000000 --block 2 --out gpurun_out/bench_reset_n128.json ;;
     breset32) step bench_reset32 600 python tools/bench_reset.py --n 32 --N 1000000 --seed 2980 --block 2 --out gpurun_out/bench_reset_n32.json ;;
     profreset) step prof_reset 600 bash -c 'export TMPDIR=/tmp; mkdir -p gpurun_out/prof_reset; rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_reset -o run -- python tools/bench_reset.py --n 128 --N 1000000 --block 2 --steps 1' ;;
