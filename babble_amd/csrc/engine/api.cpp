@@ -467,11 +467,11 @@ int rounds_loop(bh_handle *h) {
       fprintf(stderr, "[k_fiat] max round %d, chains done %d of %d, events visited %d, chunks %d (r0 %d)\n", fs[0], fs[1],
               d.n, fs[2], fs[3], d.r0);
       if (d.diag) {
-        unsigned long long g[5] = {0, 0, 0, 0, 0};
+        unsigned long long g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         HIPCHK(h, hipMemcpy(g, d.diag + 24, sizeof g, hipMemcpyDeviceToHost));
         const double e = (double)(g[4] ? g[4] : 1);
-        fprintf(stderr, "[k_fiat] cycles per event: pr %.0f, counts %.0f, results %.0f, witness rows %.0f (%llu events)\n",
-                g[0] / e, g[1] / e, g[2] / e, g[3] / e, g[4]);
+        fprintf(stderr, "[k_fiat] cycles per event: finalize + pr %.0f, witness rows %.0f, counts %.0f (%llu events); round stagings %llu\n",
+                g[0] / e, g[1] / e, g[2] / e, g[4], g[7]);
         HIPCHK(h, hipMemset(d.diag + 24, 0, sizeof g));
       }
     }

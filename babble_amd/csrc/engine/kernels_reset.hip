@@ -57,6 +57,8 @@ void launch_reset_coords(const Dev &d, hipStream_t s) {
 }
 
 constexpr int FI_MAXN = 512;
+constexpr int FI_CN = 128;
+constexpr int32_t PR_SKIP = INT32_MIN;  // L.pr of an event on a done chain (or none)  // one round's witness FD rows held in LDS up to this many chains
 
 // a workgroup barrier that waits for LDS traffic only: the per-event
 // hand-offs of k_fiat go through LDS, so loads in flight (the next event's
@@ -75,7 +77,12 @@ struct FiatLds {
   int32_t csp[1024], cop[1024], cep[1024];
   int8_t cfl[1024];
   int32_t rnext[FI_MAXN], rspr[FI_MAXN];  // Root.NextRound / SelfParent.Round
-  int32_t cnt, ndone, pr, ss, stop, fmax, nvis, nch, neww, newslot;
+  int32_t cnt, ndone, pr, ss, stop, fmax, nvis, nch, neww, newslot, cache_r;
+  // n <= FI_CN: round cache_r's witnesses (cw[q], -1 none) and their FD rows
+  // (fdc[q][i], FD_NONE past n), the counts' operand read from LDS: the whole
+  // round is read per event, which from global memory is a compute unit's
+  // load bandwidth (≈ 2k cycles per event at n = 128)
+  int32_t cw[FI_CN], fdc[FI_CN * FI_CN];
 };
 
 __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
@@ -88,7 +95,11 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
     L.rnext[c] = d.root_next[c];
     L.rspr[c] = d.root_sp_round[c];
   }
-  if (t == 0) { L.ndone = 0; L.stop = 0; L.fmax = -1; L.nvis = 0; L.nch = 0; L.neww = -1; }
+  if (t == 0) { L.ndone = 0; L.stop = 0; L.fmax = -1; L.nvis = 0; L.nch = 0; L.neww = -1; L.cache_r = -1; }
+  const bool cached = n <= FI_CN;
+  // thread 0: the event counted last, finalized at the next event
+  bool pend = false;
+  int32_t p_pr = 0, p_spr = 0, p_c = 0, p_k = 0, p_xi = 0;
   for (int i = t; i < 1024; i += 1024) L.cc[i] = -1;
   __syncthreads();
   for (int64_t base = 0; base < d.N; base += 1024) {
@@ -134,51 +145,132 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
       if (lane < n) nla0 = d.la[rx * npad + lane];
       if (lane + 64 < n) nla1 = d.la[rx * npad + lane + 64];
     }
-    for (int32_t j = 0; j < cnt; ++j) {
-      const int32_t xi = L.list[j];
-      const int32_t x = (int32_t)(base + xi), c = L.cc[1024 + xi];
+    // Event j: thread 0 first finalizes event j-1 (its round from the count
+    // j-1's waves left in L.ss: witness flag, fw, done) and then computes
+    // j's parent round pr; a new witness's FD row is copied; the waves count
+    // j's strongly-seen witnesses.  Two LDS barriers per event; j == cnt
+    // finalizes the chunk's last event only.
+    for (int32_t j = 0; j <= cnt; ++j) {
+      const bool have = j < cnt;
+      const int32_t xi = have ? L.list[j] : 0;
       const int32_t la0 = nla0, la1 = nla1;
       if (j + 1 < cnt) {
         const int64_t rn = L.cep[L.list[j + 1]];
         if (lane < n) nla0 = d.la[rn * npad + lane];
         if (lane + 64 < n) nla1 = d.la[rn * npad + lane + 64];
       }
-      if (L.done[c]) continue;  // uniform: done[] only changes behind barriers
       const int64_t rx = L.cep[xi];
       const bool dg = d.diag != nullptr && t == 0;
       const unsigned long long q0t = dg ? __builtin_amdgcn_s_memtime() : 0;
       if (t == 0) {
-        // round of an event before x: "at least r0" if its chain was done at
-        // or before it, else the round this pass gave it
-        auto round_of = [&](int32_t y) -> int32_t {
-          int32_t cy, ky, ry;
-          if (y >= base - (base > 0 ? 1024 : 0)) {
-            const int32_t sl = (int32_t)(y - base + 1024);
-            cy = L.cc[sl]; ky = L.ck[sl]; ry = L.crd[sl];
+        if (pend) {  // finalize the previous event
+          pend = false;
+          int32_t r;
+          if (p_pr < 0) r = -1 - p_pr;
+          else r = p_pr < r0 && L.ss >= d.sm ? p_pr + 1 : p_pr;
+          if (r >= r0) {  // it opens round >= r0 on its chain: the closed form's candidate
+            L.done[p_c] = 1;
+            L.bfirst[p_c] = p_k;
+            if (++L.ndone == n) L.stop = 1;
           } else {
-            cy = d.creator[y]; ky = d.index[y]; ry = __builtin_nontemporal_load(d.round + y);
+            const bool w = r > p_spr;  // witness (hashgraph.go:281-296)
+            d.round[base + p_xi] = r;
+            d.witness[base + p_xi] = w ? 1 : 0;
+            L.crd[1024 + p_xi] = r;
+            d.rexists[r] = 1;
+            if (w) {
+              d.fw[(int64_t)(r - rlo) * n + p_c] = (int32_t)(base + p_xi);
+              L.neww = (int32_t)(base + p_xi);
+              L.newslot = (r - rlo) * n + p_c;
+            }
+            L.fmax = max(L.fmax, r);
           }
-          return (L.done[cy] && ky >= L.bfirst[cy]) ? r0 : ry;
-        };
-        const int32_t sp = L.csp[xi], op = L.cop[xi];
-        const bool oth = L.cfl[xi] & 1;                 // Root.Others[x] names x's other-parent
-        const bool op_empty = op < 0 && !(L.cfl[xi] & 2);  // no other-parent at all
-        int32_t pr;
-        if (sp < 0 && (oth || op_empty)) {
-          pr = -1 - L.rnext[c];  // attached to the Root: NextRound by fiat (encoded < 0)
-        } else {
-          pr = sp < 0 ? L.rspr[c] : round_of(sp);
-          if (oth) pr = max(pr, L.rnext[c]);
-          else if (op >= 0) pr = max(pr, round_of(op));
+        }
+        int32_t pr = PR_SKIP;
+        const int32_t c = have ? L.cc[1024 + xi] : 0;
+        if (have && !L.done[c]) {
+          // round of an event before x: "at least r0" if its chain was done at
+          // or before it, else the round this pass gave it
+          auto round_of = [&](int32_t y) -> int32_t {
+            int32_t cy, ky, ry;
+            if (y >= base - (base > 0 ? 1024 : 0)) {
+              const int32_t sl = (int32_t)(y - base + 1024);
+              cy = L.cc[sl]; ky = L.ck[sl]; ry = L.crd[sl];
+            } else {
+              cy = d.creator[y]; ky = d.index[y]; ry = __builtin_nontemporal_load(d.round + y);
+            }
+            return (L.done[cy] && ky >= L.bfirst[cy]) ? r0 : ry;
+          };
+          const int32_t sp = L.csp[xi], op = L.cop[xi];
+          const bool oth = L.cfl[xi] & 1;                 // Root.Others[x] names x's other-parent
+          const bool op_empty = op < 0 && !(L.cfl[xi] & 2);  // no other-parent at all
+          // the self-parent's round (x's chain is not done: the round this pass gave it)
+          const int32_t spr = sp < 0 ? L.rspr[c] : round_of(sp);
+          if (sp < 0 && (oth || op_empty)) {
+            pr = -1 - L.rnext[c];  // attached to the Root: NextRound by fiat (encoded < 0)
+          } else {
+            pr = spr;
+            if (oth) pr = max(pr, L.rnext[c]);
+            else if (op >= 0) pr = max(pr, round_of(op));
+          }
+          pend = true;
+          p_pr = pr; p_spr = spr; p_c = c; p_k = L.ck[1024 + xi]; p_xi = xi;
+          L.ss = 0;
+          L.nvis++;
         }
         L.pr = pr;
-        L.ss = 0;
-        L.nvis++;
       }
       lds_barrier();
       const unsigned long long q1t = dg ? __builtin_amdgcn_s_memtime() : 0;
+      if (L.neww >= 0) {  // a new witness: its FD row, chain-major, for the counts
+        const int64_t rw = L.cep[L.neww - base];
+        const bool inc = cached && L.newslot / n + rlo == L.cache_r;  // the staged round gains a witness
+        const int q = L.newslot % n;
+        for (int i = t; i < npad; i += 1024) {
+          const int32_t v = i < n ? d.fdt[fdt_pos(rw, i, npad)] : FD_NONE;
+          d.wfd[(int64_t)L.newslot * npad + i] = v;
+          if (inc) L.fdc[q * FI_CN + i] = v;
+        }
+        if (inc && t == 0) L.cw[q] = L.neww;
+        __syncthreads();  // (stores then loads within the workgroup: one compute unit's cache)
+        if (t == 0) L.neww = -1;
+        __syncthreads();
+      }
+      const unsigned long long q2t = dg ? __builtin_amdgcn_s_memtime() : 0;
       const int32_t pr = L.pr;
-      if (pr >= 0 && pr < r0 && pr >= rlo) {
+      if (pr == PR_SKIP) continue;  // uniform
+      if (pr >= 0 && pr < r0 && pr >= rlo && cached) {
+        if (L.cache_r != pr) {  // stage round pr (chain-major rows, coalesced)
+          const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
+          const int32_t *frow = d.wfd + (int64_t)(pr - rlo) * n * npad;
+          for (int k = t; k < n * FI_CN; k += 1024) {
+            const int q = k / FI_CN, i = k % FI_CN;
+            L.fdc[k] = i < n ? frow[(int64_t)q * npad + i] : FD_NONE;
+          }
+          if (t < FI_CN) L.cw[t] = t < n ? wrow[t] : -1;
+          lds_barrier();
+          if (t == 0) L.cache_r = pr;
+          if (dg) d.diag[31] += 1;
+        }
+        // #witnesses of round pr that x strongly sees: a wave takes every 16th
+        // witness row (q = wave + 16u; rows past n are absent), a lane two
+        // columns; every LDS read of the wave issued before the first use
+        int32_t w[FI_CN / 16], f0[FI_CN / 16], f1[FI_CN / 16];
+#pragma unroll
+        for (int u = 0; u < FI_CN / 16; ++u) {
+          const int q = wave + 16 * u;
+          w[u] = L.cw[q];
+          f0[u] = L.fdc[q * FI_CN + lane];
+          f1[u] = L.fdc[q * FI_CN + lane + 64];
+        }
+        int ssw = 0;
+#pragma unroll
+        for (int u = 0; u < FI_CN / 16; ++u) {
+          const int cntc = __popcll(__ballot(la0 >= f0[u])) + __popcll(__ballot(la1 >= f1[u]));
+          ssw += w[u] >= 0 && wave + 16 * u < n && cntc >= d.sm;
+        }
+        if (lane == 0 && ssw) atomicAdd(&L.ss, ssw);
+      } else if (pr >= 0 && pr < r0 && pr >= rlo) {
         // #witnesses of round pr that x strongly sees (_stronglySee :172-191)
         // the round's witnesses' FD rows, chain-major (wfd, written as each
         // witness is found): a wave takes every 16th chain, loads all its
@@ -189,16 +281,17 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
         for (int q0 = wave; q0 < n; q0 += 16 * 8) {
           int32_t f0[8], f1[8];
           bool has[8];
-          // every load of the batch issued at once (one L2 round trip): rows of
-          // absent witnesses are read too and masked after.  L2-served loads:
-          // this workgroup stored fw / wfd moments ago
+          // every load of the batch issued at once (one cache round trip): rows
+          // of absent witnesses are read too and masked after.  Plain loads: this
+          // workgroup stored fw / wfd (write-through, one compute unit's L1), and
+          // a round's rows are re-read by every event that counts against it
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const int q = min(q0 + 16 * u, n - 1);
             const int32_t *fr = frow + (int64_t)q * npad;
-            has[u] = __builtin_nontemporal_load(wrow + q) >= 0 && q0 + 16 * u < n;
-            f0[u] = __builtin_nontemporal_load(fr + min(lane, npad - 1));
-            f1[u] = __builtin_nontemporal_load(fr + min(lane + 64, npad - 1));
+            has[u] = wrow[q] >= 0 && q0 + 16 * u < n;
+            f0[u] = fr[min(lane, npad - 1)];
+            f1[u] = fr[min(lane + 64, npad - 1)];
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
@@ -219,50 +312,11 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
         if (lane == 0 && ssw) atomicAdd(&L.ss, ssw);
       }
       lds_barrier();
-      const unsigned long long q2t = dg ? __builtin_amdgcn_s_memtime() : 0;
-      if (t == 0) {
-        int32_t r;
-        if (pr < 0) r = -1 - pr;
-        else r = pr < r0 && L.ss >= d.sm ? pr + 1 : pr;
-        const int32_t k = L.ck[1024 + xi];
-        if (r >= r0) {  // x opens round >= r0 on its chain: the closed form's candidate
-          L.done[c] = 1;
-          L.bfirst[c] = k;
-          if (++L.ndone == n) L.stop = 1;
-        } else {
-          const int32_t sp = L.csp[xi];
-          const int32_t spr = sp < 0 ? L.rspr[c]
-                            : sp >= base - (base > 0 ? 1024 : 0) ? L.crd[sp - base + 1024]
-                                                                  : __builtin_nontemporal_load(d.round + sp);
-          const bool w = r > spr;  // witness (hashgraph.go:281-296)
-          d.round[x] = r;
-          d.witness[x] = w ? 1 : 0;
-          L.crd[1024 + xi] = r;
-          d.rexists[r] = 1;
-          if (w) {
-            d.fw[(int64_t)(r - rlo) * n + c] = x;
-            L.neww = x;
-            L.newslot = (r - rlo) * n + c;
-          }
-          L.fmax = max(L.fmax, r);
-        }
-      }
-      lds_barrier();
-      const unsigned long long q3t = dg ? __builtin_amdgcn_s_memtime() : 0;
-      if (L.neww >= 0) {  // a new witness: its FD row, chain-major, for the counts
-        const int64_t rw = L.cep[L.neww - base];
-        for (int i = t; i < npad; i += 1024)
-          d.wfd[(int64_t)L.newslot * npad + i] = i < n ? d.fdt[fdt_pos(rw, i, npad)] : FD_NONE;
-        __syncthreads();  // (stores then loads within the workgroup: one compute unit's cache)
-        if (t == 0) L.neww = -1;
-        __syncthreads();
-      }
-      if (dg) {  // phase cycles (BH_DIAG): pr, counts, results, witness rows
-        const unsigned long long q4t = __builtin_amdgcn_s_memtime();
+      if (dg) {  // phase cycles (BH_DIAG): finalize + pr, witness rows, counts
+        const unsigned long long q3t = __builtin_amdgcn_s_memtime();
         d.diag[24] += q1t - q0t;
         d.diag[25] += q2t - q1t;
         d.diag[26] += q3t - q2t;
-        d.diag[27] += q4t - q3t;
         d.diag[28] += 1;
       }
     }
