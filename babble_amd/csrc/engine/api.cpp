@@ -1048,6 +1048,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.opdesc, (size_t)2 * (L + 128));  // k_flow32: int2 entries
   A(&d.lt_row, (size_t)L + 64);
   d.fd_cols = d.npad <= 128;
+  d.round_p8 = getenv("BH_ROUND_P8") ? std::clamp(atoi(getenv("BH_ROUND_P8")), 0, bh::P8_XMAX) : bh::P8_XMAX;
   if (d.fd_cols) {
     A(&d.ssm, R1 * n * 16);
     d.round_lpc = d.npad <= 64 ? 4 : 8;

@@ -26,6 +26,7 @@ namespace bh {
 constexpr int32_t UNSET = INT32_MIN;    // Go nil
 constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
 constexpr int32_t P16_MAXLEN = 65000;  // longest chain the 16-bit round loop takes
+constexpr int P8_XMAX = 126;  // largest window-relative LA of k_round_wide's 8-bit rows (bit 7 is the compare's)
 constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 8192;     // frames sorted in LDS up to this size (96 KiB)
 constexpr int FL_MAXN = 128;            // participants the dataflow sweep (k_flow) handles
@@ -112,6 +113,8 @@ struct Dev {
   // q * LPC / 64 = candidate (c, B[r][c]) strongly sees (q, B[r-1][q])
   unsigned long long *ssm;
   int32_t round_lpc;  // LPC of k_round2 (4 or 8)
+  int32_t round_p8;   // k_round_wide<*, true>: 8-bit window-relative rows where the window's LA spread is at most this
+                      // (P8_XMAX; BH_ROUND_P8=<x> lowers it to force the 16-bit fallback, 0: off)
   // [n][R_cap + 1][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
   // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])
   unsigned long long *ssw;

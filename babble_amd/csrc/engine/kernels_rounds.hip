@@ -99,6 +99,26 @@ __device__ __forceinline__ uint32_t pack_la16(int32_t a, int32_t b) {
   return (uint32_t)(a + 1) | ((uint32_t)(b + 1) << 16);
 }
 
+// 8-bit window-relative rows (k_round_wide, P16 windows whose LA spread fits):
+// per column i, base_i = max(LA[first window row][i], 0); a window row's LA
+// is x = LA + 1 - base in [0, 126] (LA is non-decreasing down the window, so
+// the last row bounds it), a candidate's FD f = min(max(FD + 1 - base, 0),
+// 127).  Then LA >= FD <=> x >= f: below the window's first row f = 0 <= x
+// (LA >= base > FD), past its last row f = 127 > x, exact in between.  Four
+// columns per dword, x stored with bit 7 set: ((x | 0x80) - f) & 0x80 is set
+// iff x >= f, with no borrow between bytes, counted by v_bcnt.
+// two 16-bit FD + 1 values (0xFFFF: none) less base (saturating), capped at 127
+__device__ __forceinline__ uint32_t fd8x2(uint32_t f, uint32_t b) {
+  uint32_t dd;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(dd) : "v"(f), "v"(b));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(dd) : "v"(dd), "v"(0x007F007Fu));
+  return dd;
+}
+// columns (lo.l, lo.h, hi.l, hi.h) as bytes 0..3
+__device__ __forceinline__ uint32_t pack8(uint32_t lo, uint32_t hi) {
+  return __builtin_amdgcn_perm(hi, lo, 0x06040200u);
+}
+
 template <int LPC>
 __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
@@ -267,6 +287,9 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   __shared__ int32_t hist[WROWS + 1];
   __shared__ int32_t sh_res, sh_nc;
   __shared__ int8_t tq_s[512];  // T_q of every candidate in the current window (ssw, n <= 512)
+  __shared__ uint32_t wbase2[256];  // P8: base of columns 2j, 2j + 1 as 16-bit pairs
+  __shared__ int32_t sh_wide;       // P8: some column's LA spread exceeds P8_XMAX (16-bit window)
+
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
@@ -293,11 +316,55 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   __syncthreads();
   int32_t wk0 = Bp[c];
   int32_t result = len;
+  constexpr int PP8 = PP / 2, WRS8 = LPC * (PP8 + 1);  // P8: 16-B pieces of 16 columns per lane
   for (;;) {
     const int wrows = min(WROWS, len - wk0);
     if (wrows <= 0) break;
+    bool p8 = false;
+    if constexpr (P16) {
+      if (d.round_p8) {
+        // P8 when every column's spread down the window fits (first row: the
+        // base, last row: the largest LA)
+        if (t == 0) sh_wide = 0;
+        __syncthreads();
+        const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
+        bool bad = false;
+        for (int j = t; j < 256; j += 256) {
+          const int i0 = 2 * j, i1 = 2 * j + 1;
+          const int32_t b0 = i0 < npad ? max(r0p[i0], 0) : 0, b1 = i1 < npad ? max(r0p[i1], 0) : 0;
+          wbase2[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+          if (i0 < npad) bad |= r1p[i0] + 1 - b0 > d.round_p8;
+          if (i1 < npad) bad |= r1p[i1] + 1 - b1 > d.round_p8;
+        }
+        if (__any(bad) && lane == 0) sh_wide = 1;
+        __syncthreads();
+        p8 = !sh_wide;
+      }
+    }
     __syncthreads();
-    {
+    if (p8) {
+      // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
+      constexpr int RP8 = LPC * PP8;
+      const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+      for (int i = t; i < wrows * RP8; i += 256) {
+        const int row = i / RP8, pc = i - row * RP8;
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
+          uint32_t v = 0x80808080u;
+          if (col < npad) {
+            const int4 a = src[row * q4 + col / 4];
+            const uint32_t b01 = wbase2[col / 2], b23 = wbase2[col / 2 + 1];
+            const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
+            const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
+            v = (x0 | (x1 << 8) | (x2 << 16) | (x3 << 24)) | 0x80808080u;
+          }
+          w[h] = v;
+        }
+        win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+      }
+    } else {
       constexpr int RP = LPC * PP;  // pieces per padded row
       const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
       for (int i = t; i < wrows * RP; i += 256) {
@@ -321,6 +388,52 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       int32_t bq = 0, lq = 0, sq = 0;
       if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
       const bool act = q < n && bq < lq;
+      int tw = WROWS;
+      if (p8) {
+        // the candidate's 16-bit FD row, window-relative 8-bit (fd8x2 / pack8)
+        const int f16q = (npad + 7) / 8;
+        const int4 *fr = reinterpret_cast<const int4 *>(d.fd16) + (int64_t)(act ? sq + bq : 0) * f16q + part * PP;
+        const int nvalid = f16q - part * PP;
+        const uint4 *bb = reinterpret_cast<const uint4 *>(wbase2) + part * PP;
+        uint32_t f8[4 * PP8];
+#pragma unroll
+        for (int u = 0; u < PP; ++u) {
+          const int4 v = fr[min(u, max(nvalid - 1, 0))];
+          const uint4 b = bb[u];
+          const bool ok = u < nvalid;
+          const uint32_t e0 = fd8x2(ok ? (uint32_t)v.x : 0xFFFFFFFFu, b.x), e1 = fd8x2(ok ? (uint32_t)v.y : 0xFFFFFFFFu, b.y);
+          const uint32_t e2 = fd8x2(ok ? (uint32_t)v.z : 0xFFFFFFFFu, b.z), e3 = fd8x2(ok ? (uint32_t)v.w : 0xFFFFFFFFu, b.w);
+          f8[2 * u] = pack8(e0, e1);
+          f8[2 * u + 1] = pack8(e2, e3);
+        }
+        const int4 *xb8 = win4 + part * (PP8 + 1);
+        auto ss8 = [&](int row) -> bool {
+          const int4 *x4 = xb8 + row * WRS8;
+          int4 x[PP8];
+#pragma unroll
+          for (int u = 0; u < PP8; ++u) x[u] = x4[u];
+          int ge = 0;
+#pragma unroll
+          for (int u = 0; u < PP8; ++u) {
+            ge += __builtin_popcount(((uint32_t)x[u].x - f8[4 * u]) & 0x80808080u);
+            ge += __builtin_popcount(((uint32_t)x[u].y - f8[4 * u + 1]) & 0x80808080u);
+            ge += __builtin_popcount(((uint32_t)x[u].z - f8[4 * u + 2]) & 0x80808080u);
+            ge += __builtin_popcount(((uint32_t)x[u].w - f8[4 * u + 3]) & 0x80808080u);
+          }
+          return group_total<LPC>(ge) >= sm;
+        };
+        if (ss8(wrows - 1)) {
+          int lo = 0, hi = wrows - 1;
+#pragma unroll
+          for (int it = 0; it < 5; ++it) {
+            const int mid = (lo + hi) >> 1;
+            const bool s = ss8(mid);
+            hi = s ? mid : hi;
+            lo = s ? lo : mid + 1;
+          }
+          tw = lo;
+        }
+      } else {
       int4 f[PP];
       if constexpr (P16) {
         const int f16q = (npad + 7) / 8;  // 16-B pieces per fd16 row
@@ -368,7 +481,6 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
         constexpr int COLS = LPC * PP * (P16 ? 8 : 4);  // columns per group, padding included
         return COLS - group_total<LPC>(lt) >= sm;
       };
-      int tw = WROWS;
       if (ss(wrows - 1)) {
         int lo = 0, hi = wrows - 1;
 #pragma unroll
@@ -379,6 +491,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
           lo = s ? lo : mid + 1;
         }
         tw = lo;
+      }
       }
       if (act && part == 0 && tw < WROWS) atomicAdd(&hist[tw], 1);
       if (d.ssw && part == 0 && q < n) tq_s[q] = (int8_t)(act ? tw : WROWS);

@@ -358,13 +358,20 @@ def test_chunk_sweep_wild(monkeypatch):
     _wild_parity(8, 30_000, 41, 25_000)
 
 
-@pytest.mark.parametrize("p16", [True, False])
+@pytest.mark.parametrize("rows", ["p8", "p8_mixed", "p16", "p32"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
-def test_wide_parity(monkeypatch, n, N, seed, p16):
+def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
-    over 16-bit rows (fd16; n = 300 has a half-filled last piece) and over
-    the 32-bit rows (BH_NO_P16, the path for chains beyond P16_MAXLEN)."""
-    if not p16:
+    over 8-bit window-relative rows (the default where a window's LA spread
+    fits; p8_mixed lowers the spread limit so windows alternate with the
+    16-bit fallback), over 16-bit rows (fd16; n = 300 has a half-filled last
+    piece) and over the 32-bit rows (BH_NO_P16, the path for chains beyond
+    P16_MAXLEN)."""
+    if rows == "p8_mixed":
+        monkeypatch.setenv("BH_ROUND_P8", "40")
+    if rows == "p16":
+        monkeypatch.setenv("BH_ROUND_P8", "0")
+    if rows == "p32":
         monkeypatch.setenv("BH_NO_P16", "1")
     _random_parity(n, N, seed)
 
