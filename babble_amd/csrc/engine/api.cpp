@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fd16, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
                   d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.wfd, d.rexists};
   for (void *p : ptrs)
@@ -1055,10 +1055,10 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   } else {
     A(&d.fd, (size_t)(C + 64) * d.npad);
     if (n <= 512) A(&d.ssw, R1 * n * 8);  // k_round_wide's masks for k_fame_masks<16>
-    if (n <= 512) A(&d.fd16, (size_t)(C + 64) * ((d.npad + 7) / 8 * 4));
   }
   A(&d.last_la, (size_t)(n + 1) * d.npad);
   A(&d.candfd, (size_t)2 * n * d.npad);
+  d.cand16 = !d.fd_cols && n <= 512 ? reinterpret_cast<uint32_t *>(d.candfd) : nullptr;  // (npad + 7) / 8 * 4 <= npad dwords a row
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);

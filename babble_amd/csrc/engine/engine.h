@@ -97,8 +97,9 @@ struct Dev {
   int32_t *Bp;     // [2][n] B[r] / B[r+1] by round parity
   // firstDescendants of every event (updateAncestorFirstDescendant)
   int32_t *fd;      // [la_rows + 64][npad] chain-major rows
-  uint32_t *fd16;   // [la_rows + 64][(npad + 7) / 8 * 4] the same rows as 16-bit FD + 1 (0xFFFF: none),
-                    // two per dword, for k_round_wide<*, true> (n <= 512, chains <= P16_MAXLEN)
+  uint32_t *cand16;  // [2][n][(npad + 7) / 8 * 4] k_round_wide<*, true>: the candidates' FD rows as 16-bit FD + 1
+                     // (0xFFFF: none), two per dword, by round parity -- gathered from FDT by the workgroup that
+                     // finds the candidate (the hand-off); aliases candfd (n > 128 only)
   int32_t *fdt;     // walk output, tiled by 64 chain-major rows (fdt_pos; shares la_ev's allocation)
   // fd_cols (npad <= 128): FDT is complete (the walks write MaxInt32 where
   // no event of a chain sees a row) and is the only per-event FD table; the
@@ -301,7 +302,7 @@ void launch_query(const Dev &d, int32_t kind, int64_t count, const int64_t *x, c
                   hipStream_t s);
 void configure_fd_kernels();
 void launch_first_descendants(const Dev &d, hipStream_t s, bool walked);
-// the 16-bit wide round loop applies (fd16 rows, chains <= P16_MAXLEN)
+// the 16-bit wide round loop applies (cand16 rows, chains <= P16_MAXLEN)
 bool round_p16(const Dev &d);  // fd from la (FDT already written by k_flow_transpose when walked)
 
 }  // namespace bh

@@ -163,12 +163,6 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
       o[u] = x;
     }
     if (d.fd_rows) *reinterpret_cast<int4 *>(d.fd + (row0 + r) * npad + i4) = make_int4(o[0], o[1], o[2], o[3]);
-    if (d.fd16) {  // FD + 1 as 16 bits, FD_NONE -> 0xFFFF (its + 1 wraps to 2^31)
-      auto h16 = [](int32_t v) { return min((uint32_t)v + 1u, 0xFFFFu); };
-      const int64_t w0 = (row0 + r) * ((npad + 7) / 8 * 4) + i4 / 2;
-      *reinterpret_cast<uint2 *>(d.fd16 + w0) = make_uint2(h16(o[0]) | h16(o[1]) << 16, h16(o[2]) | h16(o[3]) << 16);
-      if ((npad & 4) && i4 + 4 == npad) *reinterpret_cast<uint2 *>(d.fd16 + w0 + 2) = make_uint2(~0u, ~0u);
-    }
   }
 }
 
@@ -181,6 +175,9 @@ void launch_first_descendants(const Dev &d, hipStream_t s, bool walked) {
   if (d.fd_cols) return;  // FDT complete; no chain-major rows
   k_last_la_init<<<1, 256, 0, s>>>(d);
   k_last_la<<<d.n, 256, 0, s>>>(d);
+  // the 16-bit wide loop gathers its candidates' rows from the complete FDT
+  // (cand16); chain-major rows are written only for the 32-bit loop
+  if (!d.fd_rows) return;
   // tile rows: LDS is npad x (TR + 1) words, so wide groups take short
   // tiles and several workgroups per compute unit (the kernel is bound by
   // its loads' latency: n = 512 with 64-row tiles left one 4-wave workgroup

@@ -107,6 +107,19 @@ __device__ __forceinline__ uint32_t pack_la16(int32_t a, int32_t b) {
 // (LA >= base > FD), past its last row f = 127 > x, exact in between.  Four
 // columns per dword, x stored with bit 7 set: ((x | 0x80) - f) & 0x80 is set
 // iff x >= f, with no borrow between bytes, counted by v_bcnt.
+// the FD row of event `row` (chain-major) from FDT into dst as 16-bit FD + 1
+// pairs (cand16); every thread of the workgroup calls it
+__device__ __forceinline__ void gather_cand16(const Dev &d, int64_t row, uint32_t *dst) {
+  const int npad = d.npad, n = d.n, w = (npad + 7) / 8 * 4;
+  auto h16 = [](int32_t v) { return min((uint32_t)v + 1u, 0xFFFFu); };  // FD_NONE + 1 wraps to 2^31
+  for (int j = threadIdx.x; j < w; j += blockDim.x) {
+    const int i0 = 2 * j, i1 = 2 * j + 1;
+    const int32_t v0 = i0 < n ? d.fdt[fdt_pos(row, i0, npad)] : FD_NONE;
+    const int32_t v1 = i1 < n ? d.fdt[fdt_pos(row, i1, npad)] : FD_NONE;
+    dst[j] = h16(v0) | (h16(v1) << 16);
+  }
+}
+
 // two 16-bit FD + 1 values (0xFFFF: none) less base (saturating), capped at 127
 __device__ __forceinline__ uint32_t fd8x2(uint32_t f, uint32_t b) {
   uint32_t dd;
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // with immediate offsets, issued back to back, and 4 * PIECES compares.
 // Pieces past the row (pc >= q4) are -1 in LDS and FD_NONE in registers.
 //
-// P16: the same search over 16-bit rows (fd16, LA converted while staged):
+// P16: the same search over 16-bit rows (cand16, LA converted while staged):
 // lane `part` owns 8 pieces of 8 columns, half the LDS reads and 3/5 of the
 // compare work per probe.
 template <int LPC, bool P16>
@@ -392,7 +405,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       if (p8) {
         // the candidate's 16-bit FD row, window-relative 8-bit (fd8x2 / pack8)
         const int f16q = (npad + 7) / 8;
-        const int4 *fr = reinterpret_cast<const int4 *>(d.fd16) + (int64_t)(act ? sq + bq : 0) * f16q + part * PP;
+        const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
         const int nvalid = f16q - part * PP;
         const uint4 *bb = reinterpret_cast<const uint4 *>(wbase2) + part * PP;
         uint32_t f8[4 * PP8];
@@ -436,8 +449,8 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       } else {
       int4 f[PP];
       if constexpr (P16) {
-        const int f16q = (npad + 7) / 8;  // 16-B pieces per fd16 row
-        const int4 *fr = reinterpret_cast<const int4 *>(d.fd16) + (int64_t)(act ? sq + bq : 0) * f16q + part * PP;
+        const int f16q = (npad + 7) / 8;  // 16-B pieces per cand16 row
+        const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
         const int nvalid = f16q - part * PP;
 #pragma unroll
         for (int u = 0; u < PP; ++u) {
@@ -523,6 +536,9 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       if (lane == 0) d.ssw[((int64_t)c * (d.R_cap + 1) + r + 1) * 8 + (q0 >> 6) + wave] = m;
     }
   }
+  // the hand-off: the new candidate's FD row for the next iteration
+  if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap)
+    gather_cand16(d, (int64_t)cs + result, d.cand16 + ((int64_t)(p ^ 1) * n + c) * ((npad + 7) / 8 * 4));
   if (t == 0) {
     if (sh_nc == 0) {
       if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
@@ -848,9 +864,14 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
   const int32_t r0 = d.state[ST_RESUME];
   const int32_t b = d.B[(int64_t)r0 * d.n + c], len = d.chain_len[c], cs = d.chain_start[c];
   if (threadIdx.x == 0) d.Bp[c] = b;
-  int32_t *cf = d.candfd + (int64_t)c * d.npad;
-  if (b < len)
-    for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs + b, i, d.npad)] : FD_NONE;
+  if (b < len) {
+    if (d.fd_cols) {
+      int32_t *cf = d.candfd + (int64_t)c * d.npad;
+      for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs + b, i, d.npad)] : FD_NONE;
+    } else if (d.cand16 && !d.fd_rows) {
+      gather_cand16(d, (int64_t)cs + b, d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
+    }
+  }
   if (c == 0 && threadIdx.x == 0) {
     d.state[ST_CUR0] = r0;
     d.state[ST_CUR0 + 1] = 0;
@@ -884,12 +905,19 @@ void launch_fd_idle(const Dev &d, hipStream_t s) { k_fd_idle<<<d.n, 256, 0, s>>>
 
 bool round2_eligible(const Dev &d) { return d.fd_cols != 0; }
 
-// the 16-bit wide loop: fd16 rows exist (k_fd_transpose wrote them) and
+// the 16-bit wide loop: cand16 exists (n <= 512) and
 // every LA / FD value + 1 fits below 0xFFFF
-bool round_p16(const Dev &d) { return d.fd16 != nullptr && d.max_chain_len <= P16_MAXLEN && !getenv("BH_NO_P16"); }
+bool round_p16(const Dev &d) { return d.cand16 != nullptr && d.max_chain_len <= P16_MAXLEN && !getenv("BH_NO_P16"); }
+
+// candidate (c, 0) of every chain for the 16-bit wide loop
+__global__ __launch_bounds__(256) void k_cand16_init(Dev d) {
+  const int c = blockIdx.x;
+  if (d.chain_len[c] > 0) gather_cand16(d, d.chain_start[c], d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
+}
 
 void launch_round_init(const Dev &d, hipStream_t s) {
   if (round2_eligible(d)) k_round2_init<<<d.n, 256, 0, s>>>(d);
+  else if (d.cand16 && !d.fd_rows) k_cand16_init<<<d.n, 256, 0, s>>>(d);
 }
 
 static int lanes_per_candidate(int npad) {
@@ -925,7 +953,7 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   }
   const int lpc = lanes_per_candidate(d.npad);
   const bool wide = d.n > 256 / lpc;
-  if (wide && round_p16(d) && (lpc == 4 || lpc == 8)) {
+  if (wide && round_p16(d) && !d.fd_rows && (lpc == 4 || lpc == 8)) {
     const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
     if (lpc == 4) k_round_wide<4, true><<<d.n, 256, wb16, s>>>(d, p);
     else k_round_wide<8, true><<<d.n, 256, wb16, s>>>(d, p);
