@@ -359,7 +359,7 @@ int reset_coords(bh_handle *h, hipStream_t s) {
       h->sweep_kernel = "k_flow32";
     } else {
       bh::launch_floww(vb, s);
-      h->sweep_kernel = "k_floww";
+      h->sweep_kernel = bh::floww_kernel(d);
     }
     bh::launch_flow_transpose(vb, s);
     bh::launch_fd_idle(vb, s);
@@ -397,7 +397,7 @@ int rounds_coords(bh_handle *h) {
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
     bh::launch_floww(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
-    h->sweep_kernel = "k_floww";
+    h->sweep_kernel = bh::floww_kernel(d);
   } else {
     bh::launch_chunk_depth(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));

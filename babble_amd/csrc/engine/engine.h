@@ -248,6 +248,7 @@ void launch_flow_transpose(const Dev &d, hipStream_t s);
 // LA + LT rows; LA rows come from launch_flow_transpose, FD from kernels_fd
 bool floww_eligible(const Dev &d);
 void launch_floww(const Dev &d, hipStream_t s);
+const char *floww_kernel(const Dev &d);  // k_floww2 (two values per workgroup) or k_floww
 void launch_prep(const Dev &d, hipStream_t s);  // every event: chain table (gap rows -1), loop state
 void launch_chain_scatter(const Dev &d, int64_t e_begin, hipStream_t s);  // events [e_begin, N)
 void launch_coordinates(const Dev &d, hipStream_t s);  // = chunk_depth + la_sweep

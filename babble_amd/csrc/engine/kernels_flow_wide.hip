@@ -252,15 +252,303 @@ __global__ __launch_bounds__(64 * (FW_MAXN / 64 + FW_PW)) void k_floww(Dev d) {
   else floww_body<false>(d, L);
 }
 
+// ---------------------------------------------------------------------------
+// k_floww2: the same dataflow with two values per workgroup, so that n = 512
+// columns + LT need 256 workgroups -- one per compute unit, one pass -- where
+// k_floww's 513 take three (its LDS admits one workgroup per compute unit).
+// Every column follows the same schedule (a lane advances when the
+// other-parent's slot holds its event, whatever the column), so a lane
+// carries two values per step; the slot grows to 8 bytes and the value ring
+// shrinks to 16 events per chain:
+//   low dword  = generation (k / 16, 15 bits) << 17 | A + 1   (17 bits)
+//   high dword = B + 1 (32 bits), or B + 1 | (C + 1) << 16 for the one
+//                workgroup that carries three LA columns (MODE 1; chain
+//                positions < 65,535)
+// Workgroups: values 0 .. ncol - 1 are LA columns col0 + v, value ncol is LT
+// (always a B: the high dword's 32 bits).  ncol + 1 even: workgroup w takes
+// values 2w, 2w + 1; odd: workgroup 0 takes three columns and w >= 1 takes
+// 2w + 1, 2w + 2.  A step is one 8-byte slot read, one 8-byte ring write and
+// two (three) HBM stores.
+constexpr int F2_R = 16, F2_RS = F2_R + 1;
+constexpr uint32_t F2_VMASK = 0x1FFFFu;
+constexpr uint32_t F2_GNOOP = 0x7FFF, F2_GWAIT = 0x7FFE, F2_GINIT = 0x7FFF;
+
+__host__ __device__ constexpr uint32_t f2_desc(int32_t dch, int32_t j) {
+  return ((uint32_t)(j >> 4) << 17) | (uint32_t)((dch * F2_RS + (j & (F2_R - 1))) * 8);
+}
+__host__ __device__ constexpr uint32_t f2_noop(int n) { return (F2_GNOOP << 17) | (uint32_t)((n * F2_RS + F2_R - 1) * 8); }
+__host__ __device__ constexpr uint32_t f2_wait(int n) { return (F2_GWAIT << 17) | (uint32_t)((n * F2_RS + F2_R - 2) * 8); }
+
+__global__ void k_flow_descw2(Dev d) {
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  const int32_t o = d.op[e];
+  d.opdesc[d.epos[e]] = (int32_t)(o < 0 ? f2_noop(d.n) : f2_desc(d.creator[o], d.index[o]));
+}
+
+struct FlowLdsW2 {
+  uint2 vring[FW_MAXN + 1][F2_RS];  // 68 KiB, LDS offset 0
+  int32_t dring[FW_MAXN][FW_DRS];   // 66 KiB
+  int32_t filled[FW_MAXN], consumed[FW_MAXN], pub[FW_MAXN], cs[FW_MAXN];
+  int32_t abort_;
+};
+
+// MODE 0: LA columns A, B; 1: LA columns A, B, C (16-bit B, C); 2: LA column A, LT in B
+template <int MODE>
+__device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA, int colB, int colC) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = d.n;
+  const int nw = (n + 63) >> 6;
+  const int64_t stride = d.la_rows + 64;
+  int32_t *const outA = d.la_col + (int64_t)colA * stride;
+  int32_t *const outB = MODE == 2 ? d.lt_row : d.la_col + (int64_t)colB * stride;
+  int32_t *const outC = MODE == 1 ? d.la_col + (int64_t)colC * stride : outA;
+  for (int c = t; c < n; c += blockDim.x) {
+    const int32_t lo = d.seg_lo[c];
+    L.filled[c] = lo;
+    L.consumed[c] = lo;
+    L.pub[c] = lo;
+    L.cs[c] = d.chain_start[c];
+    for (int s = 0; s < F2_R; ++s) L.vring[c][s] = make_uint2(F2_GINIT << 17, 0u);  // matches no real event
+  }
+  for (int s = t; s < F2_R; s += blockDim.x) L.vring[n][s] = make_uint2(s == F2_R - 1 ? (F2_GNOOP << 17) : 0u, 0u);
+  if (t == 0) L.abort_ = 0;
+  __syncthreads();
+  lds_vint_w *filled = (lds_vint_w *)L.filled, *consumed = (lds_vint_w *)L.consumed, *pub = (lds_vint_w *)L.pub;
+  lds_vint_w *abort_ = (lds_vint_w *)&L.abort_;
+
+  if (wave >= nw) {
+    // ---------------- prefetch waves: descriptor rings (as k_floww) ----------------
+    constexpr int H = FW_MAXN / 64 / FW_PW;
+    const int h0 = (wave - nw) * H;
+    if (h0 >= (n + 63) / 64) return;
+    int32_t f[H], len[H], cs[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int c = lane + 64 * (h0 + h);
+      len[h] = c < n ? d.chain_len[c] : 0;
+      const int32_t lo = c < n ? d.seg_lo[c] : 0;
+      f[h] = lo & ~(FW_REFILL - 1);
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (;;) {
+      bool left = false;
+      bool need[H];
+      int32_t v[H][FW_REFILL];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int c = lane + 64 * (h0 + h);
+        const int32_t cons = c < n ? consumed[c] : 0;
+        need[h] = f[h] < len[h] && f[h] - cons <= FW_DR - FW_REFILL;
+        left |= f[h] < len[h];
+        const int32_t *src = d.opdesc + cs[h] + f[h];
+#pragma unroll
+        for (int i = 0; i < FW_REFILL; ++i) v[h][i] = need[h] ? __builtin_nontemporal_load(src + i) : 0;
+      }
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int c = lane + 64 * (h0 + h);
+        if (need[h]) {
+          int32_t *dst = &L.dring[c][f[h] & (FW_DR - 1)];
+#pragma unroll
+          for (int i = 0; i < FW_REFILL; ++i) dst[i] = v[h][i];
+          f[h] += FW_REFILL;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const int c = lane + 64 * (h0 + h);
+        if (c < n) filled[c] = min(f[h], len[h]);
+      }
+      if (!__any(left) || *abort_) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return;
+  }
+  int32_t stall = 0;
+
+  // ---------------- compute waves: one chain per lane ----------------
+  const int c = wave * 64 + lane;
+  const bool valid = c < n;
+  const int32_t len = valid ? d.chain_len[c] : 0;
+  const int cc = valid ? c : 0;
+  const int32_t incA = c == colA ? 1 : 0;
+  const int32_t incB = MODE == 2 ? 1 : (c == colB ? 1 : 0);
+  const int32_t incC = MODE == 1 && c == colC ? 1 : 0;
+  const uint32_t ring_c = (uint32_t)(cc * F2_RS * 8);
+  const uint32_t wscratch = (uint32_t)((n * F2_RS + (lane & 7)) * 8);  // slots 0..7 of the sentinel row
+  const uint32_t WAIT = f2_wait(n);
+  char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);
+  const int32_t *dring_c = &L.dring[cc][0];
+  const int64_t cso = valid ? d.chain_start[c] : 0;
+  int32_t k = valid ? d.seg_lo[c] : 0, curA = 0, curB = 0, curC = 0, lim = 0;
+  if (k > 0) {
+    curA = outA[cso + k - 1] + 1;
+    curB = outB[cso + k - 1] + 1;
+    if (MODE == 1) curC = outC[cso + k - 1] + 1;
+  } else if (MODE == 2 && valid && d.lt_seed) {
+    curB = d.lt_seed[c] + 1;  // a Reset root's SelfParent LamportTimestamp
+  }
+  int32_t k1 = k, k2 = k;
+  const bool dg = d.diag != nullptr && blockIdx.x == 0 && wave == 0;
+  const unsigned long long t_start = dg ? stamp() : 0;
+  int32_t step = 0;
+  uint32_t dsc = WAIT;
+  const int32_t ltclamp = min(d.flow_ltclamp, FW_LTCLAMP);
+#define F2_STEP()                                                                          \
+  do {                                                                                     \
+    const uint2 slot_ = *reinterpret_cast<const uint2 *>(lds + (dsc & 0x1FFFFu));          \
+    const int32_t kn_ = k + 1;                                                             \
+    const uint32_t dn_ = (uint32_t)dring_c[kn_ & (FW_DR - 1)];                             \
+    const bool ready_ = (slot_.x ^ dsc) < (1u << 17);                                      \
+    const int32_t a_ = max(curA, (int32_t)(slot_.x & F2_VMASK)) + incA;                    \
+    int32_t b_, c_ = 0;                                                                    \
+    uint32_t hi_;                                                                          \
+    if constexpr (MODE == 1) {                                                             \
+      b_ = max(curB, (int32_t)(slot_.y & 0xFFFFu)) + incB;                                 \
+      c_ = max(curC, (int32_t)(slot_.y >> 16)) + incC;                                     \
+      hi_ = (uint32_t)b_ | ((uint32_t)c_ << 16);                                           \
+    } else {                                                                               \
+      b_ = max(curB, (int32_t)slot_.y) + incB;                                             \
+      hi_ = (uint32_t)b_;                                                                  \
+    }                                                                                      \
+    const uint32_t wa_ = ready_ ? ring_c + ((uint32_t)(k & (F2_R - 1)) << 3) : wscratch;   \
+    *reinterpret_cast<uint2 *>(lds + wa_) = make_uint2(((uint32_t)(k >> 4) << 17) | (uint32_t)a_, hi_); \
+    if (ready_) {                                                                          \
+      outA[cso + k] = a_ - 1;                                                              \
+      outB[cso + k] = b_ - 1;                                                              \
+      if constexpr (MODE == 1) outC[cso + k] = c_ - 1;                                     \
+    }                                                                                      \
+    curA = ready_ ? a_ : curA;                                                             \
+    curB = ready_ ? b_ : curB;                                                             \
+    if constexpr (MODE == 1) curC = ready_ ? c_ : curC;                                    \
+    dsc = ready_ ? (kn_ < lim ? dn_ : WAIT) : dsc;                                         \
+    k = ready_ ? kn_ : k;                                                                  \
+  } while (0)
+  for (;;) {
+    // header: publish, limits, stalled descriptors, LT clamp, read-backs, exit
+    // (2 or 3 stores a step: vmcnt(24) covers the last 8 steps' stores)
+    if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if (valid) {
+      pub[c] = k2;
+      consumed[c] = k;
+    }
+    k2 = k1;
+    k1 = k;
+    lim = valid ? filled[cc] : 0;
+    if (dsc == WAIT && k < lim) dsc = (uint32_t)dring_c[k & (FW_DR - 1)];
+    if (MODE == 2 && __builtin_expect(__any(curB > ltclamp), 0)) {
+      if (curB > ltclamp) {
+        curB = ltclamp;
+        atomicMax(&d.state[ST_FLOWOVF], 1);
+      }
+    }
+    if (!__any(k < len)) break;
+    stall = __any(k != k2) ? 0 : stall + 1;
+    if (stall > FW_WATCHDOG || *abort_) {
+      if (lane == 0) {
+        *abort_ = 1;
+        atomicMax(&d.state[ST_FLOWOVF], 2);
+      }
+      break;
+    }
+    {
+      // a parent its ring has moved past: read it back once published
+      const uint32_t sa = dsc & 0x1FFFFu;
+      const uint32_t slot = *reinterpret_cast<const uint32_t *>(lds + sa);
+      const int32_t si = (int32_t)(sa >> 3), dd = si / F2_RS;
+      const int32_t jj = (int32_t)((dsc >> 17) << 4) | (si - dd * F2_RS);
+      const bool far = (slot & ~F2_VMASK) > (dsc & ~F2_VMASK) && dd < n && pub[dd] > jj;
+      if (__builtin_expect(__any(far), 0)) {
+        if (far) {
+          const int64_t pr = (int64_t)L.cs[dd] + jj;
+          // one asm statement: the compiler must not touch the destinations
+          // before the wait
+          int32_t va, vb, vc = -1;
+          if constexpr (MODE == 1)
+            asm volatile("global_load_dword %0, %3, off nt\n\tglobal_load_dword %1, %4, off nt\n\t"
+                         "global_load_dword %2, %5, off nt\n\ts_waitcnt vmcnt(0)"
+                         : "=&v"(va), "=&v"(vb), "=&v"(vc)
+                         : "v"(outA + pr), "v"(outB + pr), "v"(outC + pr)
+                         : "memory");
+          else
+            asm volatile("global_load_dword %0, %2, off nt\n\tglobal_load_dword %1, %3, off nt\n\ts_waitcnt vmcnt(0)"
+                         : "=&v"(va), "=&v"(vb)
+                         : "v"(outA + pr), "v"(outB + pr)
+                         : "memory");
+          const int32_t a = max(curA, va + 1) + incA, b = max(curB, vb + 1) + incB;
+          const int32_t c3 = MODE == 1 ? max(curC, vc + 1) + incC : 0;
+          const uint32_t hi = MODE == 1 ? ((uint32_t)b | ((uint32_t)c3 << 16)) : (uint32_t)b;
+          *reinterpret_cast<uint2 *>(lds + ring_c + ((uint32_t)(k & (F2_R - 1)) << 3)) =
+              make_uint2(((uint32_t)(k >> 4) << 17) | (uint32_t)a, hi);
+          outA[cso + k] = a - 1;
+          outB[cso + k] = b - 1;
+          if (MODE == 1) outC[cso + k] = c3 - 1;
+          curA = a;
+          curB = b;
+          if (MODE == 1) curC = c3;
+          ++k;
+          dsc = k < lim ? (uint32_t)dring_c[k & (FW_DR - 1)] : WAIT;
+        }
+      }
+    }
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+    F2_STEP(); F2_STEP(); F2_STEP(); F2_STEP();
+    step += 8;
+  }
+#undef F2_STEP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (valid) {
+    pub[c] = len;
+    consumed[c] = len;
+  }
+  if (dg && lane == 0) {
+    d.diag[DG_FL_STEPS] = step;
+    d.diag[DG_FL_CYC] = stamp() - t_start;
+  }
+}
+
+__global__ __launch_bounds__(64 * (FW_MAXN / 64 + FW_PW)) void k_floww2(Dev d) {
+  __shared__ FlowLdsW2 L;  // static: the ring's LDS base is the constant 0
+  const int w = (int)blockIdx.x, nc = d.ncol, c0 = d.col0;
+  if (((nc + 1) & 1) == 0) {  // values 2w, 2w + 1
+    const int v = 2 * w;
+    if (v + 1 == nc) floww2_body<2>(d, L, c0 + v, 0, 0);
+    else floww2_body<0>(d, L, c0 + v, c0 + v + 1, 0);
+  } else if (w == 0) {
+    floww2_body<1>(d, L, c0, c0 + 1, c0 + 2);
+  } else {
+    const int v = 2 * w + 1;
+    if (v + 1 == nc) floww2_body<2>(d, L, c0 + v, 0, 0);
+    else floww2_body<0>(d, L, c0 + v, c0 + v + 1, 0);
+  }
+}
+
+// the two-value kernel: at least 4 columns (so that a three-column
+// workgroup and the LT workgroup are distinct); BH_FLOWW=1 keeps k_floww
+static bool floww2_on(const Dev &d) {
+  const bool off = getenv("BH_FLOWW") && atoi(getenv("BH_FLOWW")) == 1;
+  return !off && d.ncol >= 4;
+}
+
 bool floww_eligible(const Dev &d) {
   const char *e = getenv("BH_SWEEP");
   return d.n > FL_MAXN && d.n <= FW_MAXN && d.max_chain_len <= FW_MAXLEN && !(e && !strcmp(e, "chunk"));
 }
 
+const char *floww_kernel(const Dev &d) { return floww2_on(d) ? "k_floww2" : "k_floww"; }
+
 void launch_floww(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
-  if (d.N > d.e0) k_flow_descw<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
   const int nw = (d.n + 63) / 64;
+  if (floww2_on(d)) {
+    if (d.N > d.e0) k_flow_descw2<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+    k_floww2<<<(d.ncol + 1) / 2, (nw + FW_PW) * 64, 0, s>>>(d);
+    return;
+  }
+  if (d.N > d.e0) k_flow_descw<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
   k_floww<<<d.ncol + 1, (nw + FW_PW) * 64, 0, s>>>(d);
 }
 

@@ -415,14 +415,21 @@ def test_flow32_lt_fallback(monkeypatch):
     assert hg.results()["lamport"].max() > 300
 
 
-def test_floww_parity_and_lt_fallback(monkeypatch):
-    """The wide dataflow (k_floww, 128 < n <= 512): parity on random and
-    lagging DAGs against the oracle and against the chunked sweep, then with
-    a lowered LT limit that sends the timestamps to the sweep fallback."""
+@pytest.mark.parametrize("kernel", ["k_floww2", "k_floww"])
+def test_floww_parity_and_lt_fallback(monkeypatch, kernel):
+    """The wide dataflow (128 < n <= 512; k_floww2: two values per
+    workgroup, k_floww: one, BH_FLOWW=1): parity on random and lagging DAGs
+    against the oracle and against the chunked sweep -- n + 1 values odd (one
+    three-column workgroup) and even (pairs only) -- then with a lowered LT
+    limit that sends the timestamps to the sweep fallback."""
+    if kernel == "k_floww":
+        monkeypatch.setenv("BH_FLOWW", "1")
     hg = _random_parity(200, 30_000, 74, 0)
-    assert hg.profile_kernel() == "k_floww"  # not its watchdog's sweep fallback
+    assert hg.profile_kernel() == kernel  # not its watchdog's sweep fallback
+    hg = _random_parity(201, 30_000, 78, 2)
+    assert hg.profile_kernel() == kernel
     hg = _random_parity(512, 25_000, 75, 3)
-    assert hg.profile_kernel() == "k_floww"
+    assert hg.profile_kernel() == kernel
     _wild_parity(150, 30_000, 76, 20_000)
     monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
     hg = _random_parity(160, 20_000, 77, 2)

@@ -21,7 +21,8 @@ for s in "$@"; do
   case $s in
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
     treset) step pytest_reset 600 python -u -m pytest tests/test_gpu_reset.py -m gpu -v --timeout 120 --timeout-method thread -rf ;;
-    twide) step pytest_wide 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "wide or 512 or 300 or c4 or C4" ;;
+    twide) step pytest_wide 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "wide or 512 or 300 or c4 or C4 or floww" ;;
+    tfloww) step pytest_floww 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 300 --timeout-method thread -rf -x -k "floww" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench2) step bench_c2 600 python bench.py --cfg 2 --steps 3 --warmup 1 ;;
     bench3) step bench_c3 900 python bench.py --cfg 3 --steps 3 --warmup 1 ;;
