@@ -1030,7 +1030,8 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   // chain-major rows: with n <= 128 each chain's region keeps slack rows
   // (set_chain_tables) so appended events extend it in place and a call can
   // resume where the last one stopped; room for C/8 + 1024 per chain of it
-  const int64_t L = n <= bh::FL_MAXN ? C + C / 8 + (int64_t)n * 1024 : C;
+  // (a multiple of 64 rows: LA columns start 16-B aligned for k_floww2's 4-row stores)
+  const int64_t L = ((n <= bh::FL_MAXN ? C + C / 8 + (int64_t)n * 1024 : C) + 63) & ~(int64_t)63;
   A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, (size_t)L); A(&d.epos, C);
   d.la_rows = L;
   A(&d.la, (size_t)(L + 64) * d.npad);

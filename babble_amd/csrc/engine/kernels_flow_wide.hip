@@ -390,7 +390,71 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
   } else if (MODE == 2 && valid && d.lt_seed) {
     curB = d.lt_seed[c] + 1;  // a Reset root's SelfParent LamportTimestamp
   }
-  int32_t k1 = k, k2 = k;
+  // the stores: buffer stores at one per-lane byte offset (row * 4) into
+  // each value's column (wave-uniform descriptors: no 64-bit address math
+  // per store)
+  auto rsrc = [&](int32_t *p) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(stride * 4), 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rA = rsrc(outA), rB = rsrc(outB), rC = rsrc(outC);
+  // events [kf, k) are computed but not yet stored: the ring holds them (at
+  // most 3 + 9 < 16 at a header); a header stores complete 4-row groups
+  // (rows cso + kf = 0 mod 4: 16-B stores, a quarter of the store
+  // instructions -- each one touches 64 chains' lines, which is what bounds a
+  // step) and single rows at a chain's ends
+  int32_t kf = k;
+  auto slot_vals = [&](int32_t j, int32_t &a, int32_t &b, int32_t &c3) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(lds + ring_c + ((uint32_t)(j & (F2_R - 1)) << 3));
+    a = (int32_t)(v.x & F2_VMASK) - 1;
+    if constexpr (MODE == 1) {
+      b = (int32_t)(v.y & 0xFFFFu) - 1;
+      c3 = (int32_t)(v.y >> 16) - 1;
+    } else {
+      b = (int32_t)v.y - 1;
+      c3 = 0;
+    }
+  };
+  auto store1 = [&](int32_t j) {
+    int32_t a, b, c3;
+    slot_vals(j, a, b, c3);
+    const int o = (int)((cso + j) * 4);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)a, rA, o, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32((uint32_t)b, rB, o, 0, 0);
+    if constexpr (MODE == 1) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)c3, rC, o, 0, 0);
+  };
+  auto flush = [&](bool tail) {
+    for (;;) {  // rows before the first aligned group (a chain's start)
+      const bool go = kf < k && ((cso + kf) & 3) != 0;
+      if (!__any(go)) break;
+      if (go) { store1(kf); ++kf; }
+    }
+    for (;;) {
+      const bool go = kf + 4 <= k;
+      if (!__any(go)) break;
+      if (go) {
+        int32_t a[4], b[4], c3[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) slot_vals(kf + u, a[u], b[u], c3[u]);
+        const int o = (int)((cso + kf) * 4);
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)a[0], (unsigned)a[1], (unsigned)a[2], (unsigned)a[3]}, rA, o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)b[0], (unsigned)b[1], (unsigned)b[2], (unsigned)b[3]}, rB, o, 0, 0);
+        if constexpr (MODE == 1)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)c3[0], (unsigned)c3[1], (unsigned)c3[2], (unsigned)c3[3]}, rC, o, 0, 0);
+        kf += 4;
+      }
+    }
+    if (tail) {
+      for (;;) {
+        const bool go = kf < k;
+        if (!__any(go)) break;
+        if (go) { store1(kf); ++kf; }
+      }
+    }
+  };
+  int32_t hdr = 0, k1 = k, k2 = k;  // k at the previous two headers (the watchdog)
   const bool dg = d.diag != nullptr && blockIdx.x == 0 && wave == 0;
   const unsigned long long t_start = dg ? stamp() : 0;
   int32_t step = 0;
@@ -415,11 +479,6 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
     }                                                                                      \
     const uint32_t wa_ = ready_ ? ring_c + ((uint32_t)(k & (F2_R - 1)) << 3) : wscratch;   \
     *reinterpret_cast<uint2 *>(lds + wa_) = make_uint2(((uint32_t)(k >> 4) << 17) | (uint32_t)a_, hi_); \
-    if (ready_) {                                                                          \
-      outA[cso + k] = a_ - 1;                                                              \
-      outB[cso + k] = b_ - 1;                                                              \
-      if constexpr (MODE == 1) outC[cso + k] = c_ - 1;                                     \
-    }                                                                                      \
     curA = ready_ ? a_ : curA;                                                             \
     curB = ready_ ? b_ : curB;                                                             \
     if constexpr (MODE == 1) curC = ready_ ? c_ : curC;                                    \
@@ -427,14 +486,15 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
     k = ready_ ? kn_ : k;                                                                  \
   } while (0)
   for (;;) {
-    // header: publish, limits, stalled descriptors, LT clamp, read-backs, exit
-    // (2 or 3 stores a step: vmcnt(24) covers the last 8 steps' stores)
-    if constexpr (MODE == 1) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    if (valid) {
-      pub[c] = k2;
-      consumed[c] = k;
+    // header: publish, store, limits, stalled descriptors, LT clamp,
+    // read-backs, exit.  Every 4th header drains the stores and publishes
+    // what was stored before it (far readers read those from HBM)
+    if ((hdr++ & 3) == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (valid) pub[c] = kf;
     }
+    if (valid) consumed[c] = k;
+    flush(false);
     k2 = k1;
     k1 = k;
     lim = valid ? filled[cc] : 0;
@@ -483,9 +543,6 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
           const uint32_t hi = MODE == 1 ? ((uint32_t)b | ((uint32_t)c3 << 16)) : (uint32_t)b;
           *reinterpret_cast<uint2 *>(lds + ring_c + ((uint32_t)(k & (F2_R - 1)) << 3)) =
               make_uint2(((uint32_t)(k >> 4) << 17) | (uint32_t)a, hi);
-          outA[cso + k] = a - 1;
-          outB[cso + k] = b - 1;
-          if (MODE == 1) outC[cso + k] = c3 - 1;
           curA = a;
           curB = b;
           if (MODE == 1) curC = c3;
@@ -499,6 +556,7 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
     step += 8;
   }
 #undef F2_STEP
+  flush(true);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (valid) {
     pub[c] = len;

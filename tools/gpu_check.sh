@@ -39,6 +39,8 @@ for s in "$@"; do
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     bench4q) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    diag4) step diag_c4 900 env BH_DIAG=1 python bench.py --cfg 4 --steps 1 --warmup 0 --cpu-sample 0 ;;
+    diag4old) step diag_c4_old 900 env BH_DIAG=1 BH_FLOWW=1 python bench.py --cfg 4 --steps 1 --warmup 0 --cpu-sample 0 ;;
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
     pmc3) step pmc_c3 900 bash tools/pmc.sh c3 "k_" --cfg 3 ;;
     pmc4) step pmc_c4 1100 bash tools/pmc.sh c4 "k_" --cfg 4 ;;
