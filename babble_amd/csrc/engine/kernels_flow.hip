@@ -433,18 +433,35 @@ __device__ __forceinline__ void flow32_body(const Dev &d, FlowLds32 &L) {
       cs[h] = c < n ? d.chain_start[c] : 0;
       sp[h] = c < n ? d.seg_lo[c] : 0;
     }
+    // rows cs + sp = 0 mod 4 go out as one 16-B store of four events (a
+    // store instruction touches a line per chain whatever its width, so this
+    // quarters the wave's store work); a chain's first and last rows singly
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, (int)(stride * 4), 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    auto gen_ok = [](uint32_t v, int32_t j) { return (v ^ ((uint32_t)(j >> 7) << 21)) < (1u << 21); };
     for (int pass = 1;; ++pass) {
       bool left = false;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int c = min(lane + 64 * h, n);
         for (int it = 0; it < 8; ++it) {
-          const uint32_t v = L.vring[c][sp[h] & (F2_R - 1)];
-          const bool ok = sp[h] < len[h] && (v ^ ((uint32_t)(sp[h] >> 7) << 21)) < (1u << 21);
+          const int32_t j = sp[h];
+          const bool grp = ((cs[h] + j) & 3) == 0 && j + 4 <= len[h];
+          const uint32_t v3 = L.vring[c][(j + (grp ? 3 : 0)) & (F2_R - 1)];
+          const bool ok = j < len[h] && gen_ok(v3, j + (grp ? 3 : 0));
           if (!__any(ok)) break;
           if (ok) {
-            out[cs[h] + sp[h]] = (int32_t)(v & F2_VMASK) - 1;
-            ++sp[h];
+            if (grp) {
+              const uint32_t v0 = L.vring[c][j & (F2_R - 1)], v1 = L.vring[c][(j + 1) & (F2_R - 1)],
+                             v2 = L.vring[c][(j + 2) & (F2_R - 1)];
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  u32x4{(v0 & F2_VMASK) - 1u, (v1 & F2_VMASK) - 1u, (v2 & F2_VMASK) - 1u, (v3 & F2_VMASK) - 1u}, ro,
+                  (int)((cs[h] + j) * 4), 0, 0);
+              sp[h] = j + 4;
+            } else {
+              __builtin_amdgcn_raw_buffer_store_b32((v3 & F2_VMASK) - 1u, ro, (int)((cs[h] + j) * 4), 0, 0);
+              sp[h] = j + 1;
+            }
           }
         }
         left |= sp[h] < len[h];

@@ -36,6 +36,7 @@ for s in "$@"; do
     bench4tr32) step bench_c4_tr32 1100 env BH_FDT_TR=32 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench4x16) step bench_c4_x16 1100 env BH_XPOSE_TR=16 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench4tr64) step bench_c4_tr64 1100 env BH_FDT_TR=64 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    bench3p32) step bench_c3_p32 900 env BH_ROUND_P8=0 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     bench4q) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
