@@ -470,7 +470,8 @@ int rounds_loop(bh_handle *h) {
         unsigned long long g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         HIPCHK(h, hipMemcpy(g, d.diag + 24, sizeof g, hipMemcpyDeviceToHost));
         const double e = (double)(g[4] ? g[4] : 1);
-        fprintf(stderr, "[k_fiat] cycles per event: finalize + pr %.0f, witness rows %.0f, counts %.0f (%llu events); round stagings %llu\n",
+        fprintf(stderr, "[k_fiat] cycles per event (BH_FIAT=serial: finalize + pr, witness rows, counts) or per step "
+                "(level-synchronous: parents, counts, rounds): %.0f, %.0f, %.0f (%llu); round stagings %llu\n",
                 g[0] / e, g[1] / e, g[2] / e, g[4], g[7]);
         HIPCHK(h, hipMemset(d.diag + 24, 0, sizeof g));
       }

@@ -26,6 +26,9 @@
 // 1024 at a time.
 #include "engine.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace bh {
 
 __global__ __launch_bounds__(1024) void k_reset_coords(Dev d) {
@@ -57,8 +60,8 @@ void launch_reset_coords(const Dev &d, hipStream_t s) {
 }
 
 constexpr int FI_MAXN = 512;
-constexpr int FI_CN = 128;
-constexpr int32_t PR_SKIP = INT32_MIN;  // L.pr of an event on a done chain (or none)  // one round's witness FD rows held in LDS up to this many chains
+constexpr int FI_CN = 128;               // one round's witness FD rows held in LDS up to this many chains
+constexpr int32_t PR_SKIP = INT32_MIN;  // L.pr of an event on a done chain (or none)
 
 // a workgroup barrier that waits for LDS traffic only: the per-event
 // hand-offs of k_fiat go through LDS, so loads in flight (the next event's
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
           for (int u = 0; u < 8; ++u) {
             const int q = min(q0 + 16 * u, n - 1);
             const int32_t *fr = frow + (int64_t)q * npad;
-            has[u] = wrow[q] >= 0 && q0 + 16 * u < n;
+            has[u] = __builtin_nontemporal_load(wrow + q) >= 0 && q0 + 16 * u < n;  // (vector load: see fiat_count)
             f0[u] = fr[min(lane, npad - 1)];
             f1[u] = fr[min(lane + 64, npad - 1)];
           }
@@ -333,8 +336,200 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_fiat_ls: the same rounds, level-synchronously.  An event's round depends
+// only on its ancestors (the witnesses it can strongly see are ancestors:
+// LA[x][i] >= FD[w][i] means x has an ancestor descending from w), so any
+// topological order gives Go's rounds, and every event whose parents are
+// done can be computed at once.  A step: (A) each chain's next event, if its
+// other-parent is done, takes pr from its parents; (B) the counts, as items
+// (ready event, block of witnesses) spread over the waves, each item's
+// witness FD rows loaded at once from wfd; (C) one wave per ready event sets
+// its round and, for a new witness, writes its FD row to wfd and then fw --
+// after every count of the step (a same-step witness is no ancestor of a
+// same-step event, so it would count zero, but a half-written row must not
+// be read).  Steps ~ the fiat region's depth instead of its events.
+constexpr int FL_MAXREADY = FI_MAXN;
+
+struct FiatLsLds {
+  int32_t cur[FI_MAXN], done[FI_MAXN], bfirst[FI_MAXN], lastr[FI_MAXN];
+  int32_t rnext[FI_MAXN], rspr[FI_MAXN], len[FI_MAXN], cs[FI_MAXN];
+  int32_t rx[FL_MAXREADY], rc[FL_MAXREADY], rpr[FL_MAXREADY], rsp[FL_MAXREADY], ss[FL_MAXREADY];
+  int32_t rcnt[2], ndone, fmax, nvis, steps;
+};
+
+// #witnesses q0 .. q0 + IW - 1 of round pr that the event at chain-major row
+// xrow strongly sees (_stronglySee :172-191): LA row in registers (NV
+// 64-column groups), the IW witness FD rows loaded at once
+template <int NV, int IW>
+__device__ __forceinline__ int fiat_count(const Dev &d, int64_t xrow, int32_t pr, int q0, int lane) {
+  const int n = d.n, npad = d.npad, rlo = d.rlo;
+  int32_t la[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int i = lane + 64 * v;
+    la[v] = i < n ? d.la[xrow * npad + i] : -1;
+  }
+  const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
+  const int32_t *frow = d.wfd + (int64_t)(pr - rlo) * n * npad;
+  // which of the block's witnesses exist: one lane-indexed (vector) load --
+  // fw is stored by this kernel, and a wave-uniform load could be served by
+  // the scalar cache, which vector stores do not update
+  const int32_t wl = lane < IW && q0 + lane < n ? wrow[q0 + lane] : -1;
+  const unsigned long long hm = __ballot(wl >= 0);
+  int32_t f[IW][NV];
+#pragma unroll
+  for (int u = 0; u < IW; ++u) {
+    const int q = min(q0 + u, n - 1);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) f[u][v] = frow[(int64_t)q * npad + min(lane + 64 * v, npad - 1)];
+  }
+  int ssw = 0;
+#pragma unroll
+  for (int u = 0; u < IW; ++u) {
+    int cnt = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) cnt += __popcll(__ballot(lane + 64 * v < n && la[v] >= f[u][v]));
+    ssw += ((hm >> u) & 1) && cnt >= d.sm;
+  }
+  return ssw;
+}
+
+// NV: 64-column groups of a row (n <= 64 NV), one instantiation per width
+// (all four in one kernel spill registers)
+template <int NV>
+__global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
+  __shared__ FiatLsLds L;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, n = d.n, npad = d.npad;
+  const int32_t r0 = d.r0, rlo = d.rlo;
+  for (int c = t; c < n; c += 1024) {
+    L.cur[c] = 0;
+    L.done[c] = 0;
+    L.bfirst[c] = d.chain_len[c];
+    L.lastr[c] = 0;
+    L.rnext[c] = d.root_next[c];
+    L.rspr[c] = d.root_sp_round[c];
+    L.len[c] = d.chain_len[c];
+    L.cs[c] = d.chain_start[c];
+  }
+  if (t == 0) { L.rcnt[0] = L.rcnt[1] = 0; L.ndone = 0; L.fmax = -1; L.nvis = 0; L.steps = 0; }
+  __syncthreads();
+  const bool dg = d.diag != nullptr && t == 0;
+  for (int s = 0;; ++s) {
+    const int par = s & 1;
+    const unsigned long long q0t = dg ? __builtin_amdgcn_s_memtime() : 0;
+    // (A) each chain's next event, if its other-parent is done: the parents' round
+    if (t < n && !L.done[t] && L.cur[t] < L.len[t]) {
+      const int c = t, k = L.cur[c];
+      const int32_t x = d.chain_ids[L.cs[c] + k];
+      const int32_t op = d.op[x], sp = d.sp[x];
+      const int8_t fl = d.rflag[x];
+      bool ready = true;
+      int32_t opr = 0;
+      if (op >= 0) {
+        const int32_t cy = d.creator[op], ky = d.index[op];
+        ready = ky < L.cur[cy] || L.done[cy];
+        // a parent at or past its chain's first event of round >= r0 counts as r0
+        if (ready) opr = (L.done[cy] && ky >= L.bfirst[cy]) ? r0 : __builtin_nontemporal_load(d.round + op);
+      }
+      if (ready) {
+        const int32_t spr = sp < 0 ? L.rspr[c] : L.lastr[c];  // the self-parent: chain c's previous event
+        const bool oth = fl & 1, op_empty = op < 0 && !(fl & 2);
+        int32_t pr;
+        if (sp < 0 && (oth || op_empty)) {
+          pr = -1 - L.rnext[c];  // attached to the Root: NextRound by fiat (encoded < 0)
+        } else {
+          pr = spr;
+          if (oth) pr = max(pr, L.rnext[c]);  // Root.Others names the other-parent
+          else if (op >= 0) pr = max(pr, opr);
+        }
+        const int j = atomicAdd(&L.rcnt[par], 1);
+        L.rx[j] = x;
+        L.rc[j] = c;
+        L.rpr[j] = pr;
+        L.rsp[j] = spr;
+        L.ss[j] = 0;
+      }
+    }
+    __syncthreads();
+    const int cnt = L.rcnt[par];
+    if (cnt == 0) break;  // every chain done or exhausted
+    const unsigned long long q1t = dg ? __builtin_amdgcn_s_memtime() : 0;
+    // (B) counts: items (ready event j, a block of IW witnesses) over the waves
+    {
+      constexpr int IW = 64 / NV;  // witnesses per item (64 FD values per lane in flight)
+      const int per = (n + IW - 1) / IW;
+      for (int it = wave; it < cnt * per; it += 16) {
+        const int j = it / per, q0 = (it - j * per) * IW;
+        const int32_t pr = L.rpr[j];
+        if (!(pr >= 0 && pr < r0 && pr >= rlo)) continue;
+        const int32_t c = L.rc[j];
+        const int64_t xrow = (int64_t)L.cs[c] + L.cur[c];
+        const int ssw = fiat_count<NV, IW>(d, xrow, pr, q0, lane);
+        if (lane == 0 && ssw) atomicAdd(&L.ss[j], ssw);
+      }
+    }
+    __syncthreads();
+    const unsigned long long q2t = dg ? __builtin_amdgcn_s_memtime() : 0;
+    // (C) one wave per ready event: its round; a new witness's FD row, then fw
+    for (int j = wave; j < cnt; j += 16) {
+      const int32_t x = L.rx[j], c = L.rc[j], pr = L.rpr[j];
+      const int32_t k = L.cur[c];
+      const int64_t xrow = (int64_t)L.cs[c] + k;
+      const int32_t r = pr < 0 ? -1 - pr : (pr < r0 && L.ss[j] >= d.sm ? pr + 1 : pr);
+      const bool w = r < r0 && r > L.rsp[j];  // witness (hashgraph.go:281-296)
+      if (w) {
+        const int64_t slot = (int64_t)(r - rlo) * n + c;
+        for (int i = lane; i < npad; i += 64) d.wfd[slot * npad + i] = i < n ? d.fdt[fdt_pos(xrow, i, npad)] : FD_NONE;
+        if (lane == 0) d.fw[slot] = x;
+      }
+      if (lane == 0) {
+        atomicAdd(&L.nvis, 1);
+        if (r >= r0) {  // x opens round >= r0 on its chain: the closed form's candidate
+          L.done[c] = 1;
+          L.bfirst[c] = k;
+          atomicAdd(&L.ndone, 1);
+        } else {
+          d.round[x] = r;
+          d.witness[x] = w ? 1 : 0;
+          d.rexists[r] = 1;
+          L.lastr[c] = r;
+          L.cur[c] = k + 1;
+          atomicMax(&L.fmax, r);
+        }
+      }
+    }
+    if (t == 0) {
+      L.rcnt[par ^ 1] = 0;
+      L.steps = s + 1;
+    }
+    __syncthreads();  // (rounds / fw / wfd stored before the next step loads them)
+    if (dg) {  // phase cycles per step (BH_DIAG): A, B, C
+      const unsigned long long q3t = __builtin_amdgcn_s_memtime();
+      d.diag[24] += q1t - q0t;
+      d.diag[25] += q2t - q1t;
+      d.diag[26] += q3t - q2t;
+      d.diag[28] += 1;
+    }
+  }
+  for (int c = t; c < n; c += 1024) d.B[(int64_t)r0 * n + c] = L.bfirst[c];
+  if (t == 0) {
+    d.state[ST_RESUME] = r0;
+    d.state[ST_FIATMAX] = L.fmax;
+    d.state[ST_FIATDONE] = L.ndone;
+    d.state[ST_FIATEV] = L.nvis;
+    d.state[ST_FIATCH] = L.steps;
+  }
+}
+
+// BH_FIAT=serial: the event-by-event pass (A/B; the tests run both)
 void launch_fiat(const Dev &d, hipStream_t s) {
-  k_fiat<<<1, 1024, 0, s>>>(d);
+  const char *e = getenv("BH_FIAT");
+  if (e && !strcmp(e, "serial")) k_fiat<<<1, 1024, 0, s>>>(d);
+  else if (d.n <= 64) k_fiat_ls<1><<<1, 1024, 0, s>>>(d);
+  else if (d.n <= 128) k_fiat_ls<2><<<1, 1024, 0, s>>>(d);
+  else if (d.n <= 256) k_fiat_ls<4><<<1, 1024, 0, s>>>(d);
+  else k_fiat_ls<8><<<1, 1024, 0, s>>>(d);
 }
 
 }  // namespace bh

@@ -119,6 +119,15 @@ def test_reset_generated(n, N, seed, lag, block, batches):
     _run_pair(d, block, batches)
 
 
+@pytest.mark.parametrize("n,N,seed,lag,block,batches", [(16, 8000, 0xBA3, 5, 2, 1), (128, 20000, 0xBA6, 0, 3, 2),
+                                                        (160, 30000, 0xBA7, 0, 3, 2)])
+def test_reset_serial_fiat(monkeypatch, n, N, seed, lag, block, batches):
+    """The event-by-event fiat pass (BH_FIAT=serial, k_fiat) against the
+    oracle too: the default is the level-synchronous k_fiat_ls"""
+    monkeypatch.setenv("BH_FIAT", "serial")
+    _run_pair(DagArrays(Dag(n, N, seed, lagging=lag)), block, batches)
+
+
 @pytest.mark.parametrize("block,p", [(6, 0), (10, 2), (20, 1)])
 def test_reset_missing_rounds(block, p):
     """Roots whose NextRounds leave rounds below the block's empty: GetRound

@@ -37,6 +37,9 @@ for s in "$@"; do
     bench4x16) step bench_c4_x16 1100 env BH_XPOSE_TR=16 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench4tr64) step bench_c4_tr64 1100 env BH_FDT_TR=64 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench3p32) step bench_c3_p32 900 env BH_ROUND_P8=0 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench3s16) step bench_c3_s16 900 env BH_SEGMENTS=16 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench3s12) step bench_c3_s12 900 env BH_SEGMENTS=12 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench3s6) step bench_c3_s6 900 env BH_SEGMENTS=6 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     bench4q) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
