@@ -270,6 +270,9 @@ __global__ __launch_bounds__(64 * (FW_MAXN / 64 + FW_PW)) void k_floww(Dev d) {
 // 2w + 1, 2w + 2.  A step is one 8-byte slot read, one 8-byte ring write and
 // two (three) HBM stores.
 constexpr int F2_R = 16, F2_RS = F2_R + 1;
+// rows per store group (aligned on the row): at a header at most F2_G - 1
+// + 9 (8 steps and a read-back) events are unstored, within the 16-event ring
+constexpr int F2_G = 8;
 constexpr uint32_t F2_VMASK = 0x1FFFFu;
 constexpr uint32_t F2_GNOOP = 0x7FFF, F2_GWAIT = 0x7FFE, F2_GINIT = 0x7FFF;
 
@@ -400,10 +403,11 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
   };
   const __amdgpu_buffer_rsrc_t rA = rsrc(outA), rB = rsrc(outB), rC = rsrc(outC);
   // events [kf, k) are computed but not yet stored: the ring holds them (at
-  // most 3 + 9 < 16 at a header); a header stores complete 4-row groups
-  // (rows cso + kf = 0 mod 4: 16-B stores, a quarter of the store
+  // most F2_G - 1 + 9 <= 16 at a header); a header stores complete F2_G-row
+  // groups (rows cso + kf = 0 mod F2_G: 16-B stores, a quarter of the store
   // instructions -- each one touches 64 chains' lines, which is what bounds a
-  // step) and single rows at a chain's ends
+  // step -- and 32 B of a line at once, fewer partial-line evictions) and
+  // single rows at a chain's ends
   int32_t kf = k;
   auto slot_vals = [&](int32_t j, int32_t &a, int32_t &b, int32_t &c3) {
     const uint2 v = *reinterpret_cast<const uint2 *>(lds + ring_c + ((uint32_t)(j & (F2_R - 1)) << 3));
@@ -426,24 +430,27 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
   };
   auto flush = [&](bool tail) {
     for (;;) {  // rows before the first aligned group (a chain's start)
-      const bool go = kf < k && ((cso + kf) & 3) != 0;
+      const bool go = kf < k && ((cso + kf) & (F2_G - 1)) != 0;
       if (!__any(go)) break;
       if (go) { store1(kf); ++kf; }
     }
     for (;;) {
-      const bool go = kf + 4 <= k;
+      const bool go = kf + F2_G <= k;
       if (!__any(go)) break;
       if (go) {
-        int32_t a[4], b[4], c3[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) slot_vals(kf + u, a[u], b[u], c3[u]);
-        const int o = (int)((cso + kf) * 4);
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)a[0], (unsigned)a[1], (unsigned)a[2], (unsigned)a[3]}, rA, o, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)b[0], (unsigned)b[1], (unsigned)b[2], (unsigned)b[3]}, rB, o, 0, 0);
-        if constexpr (MODE == 1)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)c3[0], (unsigned)c3[1], (unsigned)c3[2], (unsigned)c3[3]}, rC, o, 0, 0);
-        kf += 4;
+#pragma unroll
+        for (int h = 0; h < F2_G; h += 4) {  // 16-B stores of one 32-B (F2_G rows) piece, back to back
+          int32_t a[4], b[4], c3[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) slot_vals(kf + h + u, a[u], b[u], c3[u]);
+          const int o = (int)((cso + kf + h) * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)a[0], (unsigned)a[1], (unsigned)a[2], (unsigned)a[3]}, rA, o, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)b[0], (unsigned)b[1], (unsigned)b[2], (unsigned)b[3]}, rB, o, 0, 0);
+          if constexpr (MODE == 1)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)c3[0], (unsigned)c3[1], (unsigned)c3[2], (unsigned)c3[3]}, rC, o, 0, 0);
+        }
+        kf += F2_G;
       }
     }
     if (tail) {
