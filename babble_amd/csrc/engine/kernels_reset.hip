@@ -350,12 +350,19 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
 // same-step event, so it would count zero, but a half-written row must not
 // be read).  Steps ~ the fiat region's depth instead of its events.
 constexpr int FL_MAXREADY = FI_MAXN;
+constexpr int FL_WC = 56 * 1024;   // 16-bit witness FD entries cached in LDS (112 KiB)
+constexpr int FL_WFL = 4096;       // witness presence flags ((r0 - rlo) n)
 
 struct FiatLsLds {
   int32_t cur[FI_MAXN], done[FI_MAXN], bfirst[FI_MAXN], lastr[FI_MAXN];
   int32_t rnext[FI_MAXN], rspr[FI_MAXN], len[FI_MAXN], cs[FI_MAXN];
   int32_t rx[FL_MAXREADY], rc[FL_MAXREADY], rpr[FL_MAXREADY], rsp[FL_MAXREADY], ss[FL_MAXREADY];
   int32_t rcnt[2], ndone, fmax, nvis, steps;
+  // the fiat rounds' witness FD rows as 16-bit FD + 1 (0xFFFF: none), when
+  // they fit ((r0 - rlo) n npad <= FL_WC and chains <= P16_MAXLEN), and
+  // their presence flags: the counts then read LDS instead of L2
+  uint16_t wc[FL_WC];
+  int8_t wfl[FL_WFL];
 };
 
 // #witnesses q0 .. q0 + IW - 1 of round pr that the event at chain-major row
@@ -397,6 +404,40 @@ __device__ __forceinline__ int fiat_count(const Dev &d, int64_t xrow, int32_t pr
 
 // NV: 64-column groups of a row (n <= 64 NV), one instantiation per width
 // (all four in one kernel spill registers)
+// fiat_count over the LDS copy: LA + 1 against FD + 1, 16-bit
+template <int NV, int IW>
+__device__ __forceinline__ int fiat_count_lds(const Dev &d, const uint16_t *wc, const int8_t *wfl, int64_t xrow,
+                                              int32_t pr, int q0, int lane) {
+  const int n = d.n, npad = d.npad, rlo = d.rlo;
+  int32_t la[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int i = lane + 64 * v;
+    la[v] = i < n ? d.la[xrow * npad + i] + 1 : 0;
+  }
+  const uint16_t *frow = wc + (int64_t)(pr - rlo) * n * npad;
+  const int8_t *wrow = wfl + (pr - rlo) * n;
+  // every LDS read of the item first (one round trip), then the compares
+  int32_t f[IW][NV];
+  const int32_t wl = lane < IW && q0 + lane < n ? wrow[q0 + lane] : 0;
+  const unsigned long long hm = __ballot(wl != 0);
+#pragma unroll
+  for (int u = 0; u < IW; ++u) {
+    const int q = min(q0 + u, n - 1);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) f[u][v] = frow[q * npad + min(lane + 64 * v, npad - 1)];
+  }
+  int ssw = 0;
+#pragma unroll
+  for (int u = 0; u < IW; ++u) {
+    int cnt = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) cnt += __popcll(__ballot(lane + 64 * v < n && la[v] >= f[u][v]));
+    ssw += ((hm >> u) & 1) && cnt >= d.sm;
+  }
+  return ssw;
+}
+
 template <int NV>
 __global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
   __shared__ FiatLsLds L;
@@ -413,6 +454,9 @@ __global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
     L.cs[c] = d.chain_start[c];
   }
   if (t == 0) { L.rcnt[0] = L.rcnt[1] = 0; L.ndone = 0; L.fmax = -1; L.nvis = 0; L.steps = 0; }
+  const bool cached = (int64_t)(r0 - rlo) * n * npad <= FL_WC && (r0 - rlo) * n <= FL_WFL && d.max_chain_len <= P16_MAXLEN;
+  if (cached)
+    for (int i = t; i < (r0 - rlo) * n; i += 1024) L.wfl[i] = 0;
   __syncthreads();
   const bool dg = d.diag != nullptr && t == 0;
   for (int s = 0;; ++s) {
@@ -465,7 +509,8 @@ __global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
         if (!(pr >= 0 && pr < r0 && pr >= rlo)) continue;
         const int32_t c = L.rc[j];
         const int64_t xrow = (int64_t)L.cs[c] + L.cur[c];
-        const int ssw = fiat_count<NV, IW>(d, xrow, pr, q0, lane);
+        const int ssw = cached ? fiat_count_lds<NV, IW>(d, L.wc, L.wfl, xrow, pr, q0, lane)
+                               : fiat_count<NV, IW>(d, xrow, pr, q0, lane);
         if (lane == 0 && ssw) atomicAdd(&L.ss[j], ssw);
       }
     }
@@ -480,8 +525,15 @@ __global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
       const bool w = r < r0 && r > L.rsp[j];  // witness (hashgraph.go:281-296)
       if (w) {
         const int64_t slot = (int64_t)(r - rlo) * n + c;
-        for (int i = lane; i < npad; i += 64) d.wfd[slot * npad + i] = i < n ? d.fdt[fdt_pos(xrow, i, npad)] : FD_NONE;
-        if (lane == 0) d.fw[slot] = x;
+        for (int i = lane; i < npad; i += 64) {
+          const int32_t v = i < n ? d.fdt[fdt_pos(xrow, i, npad)] : FD_NONE;
+          d.wfd[slot * npad + i] = v;
+          if (cached) L.wc[slot * npad + i] = (uint16_t)min((uint32_t)v + 1u, 0xFFFFu);  // FD_NONE + 1 wraps to 2^31
+        }
+        if (lane == 0) {
+          d.fw[slot] = x;
+          if (cached) L.wfl[slot] = 1;
+        }
       }
       if (lane == 0) {
         atomicAdd(&L.nvis, 1);
