@@ -53,6 +53,8 @@ void free_all(bh_handle *h) {
     if (e) (void)hipEventDestroy(e);
   for (auto &e : h->ev_sweep)
     if (e) (void)hipEventDestroy(e);
+  for (auto &e : h->ev_loop)
+    if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   for (auto &g : h->seg_graph)
@@ -173,6 +175,7 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   volatile int32_t *pin = h->pinned_state;
   pin[0] = 0;
   bool done = false;
+  HIPCHK(h, hipEventRecord(h->ev_loop[0], s));  // (after any wait queued on s: loop time only)
   const int64_t max_batches = (int64_t)v.R_cap / ITER_BATCH + 2;
   for (int64_t b = 0; b < max_batches && !done; ++b) {
     if (no_graph) {
@@ -187,7 +190,10 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
       if (pin[0]) done = true;
     }
   }
+  HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
   HIPCHK(h, hipStreamSynchronize(s));
+  float lms = 0;
+  if (hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
   (void)hipEventDestroy(done_ev[0]);
   (void)hipEventDestroy(done_ev[1]);
   HIPCHK(h, hipMemcpy(st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
@@ -680,6 +686,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
 
 int stage_rounds(bh_handle *h) {
   int rc;
+  h->loop_ms_acc = 0;
   if (h->group.empty()) {  // one shard: the segment pipeline when it applies
     Dev &d = h->d;
     d.N = (int64_t)h->h_creator.size();
@@ -1108,6 +1115,8 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   for (auto &e : h->ev)
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
   for (auto &e : h->ev_sweep)
+    if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
+  for (auto &e : h->ev_loop)
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.state, 0, bh::ST_COUNT * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.counters, 0, 4 * 8) != hipSuccess) rc = BH_ERR_DEVICE;
@@ -1748,7 +1757,8 @@ int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap) {
   for (int i = 0; i < NSTAGE && i < cap; ++i) ms[i] = h->stage_ms[i];
   if (cap > NSTAGE) ms[NSTAGE] = h->xchg_ms;
   if (cap > NSTAGE + 1) ms[NSTAGE + 1] = h->frames_ms;
-  return NSTAGE + 2;
+  if (cap > NSTAGE + 2) ms[NSTAGE + 2] = h->loop_ms_acc;
+  return NSTAGE + 3;
 }
 
 int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {

@@ -86,6 +86,8 @@ struct bh_handle {
   size_t sha_cap = 0;
   hipEvent_t ev[NSTAGE + 1]{};
   hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)
+  hipEvent_t ev_loop[2]{};   // around each round loop (run_round_loop): its device time, summed per run
+  float loop_ms = 0, loop_ms_acc = 0;
   float sweep_ms = 0;
   const char *sweep_kernel = "";
   float stage_ms[NSTAGE]{};

@@ -294,8 +294,9 @@ class Hashgraph:
 
     def stage_ms(self):
         """[coordinates, rounds, fame, round_received, order, exchange,
-        projection] ms of the last run (device events; exchange: host wall
-        time; projection: bh_config.frames only)."""
+        projection, round loop] ms of the last run (device events; exchange:
+        host wall time; projection: bh_config.frames only; round loop: its
+        launches' device time, overlapped or not)."""
         buf = (C.c_float * 8)()
         k = self._L.bh_get_stage_ms(self._h, buf, 8)
         return [float(buf[i]) for i in range(k)]

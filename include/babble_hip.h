@@ -199,7 +199,10 @@ int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x,
  * [0] coordinates+lamport, [1] rounds+witnesses, [2] fame, [3] round received,
  * [4] frames/order/blocks, [5] shard exchanges (host wall time, 0 for one
  * shard), [6] block projection (bh_config.frames: roots, Frame / Block JSON
- * and their hashes; 0 without); returns the number of entries */
+ * and their hashes; 0 without), [7] the round loop's own device time (its
+ * launches summed over the run's loops; [1] is the time the rounds stage
+ * adds after the coordinates, less when a pipeline overlaps them); returns
+ * the number of entries */
 int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap);
 /* kernel statistics of the last run for the roofline report: number of
  * round-loop iterations, coordinate sweep launches' average ms */
