@@ -175,7 +175,9 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   volatile int32_t *pin = h->pinned_state;
   pin[0] = 0;
   bool done = false;
-  HIPCHK(h, hipEventRecord(h->ev_loop[0], s));  // (after any wait queued on s: loop time only)
+  // the loop's own device time (bh_get_stage_ms entry 7; BH_LOOP_TIMING=0: off, A/B)
+  static const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
+  if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));  // (after any wait queued on s: loop time only)
   const int64_t max_batches = (int64_t)v.R_cap / ITER_BATCH + 2;
   for (int64_t b = 0; b < max_batches && !done; ++b) {
     if (no_graph) {
@@ -190,10 +192,10 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
       if (pin[0]) done = true;
     }
   }
-  HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
+  if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
   HIPCHK(h, hipStreamSynchronize(s));
   float lms = 0;
-  if (hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
+  if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
   (void)hipEventDestroy(done_ev[0]);
   (void)hipEventDestroy(done_ev[1]);
   HIPCHK(h, hipMemcpy(st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));

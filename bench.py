@@ -211,7 +211,9 @@ def main():
     round_kernel = "k_round2" if npad <= 128 else "k_round_wide"
     # the loop's own device time (stage 7): with the segment pipeline the
     # rounds stage [1] only counts what runs after the coordinates
-    loop_ms = float(stage_tot[7] / args.steps) if len(stage_tot) > 7 else float(stage_tot[1] / args.steps)
+    loop_ms = float(stage_tot[7] / args.steps) if len(stage_tot) > 7 else 0.0
+    if loop_ms <= 0:  # (BH_LOOP_TIMING=0: the rounds stage instead)
+        loop_ms = float(stage_tot[1] / args.steps)
     round_avg_ms = loop_ms / max(iters, 1)
     ev_per_launch = N / max(iters, 1)
     dom_alg = ev_per_launch * B

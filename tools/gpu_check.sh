@@ -40,6 +40,7 @@ for s in "$@"; do
     bench3s16) step bench_c3_s16 900 env BH_SEGMENTS=16 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench3s12) step bench_c3_s12 900 env BH_SEGMENTS=12 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench3s6) step bench_c3_s6 900 env BH_SEGMENTS=6 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench3nolt) step bench_c3_nolt 900 env BH_LOOP_TIMING=0 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     bench4q) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
