@@ -42,7 +42,7 @@ void free_all(bh_handle *h) {
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
                   d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
-                  d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.wfd, d.rexists};
+                  d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
@@ -209,6 +209,15 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
 static bool use_flow(const bh::Dev &d) {
   const char *e = getenv("BH_SWEEP");
   return bh::flow_eligible(d) && !(e && !strcmp(e, "chunk"));
+}
+
+// the 32-bit chain-major FD rows (n > 128), allocated the first time a path
+// that writes them runs (d.fd_rows): the default wide path never does
+int ensure_fd(bh_handle *h) {
+  Dev &d = h->d;
+  if (d.fd_cols || !d.fd_rows || d.fd) return BH_OK;
+  HIPCHK(h, hipMalloc((void **)&d.fd, (size_t)(d.la_rows + 64) * d.npad * 4));
+  return BH_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -431,8 +440,20 @@ int rounds_loop(bh_handle *h) {
     int32_t ovf = 0;
     HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
+    if (ovf == 2 && h->reset_on) {
+      // the watchdog counts stalled headers, not a proven deadlock (other
+      // work sharing the compute units can starve a wave): the Reset
+      // coordinates have no sweep fallback (it knows no Root seeds), so the
+      // dataflow runs once more before the call fails
+      HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
+      int rc2 = reset_coords(h, s);
+      if (rc2) return rc2;
+      HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+    }
     if (ovf && h->reset_on)
-      return h->fail(BH_ERR_CAPACITY, "the wide dataflow gave up on a Reset hashgraph (no sweep fallback with roots)");
+      return h->fail(BH_ERR_CAPACITY, ovf == 2 ? "the wide dataflow gave up twice on a Reset hashgraph"
+                                               : "Lamport timestamps beyond the wide dataflow's range after Reset");
     if (ovf == 2) {
       HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
       bh::launch_chunk_depth(d, s);
@@ -446,6 +467,7 @@ int rounds_loop(bh_handle *h) {
   // column-major LA; n > 128 then transposes FDT into chain-major FD rows
   if ((walked || wide_flow) && !h->reset_on) bh::launch_flow_transpose(d, s);  // (reset_coords transposed already)
   d.fd_rows = !((walked || wide_flow) && bh::round_p16(d));  // 32-bit fd rows only where read
+  if ((rc = ensure_fd(h))) return rc;
   bh::launch_first_descendants(d, s, walked || wide_flow);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[1], s));
@@ -508,6 +530,10 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
       bh::launch_chunk_depth(d, s);
       bh::launch_la_sweep(d, s);
       bh::launch_permute(d, s);
+      // its slabs share FDT's memory: the next query recomputes the
+      // coordinates, the next pass starts from scratch
+      h->coords_for = -1;
+      h->fdt_lost = true;
     } else {
       bh::launch_flow_lt_fallback(d, s);
     }
@@ -530,16 +556,15 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
 // Coordinates and rounds as a pipeline over K insertion-order prefixes
 // (segments): the coordinate kernels of prefix s + 1 run on stream2 while
 // the round loop runs prefix s on `stream`, resuming at the last round the
-// previous prefix fixed (k_resume_point).  Single shard, chain dataflow
-// path (k_flow32, n <= 128) only; a shard of a multi-process group too
-// (coordinates replicated).
+// previous prefix fixed (k_resume_point).  Chain dataflow paths only:
+// n <= 128 (k_flow32 + k_round2) and 128 < n <= 512 (k_floww2 + the 16-bit
+// k_round_wide over the complete FDT); every shard of a group whose
+// coordinates are replicated (the default) runs it on its own device.
 bool segments_eligible(const bh_handle *h) {
   const Dev &d = h->d;
-  // one shard per process replicates the coordinates and the round loop
-  // unless its LA columns are split (BH_SHARD_COORDS=columns): it runs the
-  // same pipeline as a lone handle, and only fame / frame sorts exchange
-  return h->group.empty() && (h->world == 1 || !h->shard_cols) && use_flow(d) && bh::flow32_eligible(d) &&
-         d.fd_cols && !h->reset_on;
+  if (h->shard_cols || h->reset_on) return false;
+  if (d.fd_cols) return use_flow(d) && bh::flow32_eligible(d);
+  return bh::floww_eligible(d) && bh::round_p16(d);
 }
 
 // segments for `events` new events: measured at C3 (10M events): 4
@@ -556,8 +581,11 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   int rc;
   Dev &d = h->d;  // the whole prefix: every segment's view derives from it
   const int n = d.n;
+  const bool wide = !d.fd_cols;  // k_floww2 + k_round_wide (cand16 from FDT)
+  if (wide) d.fd_rows = 0;
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
+  h->fdt_lost = false;
   if ((int)h->seg_ev.size() < 3 * K) {
     for (int i = (int)h->seg_ev.size(); i < 3 * K; ++i) {
       hipEvent_t e;
@@ -572,8 +600,8 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     bh::launch_prep(d, sc);
   } else {  // only the new events' chain-table entries; loop state kept
     bh::launch_chain_scatter(d, base, sc);
-    HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, sc));
   }
+  HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, sc));
   const int64_t N = d.N;
   std::vector<int64_t> Ns((size_t)K + 1, base);
   for (int k = 1; k <= K; ++k) Ns[(size_t)k] = base + (N - base) * k / K;
@@ -612,9 +640,14 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
     v.tile_list = dtl;
     v.ntiles = nt;
-    bh::launch_flow_desc(v, sc);
-    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
-    bh::launch_flow(v, sc);
+    if (wide) {
+      HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
+      bh::launch_floww(v, sc);  // the segment's descriptors, then k_floww2
+    } else {
+      bh::launch_flow_desc(v, sc);
+      HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
+      bh::launch_flow(v, sc);
+    }
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
     bh::launch_flow_transpose(v, sc);
     bh::launch_fd_idle(v, sc);
@@ -666,51 +699,85 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
       (void)hipEventElapsedTime(&cms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k]);
       int32_t r0 = 0;
       (void)hipMemcpy(&r0, rv.state + bh::ST_RESUME, 4, hipMemcpyDeviceToHost);
-      fprintf(stderr, "[seg %d] coords %.2f ms (k_flow32 %.2f) | loop %.2f ms, rounds %d, iters %d, next resume at %d\n", k,
-              cms, fms, lms, st[bh::ST_ROUNDS], st[bh::ST_ITERS], r0);
+      fprintf(stderr, "[seg %d] coords %.2f ms (%s %.2f) | loop %.2f ms, rounds %d, iters %d, next resume at %d\n", k,
+              cms, wide ? "k_floww2" : "k_flow32", fms, lms, st[bh::ST_ROUNDS], st[bh::ST_ITERS], r0);
     }
   }
   if (lt0) (void)hipEventDestroy(lt0);
   if (lt1) (void)hipEventDestroy(lt1);
   (void)hipEventDestroy(sr_mark);
+  if (wide && st[bh::ST_FLOWOVF] == 2) {
+    // k_floww2's watchdog left a segment's coordinates unfinished: the whole
+    // DAG again through the unpipelined passes (they fall back to the
+    // chunked sweep)
+    h->inc_valid = false;
+    h->segments_used = 1;
+    HIPCHK(h, hipStreamSynchronize(sc));
+    if ((rc = rounds_coords(h))) return rc;
+    return rounds_loop(h);
+  }
   h->coords_for = (int)N;
   float ms = 0;
   h->sweep_ms = 0;
   for (int k = 0; k < K; ++k)
     if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
-  h->sweep_kernel = "k_flow32";
+  h->sweep_kernel = wide ? bh::floww_kernel(d) : "k_flow32";
   if ((rc = rounds_tail(h, st, base))) return rc;
   h->n_coord = N;
   h->lens_coord = h->lens_h;
-  h->inc_valid = true;
+  h->inc_valid = !h->fdt_lost;
   return BH_OK;
+}
+
+// DivideRounds of one shard through the segment pipeline where it applies
+// (*used = false otherwise, with nothing launched).  A call that only
+// appended events resumes from the last one (the cost
+// follows the new events)
+int rounds_segmented(bh_handle *h, bool *used) {
+  int rc;
+  *used = false;
+  Dev &d = h->d;
+  d.N = (int64_t)h->h_creator.size();
+  if (d.N == 0) return BH_OK;
+  if ((rc = upload(h))) return rc;
+  if ((rc = set_chain_tables(h))) return rc;
+  if (!segments_eligible(h)) return BH_OK;
+  *used = true;
+  d.rows = h->layout_rows;
+  d.e0 = 0;
+  d.seg_lo = h->seg_zero;
+  const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
+  if (base == d.N) {  // nothing new to divide: DivideRounds changes nothing
+    h->stage = std::max(h->stage, 1);
+    return BH_OK;
+  }
+  h->inc_calls += base > 0;
+  return rounds_pipelined(h, segments_for(d.N - base), base);
 }
 
 int stage_rounds(bh_handle *h) {
   int rc;
-  h->loop_ms_acc = 0;
-  if (h->group.empty()) {  // one shard: the segment pipeline when it applies
-    Dev &d = h->d;
-    d.N = (int64_t)h->h_creator.size();
-    if (d.N > 0) {
-      if ((rc = upload(h))) return rc;
-      if ((rc = set_chain_tables(h))) return rc;
-      if (segments_eligible(h)) {
-        d.rows = h->layout_rows;
-        d.e0 = 0;
-        d.seg_lo = h->seg_zero;
-        h->xchg_ms = 0;
-        // a call that only appended events resumes from the last one
-        // (cost follows the new events)
-        const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
-        if (base == d.N) {  // nothing new to divide: DivideRounds changes nothing
-          h->stage = std::max(h->stage, 1);
-          return BH_OK;
-        }
-        h->inc_calls += base > 0;
-        return rounds_pipelined(h, segments_for(d.N - base), base);
-      }
-    }
+  h->xchg_ms = 0;
+  for (bh_handle *x : local_shards(h)) x->loop_ms_acc = 0;
+  if (!h->shard_cols) {
+    // every shard holds the whole DAG and computes the same coordinates and
+    // rounds: each runs the segment pipeline on its own device (one host
+    // thread per shard of an in-process group), so a group is never slower
+    // than one shard
+    int nused = 0;
+    std::vector<bh_handle *> sh = local_shards(h);
+    std::vector<char> used(sh.size(), 0);
+    rc = run_local(h, [&](bh_handle *x) {
+      bool u = false;
+      const int r = rounds_segmented(x, &u);
+      for (size_t i = 0; i < sh.size(); ++i)
+        if (sh[i] == x) used[i] = u;
+      return r;
+    });
+    if (rc) return rc;
+    for (char u : used) nused += u;
+    if (nused == (int)sh.size()) return BH_OK;
+    if (nused) return h->fail(BH_ERR_STATE, "shards disagree on the segment pipeline");
   }
   if ((rc = run_local(h, rounds_coords))) return rc;
   if (h->world > 1 && h->shard_cols && use_flow(h->d)) {
@@ -1037,11 +1104,12 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   };
   A(&d.creator, C); A(&d.index, C); A(&d.sp, C); A(&d.op, C); A(&d.ntx, C);
   A(&d.coin, C); A(&d.sigw, (size_t)C * 8);
-  // chain-major rows: with n <= 128 each chain's region keeps slack rows
-  // (set_chain_tables) so appended events extend it in place and a call can
-  // resume where the last one stopped; room for C/8 + 1024 per chain of it
-  // (a multiple of 64 rows: LA columns start 16-B aligned for k_floww2's 4-row stores)
-  const int64_t L = ((n <= bh::FL_MAXN ? C + C / 8 + (int64_t)n * 1024 : C) + 63) & ~(int64_t)63;
+  // chain-major rows: on the chain dataflow paths (n <= 512) each chain's
+  // region keeps slack rows (set_chain_tables) so appended events extend it
+  // in place and a call can resume where the last one stopped; room for
+  // C/8 + 1024 per chain of it (a multiple of 64 rows: LA columns start 16-B
+  // aligned for k_floww2's 4-row stores)
+  const int64_t L = ((n <= 512 ? C + C / 8 + (int64_t)n * 1024 : C) + 63) & ~(int64_t)63;
   A(&d.chain_start, n); A(&d.chain_len, n); A(&d.chain_ids, (size_t)L); A(&d.epos, C);
   d.la_rows = L;
   A(&d.la, (size_t)(L + 64) * d.npad);
@@ -1060,11 +1128,17 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.lt_row, (size_t)L + 64);
   d.fd_cols = d.npad <= 128;
   d.round_p8 = getenv("BH_ROUND_P8") ? std::clamp(atoi(getenv("BH_ROUND_P8")), 0, bh::P8_XMAX) : bh::P8_XMAX;
+  // ballot tables: every round from 0 (bh_reset moves the base up)
+  d.rbase = 0;
+  d.rspan = (int32_t)R1;
   if (d.fd_cols) {
     A(&d.ssm, R1 * n * 16);
     d.round_lpc = d.npad <= 64 ? 4 : 8;
   } else {
-    A(&d.fd, (size_t)(C + 64) * d.npad);
+    // chain-major 32-bit FD rows (fd) are allocated on first use (ensure_fd):
+    // only the 32-bit wide loop, n > 512 fame and the chunked sweep's
+    // queries read them; the 16-bit loop reads the complete FDT
+    d.fd = nullptr;
     if (n <= 512) A(&d.ssw, R1 * n * 8);  // k_round_wide's masks for k_fame_masks<16>
   }
   A(&d.last_la, (size_t)(n + 1) * d.npad);
@@ -1157,6 +1231,7 @@ void bh_destroy(bh_handle *h) {
 const char *bh_last_error(const bh_handle *h) { return h ? h->err.c_str() : "null handle"; }
 
 static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted);
+static inline uint64_t others_key(int32_t root, int32_t creator, int32_t index);
 
 int bh_insert_events(bh_handle *h, const bh_events *ev, int32_t *status, int64_t *n_accepted) {
   if (!h || !ev) return BH_ERR_INVALID;
@@ -1226,11 +1301,8 @@ static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_
               // ReadWireInfo: the creator's Root.Others entry with this
               // (CreatorID, Index) (:1435-1456), then checkOtherParent: the
               // entry keyed by the event's own hash must name the same hash
-              int32_t e1 = -1;
-              for (size_t q = 0; q < h->others.size() && e1 < 0; ++q) {
-                const auto &o = h->others[q];
-                if (o.root == c && o.creator == oslot && o.index == ev->other_parent_index[i]) e1 = (int32_t)q;
-              }
+              const auto i1 = h->oth_by_index.find(others_key(c, oslot, ev->other_parent_index[i]));
+              const int32_t e1 = i1 == h->oth_by_index.end() ? -1 : i1->second;
               if (e1 >= 0 && e2 >= 0 && !memcmp(h->others[(size_t)e1].hash, h->others[(size_t)e2].hash, 32)) {
                 oth = e2;
                 ext = true;
@@ -1353,35 +1425,71 @@ int bh_reset_consensus(bh_handle *h) {
   return BH_OK;
 }
 
-// the per-round tables for R_cap rounds (a Reset hashgraph starts at the
-// frame's round, so its tables must reach past it); contents start zeroed
-static int realloc_round_tables(bh_handle *h, int32_t R_cap) {
-  Dev &d = h->d;
-  void **pp[] = {(void **)&d.ssm, (void **)&d.ssw, (void **)&d.B, (void **)&d.wofs, (void **)&d.wcnt,
-                 (void **)&d.blocked, (void **)&d.frame_loaded, (void **)&d.decided, (void **)&d.nfam,
-                 (void **)&d.minla, (void **)&d.frame_cnt, (void **)&d.frame_ofs, (void **)&d.frame_cur,
-                 (void **)&d.blk_of_frame, (void **)&d.frame_ntx, (void **)&d.rexists};
-  const bool had_ssm = d.ssm != nullptr, had_ssw = d.ssw != nullptr;
-  for (void **p : pp)
-    if (*p) {
-      (void)hipFree(*p);
-      *p = nullptr;
-    }
-  d.R_cap = R_cap;
-  const size_t R1 = (size_t)R_cap + 1;
-  const int n = d.n;
+// The per-round tables for R_cap rounds (a Reset hashgraph starts at the
+// frame's round, so its tables must reach past it), allocated into `t`'s
+// fields (contents zeroed); the ballot tables hold only rounds [rbase,
+// R_cap].  On failure everything allocated here is freed and `t` keeps no
+// pointer of it.
+struct RoundTables {
+  unsigned long long *ssm = nullptr, *ssw = nullptr;
+  int32_t *B = nullptr, *wofs = nullptr, *wcnt = nullptr, *blocked = nullptr, *frame_loaded = nullptr, *nfam = nullptr,
+          *minla = nullptr, *frame_cnt = nullptr, *frame_ofs = nullptr, *frame_cur = nullptr, *blk_of_frame = nullptr;
+  int8_t *decided = nullptr, *rexists = nullptr;
+  int64_t *frame_ntx = nullptr;
+  void *all(int i) {
+    void *p[] = {ssm, ssw, B, wofs, wcnt, blocked, frame_loaded, nfam, minla, frame_cnt, frame_ofs, frame_cur,
+                 blk_of_frame, decided, rexists, frame_ntx};
+    return i < 16 ? p[i] : nullptr;
+  }
+  void free_all() {
+    for (int i = 0; i < 16; ++i)
+      if (void *p = all(i)) (void)hipFree(p);
+    *this = RoundTables{};
+  }
+};
+
+static int alloc_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int32_t rbase, bool ssm, bool ssw) {
+  const size_t R1 = (size_t)R_cap + 1, span = R1 - (size_t)rbase;
+  const int n = h->d.n;
   int rc = BH_OK;
-  auto A = [&](auto **p, size_t cnt, size_t esz) {
+  auto A = [&](auto **p, size_t cnt) {
     if (rc == BH_OK) rc = dalloc(h, p, cnt);
-    if (rc == BH_OK && hipMemset(*p, 0, std::max<size_t>(cnt, 1) * esz) != hipSuccess) rc = BH_ERR_DEVICE;
+    if (rc == BH_OK && hipMemset(*p, 0, std::max<size_t>(cnt, 1) * sizeof(**p)) != hipSuccess) rc = BH_ERR_DEVICE;
   };
-  if (had_ssm) A(&d.ssm, R1 * n * 16, 8);
-  if (had_ssw) A(&d.ssw, R1 * n * 8, 8);
-  A(&d.B, R1 * n, 4); A(&d.wofs, R1, 4); A(&d.wcnt, R1, 4); A(&d.blocked, R1, 4); A(&d.frame_loaded, R1, 4);
-  A(&d.decided, R1, 1); A(&d.nfam, R1, 4); A(&d.minla, R1 * d.npad, 4); A(&d.frame_cnt, R1, 4);
-  A(&d.frame_ofs, R1, 4); A(&d.frame_cur, R1, 4); A(&d.blk_of_frame, R1, 4); A(&d.frame_ntx, R1, 8);
-  A(&d.rexists, R1, 1);
-  return rc == BH_OK ? BH_OK : h->fail(rc, "round tables for %d rounds", R_cap);
+  if (ssm) A(&t.ssm, span * n * 16);
+  if (ssw) A(&t.ssw, span * n * 8);
+  A(&t.B, R1 * n); A(&t.wofs, R1); A(&t.wcnt, R1); A(&t.blocked, R1); A(&t.frame_loaded, R1);
+  A(&t.decided, R1); A(&t.nfam, R1); A(&t.minla, R1 * h->d.npad); A(&t.frame_cnt, R1);
+  A(&t.frame_ofs, R1); A(&t.frame_cur, R1); A(&t.blk_of_frame, R1); A(&t.frame_ntx, R1);
+  A(&t.rexists, R1);
+  if (rc != BH_OK) {
+    t.free_all();
+    return h->fail(rc, "round tables for %d rounds: %s", R_cap, h->err.c_str());
+  }
+  return BH_OK;
+}
+
+// the handle's round tables become t's (the old ones are freed)
+static void commit_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int32_t rbase) {
+  Dev &d = h->d;
+  void *old[] = {d.ssm, d.ssw, d.B, d.wofs, d.wcnt, d.blocked, d.frame_loaded, d.nfam, d.minla, d.frame_cnt,
+                 d.frame_ofs, d.frame_cur, d.blk_of_frame, d.decided, d.rexists, d.frame_ntx};
+  for (void *p : old)
+    if (p) (void)hipFree(p);
+  d.ssm = t.ssm; d.ssw = t.ssw; d.B = t.B; d.wofs = t.wofs; d.wcnt = t.wcnt; d.blocked = t.blocked;
+  d.frame_loaded = t.frame_loaded; d.nfam = t.nfam; d.minla = t.minla; d.frame_cnt = t.frame_cnt;
+  d.frame_ofs = t.frame_ofs; d.frame_cur = t.frame_cur; d.blk_of_frame = t.blk_of_frame; d.decided = t.decided;
+  d.rexists = t.rexists; d.frame_ntx = t.frame_ntx;
+  d.R_cap = R_cap;
+  d.rbase = rbase;
+  d.rspan = R_cap + 1 - rbase;
+  t = RoundTables{};
+}
+
+// Root.Others lookup by (root slot, creator slot, Index): ReadWireInfo's
+// search for an other-parent the Store does not hold (hashgraph.go:1435-1456)
+static inline uint64_t others_key(int32_t root, int32_t creator, int32_t index) {
+  return ((uint64_t)(uint32_t)root << 48) ^ ((uint64_t)(uint32_t)creator << 32) ^ (uint64_t)(uint32_t)index;
 }
 
 int bh_reset(bh_handle *h, const bh_roots *rt) {
@@ -1396,6 +1504,14 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
     return h->fail(BH_ERR_STATE, "bh_reset: one shard, block projection off");
   if (rt->round_received < 0 || rt->block_index < -1) return h->fail(BH_ERR_INVALID, "bh_reset: bad block");
   (void)hipSetDevice(h->device);
+  struct FailHook {  // the test hook covers this call only
+    bh_handle *h;
+    explicit FailHook(bh_handle *x) : h(x) {
+      const char *e = getenv("BH_TEST_FAIL_ALLOC");
+      h->fail_alloc_in = e && atoi(e) > 0 ? atoi(e) - 1 : -1;
+    }
+    ~FailHook() { h->fail_alloc_in = -1; }
+  } hook(h);
   Dev &d = h->d;
   const int n = d.n;
   int32_t F = -1, lo = INT32_MAX;
@@ -1410,13 +1526,9 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   if (F >= rt->round_received)
     return h->fail(BH_ERR_INVALID, "bh_reset: a root's round %d is not below the block's round %d", F,
                    rt->round_received);
-  h->base_h.resize((size_t)n);
-  h->next_h.assign(rt->next_round, rt->next_round + n);
-  h->sp_round_h.assign(rt->self_parent_round, rt->self_parent_round + n);
-  h->sp_lt_h.assign(rt->self_parent_lamport, rt->self_parent_lamport + n);
-  for (int c = 0; c < n; ++c) h->base_h[(size_t)c] = rt->self_parent_index[c] + 1;
-  h->others.clear();
-  h->oth_by_key.clear();
+  std::vector<bh_handle::Other> others;
+  std::unordered_map<std::string, int32_t> by_key;
+  std::unordered_map<uint64_t, int32_t> by_index;
   for (int32_t k = 0; k < rt->n_others; ++k) {
     bh_handle::Other o{};
     o.root = rt->other_root[k];
@@ -1430,30 +1542,52 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
     memcpy(o.hash, rt->other_hash + (size_t)k * 32, 32);
     std::string key((const char *)&o.root, 4);
     key.append((const char *)o.key, 32);
-    h->oth_by_key.emplace(key, (int32_t)h->others.size());  // a Go map holds one entry per key
-    h->others.push_back(o);
+    by_key.emplace(key, (int32_t)others.size());  // a Go map holds one entry per key
+    by_index.emplace(others_key(o.root, o.creator, o.index), (int32_t)others.size());  // the first match, as the scan
+    others.push_back(o);
   }
-  // the round tables reach past the block's round
   const int64_t C = std::max<int64_t>(h->cap, 1);
   const int64_t need = (int64_t)rt->round_received + C / d.sm + 2;
   if (need > INT32_MAX / 2) return h->fail(BH_ERR_CAPACITY, "bh_reset: round %d too large", rt->round_received);
+  const int32_t r0 = F + 1, rlo = std::max(0, lo);
+  const int32_t R_cap = (int32_t)std::max<int64_t>(d.R_cap, need);
+  // every allocation first; the handle changes only once all of them succeeded
+  RoundTables t;
   int rc;
-  if ((rc = realloc_round_tables(h, (int32_t)std::max<int64_t>(d.R_cap, need)))) return rc;
-  d.r0 = F + 1;
-  d.rlo = std::max(0, lo);
-  d.frame_lo = rt->round_received + 1;  // round_received's frame is the block itself (hashgraph.go:1063-1065)
-  auto up = [&](int32_t **p, const std::vector<int32_t> &v) -> int {
+  if ((rc = alloc_round_tables(h, t, R_cap, r0, d.ssm != nullptr, d.ssw != nullptr))) return rc;
+  int32_t *cb = nullptr, *ls = nullptr, *rn = nullptr, *rs = nullptr, *elt = nullptr, *fw = nullptr;
+  int8_t *rf = nullptr;
+  std::vector<int32_t> base_h((size_t)n);
+  for (int c = 0; c < n; ++c) base_h[(size_t)c] = rt->self_parent_index[c] + 1;
+  auto up = [&](int32_t **p, const int32_t *v) -> int {
     if (dalloc(h, p, (size_t)n)) return BH_ERR_DEVICE;
-    HIPCHK(h, hipMemcpy(*p, v.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(*p, v, (size_t)n * 4, hipMemcpyHostToDevice));
     return BH_OK;
   };
-  if ((rc = up(&d.chain_base, h->base_h)) || (rc = up(&d.lt_seed, h->sp_lt_h)) || (rc = up(&d.root_next, h->next_h)) ||
-      (rc = up(&d.root_sp_round, h->sp_round_h)))
+  if ((rc = up(&cb, base_h.data())) || (rc = up(&ls, rt->self_parent_lamport)) || (rc = up(&rn, rt->next_round)) ||
+      (rc = up(&rs, rt->self_parent_round)) || (rc = dalloc(h, &rf, (size_t)C)) || (rc = dalloc(h, &elt, (size_t)C)) ||
+      (rc = dalloc(h, &fw, (size_t)(r0 - rlo) * n))) {
+    for (void *p : {(void *)cb, (void *)ls, (void *)rn, (void *)rs, (void *)rf, (void *)elt, (void *)fw})
+      if (p) (void)hipFree(p);
+    t.free_all();
     return rc;
-  if ((rc = dalloc(h, &d.rflag, (size_t)C)) || (rc = dalloc(h, &d.ext_lt, (size_t)C)) ||
-      (rc = dalloc(h, &d.fw, (size_t)(d.r0 - d.rlo) * n)) ||
-      (rc = dalloc(h, &d.wfd, (size_t)(d.r0 - d.rlo) * n * d.npad)))
-    return rc;
+  }
+  // commit
+  commit_round_tables(h, t, R_cap, r0);
+  for (void *p : {(void *)d.chain_base, (void *)d.lt_seed, (void *)d.root_next, (void *)d.root_sp_round, (void *)d.rflag,
+                  (void *)d.ext_lt, (void *)d.fw})
+    if (p) (void)hipFree(p);
+  d.chain_base = cb; d.lt_seed = ls; d.root_next = rn; d.root_sp_round = rs; d.rflag = rf; d.ext_lt = elt; d.fw = fw;
+  d.r0 = r0;
+  d.rlo = rlo;
+  d.frame_lo = rt->round_received + 1;  // round_received's frame is the block itself (hashgraph.go:1063-1065)
+  h->base_h = std::move(base_h);
+  h->next_h.assign(rt->next_round, rt->next_round + n);
+  h->sp_round_h.assign(rt->self_parent_round, rt->self_parent_round + n);
+  h->sp_lt_h.assign(rt->self_parent_lamport, rt->self_parent_lamport + n);
+  h->others = std::move(others);
+  h->oth_by_key = std::move(by_key);
+  h->oth_by_index = std::move(by_index);
   h->reset_on = true;
   h->reset_lcr = rt->round_received;
   h->reset_block = rt->block_index;
@@ -1660,37 +1794,71 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
 
 // the coordinates of every inserted event on the device (they are produced
 // lazily by the first pass; a query between an insert and the next
-// DivideRounds computes them here)
+// DivideRounds computes them here).  Go's ancestor / see / stronglySee read
+// the Store and change no pass state, so neither does this: the stage and
+// the round loop's resume point stay, and on the chain dataflow paths (FDT
+// complete, the same values the next segment would write) the next
+// DivideRounds still resumes incrementally.
 static int ensure_coords(bh_handle *h) {
   Dev &d = h->d;
   const int64_t N = (int64_t)h->h_creator.size();
   if (h->coords_for != N) {
     int rc;
+    hipStream_t s = h->stream;
     if ((rc = upload(h))) return rc;
     d.N = N;
     d.e0 = 0;
     d.seg_lo = h->seg_zero;
     if ((rc = set_chain_tables(h))) return rc;
     d.rows = h->layout_rows;
-    bh::launch_prep(d, h->stream);
+    // the chain table only (launch_prep would also reset the loop state)
+    if (d.rows > 0) HIPCHK(h, hipMemsetAsync(d.chain_ids, 0xFF, (size_t)d.rows * 4, s));
+    bh::launch_chain_scatter(d, 0, s);
+    HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
     const bool walked = use_flow(d);
+    bool wide = !walked && bh::floww_eligible(d) && !h->reset_on;
+    bool keep = walked && !h->layout_changed && !h->reset_on;
+    if (h->reset_on) {
+      if ((rc = reset_coords(h, s))) return rc;
+      d.fd_rows = !bh::round_p16(d);
+    } else if (walked) {
+      d.fd_rows = 1;
+    } else if (wide) {
+      d.fd_rows = !bh::round_p16(d);
+      Dev full = d;
+      full.col0 = 0;
+      full.ncol = d.n;
+      bh::launch_floww(full, s);
+      int32_t ovf = 0;
+      HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      if (ovf) {  // the watchdog or the LT clamp: the chunked sweep below
+        HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
+        wide = false;
+      } else {
+        keep = !h->layout_changed && bh::round_p16(d);
+      }
+    }
+    if (!walked && !wide && !h->reset_on) d.fd_rows = 1;  // (the chunked sweep's FDT is not complete)
+    if ((rc = ensure_fd(h))) return rc;
     Dev full = d;  // every LA column, whatever this shard's share of the dataflow
     full.col0 = 0;
     full.ncol = d.n;
     if (h->reset_on) {
-      if ((rc = reset_coords(h, h->stream))) return rc;
-      d.fd_rows = full.fd_rows = !bh::round_p16(d);
-      bh::launch_first_descendants(full, h->stream, true);
+      bh::launch_first_descendants(full, s, true);
+    } else if (walked) {
+      bh::launch_flow_coordinates(full, s);
+      bh::launch_first_descendants(full, s, true);
+    } else if (wide) {
+      bh::launch_flow_transpose(full, s);
+      bh::launch_first_descendants(full, s, true);
     } else {
-      if (walked) bh::launch_flow_coordinates(full, h->stream);
-      else bh::launch_coordinates(full, h->stream);
-      d.fd_rows = full.fd_rows = 1;  // (the chunked sweep's FDT is not complete)
-      bh::launch_first_descendants(full, h->stream, walked);
+      bh::launch_coordinates(full, s);
+      bh::launch_first_descendants(full, s, false);
     }
-    h->inc_valid = false;  // the loop state no longer matches the layout / prefix
+    if (!keep) h->inc_valid = false;
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
-    h->stage = 0;
   }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return BH_OK;
@@ -1772,6 +1940,13 @@ int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {
 
 const char *bh_get_profile_kernel(const bh_handle *h) { return h ? h->sweep_kernel : ""; }
 
+int bh_get_pipeline(bh_handle *h, int32_t *segments, int64_t *incremental_calls) {
+  if (!h) return BH_ERR_INVALID;
+  if (segments) *segments = h->segments_used;
+  if (incremental_calls) *incremental_calls = h->inc_calls;
+  return BH_OK;
+}
+
 int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, int64_t count,
                    uint8_t *digests) {
   if (!h) return BH_ERR_INVALID;
@@ -1794,7 +1969,6 @@ int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, i
   const size_t need = nb + (size_t)count * (8 + 4 + 32);
   if (need > h->sha_cap) {
     if (h->sha_buf) (void)hipFree(h->sha_buf);
-  if (h->q_buf) (void)hipFree(h->q_buf);
     h->sha_buf = nullptr;
     h->sha_cap = 0;
     HIPCHK(h, hipMalloc((void **)&h->sha_buf, need));
@@ -1827,7 +2001,6 @@ int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig
   const size_t need = (size_t)count * (3 * 32 + 4 + 1) + (size_t)n_keys * 64 + 64;
   if (need > h->sha_cap) {  // shares the hashing scratch buffer
     if (h->sha_buf) (void)hipFree(h->sha_buf);
-  if (h->q_buf) (void)hipFree(h->q_buf);
     h->sha_buf = nullptr;
     h->sha_cap = 0;
     HIPCHK(h, hipMalloc((void **)&h->sha_buf, need));

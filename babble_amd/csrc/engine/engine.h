@@ -110,13 +110,18 @@ struct Dev {
   // the 16-bit loop runs on a complete FDT (k_flow_transpose walked it), and
   // FD readers then read FDT
   int32_t fd_rows;
-  // [n][R_cap + 1][16 waves] k_round2 ballots: lane (q * LPC) % 64 of wave
-  // q * LPC / 64 = candidate (c, B[r][c]) strongly sees (q, B[r-1][q])
+  // [n][rspan][16 waves] k_round2 ballots: lane (q * LPC) % 64 of wave
+  // q * LPC / 64 = candidate (c, B[r][c]) strongly sees (q, B[r-1][q]);
+  // row ballot_row(d, c, r).  The ballot tables hold rounds [rbase, rbase +
+  // rspan): the round loop only writes rounds above the first one it
+  // starts from (0, or a Reset hashgraph's r0), so a Reset at a high round
+  // does not pay for the rounds below it
   unsigned long long *ssm;
+  int32_t rbase, rspan;
   int32_t round_lpc;  // LPC of k_round2 (4 or 8)
   int32_t round_p8;   // k_round_wide<*, true>: 8-bit window-relative rows where the window's LA spread is at most this
                       // (P8_XMAX; BH_ROUND_P8=<x> lowers it to force the 16-bit fallback, 0: off)
-  // [n][R_cap + 1][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
+  // [n][rspan][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
   // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])
   unsigned long long *ssw;
   int32_t *last_la; // [n][npad] LA row of each chain's last event
@@ -162,14 +167,19 @@ struct Dev {
   // The closed form of the round loop holds from round r0 = F + 1 on, F the
   // highest NextRound / SelfParent.Round of a root;
   // k_fiat computes rounds below it event by event.  fw[(r - rlo) * n + c]:
-  // chain c's witness of fiat round r (-1: none); rexists[r]: round r < r0
-  // has an event (RoundInfo exists, inmem_store.go:185-191).
+  // chain c's witness of fiat round r (-1: none; its FD row is read from
+  // FDT, so the table costs one word per (round, chain) whatever n);
+  // rexists[r]: round r < r0 has an event (RoundInfo exists,
+  // inmem_store.go:185-191).
   int32_t r0, rlo;
   int32_t *fw;
-  int32_t *wfd;  // [(r0 - rlo) * n][npad]: FD row of fw's witness (k_fiat's stronglySee counts)
   int8_t *rexists;
   int32_t frame_lo;  // frames below it are never emitted (Reset: LastConsensusRound's, hashgraph.go:1063-1065)
 };
+// row of (chain c, round r) in the ballot tables ssm / ssw
+__host__ __device__ inline int64_t ballot_row(const Dev &d, int c, int r) {
+  return (int64_t)c * d.rspan + (r - d.rbase);
+}
 constexpr int32_t RR_DROP = INT32_MIN + 1;  // left UndeterminedEvents with no round received (hashgraph.go:970-977)
 
 // Block projection (kernels_frames.hip, frames.cpp): the

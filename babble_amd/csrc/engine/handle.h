@@ -114,6 +114,7 @@ struct bh_handle {
   // more segment): coordinates and round loop hold the first n_coord events
   // of the current layout; lens_coord their chain lengths
   bool inc_valid = false;
+  bool fdt_lost = false;  // the wide LT fallback's sweep overwrote FDT (no resume from it)
   int64_t n_coord = 0;
   int64_t inc_calls = 0;  // DivideRounds calls that resumed (statistics)
   std::vector<int32_t> lens_coord;
@@ -149,11 +150,17 @@ struct bh_handle {
   };
   std::vector<Other> others;
   std::unordered_map<std::string, int32_t> oth_by_key;  // root slot bytes + key hash -> entry
+  std::unordered_map<uint64_t, int32_t> oth_by_index;   // (root slot, creator slot, Index) -> entry
   std::vector<uint8_t> h_hashes;                        // every event's hash (Others matching)
   std::vector<int8_t> h_rflag;                          // Dev::rflag
   std::vector<int32_t> h_ext_lt;                        // Dev::ext_lt
   int64_t E0 = 0;  // events [0, E0) hold every other-parent only Root.Others knows
   int32_t fiat_max = -1;
+
+  // test hook: BH_TEST_FAIL_ALLOC=k makes the k-th device allocation of a
+  // bh_reset call fail (tests check that a failed call leaves the handle as
+  // it was); -1 otherwise
+  int fail_alloc_in = -1;
 
   int fail(int code, const char *fmt, ...) {
     char buf[512];
@@ -176,6 +183,10 @@ struct bh_handle {
 
 template <class T>
 inline int dalloc(bh_handle *h, T **p, size_t count) {
+  if (h->fail_alloc_in >= 0 && h->fail_alloc_in-- == 0) {  // test hook (bh_reset, BH_TEST_FAIL_ALLOC)
+    *p = nullptr;
+    return h->fail(BH_ERR_DEVICE, "injected allocation failure");
+  }
   HIPCHK(h, hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T)));
   return BH_OK;
 }

@@ -249,8 +249,8 @@ struct FameLds {
 // S_j[y] word w: the W(j-1) chains y = (chain, B[j]) strongly sees
 template <int NW>
 __device__ __forceinline__ uint32_t fame_ss_word(const Dev &d, int y, int j, int w) {
-  if (NW == 4) return fame_ballot_word(d.ssm + ((int64_t)y * (d.R_cap + 1) + j) * 16, d.round_lpc, w);
-  const unsigned long long m = d.ssw[((int64_t)y * (d.R_cap + 1) + j) * 8 + (w >> 1)];
+  if (NW == 4) return fame_ballot_word(d.ssm + ballot_row(d, y, j) * 16, d.round_lpc, w);
+  const unsigned long long m = d.ssw[ballot_row(d, y, j) * 8 + (w >> 1)];
   return (uint32_t)(m >> (32 * (w & 1)));
 }
 

@@ -66,7 +66,7 @@ constexpr int32_t PR_SKIP = INT32_MIN;  // L.pr of an event on a done chain (or 
 // a workgroup barrier that waits for LDS traffic only: the per-event
 // hand-offs of k_fiat go through LDS, so loads in flight (the next event's
 // lastAncestors) and stores (its results) keep going across it.  Where global
-// data one wave stored is read by another (fw / wfd) a full __syncthreads
+// data one wave stored is read by another (fw) a full __syncthreads
 // stays.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -225,17 +225,14 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
       }
       lds_barrier();
       const unsigned long long q1t = dg ? __builtin_amdgcn_s_memtime() : 0;
-      if (L.neww >= 0) {  // a new witness: its FD row, chain-major, for the counts
+      if (L.neww >= 0) {  // a new witness of the staged round: its FD row into the LDS copy
         const int64_t rw = L.cep[L.neww - base];
-        const bool inc = cached && L.newslot / n + rlo == L.cache_r;  // the staged round gains a witness
+        const bool inc = cached && L.newslot / n + rlo == L.cache_r;
         const int q = L.newslot % n;
-        for (int i = t; i < npad; i += 1024) {
-          const int32_t v = i < n ? d.fdt[fdt_pos(rw, i, npad)] : FD_NONE;
-          d.wfd[(int64_t)L.newslot * npad + i] = v;
-          if (inc) L.fdc[q * FI_CN + i] = v;
-        }
+        if (inc)
+          for (int i = t; i < FI_CN; i += 1024) L.fdc[q * FI_CN + i] = i < n ? d.fdt[fdt_pos(rw, i, npad)] : FD_NONE;
         if (inc && t == 0) L.cw[q] = L.neww;
-        __syncthreads();  // (stores then loads within the workgroup: one compute unit's cache)
+        __syncthreads();  // (fw stored, then loaded within the workgroup: one compute unit's cache)
         if (t == 0) L.neww = -1;
         __syncthreads();
       }
@@ -244,11 +241,13 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
       if (pr == PR_SKIP) continue;  // uniform
       if (pr >= 0 && pr < r0 && pr >= rlo && cached) {
         if (L.cache_r != pr) {  // stage round pr (chain-major rows, coalesced)
+          // the round's witnesses' FD rows, gathered from FDT (complete: the
+          // walks write MaxInt32 where no event of a chain sees a row)
           const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
-          const int32_t *frow = d.wfd + (int64_t)(pr - rlo) * n * npad;
           for (int k = t; k < n * FI_CN; k += 1024) {
             const int q = k / FI_CN, i = k % FI_CN;
-            L.fdc[k] = i < n ? frow[(int64_t)q * npad + i] : FD_NONE;
+            const int32_t w = __builtin_nontemporal_load(wrow + q);  // (vector load: see fiat_count)
+            L.fdc[k] = i < n && w >= 0 ? d.fdt[fdt_pos(d.epos[w], i, npad)] : FD_NONE;
           }
           if (t < FI_CN) L.cw[t] = t < n ? wrow[t] : -1;
           lds_barrier();
@@ -275,26 +274,28 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
         if (lane == 0 && ssw) atomicAdd(&L.ss, ssw);
       } else if (pr >= 0 && pr < r0 && pr >= rlo) {
         // #witnesses of round pr that x strongly sees (_stronglySee :172-191)
-        // the round's witnesses' FD rows, chain-major (wfd, written as each
-        // witness is found): a wave takes every 16th chain, loads all its
-        // rows' columns first, then counts columns by ballot
+        // the round's witnesses' FD rows from FDT (fw names each witness): a
+        // wave takes every 16th chain, loads all its rows' columns first,
+        // then counts columns by ballot
         const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
-        const int32_t *frow = d.wfd + (int64_t)(pr - rlo) * n * npad;
         int ssw = 0;
         for (int q0 = wave; q0 < n; q0 += 16 * 8) {
           int32_t f0[8], f1[8];
+          int64_t wr[8];
           bool has[8];
           // every load of the batch issued at once (one cache round trip): rows
-          // of absent witnesses are read too and masked after.  Plain loads: this
-          // workgroup stored fw / wfd (write-through, one compute unit's L1), and
-          // a round's rows are re-read by every event that counts against it
+          // of absent witnesses are read too and masked after
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
             const int q = min(q0 + 16 * u, n - 1);
-            const int32_t *fr = frow + (int64_t)q * npad;
-            has[u] = __builtin_nontemporal_load(wrow + q) >= 0 && q0 + 16 * u < n;  // (vector load: see fiat_count)
-            f0[u] = fr[min(lane, npad - 1)];
-            f1[u] = fr[min(lane + 64, npad - 1)];
+            const int32_t w = __builtin_nontemporal_load(wrow + q);  // (vector load: see fiat_count)
+            has[u] = w >= 0 && q0 + 16 * u < n;
+            wr[u] = d.epos[max(w, 0)];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            f0[u] = d.fdt[fdt_pos(wr[u], min(lane, npad - 1), npad)];
+            f1[u] = d.fdt[fdt_pos(wr[u], min(lane + 64, npad - 1), npad)];
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
@@ -306,8 +307,7 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
             int cntc = __popcll(__ballot(la0 >= f0[u])) + __popcll(__ballot(la1 >= f1[u]));
             for (int i0 = 128; i0 < n; i0 += 64) {  // chains beyond 128 (n <= 512)
               const int i = i0 + lane;
-              cntc += __popcll(__ballot(has[u] && i < n &&
-                                        d.la[rx * npad + i] >= __builtin_nontemporal_load(frow + (int64_t)(q0 + 16 * u) * npad + i)));
+              cntc += __popcll(__ballot(has[u] && i < n && d.la[rx * npad + i] >= d.fdt[fdt_pos(wr[u], min(i, npad - 1), npad)]));
             }
             ssw += has[u] && cntc >= d.sm;
           }
@@ -344,8 +344,8 @@ __global__ __launch_bounds__(1024) void k_fiat(Dev d) {
 // done can be computed at once.  A step: (A) each chain's next event, if its
 // other-parent is done, takes pr from its parents; (B) the counts, as items
 // (ready event, block of witnesses) spread over the waves, each item's
-// witness FD rows loaded at once from wfd; (C) one wave per ready event sets
-// its round and, for a new witness, writes its FD row to wfd and then fw --
+// witness FD rows loaded at once from FDT; (C) one wave per ready event sets
+// its round and, for a new witness, fw (and its FD row in the LDS copy) --
 // after every count of the step (a same-step witness is no ancestor of a
 // same-step event, so it would count zero, but a half-written row must not
 // be read).  Steps ~ the fiat region's depth instead of its events.
@@ -378,18 +378,19 @@ __device__ __forceinline__ int fiat_count(const Dev &d, int64_t xrow, int32_t pr
     la[v] = i < n ? d.la[xrow * npad + i] : -1;
   }
   const int32_t *wrow = d.fw + (int64_t)(pr - rlo) * n;
-  const int32_t *frow = d.wfd + (int64_t)(pr - rlo) * n * npad;
   // which of the block's witnesses exist: one lane-indexed (vector) load --
   // fw is stored by this kernel, and a wave-uniform load could be served by
   // the scalar cache, which vector stores do not update
   const int32_t wl = lane < IW && q0 + lane < n ? wrow[q0 + lane] : -1;
   const unsigned long long hm = __ballot(wl >= 0);
+  // each witness's FD row straight from FDT (its chain-major row from epos)
+  const int64_t wrl = d.epos[max(wl, 0)];
   int32_t f[IW][NV];
 #pragma unroll
   for (int u = 0; u < IW; ++u) {
-    const int q = min(q0 + u, n - 1);
+    const int64_t wr = __shfl(wrl, u);
 #pragma unroll
-    for (int v = 0; v < NV; ++v) f[u][v] = frow[(int64_t)q * npad + min(lane + 64 * v, npad - 1)];
+    for (int v = 0; v < NV; ++v) f[u][v] = d.fdt[fdt_pos(wr, min(lane + 64 * v, npad - 1), npad)];
   }
   int ssw = 0;
 #pragma unroll
@@ -525,11 +526,11 @@ __global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
       const bool w = r < r0 && r > L.rsp[j];  // witness (hashgraph.go:281-296)
       if (w) {
         const int64_t slot = (int64_t)(r - rlo) * n + c;
-        for (int i = lane; i < npad; i += 64) {
-          const int32_t v = i < n ? d.fdt[fdt_pos(xrow, i, npad)] : FD_NONE;
-          d.wfd[slot * npad + i] = v;
-          if (cached) L.wc[slot * npad + i] = (uint16_t)min((uint32_t)v + 1u, 0xFFFFu);  // FD_NONE + 1 wraps to 2^31
-        }
+        if (cached)
+          for (int i = lane; i < npad; i += 64) {
+            const int32_t v = i < n ? d.fdt[fdt_pos(xrow, i, npad)] : FD_NONE;
+            L.wc[slot * npad + i] = (uint16_t)min((uint32_t)v + 1u, 0xFFFFu);  // FD_NONE + 1 wraps to 2^31
+          }
         if (lane == 0) {
           d.fw[slot] = x;
           if (cached) L.wfl[slot] = 1;
@@ -555,7 +556,7 @@ __global__ __launch_bounds__(1024) void k_fiat_ls(Dev d) {
       L.rcnt[par ^ 1] = 0;
       L.steps = s + 1;
     }
-    __syncthreads();  // (rounds / fw / wfd stored before the next step loads them)
+    __syncthreads();  // (rounds / fw stored before the next step loads them)
     if (dg) {  // phase cycles per step (BH_DIAG): A, B, C
       const unsigned long long q3t = __builtin_amdgcn_s_memtime();
       d.diag[24] += q1t - q0t;

@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     for (int q0 = 0; q0 < 512; q0 += 256) {
       const int q = q0 + t;
       const unsigned long long m = __ballot(q < n && tq_s[q] <= res);
-      if (lane == 0) d.ssw[((int64_t)c * (d.R_cap + 1) + r + 1) * 8 + (q0 >> 6) + wave] = m;
+      if (lane == 0) d.ssw[ballot_row(d, c, r + 1) * 8 + (q0 >> 6) + wave] = m;
     }
   }
   // the hand-off: the new candidate's FD row for the next iteration
@@ -792,7 +792,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     // y's row.  Raw ballots, one aligned 8-B word per wave (fame packs the
     // LPC-strided bits), chain-major [c][round]; issued last, since a later
     // vmcnt wait would include them
-    if (lane == 0) d.ssm[((int64_t)c * (d.R_cap + 1) + r + 1) * 16 + wave] = ssb;
+    if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
   }
   if (dg) {
     const unsigned long long te = stamp();

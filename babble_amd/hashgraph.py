@@ -307,6 +307,14 @@ class Hashgraph:
         self._check(self._L.bh_get_profile(self._h, C.byref(it), C.byref(ms)))
         return int(it.value), float(ms.value)
 
+    def pipeline(self):
+        """(segments the last DivideRounds pipelined over, DivideRounds calls
+        so far that resumed from the previous call's device state)"""
+        seg = C.c_int32()
+        inc = C.c_int64()
+        self._check(self._L.bh_get_pipeline(self._h, C.byref(seg), C.byref(inc)))
+        return int(seg.value), int(inc.value)
+
     def profile_kernel(self):
         """Name of the coordinate kernel the last run timed."""
         return self._L.bh_get_profile_kernel(self._h).decode()

@@ -210,6 +210,12 @@ int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms);
 /* name of the coordinate kernel the last run timed ("k_flow32" / "k_flow":
  * chain dataflow; "k_la_sweep": chunked sweep); "" before the first run */
 const char *bh_get_profile_kernel(const bh_handle *h);
+/* how the last DivideRounds ran (no reference counterpart: engine
+ * introspection for tests and reports): the insertion-order segments its
+ * coordinate / round-loop pipeline used (1 = unpipelined), and the number of
+ * DivideRounds calls so far that resumed from the previous call's device
+ * state instead of recomputing the whole DAG */
+int bh_get_pipeline(bh_handle *h, int32_t *segments, int64_t *incremental_calls);
 /* SHA-256 of a batch of event bodies on the device:
  * Event.Hash() = SHA-256 of the body's Go-JSON bytes (event.go:50-56), the
  * digest InsertEvent keys, verifies and takes the coin from

@@ -131,3 +131,39 @@ class DagArrays:
         self.ntx = np.asarray(d.ntx)
         self.participant_ids = np.asarray(d.participant_ids)
         self.n = len(self.participant_ids)
+
+
+class SilentDag:
+    """A gossip DAG in which participant `silent` creates no event before
+    insertion position `join` (a peer that joins late): GetFrame gives it a
+    base Root (SelfParent Index / Round -1, NextRound 0) in every frame
+    before its first consensus event, while the other roots sit at a high
+    round -- the FastSync case of a long-running network with a new peer.
+    Random other-parents among the active peers' heads; random hashes /
+    signature bytes (the engine and the oracle read them as opaque keys)."""
+
+    def __init__(self, n, N, seed, silent, join):
+        rng = np.random.default_rng(seed)
+        creator, index = np.empty(N, np.int32), np.empty(N, np.int32)
+        sp, op = np.empty(N, np.int32), np.empty(N, np.int32)
+        last, cnt = np.full(n, -1, np.int64), np.zeros(n, np.int32)
+        e = 0
+        for c in range(n):
+            if c != silent:
+                creator[e], index[e], sp[e], op[e] = c, 0, -1, -1
+                last[c], cnt[c], e = e, 1, e + 1
+        while e < N:
+            active = [c for c in range(n) if c != silent or e >= join]
+            c = active[int(rng.integers(len(active)))]
+            others = [x for x in active if x != c and last[x] >= 0]
+            f = others[int(rng.integers(len(others)))]
+            creator[e], index[e], sp[e], op[e] = c, cnt[c], last[c], last[f]
+            last[c], e = e, e + 1
+            cnt[c] += 1
+        self.creator, self.index, self.sp, self.op = creator, index, sp, op
+        self.hashes = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+        self.sig_r = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+        self.ntx = (rng.random(N) < 0.5).astype(np.int32)
+        self.participant_ids = np.sort(rng.choice(2**31 - 1, n, replace=False)).astype(np.int64)
+        self.n = n
+        self.silent = silent

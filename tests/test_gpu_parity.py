@@ -495,13 +495,31 @@ def test_participant_lookup_rejects_unknown_ids():
     (7, 64, 50_000, 92, 21),
     (2, 32, 40_000, 93, 0),
     (13, 9, 30_000, 94, 3),
+    (4, 200, 30_000, 111, 0),    # wide: k_floww2 segments + 16-bit k_round_wide resumes
+    (6, 300, 30_000, 112, 5),
+    (3, 512, 25_000, 113, 0),
+    (5, 129, 30_000, 114, 2),
 ])
 def test_segment_pipeline_parity(monkeypatch, K, n, N, seed, lag):
     """Coordinates of prefix s + 1 overlapped with the round loop on prefix s,
     the loop resuming at the last round the prefix fixed (BH_SEGMENTS=K;
     full-size DAGs take 4 segments by default)."""
     monkeypatch.setenv("BH_SEGMENTS", str(K))
-    _random_parity(n, N, seed, lag)
+    hg = _random_parity(n, N, seed, lag)
+    assert hg.pipeline()[0] == K
+
+
+@pytest.mark.parametrize("p8", ["p8", "p8_mixed", "p16"])
+def test_segment_pipeline_wide_rows(monkeypatch, p8):
+    """The wide loop's resumed windows on 8-bit rows, alternating with the
+    16-bit fallback, and on 16-bit rows only, through 4 segments"""
+    monkeypatch.setenv("BH_SEGMENTS", "4")
+    if p8 == "p8_mixed":
+        monkeypatch.setenv("BH_ROUND_P8", "40")
+    if p8 == "p16":
+        monkeypatch.setenv("BH_ROUND_P8", "0")
+    hg = _random_parity(160, 30_000, 115, 0)
+    assert hg.pipeline()[0] == 4 and hg.profile_kernel() == "k_floww2"
 
 
 @pytest.mark.parametrize("K", [2, 6])
@@ -511,6 +529,7 @@ def test_segment_pipeline_wild(monkeypatch, K):
     monkeypatch.setenv("BH_SEGMENTS", str(K))
     _wild_parity(24, 40_000, 95, 30_000)
     _wild_parity(128, 40_000, 96, 35_000)
+    _wild_parity(170, 30_000, 116, 25_000)  # wide: far parents read back by the resumed k_floww2
 
 
 def test_segment_pipeline_lt_fallback(monkeypatch):

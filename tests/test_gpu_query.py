@@ -82,3 +82,47 @@ def test_query_random_pairs(n, N, seed):
         got = hg.query(kind, x, y)
         assert got.tolist() == [int(v) if kind == "round_diff" else bool(v) for v in w], kind
     assert 0 < sum(want["strongly_see"]) < len(x) and 0 < sum(want["ancestor"]) < len(x)
+
+
+@pytest.mark.parametrize("n,N,seed", [(16, 12_000, 95), (160, 12_000, 96)])
+def test_query_between_passes(n, N, seed):
+    """Go's ancestor / see / stronglySee read the Store and touch no pass
+    state: a query between InsertEvent and the next pass computes the new
+    events' coordinates on the device, and DecideFame / DecideRoundReceived /
+    ProcessDecidedRounds then continue from where DivideRounds left the state
+    -- as in Go -- and the next DivideRounds still resumes incrementally."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    from test_gpu_parity import _compare
+    from test_gpu_schedule import _wire_batches
+    d = Dag(n, N, seed, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    batch = _wire_batches(d)
+    h1, h2 = N // 3, 2 * N // 3
+    o.insert_dag(*(a[:h1] for a in args))
+    hg.insert_events(*batch(0, h1))
+    o.run_consensus()
+    hg.run_consensus()
+    o.insert_dag(*(a[h1:h2] for a in args))
+    hg.insert_events(*batch(h1, h2))
+    o.divide_rounds()
+    hg.divide_rounds()
+    o.insert_dag(*(a[h2:] for a in args))
+    hg.insert_events(*batch(h2, N))
+    rng = np.random.default_rng(seed)
+    x = rng.integers(h2, N, 400)
+    y = np.clip(x - rng.integers(0, 3000, 400), 0, N - 1)
+    got = hg.query("strongly_see", x, y)
+    assert got.tolist() == [o.strongly_see(int(a), int(b)) for a, b in zip(x, y)]
+    assert hg.query("see", x, y).tolist() == [o.see(int(a), int(b)) for a, b in zip(x, y)]
+    for p in ("decide_fame", "decide_round_received", "process_decided_rounds"):
+        getattr(o, p)()
+        getattr(hg, p)()
+        _compare(o, hg, f"after the query, {p}")
+    inc = hg.pipeline()[1]
+    o.run_consensus()
+    hg.run_consensus()
+    _compare(o, hg, "next RunConsensus")
+    assert hg.pipeline()[1] == inc + 1

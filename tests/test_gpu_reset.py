@@ -168,3 +168,67 @@ def test_reset_round_info_and_errors():
     h2 = Hashgraph(pid, 100)
     with pytest.raises(HashgraphError):
         h2.reset(1, 0, [5] * 8, [-1] * 8, [-1] * 8, [-1] * 8)
+
+
+@pytest.mark.parametrize("n,N,seed,silent,join", [(5, 60_000, 7, 2, 45_000), (16, 60_000, 8, 9, 50_000)])
+def test_reset_high_round_silent_peer(n, N, seed, silent, join):
+    """FastSync of a long-running network: Reset from the last
+    block before a late-joining peer's first consensus event -- its Root is
+    a base Root (SelfParent Round -1, NextRound 0) while the others sit at a
+    round in the hundreds or thousands.  The engine's round tables and
+    ballots then cover only the rounds the Reset hashgraph can reach (no
+    per-round storage from round 0 up), and every output matches the
+    oracle's Reset restatement, the silent peer's joining events included."""
+    from reset import SilentDag
+    d = SilentDag(n, N, seed, silent, join)
+    o = _oracle_run(d)
+    res = o.results()
+    first = int(np.nonzero(d.creator == silent)[0][0])
+    rr_first = int(res["round_received"][first])
+    b = o.blocks()
+    blk = max(i for i, r in enumerate(b["round_received"].tolist()) if r < rr_first)
+    rs = ResetInputs(o, d, blk)
+    assert rs.sp_index[silent] == -1 and rs.next_round[silent] == 0 and rs.round_received > 100
+    o2, hg, rs = _run_pair(d, blk, batches=3)
+    assert (o2.results()["round"][hg.stats().n_events - 1]) > rs.round_received
+
+
+def test_reset_allocation_failure(monkeypatch):
+    """A bh_reset whose k-th device allocation fails (BH_TEST_FAIL_ALLOC=k,
+    for every k up to the call's last allocation) returns the error and
+    leaves the handle a fresh one: the same handle then takes the Reset and
+    the events and matches the oracle."""
+    from babble_amd import Hashgraph
+    from babble_amd.hashgraph import HashgraphError
+    d = DagArrays(Dag(8, 4000, 0xBA8))
+    o = _oracle_run(d)
+    rs = ResetInputs(o, d, 4)
+    pid = np.asarray(d.participant_ids, np.int64)
+    args = (rs.round_received, rs.block_index, rs.next_round, rs.sp_index, rs.sp_lt, rs.sp_round,
+            rs.oth_root, rs.oth_key, pid[np.asarray(rs.oth_creator, np.int64)] if rs.oth_creator else [],
+            rs.oth_index, rs.oth_lt, rs.oth_round, rs.oth_hash)
+    failures = 0
+    for k in range(1, 64):
+        hg = Hashgraph(pid, len(d.creator) + 64)
+        monkeypatch.setenv("BH_TEST_FAIL_ALLOC", str(k))
+        try:
+            hg.reset(*args)
+            ok = True
+        except HashgraphError as e:
+            assert e.kind == "Device", e
+            ok = False
+        monkeypatch.delenv("BH_TEST_FAIL_ALLOC")
+        if ok:
+            break
+        failures += 1
+        hg.reset(*args)  # the failed call changed nothing: the handle takes the Reset now
+        o2 = Oracle(d.n, d.participant_ids, capacity=len(d.creator) + 64)
+        rs2 = ResetInputs(o, d, 4)
+        o2.reset(rs2)
+        assert np.array_equal(oracle_insert(o2, rs2, rs2.frame) != 0, _wire(hg, d, rs2.frame) != 0)
+        assert np.array_equal(oracle_insert(o2, rs2, rs2.diff) != 0, _wire(hg, d, rs2.diff) != 0)
+        o2.run_consensus()
+        hg.run_consensus()
+        _compare(o2, hg, f"after an injected failure at allocation {k}")
+        hg.close()
+    assert failures >= 10  # every allocation of the call was covered

@@ -179,3 +179,23 @@ def test_round_info_kat():
     ores = o.results()
     for r in range(hg.last_round() + 1):
         assert hg.round_info(r)["n_consensus"] == int(np.sum(ores["round_received"] == r)), r
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n,N,seed,lag,div,step", [
+    (128, 60_000, 3067, 40, 60, 500),   # C3's width: k_flow32 + k_round2, fame from ballots
+    (200, 60_000, 4146, 60, 60, 400),   # the wide path: k_floww2 + 16-bit k_round_wide, fame from ssw masks
+])
+def test_per_sync_trap_wide(n, N, seed, lag, div, step):
+    """The per-sync schedule at C3's width and on the wide path, state
+    compared after EVERY call; seeded so that the A.12 trap occurs (a lagging
+    peer's witness lands in a round already processed: never queued again,
+    its fame stays Undefined, hashgraph.go:809-815, 984-986).  Every call
+    after the first resumes from the previous call's device state."""
+    d, o, hg = _schedule(n, N, seed, lag, div, step)
+    res = o.results()
+    lcr = o.last_consensus_round()
+    trapped = np.nonzero((res["witness"] == 1) & (res["fame"] == 0) & (res["round"] < lcr))[0]
+    assert len(trapped) >= 1, "the seed no longer produces a trapped witness"
+    calls = (N + step - 1) // step
+    assert hg.pipeline()[1] >= calls - 2

@@ -94,3 +94,30 @@ def test_group_per_sync_schedule(monkeypatch):
         grp.run_consensus()
         if hi % (step * 20) == 0 or hi == N:
             _compare(o, grp, f"group after [0, {hi})")
+
+
+@pytest.mark.parametrize("n,N,step", [(32, 40_000, 4_000), (160, 30_000, 3_000)])
+def test_group_pipelined_incremental(monkeypatch, n, N, step):
+    """The in-process group -- the handle the Go binding holds for a node with
+    G devices -- with replicated coordinates runs the segment pipeline on
+    every shard, and its per-sync calls resume from the previous call's
+    device state (n = 32: k_flow32 + k_round2; n = 160: k_floww2 +
+    k_round_wide), matching the oracle after every call."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    from test_gpu_schedule import _wire_batches
+    monkeypatch.setenv("BH_SEGMENTS", "3")
+    d = Dag(n, N, 87 + n, lagging=2, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    grp = Hashgraph(d.participant_ids, N, devices=[0, 0])
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not np.asarray(grp.insert_events(*batch(lo, hi))).any()
+        grp.run_consensus()
+        _compare(o, grp, f"group n={n} after [0, {hi})")
+        assert grp.pipeline()[0] == 3
+    assert grp.pipeline()[1] == N // step - 1
