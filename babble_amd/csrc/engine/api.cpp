@@ -1859,6 +1859,23 @@ static int ensure_coords(bh_handle *h) {
     if (!keep) h->inc_valid = false;
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
+    if (h->n_div < N) {
+      // the passes that follow (DecideFame, DecideRoundReceived,
+      // ProcessDecidedRounds) see the events DivideRounds covered, as Go's
+      // do -- its rounds' Store entries: the divided prefix's chain lengths
+      // and event count go back to the device view
+      std::vector<int32_t> lens((size_t)d.n);
+      for (int c = 0; c < d.n; ++c) {
+        const auto &ch = h->chain[(size_t)c];
+        lens[(size_t)c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)h->n_div) - ch.begin());
+      }
+      HIPCHK(h, hipMemcpyAsync(d.chain_len, lens.data(), (size_t)d.n * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(h, hipStreamSynchronize(s));
+      d.N = h->n_div;
+      h->lens_h = lens;
+    }
+    if (h->layout_changed && h->R > 0)  // the witness tables' LA / FD rows moved with the layout
+      bh::launch_witness_tables(d, h->R, s);
   }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return BH_OK;

@@ -114,7 +114,9 @@ __global__ __launch_bounds__(256) void k_fd_walk(Dev d) {
 }
 
 // FD[row][i] for a TR_ROWS-row tile; rows are chain-major (row of (c, j) =
-// chain_start[c] + j); creator/index of a row come from chain_ids.
+// chain_start[c] + j) over the whole layout (d.rows; gap rows of a chain's
+// region have chain_ids -1 and are skipped); creator/index of a row come
+// from chain_ids.
 template <int TR_ROWS>
 __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   extern __shared__ int32_t tile[];  // [npad][TR_ROWS + 1]
@@ -122,16 +124,17 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   __shared__ int32_t rc[TR_ROWS], rj[TR_ROWS], rfast[TR_ROWS];
   const int t = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * TR_ROWS;
-  const int64_t N = d.N;
+  const int64_t N = d.rows > 0 ? d.rows : d.N;
   const int n = d.n, npad = d.npad;
   const int ro = t % TR_ROWS;
   const int64_t row = min(row0 + ro, N - 1);
   if (t < TR_ROWS) {
     const int32_t e = d.chain_ids[row];
-    const int32_t c = d.creator[e], j = d.index[e];
+    const bool gap = e < 0 || row0 + t >= N;
+    const int32_t c = gap ? -1 : d.creator[e], j = gap ? 0 : d.index[e];
     rc[t] = c;
     rj[t] = j;
-    rfast[t] = j <= d.last_la[(int64_t)n * npad + c];  // every chain sees (c, j)
+    rfast[t] = !gap && j <= d.last_la[(int64_t)n * npad + c];  // every chain sees (c, j)
   }
   // phase 1: FDT[i][row0 .. row0+TR_ROWS) -> tile[i][*]; IPP columns per
   // pass, 4 passes of loads in flight
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(256) void k_fd_transpose(Dev d) {
   const int q4 = npad / 4;
   for (int p = t; p < TR_ROWS * q4; p += blockDim.x) {
     const int r = p / q4, i4 = (p - r * q4) * 4;
-    if (row0 + r >= N) continue;
+    if (row0 + r >= N || rc[r] < 0) continue;
     const int32_t c = rc[r], j = rj[r];
     const bool fast = rfast[r];
     int32_t o[4];
@@ -184,12 +187,13 @@ void launch_first_descendants(const Dev &d, hipStream_t s, bool walked) {
   // per CU, 1.2 TB/s); BH_FDT_TR overrides (A/B)
   static const int tr_env = getenv("BH_FDT_TR") ? atoi(getenv("BH_FDT_TR")) : 0;
   const int tr = tr_env ? tr_env : d.npad <= 128 ? 64 : 16;
+  const int64_t rows = d.rows > 0 ? d.rows : d.N;  // the layout's rows, gaps included
   if (tr >= 64)
-    k_fd_transpose<64><<<(unsigned)((d.N + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
+    k_fd_transpose<64><<<(unsigned)((rows + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
   else if (tr >= 32)
-    k_fd_transpose<32><<<(unsigned)((d.N + 31) / 32), 256, (size_t)d.npad * 33 * 4, s>>>(d);
+    k_fd_transpose<32><<<(unsigned)((rows + 31) / 32), 256, (size_t)d.npad * 33 * 4, s>>>(d);
   else
-    k_fd_transpose<16><<<(unsigned)((d.N + 15) / 16), 256, (size_t)d.npad * 17 * 4, s>>>(d);
+    k_fd_transpose<16><<<(unsigned)((rows + 15) / 16), 256, (size_t)d.npad * 17 * 4, s>>>(d);
 }
 
 void configure_fd_kernels() {

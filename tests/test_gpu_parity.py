@@ -506,7 +506,7 @@ def test_segment_pipeline_parity(monkeypatch, K, n, N, seed, lag):
     full-size DAGs take 4 segments by default)."""
     monkeypatch.setenv("BH_SEGMENTS", str(K))
     hg = _random_parity(n, N, seed, lag)
-    assert hg.pipeline()[0] == K
+    assert hg.pipeline()[0] == min(K, N // 4096 + 1)  # (segments of at least 4096 events)
 
 
 @pytest.mark.parametrize("p8", ["p8", "p8_mixed", "p16"])
