@@ -96,7 +96,7 @@ def test_group_per_sync_schedule(monkeypatch):
             _compare(o, grp, f"group after [0, {hi})")
 
 
-@pytest.mark.parametrize("n,N,step", [(32, 40_000, 4_000), (160, 30_000, 3_000)])
+@pytest.mark.parametrize("n,N,step", [(32, 40_000, 10_000), (160, 30_000, 10_000)])
 def test_group_pipelined_incremental(monkeypatch, n, N, step):
     """The in-process group -- the handle the Go binding holds for a node with
     G devices -- with replicated coordinates runs the segment pipeline on
