@@ -568,9 +568,14 @@ bool segments_eligible(const bh_handle *h) {
 }
 
 // segments for `events` new events: measured at C3 (10M events): 4
-// segments 73.4 ms, 8 segments 72.4 ms, one 84.3 ms (profiles/r2_segments.log)
-int segments_for(int64_t events) {
-  int K = events >= 4000000 ? 8 : events >= 1000000 ? 4 : 1;
+// segments 73.4 ms, 8 segments 72.4 ms, one 84.3 ms (profiles/r2_segments.log).
+// The wide path (n > 128) takes one: k_floww2 (145 KiB of LDS) and the
+// wide transpose leave no compute unit room for a k_round_wide workgroup,
+// so its segments run one after the other and only cost more (C4: 284 ->
+// 316 ms with 8, profiles/r3_c4_segments.log); its incremental calls still
+// run as one more segment of the same machinery
+int segments_for(const Dev &d, int64_t events) {
+  int K = !d.fd_cols ? 1 : events >= 4000000 ? 8 : events >= 1000000 ? 4 : 1;
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
 }
@@ -640,6 +645,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
     v.tile_list = dtl;
     v.ntiles = nt;
+    // a whole-DAG wide run takes the whole-layout transpose (32-row tiles,
+    // several workgroups per compute unit) instead of 64-row tile lists
+    if (wide && K == 1 && base == 0) v.tile_list = nullptr;
     if (wide) {
       HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
       bh::launch_floww(v, sc);  // the segment's descriptors, then k_floww2
@@ -752,7 +760,7 @@ int rounds_segmented(bh_handle *h, bool *used) {
     return BH_OK;
   }
   h->inc_calls += base > 0;
-  return rounds_pipelined(h, segments_for(d.N - base), base);
+  return rounds_pipelined(h, segments_for(d, d.N - base), base);
 }
 
 int stage_rounds(bh_handle *h) {

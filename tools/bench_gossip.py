@@ -55,6 +55,7 @@ def main():
                       "n": a.n, "events": a.events, "batch": a.batch, "prefill": a.prefill, "calls": len(inc),
                       "total_s": round(tot, 3), "ns_per_new_event": round(tot * 1e9 / max(new, 1), 1),
                       "consensus_ms_median": float(np.median(cons)), "consensus_ms_max": float(cons.max()),
+                      "incremental_calls": hg.pipeline()[1],
                       "prefill_call": calls[0] if a.prefill else None, "last_call": inc[-1]}))
 
 
