@@ -20,7 +20,7 @@ build/engine/%.o: babble_amd/csrc/engine/% $(ENGINE_HDR)
 	$(HIPCC) $(HIPFLAGS) -Iinclude -c -o $@ $<
 
 babble_amd/libbabble_hip.so: $(ENGINE_OBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(ENGINE_OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(ENGINE_OBJ) -L/opt/rocm/lib -lrccl -lcrypto -Wl,-rpath,/opt/rocm/lib
 
 oracle/liboracle.so: oracle/hg_oracle.c oracle/hg_oracle.h
 	$(MAKE) -C oracle

@@ -223,6 +223,11 @@ void launch_block_json_size(const Dev &d, const Frames &fr, int32_t f0, int32_t 
                             hipStream_t s);  // -> bofs[F]
 void launch_block_json_write(const Dev &d, const Frames &fr, int32_t f0, int32_t F, int64_t i0, int64_t i1,
                              bool store, hipStream_t s);  // -> bjson, bhash (store)
+// FrameHash / block hash of frames [f0, f0 + F) from digests `dig` ([F][32],
+// device memory) computed elsewhere (frames.cpp: the host's SHA-256 for a
+// call that emits few frames)
+void launch_frame_store(const Dev &d, const Frames &fr, int32_t f0, int32_t F, const uint8_t *dig, hipStream_t s);
+void launch_block_store(const Dev &d, const Frames &fr, int32_t f0, int32_t F, const uint8_t *dig, hipStream_t s);
 // root (f, p) for every p: out[3p] NextRound, out[3p+1] SelfParent event (-1 base), out[3p+2] #Others
 void launch_root_query(const Dev &d, const Frames &fr, int32_t f, int32_t *out, hipStream_t s);
 

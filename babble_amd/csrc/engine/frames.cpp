@@ -5,8 +5,12 @@
 // _json).  The kernels are in kernels_frames.hip; the algorithm and its
 // reference lines are described there.
 #include <hip/hip_runtime.h>
+#include <openssl/sha.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "babble_hip.h"
@@ -40,29 +44,105 @@ int read_i64(bh_handle *h, const int64_t *src, int64_t *out) {
   return BH_OK;
 }
 
+// Where the SHA-256 digests of the JSON a call just built are computed
+// (FrameHash, frame.go:35-41; the block hash, block.go:196-205).  SHA-256 of
+// one message is a serial chain of 64-byte compressions: on the device one
+// lane hashes one frame at ~20 MB/s (a lone wave issues a dependent VALU op
+// every 8 cycles), every frame of the call in parallel; the host's SHA
+// extensions (OpenSSL) hash ~2.5 GB/s per thread.  So a call that emits few
+// frames -- the live node's schedule, one or two per RunConsensus -- copies
+// the device-built JSON to the host and hashes it there, and a call that
+// emits thousands (a batch run over a whole DAG) hashes on the device.  The
+// choice is by estimated time: device = the longest message / 20 MB/s;
+// host = the bytes / (2.5 GB/s x threads) + the copy at 20 GB/s.
+// BH_FRAME_HASH=device | host forces one (the tests run both against the
+// oracle).  The bytes hashed are the device's either way.
+constexpr double DEV_SHA_BPS = 20e6, HOST_SHA_BPS = 2.5e9, D2H_BPS = 20e9;
+constexpr int HOST_SHA_THREADS = 8;
+
+bool hash_on_host(const std::vector<int64_t> &ofs, int32_t F) {
+  const char *e = getenv("BH_FRAME_HASH");
+  if (e && !strcmp(e, "device")) return false;
+  if (e && !strcmp(e, "host")) return true;
+  int64_t mx = 0;
+  for (int32_t j = 0; j < F; ++j) mx = std::max(mx, ofs[(size_t)j + 1] - ofs[(size_t)j]);
+  const double total = (double)ofs[(size_t)F];
+  const int th = std::max(1, std::min<int>(HOST_SHA_THREADS, F));
+  return total / (HOST_SHA_BPS * th) + total / D2H_BPS < (double)mx / DEV_SHA_BPS;
+}
+
+// digests of the F messages buf[ofs[j], ofs[j + 1]) (device memory) into
+// the device buffer dig ([F][32]), on the host
+int host_digests(bh_handle *h, const uint8_t *buf, const std::vector<int64_t> &ofs, int32_t F, uint8_t *dig) {
+  const size_t total = (size_t)ofs[(size_t)F];
+  if (total > h->host_json_cap) {
+    if (h->host_json) (void)hipHostFree(h->host_json);
+    h->host_json = nullptr;
+    h->host_json_cap = 0;
+    HIPCHK(h, hipHostMalloc((void **)&h->host_json, std::max<size_t>(total, 1 << 20), hipHostMallocDefault));
+    h->host_json_cap = std::max<size_t>(total, 1 << 20);
+  }
+  if (total) HIPCHK(h, hipMemcpyAsync(h->host_json, buf, total, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  std::vector<uint8_t> out((size_t)F * 32);
+  auto work = [&](int32_t a, int32_t b) {
+    for (int32_t j = a; j < b; ++j)
+      SHA256(h->host_json + ofs[(size_t)j], (size_t)(ofs[(size_t)j + 1] - ofs[(size_t)j]), out.data() + (size_t)j * 32);
+  };
+  const int th = std::max(1, std::min<int>(HOST_SHA_THREADS, F));
+  if (th == 1) {
+    work(0, F);
+  } else {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < th; ++t) ts.emplace_back(work, (int32_t)((int64_t)F * t / th), (int32_t)((int64_t)F * (t + 1) / th));
+    for (auto &t : ts) t.join();
+  }
+  HIPCHK(h, hipMemcpyAsync(dig, out.data(), out.size(), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
+
+int read_offsets(bh_handle *h, const int64_t *src, int32_t F, std::vector<int64_t> *ofs) {
+  ofs->resize((size_t)F + 1);
+  HIPCHK(h, hipMemcpyAsync(ofs->data(), src, ((size_t)F + 1) * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return BH_OK;
+}
+
 // Frame JSON of frames [f0, f0 + F) into fr.json (+ FrameHash when store),
 // then, with blocks, the Block JSON into fr.bjson (+ block hash when store)
 int project_json(bh_handle *h, int32_t f0, int32_t F, int64_t i0, int64_t i1, bool store, bool blocks) {
   bh::Frames &fr = h->fr;
   const Dev &d = h->d;
   hipStream_t s = h->stream;
+  std::vector<int64_t> ofs;
   bh::launch_frame_json_size(d, fr, f0, F, i0, i1, s);
   HIPCHK(h, hipGetLastError());
-  int64_t total = 0;
-  if (int rc = read_i64(h, fr.jofs + F, &total)) return rc;
-  if (int rc = ensure_buf(h, &fr.json, &h->json_cap, (size_t)total)) return rc;
-  bh::launch_frame_json_write(d, fr, f0, F, i0, i1, store, s);
+  if (int rc = read_offsets(h, fr.jofs, F, &ofs)) return rc;
+  if (int rc = ensure_buf(h, &fr.json, &h->json_cap, (size_t)ofs[(size_t)F])) return rc;
+  const bool fhost = store && hash_on_host(ofs, F);
+  bh::launch_frame_json_write(d, fr, f0, F, i0, i1, store && !fhost, s);
   HIPCHK(h, hipGetLastError());
+  if (fhost) {
+    if (int rc = host_digests(h, fr.json, ofs, F, fr.dig)) return rc;
+    bh::launch_frame_store(d, fr, f0, F, fr.dig, s);
+  }
+  h->hash_host_frames += fhost ? F : 0;
   if (!blocks) {
     HIPCHK(h, hipStreamSynchronize(s));
     return BH_OK;
   }
   bh::launch_block_json_size(d, fr, f0, F, i0, i1, s);
   HIPCHK(h, hipGetLastError());
-  if (int rc = read_i64(h, fr.bofs + F, &total)) return rc;
-  if (int rc = ensure_buf(h, &fr.bjson, &h->bjson_cap, (size_t)total)) return rc;
-  bh::launch_block_json_write(d, fr, f0, F, i0, i1, store, s);
+  if (int rc = read_offsets(h, fr.bofs, F, &ofs)) return rc;
+  if (int rc = ensure_buf(h, &fr.bjson, &h->bjson_cap, (size_t)ofs[(size_t)F])) return rc;
+  const bool bhost = store && hash_on_host(ofs, F);
+  bh::launch_block_json_write(d, fr, f0, F, i0, i1, store && !bhost, s);
   HIPCHK(h, hipGetLastError());
+  if (bhost) {
+    if (int rc = host_digests(h, fr.bjson, ofs, F, fr.dig)) return rc;
+    bh::launch_block_store(d, fr, f0, F, fr.dig, s);
+  }
   HIPCHK(h, hipStreamSynchronize(s));
   return BH_OK;
 }
@@ -120,6 +200,9 @@ void frames_free(bh_handle *h) {
   fr = bh::Frames{};
   for (auto &e : h->ev_fr)
     if (e) (void)hipEventDestroy(e);
+  if (h->host_json) (void)hipHostFree(h->host_json);
+  h->host_json = nullptr;
+  h->host_json_cap = 0;
 }
 
 // RunConsensus from scratch (bh_reset_consensus): no frame processed yet;

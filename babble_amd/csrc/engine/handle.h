@@ -133,6 +133,9 @@ struct bh_handle {
   int64_t arena_cap = 0, arena_len = 0;
   int64_t others_total = 0;        // Others of the processed frames (oofs[P * n])
   size_t json_cap = 0, bjson_cap = 0;
+  uint8_t *host_json = nullptr;  // pinned host copy of the JSON a call hashes on the host (frames.cpp)
+  size_t host_json_cap = 0;
+  int64_t hash_host_frames = 0;  // frames whose FrameHash the host computed (statistics)
   hipEvent_t ev_fr[2]{};           // around the last projection
   float frames_ms = 0;
 

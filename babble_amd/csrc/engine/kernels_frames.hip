@@ -486,8 +486,12 @@ void launch_frame_json_write(const Dev &d, const Frames &fr, int32_t f0, int32_t
   if (i1 > i0) k_frame_write_events<<<(unsigned)((i1 - i0 + 3) / 4), 256, 0, s>>>(d, fr, f0, i0, i1);
   if (store) {
     launch_sha256(fr.json, fr.jofs, fr.jlen, F, fr.dig, s);
-    k_frame_store<<<(unsigned)((F + 255) / 256), 256, 0, s>>>(d, fr, f0, F, fr.dig);
+    launch_frame_store(d, fr, f0, F, fr.dig, s);
   }
+}
+
+void launch_frame_store(const Dev &d, const Frames &fr, int32_t f0, int32_t F, const uint8_t *dig, hipStream_t s) {
+  if (F > 0) k_frame_store<<<(unsigned)((F + 255) / 256), 256, 0, s>>>(d, fr, f0, F, dig);
 }
 
 // ---------------------------------------------------------------------------
@@ -596,8 +600,12 @@ void launch_block_json_write(const Dev &d, const Frames &fr, int32_t f0, int32_t
   if (i1 > i0) k_block_write_txs<<<(unsigned)((i1 - i0 + 255) / 256), 256, 0, s>>>(d, fr, f0, i0, i1);
   if (store) {
     launch_sha256(fr.bjson, fr.bofs, fr.blen, F, fr.dig, s);
-    k_block_store<<<(unsigned)((F + 255) / 256), 256, 0, s>>>(d, fr, f0, F, fr.dig);
+    launch_block_store(d, fr, f0, F, fr.dig, s);
   }
+}
+
+void launch_block_store(const Dev &d, const Frames &fr, int32_t f0, int32_t F, const uint8_t *dig, hipStream_t s) {
+  if (F > 0) k_block_store<<<(unsigned)((F + 255) / 256), 256, 0, s>>>(d, fr, f0, F, dig);
 }
 
 __global__ void k_root_query(Dev d, Frames fr, int32_t f, int32_t *out) {

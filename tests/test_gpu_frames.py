@@ -70,11 +70,18 @@ def _wire(hg, d, lo, hi):
                             d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])
 
 
+@pytest.mark.parametrize("site", ["auto", "device", "host"])
 @pytest.mark.parametrize("n,N,seed,lag,step", [(4, 3000, 81, 0, 0), (9, 6000, 82, 2, 0),
-                                               (7, 5000, 83, 1, 450), (32, 40000, 84, 0, 0)])
-def test_frames_generated(n, N, seed, lag, step):
+                                               (7, 5000, 83, 1, 450), (32, 40000, 84, 0, 0),
+                                               (32, 40000, 87, 0, 1500)])
+def test_frames_generated(monkeypatch, site, n, N, seed, lag, step):
     """Generated DAGs whose bodies hash to their event hashes; batch and
-    per-sync schedules (bytes given with each batch)."""
+    per-sync schedules (bytes given with each batch).  The digests of the
+    device-built JSON are taken on the device or by the host's SHA-256
+    (frames.cpp: a call that emits few frames hashes on the host; site
+    forces either), byte-identical either way."""
+    if site != "auto":
+        monkeypatch.setenv("BH_FRAME_HASH", site)
     from babble_amd import Hashgraph
     d, bodies, sigs = _gen(n, N, seed, lag)
     hg = Hashgraph(d.participant_ids, N, frames=True)

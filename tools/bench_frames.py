@@ -9,6 +9,9 @@ transactions count matches the block's.  Not a headline number: the
 projection is outside bench.py's timed step.
 
   python tools/bench_frames.py --cfg 3 --steps 3
+  python tools/bench_frames.py --cfg 3 --N 2000000 --gossip 1600 --calls 40
+      (the live node's schedule: a resident DAG, then calls of ~one round of
+      events each; the projection of the frames each call emits, per call)
 """
 import argparse
 import hashlib
@@ -29,11 +32,15 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--sample", type=int, default=40)
     ap.add_argument("--out", default="")
+    ap.add_argument("--gossip", type=int, default=0, help="events per call of a per-sync run (0: batch runs)")
+    ap.add_argument("--calls", type=int, default=40)
     a = ap.parse_args()
     from babble_amd import Hashgraph
     from babble_amd.dag import CONFIGS, Dag
     c = CONFIGS[a.cfg]
     N = a.N or c["N"]
+    if a.gossip:
+        return gossip(a, c, N)
     t = time.time()
     d = Dag.config(a.cfg, N=N, sig_mode=0)
     bodies, bo, sigs, so = d.event_bytes()
@@ -86,6 +93,61 @@ def main():
                ns_per_consensus_event=float(np.mean(proj)) * 1e6 / max(1, st.consensus_events),
                sample_blocks=len(pick), sample_frame_json_mb=jbytes / 1e6,
                host_sha256_mb_s=jbytes / 1e6 / max(tsha, 1e-9), checks="FrameHash/blockhash/JSON shape ok")
+    print(json.dumps(res), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+def gossip(a, c, N):
+    """per-sync projection latency: the first N - calls * gossip events in one
+    call, then `calls` calls of `gossip` events; per call the projection's
+    device time (stage_ms[6]) and wall time of RunConsensus, the frames it
+    emitted, and every emitted FrameHash checked on the host"""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    d = Dag.config(a.cfg, N=N, sig_mode=0)
+    bodies, bo, sigs, so = d.event_bytes()
+    hg = Hashgraph(d.participant_ids, N, frames=True)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    L = hg._L
+    first = N - a.calls * a.gossip
+    bounds = [0, first] + [first + a.gossip * (k + 1) for k in range(a.calls)]
+    rows, done = [], 0
+    for k, (lo, hi) in enumerate(zip(bounds[:-1], bounds[1:])):
+        assert not np.asarray(hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi],
+                                               opi[lo:hi], d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])).any()
+        bsl, ssl = np.ascontiguousarray(bo[lo:hi + 1]), np.ascontiguousarray(so[lo:hi + 1])  # absolute offsets
+        hg._check(L.bh_set_event_bytes(hg._h, lo, hi - lo, bodies.ctypes.data, bsl.ctypes.data,
+                                       sigs.ctypes.data, ssl.ctypes.data))
+        t0 = time.perf_counter()
+        hg.run_consensus()
+        wall = (time.perf_counter() - t0) * 1e3
+        st = hg.stats()
+        nb = st.blocks - done
+        fh, bh, ok = hg.block_hashes(done, nb) if nb else (None, None, None)
+        b = hg.blocks()
+        jb = 0
+        for i in range(nb):
+            fj = hg.frame_json(int(b["round_received"][done + i]))
+            jb += len(fj)
+            assert ok[i] and hashlib.sha256(fj).digest() == fh[i].tobytes(), f"FrameHash of block {done + i}"
+            assert hashlib.sha256(hg.block_json(done + i)).digest() == bh[i].tobytes()
+        done = st.blocks
+        if k:
+            rows.append(dict(call=k, new_events=hi - lo, blocks=nb, frame_json_kb=round(jb / 1e3, 1),
+                             projection_ms=round(hg.stage_ms()[6], 3), run_consensus_ms=round(wall, 3)))
+            print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    with_b = [r for r in rows if r["blocks"]]
+    res = dict(cfg=a.cfg, n=c["n"], N=N, gossip=a.gossip, calls=len(rows), calls_with_blocks=len(with_b),
+               frame_hash=os.environ.get("BH_FRAME_HASH", "auto"),
+               projection_ms_median=float(np.median([r["projection_ms"] for r in with_b])) if with_b else None,
+               projection_ms_max=max((r["projection_ms"] for r in with_b), default=None),
+               frame_json_kb_median=float(np.median([r["frame_json_kb"] for r in with_b])) if with_b else None,
+               run_consensus_ms_median=float(np.median([r["run_consensus_ms"] for r in rows])),
+               checks="every emitted FrameHash / block hash recomputed on the host from the device's JSON")
     print(json.dumps(res), flush=True)
     if a.out:
         with open(a.out, "w") as f:
