@@ -29,7 +29,20 @@ oracle/liboracle.so: oracle/hg_oracle.c oracle/hg_oracle.h
 tests/cpp/hg_replay: tests/cpp/hg_replay.cpp include/babble_hashgraph.hpp include/babble_hip.h babble_amd/libbabble_hip.so
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lbabble_amd -lbabble_hip -Wl,-rpath,'$$ORIGIN/../../babble_amd'
 
-clean:
-	rm -rf babble_amd/*.so oracle/*.so tests/cpp/hg_replay build/engine
+# host-only AddressSanitizer build of the engine (tools/sanitize_engine.sh):
+# the host code (api.cpp, frames.cpp, the launch stubs) instrumented, the
+# gfx950 code objects unchanged (GPU ASan is not used); loaded through
+# BH_LIB_PATH with the clang ASan runtime preloaded
+ASAN_OBJ := $(patsubst babble_amd/csrc/engine/%,build/asan/%.o,$(ENGINE_SRC))
+build/asan/%.o: babble_amd/csrc/engine/% $(ENGINE_HDR)
+	@mkdir -p build/asan
+	$(HIPCC) $(HIPFLAGS) -g -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Iinclude -c -o $@ $<
+tools/asan/libbabble_hip.so: $(ASAN_OBJ)
+	@mkdir -p tools/asan
+	$(HIPCC) $(HIPFLAGS) -shared -shared-libasan -Xarch_host -fsanitize=address -o $@ $(ASAN_OBJ) -L/opt/rocm/lib -lrccl -lcrypto -Wl,-rpath,/opt/rocm/lib
+asan: tools/asan/libbabble_hip.so
 
-.PHONY: all clean
+clean:
+	rm -rf babble_amd/*.so oracle/*.so tests/cpp/hg_replay build/engine build/asan tools/asan
+
+.PHONY: all asan clean

@@ -39,7 +39,8 @@ class _Dag(C.Structure):
 def _lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "libbabble_gen.so")
+        # BH_GEN_LIB: another build of the same source (tools/sanitize.sh)
+        path = os.environ.get("BH_GEN_LIB") or os.path.join(_HERE, "libbabble_gen.so")
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run `make` (or __graft_entry__.build())")
         L = C.CDLL(path)

@@ -1050,7 +1050,8 @@ int hgo_process_decided_rounds(hgo *h) {
     if (!h->has_lcr || pr->index > h->lcr) { h->has_lcr = 1; h->lcr = pr->index; }
   }
   /* defer: h.PendingRounds = h.PendingRounds[processedIndex:] */
-  memmove(h->pend, h->pend + processed, (size_t)(h->pend_len - processed) * sizeof(pending_round));
+  if (h->pend_len > processed) /* (an empty queue may have no buffer: memmove(NULL, ...) is UB) */
+    memmove(h->pend, h->pend + processed, (size_t)(h->pend_len - processed) * sizeof(pending_round));
   h->pend_len -= processed;
   return HGO_OK;
 }

@@ -17,7 +17,9 @@ UNSET = -(2 ** 31)
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(ROOT, "oracle", "liboracle.so")
+        # BH_ORACLE_LIB: another build of the same source (tools/sanitize.sh:
+        # the ASan/UBSan one)
+        path = os.environ.get("BH_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
         if not os.path.exists(path):
             import subprocess
             subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
