@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.rq, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
                   d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
@@ -396,6 +396,7 @@ int rounds_coords(bh_handle *h) {
   h->xchg_ms = 0;
   h->segments_used = 1;
   h->inc_valid = false;
+  h->fdt_lost = false;
   if ((rc = set_chain_tables(h))) return rc;
   d.rows = h->layout_rows;
   hipStream_t s = h->stream;
@@ -510,7 +511,16 @@ int rounds_loop(bh_handle *h) {
     bh::launch_round_init(d, s);
   }
   if ((rc = run_round_loop(h, d, &h->graph, &h->graph_dev, st))) return rc;
-  return rounds_tail(h, st, 0);
+  bh::launch_resume_point(d, st[bh::ST_ROUNDS], nullptr, s);  // each chain's resume round (rq) for the next call
+  if ((rc = rounds_tail(h, st, 0))) return rc;
+  if (h->reset_on && !h->fdt_lost) {
+    // a Reset hashgraph's later calls resume from here (rounds_segmented):
+    // the chain dataflow left every LA row and a complete FDT
+    h->n_coord = d.N;
+    h->lens_coord = h->lens_h;
+    h->inc_valid = true;
+  }
+  return BH_OK;
 }
 
 // after the loop: witness tables, per-event rounds, PendingRounds.  Rounds
@@ -562,7 +572,7 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
 // coordinates are replicated (the default) runs it on its own device.
 bool segments_eligible(const bh_handle *h) {
   const Dev &d = h->d;
-  if (h->shard_cols || h->reset_on) return false;
+  if (h->shard_cols) return false;
   if (d.fd_cols) return use_flow(d) && bh::flow32_eligible(d);
   return bh::floww_eligible(d) && bh::round_p16(d);
 }
@@ -591,12 +601,24 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
   h->fdt_lost = false;
-  if ((int)h->seg_ev.size() < 3 * K) {
-    for (int i = (int)h->seg_ev.size(); i < 3 * K; ++i) {
+  if ((int)h->seg_ev.size() < 4 * K) {
+    for (int i = (int)h->seg_ev.size(); i < 4 * K; ++i) {
       hipEvent_t e;
       HIPCHK(h, hipEventCreate(&e));
       h->seg_ev.push_back(e);
     }
+  }
+  // an incremental call resumes at the last round whose boundaries lie
+  // inside the previous prefix on every chain this call extends
+  // (k_resume_point left each chain's first outside round in rq)
+  int32_t host_resume = d.r0;
+  if (base > 0) {
+    std::vector<int32_t> rq((size_t)n);
+    HIPCHK(h, hipMemcpy(rq.data(), d.rq, (size_t)n * 4, hipMemcpyDeviceToHost));
+    int32_t m = INT32_MAX;
+    for (int c = 0; c < n; ++c)
+      if (h->chain[(size_t)c].size() > (size_t)h->lens_coord[(size_t)c]) m = std::min(m, rq[(size_t)c]);
+    host_resume = std::max(d.r0, m == INT32_MAX ? d.r0 : m - 1);
   }
   // the coordinate stream starts after everything queued on the main one
   HIPCHK(h, hipEventRecord(h->ev[0], sr));
@@ -632,6 +654,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     lens_at(Ns[(size_t)k], stg);
     lens_at(Ns[(size_t)k + 1], stg + n);
     HIPCHK(h, hipMemcpyAsync(v.seg_lo, stg, (size_t)2 * n * 4, hipMemcpyHostToDevice, sc));
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sc));  // the segment's lengths are on the device
     // the 64-row tiles holding the segment's rows: each chain's run
     // [start + lo, start + hi), in layout order, shared boundary tiles once
     int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
@@ -690,14 +713,37 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     rv.chain_len = view(k).chain_len;
     if (serial) HIPCHK(h, hipStreamSynchronize(sc));
     if (dbg) HIPCHK(h, hipEventRecord(lt0, sr));
-    if (k == 0 && base == 0) bh::launch_round_init(rv, sr);
-    else bh::launch_round_resume(rv, sr);
+    if (k == 0 && base == 0) {
+      bh::launch_round_init(rv, sr);
+    } else {
+      if (k == 0) {
+        if (h->reset_on) {
+          // a Reset hashgraph: the rounds below r0 again, event by event
+          // (k_fiat_ls, the fiat region only), which also re-derives B[r0]
+          HIPCHK(h, hipMemsetAsync(d.rexists, 0, (size_t)d.R_cap + 1, sr));
+          HIPCHK(h, hipMemsetAsync(d.fw, 0xFF, (size_t)(d.r0 - d.rlo) * n * 4, sr));
+          HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FIATMAX, 0xFF, 4, sr));
+          bh::launch_fiat(rv, sr);
+          HIPCHK(h, hipGetLastError());
+          HIPCHK(h, hipMemcpyAsync(h->pinned_state + bh::ST_COUNT + 2, d.state + bh::ST_FIATMAX, 4,
+                                   hipMemcpyDeviceToHost, sr));
+        }
+        h->pinned_state[bh::ST_COUNT + 1] = host_resume;
+        HIPCHK(h, hipMemcpyAsync(d.state + bh::ST_RESUME, h->pinned_state + bh::ST_COUNT + 1, 4, hipMemcpyHostToDevice, sr));
+      }
+      bh::launch_round_resume(rv, sr);
+    }
     if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], st))) {
       (void)hipEventDestroy(sr_mark);
       return rc;
     }
     // where the next segment -- or the next call's new events -- resume
-    bh::launch_resume_point(rv, st[bh::ST_ROUNDS], sr);
+    const int32_t *next_len = nullptr;
+    if (k + 1 < K) {
+      HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * K + k + 1], 0));
+      next_len = view(k + 1).chain_len;
+    }
+    bh::launch_resume_point(rv, st[bh::ST_ROUNDS], next_len, sr);
     if (dbg) {
       HIPCHK(h, hipEventRecord(lt1, sr));
       HIPCHK(h, hipStreamSynchronize(sr));
@@ -730,6 +776,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   for (int k = 0; k < K; ++k)
     if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
   h->sweep_kernel = wide ? bh::floww_kernel(d) : "k_flow32";
+  if (h->reset_on && base > 0) h->fiat_max = h->pinned_state[bh::ST_COUNT + 2];
   if ((rc = rounds_tail(h, st, base))) return rc;
   h->n_coord = N;
   h->lens_coord = h->lens_h;
@@ -750,17 +797,22 @@ int rounds_segmented(bh_handle *h, bool *used) {
   if ((rc = upload(h))) return rc;
   if ((rc = set_chain_tables(h))) return rc;
   if (!segments_eligible(h)) return BH_OK;
+  const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
+  // a Reset hashgraph's first call (and any call that brings events whose
+  // other-parent only Root.Others knows) computes the whole DAG
+  // (rounds_coords / rounds_loop: k_reset_coords, the fiat pass); the calls
+  // after it append a segment like any other handle
+  if (h->reset_on && (base == 0 || h->E0 > base)) return BH_OK;
   *used = true;
   d.rows = h->layout_rows;
   d.e0 = 0;
   d.seg_lo = h->seg_zero;
-  const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
   if (base == d.N) {  // nothing new to divide: DivideRounds changes nothing
     h->stage = std::max(h->stage, 1);
     return BH_OK;
   }
   h->inc_calls += base > 0;
-  return rounds_pipelined(h, segments_for(d, d.N - base), base);
+  return rounds_pipelined(h, h->reset_on ? 1 : segments_for(d, d.N - base), base);
 }
 
 int stage_rounds(bh_handle *h) {
@@ -1150,6 +1202,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
     if (n <= 512) A(&d.ssw, R1 * n * 8);  // k_round_wide's masks for k_fame_masks<16>
   }
   A(&d.last_la, (size_t)(n + 1) * d.npad);
+  A(&d.rq, (size_t)n);
   A(&d.candfd, (size_t)2 * n * d.npad);
   d.cand16 = !d.fd_cols && n <= 512 ? reinterpret_cast<uint32_t *>(d.candfd) : nullptr;  // (npad + 7) / 8 * 4 <= npad dwords a row
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);

@@ -125,6 +125,7 @@ struct Dev {
   // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])
   unsigned long long *ssw;
   int32_t *last_la; // [n][npad] LA row of each chain's last event
+  int32_t *rq;      // [n] k_resume_point: each chain's first round whose boundary left the prefix
   int32_t max_chain_len;
   // round-loop hand-off (k_round2, npad <= 128), by round parity
   int32_t *candfd;   // [2][n][npad] FD row of each chain's candidate (c, B[r][c])
@@ -274,9 +275,11 @@ void launch_round_init(const Dev &d, hipStream_t s);  // hand-off buffers for ro
 // resume the round loop at round ST_RESUME (boundaries B[r0] kept from a
 // prefix run): hand-off buffers and loop state for iteration r0
 void launch_round_resume(const Dev &d, hipStream_t s);
-// ST_RESUME = the last round r whose B[r][q] all lie inside the prefix
-// (chain_len), so they hold for every longer prefix
-void launch_resume_point(const Dev &d, int32_t R, hipStream_t s);
+// ST_RESUME = the last round r whose B[r][q] lie inside the prefix
+// (chain_len) for every chain q that grows in the next prefix (next_len;
+// null: every chain), so they hold for that prefix; rq[q] = chain q's
+// first r with B[r][q] >= len_q (kernels_rounds.hip)
+void launch_resume_point(const Dev &d, int32_t R, const int32_t *next_len, hipStream_t s);
 // FD entries of a segment's new rows for chains with no event in the segment
 void launch_fd_idle(const Dev &d, hipStream_t s);
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round

@@ -837,7 +837,15 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
 // run finds INSIDE the prefix (B[r][q] < prefix length) holds for the whole
 // DAG, and the loop can resume at the last round whose boundaries all lie
 // inside: r0 = min over q of (first r with B[r][q] >= len_q) - 1.
-__global__ __launch_bounds__(1024) void k_resume_point(Dev d, int32_t R) {
+// Only chains that gain events can move a boundary: a chain q with no new
+// event keeps B[r][q] for every r (its rows' counts do not change, and a
+// boundary at len_q finds no row), so the minimum runs over the chains that
+// grow in the next prefix (next_len[q] > len_q; every chain when next_len is
+// null).  rq[q] keeps each chain's first r for the host, which takes the
+// minimum over the chains a later call extends.  A chain that is empty or
+// has stopped growing therefore does not pin the resume point.  floor: the
+// closed form's first round (a Reset hashgraph's r0, else 0).
+__global__ __launch_bounds__(1024) void k_resume_point(Dev d, int32_t R, const int32_t *next_len) {
   __shared__ int32_t m;
   if (threadIdx.x == 0) m = R;
   __syncthreads();
@@ -849,13 +857,16 @@ __global__ __launch_bounds__(1024) void k_resume_point(Dev d, int32_t R) {
       if (d.B[(int64_t)mid * d.n + q] >= len) hi = mid;
       else lo = mid + 1;
     }
-    atomicMin(&m, lo);
+    if (d.rq) d.rq[q] = lo;
+    if (!next_len || next_len[q] > len) atomicMin(&m, lo);
   }
   __syncthreads();
-  if (threadIdx.x == 0) d.state[ST_RESUME] = max(0, m - 1);
+  if (threadIdx.x == 0) d.state[ST_RESUME] = max(d.r0, m - 1);
 }
 
-void launch_resume_point(const Dev &d, int32_t R, hipStream_t s) { k_resume_point<<<1, 1024, 0, s>>>(d, R); }
+void launch_resume_point(const Dev &d, int32_t R, const int32_t *next_len, hipStream_t s) {
+  k_resume_point<<<1, 1024, 0, s>>>(d, R, next_len);
+}
 
 // iteration r0's inputs, parity 0: B[r0] and the candidates' FD rows (from
 // FDT, which now covers the longer prefix); the loop state

@@ -89,6 +89,11 @@ def _run_pair(d, block, batches=1, cap_extra=64, tweak=None):
     st = hg.stats()
     assert st.blocks == rs.block_index + 1 + len(o2.blocks()["round_received"])
     _coords_sample(o2, hg)
+    if len(diff) >= batches and batches > 1 and len(d.participant_ids) <= 512:
+        # the calls after the first resume from the device state (the fiat
+        # region again, the round loop from the last round every extended
+        # chain fixed)
+        assert hg.pipeline()[1] >= 1
     return o2, hg, rs
 
 

@@ -199,3 +199,30 @@ def test_per_sync_trap_wide(n, N, seed, lag, div, step):
     assert len(trapped) >= 1, "the seed no longer produces a trapped witness"
     calls = (N + step - 1) // step
     assert hg.pipeline()[1] >= calls - 2
+
+
+@pytest.mark.parametrize("n,N,silent,join,step", [(9, 20_000, 4, 12_000, 500), (16, 30_000, 3, 40_000, 1_000)])
+def test_schedule_silent_peer(n, N, silent, join, step):
+    """A peer with no event at all (join >= N: never) or one that joins late:
+    its empty chain must not pin the incremental resume point to round 0
+    (k_resume_point only counts the chains a call extends), and every call
+    equals the oracle's state."""
+    from babble_amd import Hashgraph
+    from reset import SilentDag
+    d = SilentDag(n, N, 700 + n, silent, join)
+    pid = d.participant_ids
+    o = Oracle(n, pid, capacity=N)
+    hg = Hashgraph(pid, N)
+    spi = np.where(d.sp >= 0, d.index - 1, -1)
+    opc = np.where(d.op >= 0, pid[d.creator[np.maximum(d.op, 0)]], -1)
+    opi = np.where(d.op >= 0, d.index[np.maximum(d.op, 0)], -1)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(d.creator[lo:hi], d.index[lo:hi], d.sp[lo:hi], d.op[lo:hi], d.hashes[lo:hi], d.sig_r[lo:hi],
+                     d.ntx[lo:hi])
+        o.run_consensus()
+        assert not np.asarray(hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc[lo:hi],
+                                               opi[lo:hi], d.hashes[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])).any()
+        hg.run_consensus()
+        _compare(o, hg, f"silent peer, after [0, {hi})")
+    assert hg.pipeline()[1] >= N // step - 2
