@@ -49,7 +49,8 @@ class Roots(C.Structure):
                 ("self_parent_lamport", C.c_void_p), ("self_parent_round", C.c_void_p),
                 ("n_others", C.c_int32), ("other_root", C.c_void_p), ("other_key", C.c_void_p),
                 ("other_creator_id", C.c_void_p), ("other_index", C.c_void_p),
-                ("other_lamport", C.c_void_p), ("other_round", C.c_void_p), ("other_hash", C.c_void_p)]
+                ("other_lamport", C.c_void_p), ("other_round", C.c_void_p), ("other_hash", C.c_void_p),
+                ("self_parent_hash", C.c_void_p)]
 
 
 class Stats(C.Structure):

@@ -88,6 +88,8 @@ int upload(bh_handle *h) {
   if (h->reset_on) {
     HIPCHK(h, hipMemcpyAsync(d.rflag + a, h->h_rflag.data() + a, k, hipMemcpyHostToDevice, s));
     HIPCHK(h, hipMemcpyAsync(d.ext_lt + a, h->h_ext_lt.data() + a, k * 4, hipMemcpyHostToDevice, s));
+    if (h->fr.oth_of)
+      HIPCHK(h, hipMemcpyAsync(h->fr.oth_of + a, h->h_oth.data() + a, k * 4, hipMemcpyHostToDevice, s));
   }
   HIPCHK(h, hipStreamSynchronize(s));
   h->h_hash.clear();
@@ -1399,6 +1401,7 @@ static int insert_one(bh_handle *h, const bh_events *ev, int32_t *status, int64_
       h->h_hashes.insert(h->h_hashes.end(), ev->hash + i * 32, ev->hash + i * 32 + 32);
       h->h_rflag.push_back((int8_t)((oth >= 0 ? 1 : 0) | (ext ? 2 : 0)));
       h->h_ext_lt.push_back(ext ? h->others[(size_t)oth].lt : bh::UNSET);
+      h->h_oth.push_back(oth);
       if (ext) h->E0 = id + 1;
     }
     h->h_sp.push_back(ch.empty() ? -1 : ch.back());
@@ -1561,8 +1564,9 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
     return BH_ERR_INVALID;
   if (!h->h_creator.empty() || h->reset_on || h->stage != 0)
     return h->fail(BH_ERR_STATE, "bh_reset: a fresh handle only (no events inserted, no pass run)");
-  if (!h->group.empty() || h->world > 1 || h->frames_on)
-    return h->fail(BH_ERR_STATE, "bh_reset: one shard, block projection off");
+  if (!h->group.empty() || h->world > 1) return h->fail(BH_ERR_STATE, "bh_reset: one shard");
+  if (h->frames_on && !rt->self_parent_hash)
+    return h->fail(BH_ERR_INVALID, "bh_reset: the block projection needs each Root's SelfParent hash");
   if (rt->round_received < 0 || rt->block_index < -1) return h->fail(BH_ERR_INVALID, "bh_reset: bad block");
   (void)hipSetDevice(h->device);
   struct FailHook {  // the test hook covers this call only
@@ -1616,6 +1620,56 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   RoundTables t;
   int rc;
   if ((rc = alloc_round_tables(h, t, R_cap, r0, d.ssm != nullptr, d.ssw != nullptr))) return rc;
+  // the block projection's tables for the new round range, with the
+  // installed Roots (each Root's entries: unique keys sorted by key hash,
+  // Go's encoding/json map order; a Go map holds one entry per key)
+  bh::Frames nf{};
+  if (h->frames_on) {
+    const int32_t K = rt->n_others;
+    std::vector<int32_t> ord((size_t)K), ofs((size_t)n + 1, 0);
+    for (int32_t k = 0; k < K; ++k) ord[(size_t)k] = k;
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+      if (others[(size_t)a].root != others[(size_t)b].root) return others[(size_t)a].root < others[(size_t)b].root;
+      return memcmp(others[(size_t)a].key, others[(size_t)b].key, 32) < 0;
+    });
+    ord.erase(std::unique(ord.begin(), ord.end(),
+                          [&](int32_t a, int32_t b) {
+                            return others[(size_t)a].root == others[(size_t)b].root &&
+                                   !memcmp(others[(size_t)a].key, others[(size_t)b].key, 32);
+                          }),
+              ord.end());
+    for (int32_t k : ord) ofs[(size_t)others[(size_t)k].root + 1]++;
+    for (int c = 0; c < n; ++c) ofs[(size_t)c + 1] += ofs[(size_t)c];
+    std::vector<uint8_t> kb((size_t)K * 32 + 1), hb((size_t)K * 32 + 1);
+    std::vector<int32_t> cr((size_t)K + 1), ix((size_t)K + 1), lt((size_t)K + 1), rd((size_t)K + 1);
+    for (int32_t k = 0; k < K; ++k) {
+      const auto &o = others[(size_t)k];
+      memcpy(&kb[(size_t)k * 32], o.key, 32);
+      memcpy(&hb[(size_t)k * 32], o.hash, 32);
+      cr[(size_t)k] = o.creator;
+      ix[(size_t)k] = o.index;
+      lt[(size_t)k] = o.lt;
+      rd[(size_t)k] = o.round;
+    }
+    int rcf = frames_alloc_tables(h, nf, (int64_t)R_cap + 1, K, true);
+    auto up = [&](void *dst, const void *src, size_t bytes) {
+      if (rcf == BH_OK && bytes && hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) != hipSuccess) rcf = BH_ERR_DEVICE;
+    };
+    up(nf.rsp_hash, rt->self_parent_hash, (size_t)n * 32);
+    up(nf.ro_key, kb.data(), (size_t)K * 32);
+    up(nf.ro_hash, hb.data(), (size_t)K * 32);
+    up(nf.ro_creator, cr.data(), (size_t)K * 4);
+    up(nf.ro_index, ix.data(), (size_t)K * 4);
+    up(nf.ro_lt, lt.data(), (size_t)K * 4);
+    up(nf.ro_round, rd.data(), (size_t)K * 4);
+    up(nf.ro_ofs, ofs.data(), ((size_t)n + 1) * 4);
+    up(nf.ro_list, ord.data(), ord.size() * 4);
+    if (rcf != BH_OK) {
+      frames_free_tables(nf);
+      t.free_all();
+      return h->fail(rcf, "bh_reset: block projection tables");
+    }
+  }
   int32_t *cb = nullptr, *ls = nullptr, *rn = nullptr, *rs = nullptr, *elt = nullptr, *fw = nullptr;
   int8_t *rf = nullptr;
   std::vector<int32_t> base_h((size_t)n);
@@ -1631,10 +1685,15 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
     for (void *p : {(void *)cb, (void *)ls, (void *)rn, (void *)rs, (void *)rf, (void *)elt, (void *)fw})
       if (p) (void)hipFree(p);
     t.free_all();
+    frames_free_tables(nf);
     return rc;
   }
   // commit
   commit_round_tables(h, t, R_cap, r0);
+  if (h->frames_on) {
+    frames_free_tables(h->fr);
+    h->fr = nf;
+  }
   for (void *p : {(void *)d.chain_base, (void *)d.lt_seed, (void *)d.root_next, (void *)d.root_sp_round, (void *)d.rflag,
                   (void *)d.ext_lt, (void *)d.fw})
     if (p) (void)hipFree(p);
@@ -1642,6 +1701,7 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   d.r0 = r0;
   d.rlo = rlo;
   d.frame_lo = rt->round_received + 1;  // round_received's frame is the block itself (hashgraph.go:1063-1065)
+  d.blk_base = (int32_t)(rt->block_index + 1);  // NewBlockFromFrame(LastBlockIndex()+1, ...) (hashgraph.go:1096-1097)
   h->base_h = std::move(base_h);
   h->next_h.assign(rt->next_round, rt->next_round + n);
   h->sp_round_h.assign(rt->self_parent_round, rt->self_parent_round + n);
@@ -1655,6 +1715,7 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   h->reset_F = F;
   h->P = rt->round_received;  // rounds below LastConsensusRound are never queued (hashgraph.go:809-815)
   h->inc_valid = false;
+  if (h->frames_on) return frames_init(h);
   return BH_OK;
 }
 

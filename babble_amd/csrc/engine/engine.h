@@ -176,6 +176,7 @@ struct Dev {
   int32_t *fw;
   int8_t *rexists;
   int32_t frame_lo;  // frames below it are never emitted (Reset: LastConsensusRound's, hashgraph.go:1063-1065)
+  int32_t blk_base;  // Block.Index of the first block this handle makes (LastBlockIndex()+1: after a Reset block.Index()+1)
 };
 // row of (chain c, round r) in the ballot tables ssm / ssw
 __host__ __device__ inline int64_t ballot_row(const Dev &d, int c, int r) {
@@ -210,6 +211,18 @@ struct Frames {
   int8_t *fvalid;                // [R1] fhash / bhash computed
   uint8_t *dig;                  // [R1][32] scratch digests
   uint8_t *json, *bjson;         // materialized Frame / Block JSON of the last projection
+  // A Reset hashgraph's installed Roots (bh_reset with frames; null
+  // otherwise): a participant with no consensus event since the Reset keeps
+  // its Root whole in every frame (inmem_store.go:136-150 -> GetRoot), a
+  // first event's SelfParent RootEvent is its Root's, and an other-parent its
+  // creator's Root names (Others[ev] with the same Hash) is that entry
+  // (createOtherParentRootEvent, hashgraph.go:568-578).  Others keys / values
+  // (okey / oval) >= 0 are events; -2 - k is installed entry k.
+  uint8_t *rsp_hash;             // [n][32] Root.SelfParent.Hash (its Index, LT, Round: chain_base - 1, lt_seed, root_sp_round)
+  uint8_t *ro_key, *ro_hash;     // [K][32] entry k: the key event's hash, RootEvent.Hash
+  int32_t *ro_creator, *ro_index, *ro_lt, *ro_round;  // [K] RootEvent (creator slot, Index, LamportTimestamp, Round)
+  int32_t *ro_ofs, *ro_list;     // [n + 1], [K]: Root p's entries, unique keys sorted by key hash
+  int32_t *oth_of;               // [C] the entry of the event's creator Root naming its other-parent, -1 none
 };
 constexpr int32_t NO_FIRST = 0x7f7f7f7f;  // first_pos of a creator absent from the frame (memset 0x7f)
 

@@ -160,10 +160,11 @@ int frame_span(bh_handle *h, int32_t f, int64_t *i0, int64_t *i1) {
 
 }  // namespace
 
-int frames_alloc(bh_handle *h) {
-  bh::Frames &fr = h->fr;
-  const int64_t n = h->d.n, C = std::max<int64_t>(h->cap, 1);
-  const int64_t R1 = (int64_t)h->d.R_cap + 1, G = R1 * n;
+// the device tables of the projection for R1 rounds (and, with a Reset's
+// roots, K installed Others entries) into fr; on failure nothing stays
+// allocated.  Contents are initialized by frames_init.
+int frames_alloc_tables(bh_handle *h, bh::Frames &fr, int64_t R1, int64_t K, bool reset) {
+  const int64_t n = h->d.n, C = std::max<int64_t>(h->cap, 1), G = R1 * n;
   const int64_t S = std::max(G, C) + 1;
   int rc = BH_OK;
   auto A = [&](auto **p, int64_t cnt) {
@@ -173,31 +174,59 @@ int frames_alloc(bh_handle *h) {
   A(&fr.body_off, C); A(&fr.sig_off, C); A(&fr.body_len, C); A(&fr.sig_len, C);
   A(&fr.root_src, G); A(&fr.last_pos, n); A(&fr.first_pos, G); A(&fr.last_in, G);
   // Others: at most one per consensus event plus one per root made from a
-  // last consensus event
-  A(&fr.oofs, G + 1); A(&fr.okey, C + G); A(&fr.oval, C + G); A(&fr.ocur, std::max(G, 3 * n));
+  // last consensus event, plus a Reset's installed entries in every frame
+  // until their participant's first consensus event
+  A(&fr.oofs, G + 1); A(&fr.okey, C + G + (reset ? K * R1 : 0)); A(&fr.oval, C + G + (reset ? K * R1 : 0));
+  A(&fr.ocur, std::max(G, 3 * n));
   A(&fr.sz, S); A(&fr.sz2, S); A(&fr.part, S / 4096 + 2);
   A(&fr.missing, R1); A(&fr.jofs, R1 + 1); A(&fr.bofs, R1 + 1); A(&fr.jlen, R1); A(&fr.blen, R1);
   A(&fr.fhash, R1 * 32); A(&fr.bhash, R1 * 32); A(&fr.fvalid, R1); A(&fr.dig, R1 * 32);
-  if (rc != BH_OK) return rc;
-  HIPCHK(h, hipEventCreate(&h->ev_fr[0]));
-  HIPCHK(h, hipEventCreate(&h->ev_fr[1]));
+  if (reset) {
+    A(&fr.rsp_hash, n * 32); A(&fr.ro_key, K * 32); A(&fr.ro_hash, K * 32); A(&fr.ro_creator, K);
+    A(&fr.ro_index, K); A(&fr.ro_lt, K); A(&fr.ro_round, K); A(&fr.ro_ofs, n + 1); A(&fr.ro_list, K);
+    A(&fr.oth_of, C);
+  }
+  if (rc != BH_OK) frames_free_tables(fr);
+  return rc;
+}
+
+void frames_free_tables(bh::Frames &fr) {
+  void *ptrs[] = {fr.hash, fr.pids, fr.arena, fr.body_off, fr.sig_off, fr.body_len, fr.sig_len, fr.root_src,
+                  fr.last_pos, fr.first_pos, fr.last_in, fr.oofs, fr.okey, fr.oval, fr.ocur, fr.sz, fr.sz2,
+                  fr.part, fr.missing, fr.jofs, fr.bofs, fr.jlen, fr.blen, fr.fhash, fr.bhash, fr.fvalid,
+                  fr.dig, fr.json, fr.bjson, fr.rsp_hash, fr.ro_key, fr.ro_hash, fr.ro_creator, fr.ro_index,
+                  fr.ro_lt, fr.ro_round, fr.ro_ofs, fr.ro_list, fr.oth_of};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  fr = bh::Frames{};
+}
+
+// the tables' initial contents (no event bytes, nothing projected)
+int frames_init(bh_handle *h) {
+  bh::Frames &fr = h->fr;
+  const int64_t n = h->d.n, C = std::max<int64_t>(h->cap, 1);
   HIPCHK(h, hipMemcpy(fr.pids, h->pids.data(), (size_t)n * 8, hipMemcpyHostToDevice));
   HIPCHK(h, hipMemset(fr.body_len, 0xff, (size_t)C * 4));
   HIPCHK(h, hipMemset(fr.sig_len, 0xff, (size_t)C * 4));
+  if (fr.oth_of) HIPCHK(h, hipMemset(fr.oth_of, 0xff, (size_t)C * 4));
+  h->json_cap = h->bjson_cap = 0;
+  h->arena_cap = h->arena_len = 0;
   frames_reset(h);
+  int rc;
   if ((rc = ensure_buf(h, &fr.json, &h->json_cap, 1 << 20))) return rc;
   return ensure_buf(h, &fr.bjson, &h->bjson_cap, 1 << 20);
 }
 
+int frames_alloc(bh_handle *h) {
+  int rc;
+  if ((rc = frames_alloc_tables(h, h->fr, (int64_t)h->d.R_cap + 1, 0, false))) return rc;
+  HIPCHK(h, hipEventCreate(&h->ev_fr[0]));
+  HIPCHK(h, hipEventCreate(&h->ev_fr[1]));
+  return frames_init(h);
+}
+
 void frames_free(bh_handle *h) {
-  bh::Frames &fr = h->fr;
-  void *ptrs[] = {fr.hash, fr.pids, fr.arena, fr.body_off, fr.sig_off, fr.body_len, fr.sig_len, fr.root_src,
-                  fr.last_pos, fr.first_pos, fr.last_in, fr.oofs, fr.okey, fr.oval, fr.ocur, fr.sz, fr.sz2,
-                  fr.part, fr.missing, fr.jofs, fr.bofs, fr.jlen, fr.blen, fr.fhash, fr.bhash, fr.fvalid,
-                  fr.dig, fr.json, fr.bjson};
-  for (void *p : ptrs)
-    if (p) (void)hipFree(p);
-  fr = bh::Frames{};
+  frames_free_tables(h->fr);
   for (auto &e : h->ev_fr)
     if (e) (void)hipEventDestroy(e);
   if (h->host_json) (void)hipHostFree(h->host_json);

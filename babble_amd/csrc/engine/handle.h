@@ -157,6 +157,7 @@ struct bh_handle {
   std::vector<uint8_t> h_hashes;                        // every event's hash (Others matching)
   std::vector<int8_t> h_rflag;                          // Dev::rflag
   std::vector<int32_t> h_ext_lt;                        // Dev::ext_lt
+  std::vector<int32_t> h_oth;                           // Frames::oth_of (frames on)
   int64_t E0 = 0;  // events [0, E0) hold every other-parent only Root.Others knows
   int32_t fiat_max = -1;
 
@@ -197,6 +198,12 @@ inline int dalloc(bh_handle *h, T **p, size_t count) {
 // frames.cpp
 int frames_alloc(bh_handle *h);
 void frames_free(bh_handle *h);
+// the projection's device tables for R1 rounds into fr (with a Reset's K
+// installed Others entries: reset); frames_init gives them their initial
+// contents once they are the handle's
+int frames_alloc_tables(bh_handle *h, bh::Frames &fr, int64_t R1, int64_t K, bool reset);
+void frames_free_tables(bh::Frames &fr);
+int frames_init(bh_handle *h);
 void frames_reset(bh_handle *h);
 // roots, FrameHash and block hashes of the frames [P0, P1) just processed
 // (consensus positions [i0, i1))

@@ -150,30 +150,55 @@ __global__ __launch_bounds__(SCAN_T) void k_root_carry(Dev d, Frames fr, int32_t
   if (threadIdx.x == SCAN_T - 1) fr.last_pos[p] = carry;
 }
 
+// the installed Root entry naming e's other-parent (a Reset hashgraph), -1
+__device__ __forceinline__ int32_t root_other_of(const Frames &fr, int32_t e) { return fr.oth_of ? fr.oth_of[e] : -1; }
+
+// createOtherParentRootEvent(e) (hashgraph.go:568-600): the installed Root's
+// entry when it names e's other-parent, else the other-parent event
+__device__ __forceinline__ int32_t other_root_event(const Dev &d, const Frames &fr, int32_t e) {
+  const int32_t k = root_other_of(fr, e);
+  return k >= 0 ? -2 - k : d.op[e];
+}
+
 // Others of an event of the frame that is not its creator's first in it:
-// its other-parent, unless that is an earlier event of the same frame
+// its other-parent, unless that is an earlier event of the same frame (an
+// other-parent only a Reset Root knows never is)
 __device__ __forceinline__ bool other_entry(const Dev &d, const Frames &fr, int32_t f0, int64_t i, int32_t e,
                                             int64_t *g) {
   const int32_t op = d.op[e];
-  if (op < 0) return false;
+  if (op < 0 && root_other_of(fr, e) < 0) return false;
   const int32_t f = d.rr[e];
   *g = (int64_t)(f - f0) * d.n + d.creator[e];
   if (fr.first_pos[*g] == (int32_t)i) return false;
+  if (op < 0) return true;
   const int64_t opp = d.cons_pos[op];
   return !(opp >= d.frame_ofs[f] && opp < i);
 }
 
+// Others of each root: createRoot's entry (the source event's other-parent),
+// or, for a Reset Root kept whole, all its installed entries
 __global__ __launch_bounds__(256) void k_others_roots(Dev d, Frames fr, int32_t f0, int64_t G, bool fill) {
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= G) return;
   const int32_t s = fr.root_src[(int64_t)f0 * d.n + g];
-  const bool a = s >= 0 && d.op[s] >= 0;
+  const int32_t p = (int32_t)(g % d.n);
+  int32_t cnt = 0;
+  if (s >= 0) cnt = d.op[s] >= 0 || root_other_of(fr, s) >= 0;
+  else if (fr.ro_ofs) cnt = fr.ro_ofs[p + 1] - fr.ro_ofs[p];
   if (!fill) {
-    fr.sz[g] = a;
-  } else if (a) {
-    const int64_t k = fr.oofs[(int64_t)f0 * d.n + g] + atomicAdd(&fr.ocur[g], 1);
-    fr.okey[k] = s;
-    fr.oval[k] = d.op[s];
+    fr.sz[g] = cnt;
+  } else if (cnt) {
+    const int64_t k = fr.oofs[(int64_t)f0 * d.n + g] + atomicAdd(&fr.ocur[g], cnt);
+    if (s >= 0) {
+      fr.okey[k] = s;
+      fr.oval[k] = other_root_event(d, fr, s);
+    } else {
+      for (int32_t q = 0; q < cnt; ++q) {
+        const int32_t ent = fr.ro_list[fr.ro_ofs[p] + q];
+        fr.okey[k + q] = -2 - ent;
+        fr.oval[k + q] = -2 - ent;
+      }
+    }
   }
 }
 
@@ -189,7 +214,7 @@ __global__ __launch_bounds__(256) void k_others_events(Dev d, Frames fr, int32_t
   } else {
     const int64_t k = fr.oofs[(int64_t)f0 * d.n + g] + atomicAdd(&fr.ocur[g], 1);
     fr.okey[k] = e;
-    fr.oval[k] = d.op[e];
+    fr.oval[k] = other_root_event(d, fr, e);
   }
 }
 
@@ -198,9 +223,14 @@ __global__ __launch_bounds__(256) void k_others_base(Frames fr, int64_t at, int6
   if (g <= G) fr.oofs[at + g] = obase + fr.sz[g];
 }
 
-__device__ __forceinline__ bool hash_less(const uint8_t *hash, int32_t a, int32_t b) {
-  const uint32_t *x = reinterpret_cast<const uint32_t *>(hash + (int64_t)a * 32);
-  const uint32_t *y = reinterpret_cast<const uint32_t *>(hash + (int64_t)b * 32);
+// the hash an Others key stands for: an event's, or installed entry k's key
+__device__ __forceinline__ const uint8_t *key_ptr(const Frames &fr, int32_t key) {
+  return key >= 0 ? fr.hash + (int64_t)key * 32 : fr.ro_key + (int64_t)(-2 - key) * 32;
+}
+
+__device__ __forceinline__ bool hash_less(const Frames &fr, int32_t a, int32_t b) {
+  const uint32_t *x = reinterpret_cast<const uint32_t *>(key_ptr(fr, a));
+  const uint32_t *y = reinterpret_cast<const uint32_t *>(key_ptr(fr, b));
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const uint32_t u = __builtin_bswap32(x[q]), v = __builtin_bswap32(y[q]);
@@ -216,7 +246,7 @@ __global__ __launch_bounds__(256) void k_others_sort(Frames fr, int64_t at, int6
   for (int64_t a = lo + 1; a < hi; ++a) {
     const int32_t k = fr.okey[a], v = fr.oval[a];
     int64_t b = a - 1;
-    while (b >= lo && hash_less(fr.hash, k, fr.okey[b])) {
+    while (b >= lo && hash_less(fr, k, fr.okey[b])) {
       fr.okey[b + 1] = fr.okey[b];
       fr.oval[b + 1] = fr.oval[b];
       --b;
@@ -304,23 +334,32 @@ struct JW {
   }
 };
 
-// RootEvent (root.go:65-71); ev < 0: the base root event of slot
+// RootEvent (root.go:65-71): an event; -1: slot's Root SelfParent (the
+// base root event "Root<id>" with Index / LamportTimestamp / Round -1, or a
+// Reset Root's, root.go:75-84); -2 - k: installed Others entry k
 __device__ void root_event(JW &w, const Dev &d, const Frames &fr, int32_t ev, int32_t slot) {
+  const bool rst = d.chain_base != nullptr;
+  const int32_t spi = ev == -1 && rst ? d.chain_base[slot] - 1 : -1;  // Root.SelfParent.Index
+  const int32_t k = -2 - ev;
   w.lit("{\"Hash\":\"");
-  if (ev < 0) {
+  if (ev == -1 && spi >= 0) {
+    w.hex(fr.rsp_hash + (int64_t)slot * 32);
+  } else if (ev == -1) {
     w.lit("Root");
     w.num(fr.pids[slot]);
+  } else if (ev < -1) {
+    w.hex(fr.ro_hash + (int64_t)k * 32);
   } else {
     w.hex(fr.hash + (int64_t)ev * 32);
   }
   w.lit("\",\"CreatorID\":");
-  w.num(fr.pids[ev < 0 ? slot : d.creator[ev]]);
+  w.num(fr.pids[ev == -1 ? slot : ev < -1 ? fr.ro_creator[k] : d.creator[ev]]);
   w.lit(",\"Index\":");
-  w.num(ev < 0 ? -1 : d.index[ev]);
+  w.num(ev == -1 ? spi : ev < -1 ? fr.ro_index[k] : d.index[ev] + (rst ? d.chain_base[d.creator[ev]] : 0));
   w.lit(",\"LamportTimestamp\":");
-  w.num(ev < 0 ? -1 : d.lt[ev]);
+  w.num(ev == -1 ? (rst ? d.lt_seed[slot] : -1) : ev < -1 ? fr.ro_lt[k] : d.lt[ev]);
   w.lit(",\"Round\":");
-  w.num(ev < 0 ? -1 : d.round[ev]);
+  w.num(ev == -1 ? (rst ? d.root_sp_round[slot] : -1) : ev < -1 ? fr.ro_round[k] : d.round[ev]);
   w.lit("}");
 }
 
@@ -330,15 +369,15 @@ __device__ void root_json(JW &w, const Dev &d, const Frames &fr, int32_t f, int3
   const int32_t src = fr.root_src[g];
   if (p) w.lit(",");
   w.lit("{\"NextRound\":");
-  w.num(src < 0 ? 0 : d.round[src]);
+  w.num(src >= 0 ? d.round[src] : d.chain_base ? d.root_next[p] : 0);
   w.lit(",\"SelfParent\":");
-  root_event(w, d, fr, src < 0 ? -1 : d.sp[src], p);
+  root_event(w, d, fr, src < 0 ? -1 : max(d.sp[src], -1), p);
   w.lit(",\"Others\":{");
   const int64_t lo = fr.oofs[g], hi = fr.oofs[g + 1];
   for (int64_t k = lo; k < hi; ++k) {
     if (k > lo) w.lit(",");
     w.lit("\"");
-    w.hex(fr.hash + (int64_t)fr.okey[k] * 32);
+    w.hex(key_ptr(fr, fr.okey[k]));
     w.lit("\":");
     root_event(w, d, fr, fr.oval[k], 0);
   }
@@ -613,8 +652,8 @@ __global__ void k_root_query(Dev d, Frames fr, int32_t f, int32_t *out) {
   if (p >= d.n) return;
   const int64_t g = (int64_t)f * d.n + p;
   const int32_t src = fr.root_src[g];
-  out[3 * p] = src < 0 ? 0 : d.round[src];
-  out[3 * p + 1] = src < 0 ? -1 : d.sp[src];
+  out[3 * p] = src >= 0 ? d.round[src] : d.chain_base ? d.root_next[p] : 0;
+  out[3 * p + 1] = src < 0 ? -1 : max(d.sp[src], -1);
   out[3 * p + 2] = (int32_t)(fr.oofs[g + 1] - fr.oofs[g]);
 }
 

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(1024) void k_frame_scan(Dev d) {
   int32_t run = part[t] - s, runb = partb[t] - sb;
   for (int32_t r = lo; r < hi; ++r) {
     d.frame_ofs[r] = run;
-    d.blk_of_frame[r] = d.frame_cnt[r] > 0 ? runb : -1;
+    d.blk_of_frame[r] = d.frame_cnt[r] > 0 ? d.blk_base + runb : -1;
     run += d.frame_cnt[r];
     runb += d.frame_cnt[r] > 0;
   }

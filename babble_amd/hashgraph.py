@@ -163,11 +163,12 @@ class Hashgraph:
 
     def reset(self, round_received, block_index, next_round, self_parent_index, self_parent_lamport,
               self_parent_round, other_root=(), other_key=(), other_creator_id=(), other_index=(),
-              other_lamport=(), other_round=(), other_hash=()):
+              other_lamport=(), other_round=(), other_hash=(), self_parent_hash=None):
         """Hashgraph.Reset(block, frame) before the frame's events are
         inserted (hashgraph.go:1324-1369): the frame's Roots in participant
-        order and their Others flattened (bh_reset).  Insert frame.Events next,
-        then later events, as wire events."""
+        order and their Others flattened (bh_reset); self_parent_hash [n, 32]:
+        each Root.SelfParent.Hash (needed with frames=True).  Insert
+        frame.Events next, then later events, as wire events."""
         n = len(self.participant_ids)
         per = [np.ascontiguousarray(a, dtype=np.int32) for a in
                (next_round, self_parent_index, self_parent_lamport, self_parent_round)]
@@ -181,9 +182,14 @@ class Hashgraph:
         if oth[1].size != 32 * k or oth[6].size != 32 * k or any(oth[i].size != k for i in (0, 2, 3, 4, 5)):
             raise ValueError("Others arrays disagree in length")
         oth = [a if a.size else np.zeros(1, a.dtype) for a in oth]
+        sph = None
+        if self_parent_hash is not None:
+            sph = np.ascontiguousarray(self_parent_hash, dtype=np.uint8)
+            if sph.size != 32 * n:
+                raise ValueError("self_parent_hash must be [n, 32] bytes")
         rt = _native.Roots(int(round_received), int(block_index), *[_ptr(a) for a in per], k,
-                           *[_ptr(a) for a in oth])
-        self._keep_roots = (per, oth)
+                           *[_ptr(a) for a in oth], _ptr(sph))
+        self._keep_roots = (per, oth, sph)
         self._check(self._L.bh_reset(self._h, C.byref(rt)))
 
     def reset_consensus(self):
@@ -371,7 +377,8 @@ class Hashgraph:
 
     def block_hashes(self, first=0, count=None):
         """(frame_hash [m, 32], block_hash [m, 32], valid [m]) of blocks."""
-        b = self.stats().blocks
+        st = self.stats()
+        b = st.blocks - st.first_block  # blocks this handle made (a Reset starts after the block's Index)
         count = b - first if count is None else count
         fh = np.zeros((max(count, 1), 32), np.uint8)
         bh = np.zeros((max(count, 1), 32), np.uint8)

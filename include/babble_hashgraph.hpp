@@ -152,9 +152,12 @@ class Hashgraph {
     int32_t index, lamport_timestamp, round;
     uint8_t hash[32];     // RootEvent.Hash
   };
+  // self_parent_hash: each Root.SelfParent.Hash, 32 bytes per root (needed
+  // with frames on; empty otherwise)
   void Reset(int32_t round_received, int64_t block_index, const std::vector<int32_t> &next_round,
              const std::vector<int32_t> &self_parent_index, const std::vector<int32_t> &self_parent_lamport,
-             const std::vector<int32_t> &self_parent_round, const std::vector<RootOther> &others) {
+             const std::vector<int32_t> &self_parent_round, const std::vector<RootOther> &others,
+             const std::vector<uint8_t> &self_parent_hash = {}) {
     const size_t k = others.size();
     std::vector<int32_t> root(k), idx(k), lt(k), rnd(k);
     std::vector<int64_t> cre(k);
@@ -170,7 +173,8 @@ class Hashgraph {
     }
     bh_roots rt{round_received, block_index, next_round.data(), self_parent_index.data(),
                 self_parent_lamport.data(), self_parent_round.data(), (int32_t)k, root.data(), key.data(),
-                cre.data(), idx.data(), lt.data(), rnd.data(), hash.data()};
+                cre.data(), idx.data(), lt.data(), rnd.data(), hash.data(),
+                self_parent_hash.empty() ? nullptr : self_parent_hash.data()};
     check(bh_reset(h_, &rt));
   }
 

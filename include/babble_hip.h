@@ -112,9 +112,18 @@ int bh_reset_consensus(bh_handle *h);
  * (:1431-1457, 417-436), and rounds / Lamport timestamps follow the Root
  * cases A-F (docs/fastsync.rst:140-175).  Roots are given in participant
  * (ID) order, as Frame.Roots; Others entries flattened, each naming the
- * position of the Root that holds it.  Requires one shard, frames off, and
- * every NextRound / SelfParent.Round below round_received (as GetFrame's
- * roots are).  Blocks made afterwards have Index block_index + 1 + i. */
+ * position of the Root that holds it.  Requires one shard and every
+ * NextRound / SelfParent.Round below round_received (as GetFrame's roots
+ * are).  Blocks made afterwards have Index block_index + 1 + i.  With
+ * bh_config.frames the blocks are projected as GetFrame does on a Reset
+ * hashgraph: a participant with no consensus event since the Reset keeps
+ * the installed Root whole (InmemStore.LastConsensusEventFrom ->
+ * GetRoot, inmem_store.go:136-150), a first event's SelfParent RootEvent
+ * is its Root's (createSelfParentRootEvent, hashgraph.go:546-566), and an
+ * other-parent the Root's Others names is taken from there
+ * (createOtherParentRootEvent :568-578); self_parent_hash then gives each
+ * Root.SelfParent.Hash (ignored for Index -1, the base root event
+ * "Root<id>"; may be null when frames are off). */
 typedef struct {
   int32_t round_received;              /* block.RoundReceived() */
   int64_t block_index;                 /* block.Index() */
@@ -130,6 +139,7 @@ typedef struct {
   const int32_t *other_lamport;        /* RootEvent.LamportTimestamp */
   const int32_t *other_round;          /* RootEvent.Round */
   const uint8_t *other_hash;           /* [n_others][32] RootEvent.Hash */
+  const uint8_t *self_parent_hash;     /* [n][32] Root.SelfParent.Hash bytes (frames; null otherwise) */
 } bh_roots;
 int bh_reset(bh_handle *h, const bh_roots *roots);
 

@@ -104,6 +104,7 @@ struct hgo {
    * start at base = SelfParent.Index + 1 (the first event's Index) */
   int is_reset;
   int32_t *r_next, *r_sp_index, *r_sp_lt, *r_sp_round;
+  uint8_t *r_sp_hash; /* [n][32] SelfParent.Hash of a Reset root (Index >= 0; "Root<id>" otherwise) */
   /* Root.Others: entry k belongs to the root of slot oth_root[k], keyed by
    * the hash of the event whose other-parent it describes (oth_key) */
   int32_t n_oth;
@@ -115,9 +116,14 @@ struct hgo {
 };
 
 /* Root (root.go:88-96) of one participant in one frame: NextRound, the
- * SelfParent RootEvent (an event id, or -1 for the base root event
- * "Root<id>", root.go:75-84) and Others: key event -> RootEvent of value
- * event, sorted by key hash (Go's encoding/json sorts map keys) */
+ * SelfParent RootEvent (an event id, or -1 for the participant's Root
+ * SelfParent: the base root event "Root<id>", root.go:75-84, or after a
+ * Reset the installed Root's) and Others: key -> RootEvent, sorted by key
+ * hash (Go's encoding/json sorts map keys).  A key or value >= 0 is an
+ * event; OTH(k) = -2 - k is entry k of the Store Root's Others (after a
+ * Reset: createOtherParentRootEvent returns it, hashgraph.go:568-578, and a
+ * Root taken whole from the Store carries its map) */
+#define OTH(k) (-2 - (k))
 typedef struct {
   int32_t next_round, sp;
   int32_t n_others, cap_others;
@@ -215,6 +221,7 @@ void hgo_destroy(hgo *h) {
     free(h->roots[r]);
   }
   free(h->roots);
+  free(h->r_sp_hash);
   free(h->last_cons);
   for (int64_t e = 0; e < h->cap; e++) { free(h->body[e]); free(h->sig[e]); }
   free(h->body); free(h->sig); free(h->body_len); free(h->sig_len);
@@ -538,13 +545,17 @@ int hgo_reset(hgo *h, int32_t round_received, int64_t block_index, const int32_t
               const int32_t *sp_index, const int32_t *sp_lt, const int32_t *sp_round, int32_t n_others,
               const int32_t *oth_root, const uint8_t *oth_key32, const int32_t *oth_creator,
               const int32_t *oth_index, const int32_t *oth_lt, const int32_t *oth_round,
-              const uint8_t *oth_hash32) {
+              const uint8_t *oth_hash32, const uint8_t *sp_hash32) {
   if (h->N || h->is_reset || n_others < 0) return HGO_ERR_STATE;
   for (int32_t i = 0; i < h->n; i++) {
     h->r_next[i] = next_round[i];
     h->r_sp_index[i] = sp_index[i];
     h->r_sp_lt[i] = sp_lt[i];
     h->r_sp_round[i] = sp_round[i];
+  }
+  if (sp_hash32) {
+    h->r_sp_hash = (uint8_t *)xcalloc((size_t)h->n, 32);
+    memcpy(h->r_sp_hash, sp_hash32, (size_t)h->n * 32);
   }
   const size_t K = (size_t)n_others;
   h->n_oth = n_others;
@@ -781,15 +792,27 @@ static void root_add_other(root_t *r, int32_t key, int32_t val) {
  * createSelfParentRootEvent :546-566 reads them from the Root, root.go:73-84);
  * Others[ev] = the RootEvent of its other-parent (createOtherParentRootEvent
  * :568-600 -- a base Root has no Others to take it from) */
-static void create_root(hgo *h, int32_t ev, root_t *r) {
-  r->next_round = round_of(h, ev);
-  r->sp = h->sp[ev];
-  if (h->op[ev] >= 0) root_add_other(r, ev, h->op[ev]);
+static int32_t others_match(const hgo *h, int32_t x);
+
+/* createOtherParentRootEvent(ev) (hashgraph.go:568-600): the creator's Root
+ * entry keyed by ev when it names ev's other-parent, else the other-parent */
+static int32_t other_root_event(const hgo *h, int32_t ev) {
+  const int32_t k = others_match(h, ev);
+  return k >= 0 ? OTH(k) : h->op[ev];
 }
 
-static int cmp_hash_of(const hgo *hh, int32_t a, int32_t b) {
-  return memcmp(hh->hash + (size_t)a * 32, hh->hash + (size_t)b * 32, 32);
+static void create_root(hgo *h, int32_t ev, root_t *r) {
+  r->next_round = round_of(h, ev);
+  r->sp = h->sp[ev] >= 0 ? h->sp[ev] : -1;
+  if (h->op[ev] != -1) root_add_other(r, ev, other_root_event(h, ev));
 }
+
+/* the hash a key stands for: an event's, or Others entry k's key */
+static const uint8_t *key_hash(const hgo *h, int32_t key) {
+  return key >= 0 ? h->hash + (size_t)key * 32 : h->oth_key + (size_t)(-2 - key) * 32;
+}
+
+static int cmp_hash_of(const hgo *hh, int32_t a, int32_t b) { return memcmp(key_hash(hh, a), key_hash(hh, b), 32); }
 
 /* the roots of frame rr, whose sorted events are frame_ev[f .. f + l);
  * lastConsensusEvents as they stand before the frame's events are added */
@@ -807,11 +830,23 @@ static void frame_roots(hgo *h, int32_t rr, int64_t f, int64_t l) {
     if (!has[p]) { has[p] = 1; create_root(h, ev, &fr->r[p]); }
   }
   /* participants with no event in the frame: createRoot(last consensus
-   * event) or, with none, their Root -- a base Root here (:1174-1197) */
+   * event) or, with none, their Root from the Store (:1174-1197): a base
+   * Root, or the Root a Reset installed, whole, Others included */
   for (int32_t p = 0; p < n; p++) {
     if (has[p]) continue;
-    if (h->last_cons[p] >= 0) create_root(h, h->last_cons[p], &fr->r[p]);
-    else { fr->r[p].next_round = 0; fr->r[p].sp = -1; }
+    if (h->last_cons[p] >= 0) {
+      create_root(h, h->last_cons[p], &fr->r[p]);
+    } else {
+      fr->r[p].next_round = h->r_next[p];
+      fr->r[p].sp = -1;
+      for (int32_t k = 0; k < h->n_oth; k++) {
+        if (h->oth_root[k] != p) continue;
+        int dup = 0; /* a Go map holds one entry per key (the first here, as the engine) */
+        for (int32_t q = 0; q < k && !dup; q++)
+          dup = h->oth_root[q] == p && !memcmp(h->oth_key + (size_t)q * 32, h->oth_key + (size_t)k * 32, 32);
+        if (!dup) root_add_other(&fr->r[p], OTH(k), OTH(k));
+      }
+    }
   }
   /* other-parents outside the frame (:1199-1218): `treated` holds the
    * frame's events met so far in sorted order; an event whose other-parent
@@ -822,8 +857,9 @@ static void frame_roots(hgo *h, int32_t rr, int64_t f, int64_t l) {
     const int32_t ev = h->frame_ev[f + k];
     treated[ev] = 1;
     const int32_t op = h->op[ev];
-    if (op >= 0 && !treated[op] && h->sp[ev] != fr->r[h->creator[ev]].sp)
-      root_add_other(&fr->r[h->creator[ev]], ev, op);
+    const int32_t spr = h->sp[ev] >= 0 ? h->sp[ev] : -1;
+    if (op != -1 && !(op >= 0 && treated[op]) && spr != fr->r[h->creator[ev]].sp)
+      root_add_other(&fr->r[h->creator[ev]], ev, other_root_event(h, ev));
   }
   free(treated);
   free(has);
@@ -862,14 +898,14 @@ static void jint(jbuf *b, long long v) {
   jput(b, t, snprintf(t, sizeof t, "%lld", v));
 }
 /* Event.Hex() = fmt.Sprintf("0x%X", hash) (event.go:239-245) */
-static void jhex(jbuf *b, const hgo *h, int32_t ev) {
+static void jhexb(jbuf *b, const uint8_t *x) {
   static const char HX[] = "0123456789ABCDEF";
   char t[66];
-  const uint8_t *x = h->hash + (size_t)ev * 32;
   t[0] = '0'; t[1] = 'x';
   for (int i = 0; i < 32; i++) { t[2 + 2 * i] = HX[x[i] >> 4]; t[3 + 2 * i] = HX[x[i] & 15]; }
   jput(b, t, 66);
 }
+static void jhex(jbuf *b, const hgo *h, int32_t key) { jhexb(b, key_hash(h, key)); }
 /* []byte encodes as a base64 (StdEncoding, padded) string */
 static void jb64(jbuf *b, const uint8_t *x, int n) {
   static const char A[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
@@ -882,19 +918,23 @@ static void jb64(jbuf *b, const uint8_t *x, int n) {
     jput(b, t, 4);
   }
 }
-/* RootEvent (root.go:65-71); ev < 0: the base root event of slot p */
+/* RootEvent (root.go:65-71): an event; -1: slot p's Root SelfParent (the
+ * base root event "Root<id>" with Index / LamportTimestamp / Round -1, or a
+ * Reset root's); OTH(k): Others entry k */
 static void jroot_event(jbuf *b, hgo *h, int32_t ev, int32_t p) {
   jstr(b, "{\"Hash\":\"");
-  if (ev < 0) { jstr(b, "Root"); jint(b, h->pids[p]); }
+  if (ev == -1 && h->r_sp_index[p] >= 0 && h->r_sp_hash) jhexb(b, h->r_sp_hash + (size_t)p * 32);
+  else if (ev == -1) { jstr(b, "Root"); jint(b, h->pids[p]); }
+  else if (ev < -1) jhexb(b, h->oth_hash + (size_t)(-2 - ev) * 32);
   else jhex(b, h, ev);
   jstr(b, "\",\"CreatorID\":");
-  jint(b, h->pids[ev < 0 ? p : h->creator[ev]]);
+  jint(b, h->pids[ev == -1 ? p : ev < -1 ? h->oth_creator[-2 - ev] : h->creator[ev]]);
   jstr(b, ",\"Index\":");
-  jint(b, ev < 0 ? -1 : h->index[ev]);
+  jint(b, ev == -1 ? h->r_sp_index[p] : ev < -1 ? h->oth_index[-2 - ev] : h->index[ev]);
   jstr(b, ",\"LamportTimestamp\":");
-  jint(b, ev < 0 ? -1 : lamport_of(h, ev));
+  jint(b, ev == -1 ? h->r_sp_lt[p] : ev < -1 ? h->oth_lt[-2 - ev] : lamport_of(h, ev));
   jstr(b, ",\"Round\":");
-  jint(b, ev < 0 ? -1 : round_of(h, ev));
+  jint(b, ev == -1 ? h->r_sp_round[p] : ev < -1 ? h->oth_round[-2 - ev] : round_of(h, ev));
   jstr(b, "}");
 }
 
@@ -969,7 +1009,7 @@ static void block_json(hgo *h, int64_t blk, int body_only, jbuf *b) {
   b->len = 0;
   if (!body_only) jstr(b, "{\"Body\":");
   jstr(b, "{\"Index\":");
-  jint(b, blk);
+  jint(b, h->blk_index0 + blk); /* LastBlockIndex()+1 (block.go:100-110): after a Reset, block.Index()+1 on */
   jstr(b, ",\"RoundReceived\":");
   jint(b, rr);
   jstr(b, ",\"StateHash\":null,\"FrameHash\":\"");
@@ -1012,7 +1052,7 @@ int hgo_process_decided_rounds(hgo *h) {
     if (get_frame(h, pr->index, &f, &l) != HGO_OK) return HGO_ERR_STATE;
     /* roots before the frame's events become consensus events (not restated
      * for a Reset hashgraph, whose roots would start from the Reset roots) */
-    if (!h->is_reset) frame_roots(h, pr->index, f, l);
+    frame_roots(h, pr->index, f, l);
     if (l > 0) {
       int64_t first = h->ncons, txs = 0;
       for (int64_t k = 0; k < l; k++) {

@@ -74,7 +74,7 @@ int hgo_reset(hgo *h, int32_t round_received, int64_t block_index, const int32_t
               const int32_t *sp_index, const int32_t *sp_lt, const int32_t *sp_round, int32_t n_others,
               const int32_t *oth_root, const uint8_t *oth_key32, const int32_t *oth_creator,
               const int32_t *oth_index, const int32_t *oth_lt, const int32_t *oth_round,
-              const uint8_t *oth_hash32);
+              const uint8_t *oth_hash32, const uint8_t *sp_hash32 /* [n][32] Root SelfParent hashes, or NULL */);
 /* Store.KnownEvents: last Index per participant slot (the Root's
  * SelfParent.Index when it has no event) */
 void hgo_known(const hgo *h, int32_t *known);

@@ -33,7 +33,7 @@ def lib():
         L.hgo_insert_batch.argtypes = [P, I64, VP, VP, VP, VP, VP, VP, VP]
         L.hgo_insert_batch_ext.restype = I64
         L.hgo_insert_batch_ext.argtypes = [P, I64, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]
-        L.hgo_reset.argtypes = [P, I32, I64, VP, VP, VP, VP, I32, VP, VP, VP, VP, VP, VP, VP]
+        L.hgo_reset.argtypes = [P, I32, I64, VP, VP, VP, VP, I32, VP, VP, VP, VP, VP, VP, VP, VP]
         L.hgo_known.argtypes = [P, VP]
         for f in ("hgo_divide_rounds", "hgo_decide_fame", "hgo_decide_round_received",
                   "hgo_process_decided_rounds", "hgo_run_consensus"):
@@ -113,10 +113,11 @@ class Oracle:
         a = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in rs.root_arrays().items()}
         kh = np.ascontiguousarray(rs.oth_key, dtype=np.uint8).reshape(-1, 32)
         vh = np.ascontiguousarray(rs.oth_hash, dtype=np.uint8).reshape(-1, 32)
+        sh = np.ascontiguousarray(rs.sp_hash, dtype=np.uint8).reshape(-1, 32)
         rc = self.L.hgo_reset(self.h, rs.round_received, rs.block_index, _p(a["next_round"]),
                               _p(a["sp_index"]), _p(a["sp_lt"]), _p(a["sp_round"]), len(a["oth_root"]),
                               _p(a["oth_root"]), _p(kh), _p(a["oth_creator"]), _p(a["oth_index"]),
-                              _p(a["oth_lt"]), _p(a["oth_round"]), _p(vh))
+                              _p(a["oth_lt"]), _p(a["oth_round"]), _p(vh), _p(sh))
         if rc:
             raise RuntimeError(f"hgo_reset: {rc}")
 

@@ -39,6 +39,9 @@ class ResetInputs:
         self.sp_index = [int(d.index[e]) if e >= 0 else -1 for e in sp]
         self.sp_lt = [int(lt[e]) if e >= 0 else -1 for e in sp]
         self.sp_round = [int(rnd[e]) if e >= 0 else -1 for e in sp]
+        # Root.SelfParent.Hash (a base root event's is "Root<id>": zeros here)
+        self.sp_hash = np.stack([np.asarray(d.hashes[e], np.uint8) if e >= 0 else np.zeros(32, np.uint8)
+                                 for e in sp])
         self.oth_root, self.oth_creator, self.oth_index, self.oth_lt, self.oth_round = [], [], [], [], []
         keys, vals = [], []
         for p, (_, _, oth) in enumerate(roots):

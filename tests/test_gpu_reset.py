@@ -237,3 +237,86 @@ def test_reset_allocation_failure(monkeypatch):
         _compare(o2, hg, f"after an injected failure at allocation {k}")
         hg.close()
     assert failures >= 10  # every allocation of the call was covered
+
+
+def _event_bytes(g):
+    """EventBody.Marshal() bytes and Signature strings of every event of a
+    generated Dag or a KatDag"""
+    from frames import kat_event_bytes
+    if isinstance(g, KatDag):
+        return [list(x) for x in zip(*(kat_event_bytes(g, e) for e in range(len(g))))]
+    return [g.body_json(e) for e in range(len(g.creator))], [g.sig_string(e) for e in range(len(g.creator))]
+
+
+@pytest.mark.parametrize("src,block,batches", [
+    ("kat_funky_full", 1, 1), ("kat_sparse", 2, 2), ((4, 3000, 0xBA0), 3, 4), ((7, 4000, 0xBA1), 5, 3),
+    ((16, 8000, 0xBA2), 3, 3), ((32, 8000, 0xBA4), 2, 5), ((128, 20000, 0xBA6), 3, 3),
+    ((160, 30000, 0xBA7), 3, 2)])
+def test_reset_block_projection(src, block, batches):
+    """FastSync, then gossip, on a handle with frames (node.go fastForward ->
+    Core.FastForward -> Hashgraph.Reset, then RunConsensus per sync): after
+    every call, each new block's FrameHash and block hash, the Roots of its
+    frame -- the Reset roots (their SelfParent / Others as installed) for the
+    peers with no consensus event since the Reset -- and the Frame / Block
+    JSON byte for byte equal the oracle's Reset restatement, and Block.Index
+    continues from the Reset block's.  At n = 4 and 7 (TestFastSync's
+    setting, node_test.go:583-658 with checkGossip :741-771) every block
+    body from Index FirstConsensusRound on also equals the original
+    network's (tests/test_oracle_reset.py pins that on the oracle)."""
+    from babble_amd import Hashgraph
+    from frames import sha
+    g = KatDag(src) if isinstance(src, str) else Dag(*src)
+    d = DagArrays(g)
+    bodies, sigs = _event_bytes(g)
+    cap = len(d.creator) + 64
+    o = Oracle(d.n, d.participant_ids, capacity=cap)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    for e in range(len(d.creator)):
+        o.set_event_bytes(e, bodies[e], sigs[e])
+    o.run_consensus()
+    rs = ResetInputs(o, d, block)
+    o2 = Oracle(d.n, d.participant_ids, capacity=cap)
+    o2.reset(rs)
+    pid = np.asarray(d.participant_ids, np.int64)
+    hg = Hashgraph(pid, cap, frames=True)
+    hg.reset(rs.round_received, rs.block_index, rs.next_round, rs.sp_index, rs.sp_lt, rs.sp_round,
+             rs.oth_root, rs.oth_key, pid[np.asarray(rs.oth_creator, np.int64)] if rs.oth_creator else [],
+             rs.oth_index, rs.oth_lt, rs.oth_round, rs.oth_hash, self_parent_hash=rs.sp_hash)
+    assert hg.stats().first_block == rs.block_index + 1
+    seen = 0
+    diff = rs.diff
+    calls = [rs.frame] + [diff[len(diff) * b // batches: len(diff) * (b + 1) // batches] for b in range(batches)]
+    for c, ids in enumerate(calls):
+        n0 = o2.num_events()
+        st_o = oracle_insert(o2, rs, ids)
+        st_g = _wire(hg, d, ids)
+        assert np.array_equal(st_o != 0, st_g != 0), f"inserts of call {c}"
+        inv = {v: k for k, v in rs.new_id.items()}
+        new = range(n0, o2.num_events())
+        for e in new:
+            o2.set_event_bytes(e, bodies[inv[e]], sigs[inv[e]])
+        hg.set_event_bytes(n0, [bodies[inv[e]] for e in new], [sigs[inv[e]] for e in new])
+        o2.run_consensus()
+        hg.run_consensus()
+        _compare(o2, hg, f"call {c}")
+        ob = o2.blocks()
+        nb = len(ob["round_received"])
+        fh, bh, ok = hg.block_hashes()
+        assert len(fh) == nb and ok.all(), f"call {c}"
+        for b in range(seen, nb):
+            rr = int(ob["round_received"][b])
+            assert fh[b].tobytes() == o2.block_frame_hash(b), f"FrameHash of block {b} (frame {rr}), call {c}"
+            bj = o2.block_json(b)
+            assert bh[b].tobytes() == sha(bj), f"block hash {b}, call {c}"
+            assert hg.frame_roots(rr) == o2.frame_roots(rr), f"roots of frame {rr}"
+            assert hg.frame_json(rr) == o2.frame_json(rr), f"frame {rr} JSON"
+            assert hg.block_json(b) == bj, f"block {b} JSON"
+            if d.n <= 7:
+                idx = rs.block_index + 1 + b
+                if rs.round_received <= idx < len(o.blocks()["round_received"]):
+                    assert hg.block_json(b, body_only=True) == o.block_json(idx, body_only=True), idx
+        seen = nb
+    assert seen > 0
+    if batches > 1 and len(diff) >= batches:
+        assert hg.pipeline()[1] >= 1
+    hg.close()

@@ -128,3 +128,45 @@ def test_reset_generated(n, N, seed, lag, block):
         # their descendants, as in Go
         assert (st != 0).any()
     lamport_preserved(o, rs, o2, st)
+
+
+@pytest.mark.parametrize("n,N,seed,block", [(4, 3000, 0xBA0, 3), (4, 6000, 0xBB0, 10), (7, 4000, 0xBA1, 5)])
+def test_reset_blocks_match_network(n, N, seed, block):
+    """TestFastSync (node_test.go:583-658) through checkGossip (:741-771):
+    after a FastSync from a block and the gossip that follows, the synced
+    node's blocks from Index FirstConsensusRound (the Reset block's
+    RoundReceived) on have the same BlockBody -- FrameHash, and with it
+    every Frame's roots and events -- as the network's.  Pins the oracle's
+    Reset block projection (Reset roots in the frames, Block.Index after
+    the Reset block) at the reference test's size.  With many more peers
+    the first frames after the Reset can hold other events (rounds below
+    the frame lack the witnesses received before it, as
+    lamport_preserved's docstring says), so the property is checked where
+    the reference's own test runs it."""
+    g = Dag(n, N, seed)
+    d = DagArrays(g)
+    bodies = [g.body_json(e) for e in range(N)]
+    sigs = [g.sig_string(e) for e in range(N)]
+    o = Oracle(n, d.participant_ids, capacity=N + 64)
+    o.insert_dag(d.creator, d.index, d.sp, d.op, d.hashes, d.sig_r, d.ntx)
+    for e in range(N):
+        o.set_event_bytes(e, bodies[e], sigs[e])
+    o.run_consensus()
+    rs = ResetInputs(o, d, block)
+    o2 = Oracle(n, d.participant_ids, capacity=N + 64)
+    o2.reset(rs)
+    assert not oracle_insert(o2, rs, rs.frame).any()
+    assert not oracle_insert(o2, rs, rs.diff).any()
+    for old, new in rs.new_id.items():
+        o2.set_event_bytes(new, bodies[old], sigs[old])
+    o2.run_consensus()
+    nb, nb0 = len(o2.blocks()["round_received"]), len(o.blocks()["round_received"])
+    base = rs.block_index + 1
+    compared = 0
+    for j in range(nb):
+        if rs.round_received <= base + j < nb0:
+            assert o2.block_json(j, body_only=True) == o.block_json(base + j, body_only=True), base + j
+            bj = o2.block_json(j)
+            assert b'"Index":%d' % (base + j) in bj
+            compared += 1
+    assert compared > 50
