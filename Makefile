@@ -30,16 +30,21 @@ tests/cpp/hg_replay: tests/cpp/hg_replay.cpp include/babble_hashgraph.hpp includ
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ $< -Lbabble_amd -lbabble_hip -Wl,-rpath,'$$ORIGIN/../../babble_amd'
 
 # host-only AddressSanitizer build of the engine (tools/sanitize_engine.sh):
-# the host code (api.cpp, frames.cpp, the launch stubs) instrumented, the
-# gfx950 code objects unchanged (GPU ASan is not used); loaded through
-# BH_LIB_PATH with the clang ASan runtime preloaded
-ASAN_OBJ := $(patsubst babble_amd/csrc/engine/%,build/asan/%.o,$(ENGINE_SRC))
+# the host files (api.cpp, frames.cpp) built by g++ with -fsanitize=address
+# and UBSan, linked with the regular gfx950 kernel objects, loaded through
+# BH_LIB_PATH with GCC's ASan runtime preloaded.  (clang's ROCm ASan runtime
+# intercepts hsa_amd_memory_pool_allocate for device-side ASan, which needs
+# XNACK, and fails the first device allocation here.)
+HOST_SRC := $(wildcard babble_amd/csrc/engine/*.cpp)
+KERNEL_OBJ := $(patsubst babble_amd/csrc/engine/%,build/engine/%.o,$(wildcard babble_amd/csrc/engine/*.hip))
+ASAN_OBJ := $(patsubst babble_amd/csrc/engine/%,build/asan/%.o,$(HOST_SRC))
+ASANFLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
 build/asan/%.o: babble_amd/csrc/engine/% $(ENGINE_HDR)
 	@mkdir -p build/asan
-	$(HIPCC) $(HIPFLAGS) -g -fno-omit-frame-pointer -Xarch_host -fsanitize=address -Iinclude -c -o $@ $<
-tools/asan/libbabble_hip.so: $(ASAN_OBJ)
+	$(CXX) $(ASANFLAGS) -std=c++17 -fPIC -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -c -o $@ $<
+tools/asan/libbabble_hip.so: $(ASAN_OBJ) $(KERNEL_OBJ)
 	@mkdir -p tools/asan
-	$(HIPCC) $(HIPFLAGS) -shared -shared-libasan -Xarch_host -fsanitize=address -o $@ $(ASAN_OBJ) -L/opt/rocm/lib -lrccl -lcrypto -Wl,-rpath,/opt/rocm/lib
+	$(CXX) $(ASANFLAGS) -shared -o $@ $(ASAN_OBJ) $(KERNEL_OBJ) -L/opt/rocm/lib -lamdhip64 -lrccl -lcrypto -lpthread -Wl,-rpath,/opt/rocm/lib
 asan: tools/asan/libbabble_hip.so
 
 clean:

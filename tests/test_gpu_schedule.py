@@ -225,4 +225,6 @@ def test_schedule_silent_peer(n, N, silent, join, step):
                                                opi[lo:hi], d.hashes[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])).any()
         hg.run_consensus()
         _compare(o, hg, f"silent peer, after [0, {hi})")
-    assert hg.pipeline()[1] >= N // step - 2
+    # every call but the first and the relayouts (a chain outgrowing its
+    # slack: about every 1024 / (step / n) calls here) resumes
+    assert hg.pipeline()[1] >= N // step - 1 - (N // step) // (1024 * n // step)
