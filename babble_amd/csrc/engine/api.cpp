@@ -178,6 +178,19 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
   // captured graph (profiling / A-B; results are identical)
   static const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
+  static const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
+  if (bh::round_solo_eligible(v)) {  // one launch runs every round (k_round_solo)
+    if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));
+    bh::launch_round_solo(v, s);
+    HIPCHK(h, hipGetLastError());
+    if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
+    HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
+    float lms = 0;
+    if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
+    if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
+    if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
+    return BH_OK;
+  }
   if (!no_graph && (rc = build_graph(h, v, graph, graph_dev))) return rc;
   hipEvent_t done_ev[2];
   HIPCHK(h, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
@@ -187,7 +200,6 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   pin[0] = 0;
   bool done = false;
   // the loop's own device time (bh_get_stage_ms entry 7; BH_LOOP_TIMING=0: off, A/B)
-  static const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
   if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));  // (after any wait queued on s: loop time only)
   const int64_t max_batches = (int64_t)v.R_cap / ITER_BATCH + 2;
   for (int64_t b = 0; b < max_batches && !done; ++b) {

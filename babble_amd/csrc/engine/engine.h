@@ -298,6 +298,10 @@ void launch_resume_point(const Dev &d, int32_t R, const int32_t *next_len, hipSt
 // FD entries of a segment's new rows for chains with no event in the segment
 void launch_fd_idle(const Dev &d, hipStream_t s);
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
+// n <= 32 on the chain dataflow: the whole loop in one resident workgroup
+// (k_round_solo; opt-in with BH_ROUND_SOLO=1, measured A/B)
+bool round_solo_eligible(const Dev &d);
+void launch_round_solo(const Dev &d, hipStream_t s);
 // Reset hashgraphs: coordinates of events [0, d.N) one event at a time (the
 // batch whose other-parents only Root.Others knows), and the rounds below r0
 // in insertion order with B[r0] for the loop (kernels_reset.hip)

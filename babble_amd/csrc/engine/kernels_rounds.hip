@@ -829,6 +829,197 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
 }
 
+// k_round_solo: the whole round loop of a small hashgraph (n <= 32) in ONE
+// workgroup that stays resident until the loop ends.  At n <= 32 a round of
+// k_round2 is almost all fixed cost -- the launch boundary, and loads that
+// every launch fetches again from MALL because each launch starts with
+// invalidated L2s -- so here the state that crosses rounds stays on one
+// compute unit:
+//   * half-wave c (32 lanes) owns chain c, lane q of it candidate q;
+//   * B[r] and the candidates' FD rows live in LDS, double-buffered by
+//     round parity (one workgroup barrier per round);
+//   * chain c's LA window is a 32-row ring in LDS (slot = row & 31): a round
+//     loads only the rows its window gained (the boundary moves by about
+//     N / (n R) rows, not 32), from an L2 that no launch boundary invalidates;
+//   * the search is over rows, as k_round2's row-probe variant: every lane of
+//     a half-wave tests the same ring row (an LDS broadcast) against its own
+//     candidate, a ballot counts, B[r+1][c] = the first row reaching SM, and
+//     the ballot of the probe that verified it is fame's S_j;
+//   * the one dependent load of a round -- the new candidate's FD row -- is
+//     issued together with the next window's LA rows, and the round's outputs
+//     (B history, ssm ballots in k_round2<4>'s raw layout: word k holds
+//     candidates 16k + b at bit 4b) are stored after them, so no wait for the
+//     loads waits for the stores.
+// Windows that do not reach SM continue from global memory (rare).
+// Termination: each round ends the loop (no candidates, or a full round
+// table) or advances r toward R_cap.
+constexpr int SOLO_N = 32;
+__global__ __launch_bounds__(1024) void k_round_solo(Dev d) {
+  extern __shared__ __attribute__((aligned(16))) int4 ring4[];  // [n][32 rows][q4]
+  // candidate rows 144 B apart: the 32 lanes of a half-wave reading 32 rows
+  // with ds_read_b128 spread over the banks (128 B apart they would collide)
+  constexpr int CS = SOLO_N + 4;
+  __shared__ __attribute__((aligned(16))) int32_t cand[2][SOLO_N][CS];
+  __shared__ int32_t bsh[2][SOLO_N];
+  const int t = threadIdx.x, lane = t & 63;
+  const int c = t >> 5, q = t & 31;
+  const int n = d.n, npad = d.npad, q4 = npad / 4, sm = d.sm;
+  const unsigned long long half = (lane < 32) ? 0xFFFFFFFFull : 0xFFFFFFFF00000000ull;
+  const int hs = lane & 32;
+  const bool cv = c < n;
+  const int32_t len = cv ? d.chain_len[c] : 0, cs = cv ? d.chain_start[c] : 0;
+  const int32_t lenq = q < n ? d.chain_len[q] : 0;
+  const int4 *la4 = reinterpret_cast<const int4 *>(d.la);
+  int4 *ring = ring4 + (int64_t)(cv ? c : 0) * 32 * q4;
+  // the new LA rows [from, k0 + rows) of chain c's window into its ring:
+  // every load issued before any LDS store
+  auto load_ring = [&](int32_t from, int32_t to, int4 *lv) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int it = q + 32 * j;
+      const int32_t row = from + it / q4;
+      lv[j] = (cv && row < to) ? la4[((int64_t)cs + row) * q4 + (it - (it / q4) * q4)] : make_int4(0, 0, 0, 0);
+    }
+  };
+  auto store_ring = [&](int32_t from, int32_t to, const int4 *lv) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int it = q + 32 * j;
+      const int32_t row = from + it / q4;
+      if (cv && row < to) ring[(row & 31) * q4 + (it - (it / q4) * q4)] = lv[j];
+    }
+  };
+  int r = d.state[ST_CUR0];  // parity-0 buffers: k_round2_init / k_round_resume
+  if (t < n) bsh[0][t] = d.Bp[t];
+  for (int i = t; i < n * npad; i += blockDim.x) cand[0][i / npad][i % npad] = d.candfd[i];
+  int32_t k0 = cv ? d.Bp[c] : 0;
+  int32_t ring_lo = k0;  // rows [ring_lo, ring_lo + 32) of chain c are in the ring
+  {
+    int4 lv[8];
+    load_ring(k0, min(len, k0 + 32), lv);
+    store_ring(k0, min(len, k0 + 32), lv);
+  }
+  int err = 0;
+  // BH_DIAG: phase cycles of thread 0 (round start -> FD row read -> search
+  // done -> round-end loads + barrier), summed over rounds
+  const bool dg = d.diag != nullptr && t == 0;
+  unsigned long long c_f = 0, c_s = 0, c_e = 0, nr = 0;
+  __syncthreads();
+  for (int p = 0;; p ^= 1) {
+    const unsigned long long ts0 = dg ? stamp() : 0;
+    const int32_t bq = q < n ? bsh[p][q] : 0;
+    const bool act = q < n && bq < lenq;
+    const int nc = __popcll(__ballot(act) & half);  // the same in every half-wave
+    if (nc == 0) break;
+    if (r + 1 >= d.R_cap) { err = 1; break; }
+    const int rows = cv ? min(32, max(0, len - k0)) : 0;
+    int4 f[8];  // candidate q's FD row
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      f[u] = (act && u < q4) ? *reinterpret_cast<const int4 *>(&cand[p][q][4 * u])
+                             : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+    if (dg) { __builtin_amdgcn_s_waitcnt(0xc07f); }
+    const unsigned long long ts1 = dg ? stamp() : 0;
+    auto ss = [&](const int4 *x4, bool global) {
+      int ge = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u < q4) ge += ge4(x4[u], f[u]);
+      (void)global;
+      return act && ge >= sm;
+    };
+    // first window row whose ballot reaches SM
+    int lo = 0, hi = rows;
+    unsigned long long ssb = 0;
+    while (__any(lo < hi)) {
+      const int mid = (lo + hi) >> 1;
+      const bool sv = ss(ring + ((k0 + min(mid, max(rows - 1, 0))) & 31) * q4, false);
+      const unsigned long long m = __ballot(sv) & half;
+      if (lo < hi) {
+        if (__popcll(m) >= sm) { hi = mid; ssb = m; }
+        else lo = mid + 1;
+      }
+    }
+    int32_t result = lo < rows ? k0 + lo : len;
+    // ---- SM not reached in the window (rare): later windows from global ----
+    bool need = cv && lo >= rows && rows == 32;
+    int32_t wk = k0 + 32;
+    while (__any(need)) {
+      const int wr = need ? min(32, len - wk) : 0;
+      if (need && wr <= 0) need = false;
+      int l2 = 0, h2 = need ? wr : 0;
+      unsigned long long sb2 = 0;
+      while (__any(l2 < h2)) {
+        const int mid = (l2 + h2) >> 1;
+        const int4 *x4 = la4 + ((int64_t)cs + wk + min(mid, max(wr - 1, 0))) * q4;
+        const bool sv = need && ss(x4, true);
+        const unsigned long long m = __ballot(sv) & half;
+        if (l2 < h2) {
+          if (__popcll(m) >= sm) { h2 = mid; sb2 = m; }
+          else l2 = mid + 1;
+        }
+      }
+      if (need && l2 < wr) { result = wk + l2; ssb = sb2; need = false; }
+      wk += 32;
+    }
+    const unsigned long long ts2 = dg ? stamp() : 0;
+    // ---- round end: the hand-off load and the next window's rows together,
+    // then this round's outputs ----
+    const int32_t k1 = cv ? result : 0;
+    const int32_t from = max(k1, ring_lo + 32), to = min(len, k1 + 32);
+    int4 lv[8];
+    load_ring(from, to, lv);
+    const bool hand = cv && result < len;
+    const int32_t v = (hand && q < n) ? d.fdt[fdt_pos((int64_t)cs + result, q, npad)] : FD_NONE;
+    if (hand && q < 2) {  // fame's S_j of the new candidate (k_round2<4>'s ballot layout)
+      const uint32_t bits = (uint32_t)((ssb >> hs) >> (16 * q)) & 0xFFFFu;
+      unsigned long long w = 0;
+      for (int k = 0; k < 16; ++k) w |= (unsigned long long)((bits >> k) & 1u) << (4 * k);
+      d.ssm[ballot_row(d, c, r + 1) * 16 + q] = w;
+    } else if (hand && q < 16) {
+      d.ssm[ballot_row(d, c, r + 1) * 16 + q] = 0ull;
+    }
+    if (cv && q == 0) d.B[(int64_t)(r + 1) * n + c] = result;
+    store_ring(from, to, lv);
+    if (hand && q < npad) cand[p ^ 1][c][q] = v;
+    if (cv && q == 0) bsh[p ^ 1][c] = result;
+    ring_lo = k1;
+    k0 = k1;
+    ++r;
+    __syncthreads();
+    if (dg) {
+      const unsigned long long ts3 = stamp();
+      c_f += ts1 - ts0; c_s += ts2 - ts1; c_e += ts3 - ts2; ++nr;
+    }
+  }
+  if (dg) {
+    atomicAdd(&d.diag[DG_RD_B], c_e);
+    atomicAdd(&d.diag[DG_RD_LOAD], c_f);
+    atomicAdd(&d.diag[DG_RD_COMP], c_s);
+    atomicAdd(&d.diag[DG_RD_TOTAL], c_f + c_s + c_e);
+    atomicAdd(&d.diag[DG_RD_CALLS], nr);
+  }
+  if (t == 0) {
+    d.state[ST_ROUNDS] = r;
+    d.state[ST_ITERS] = r;
+    d.state[ST_ERR] = err;
+    d.state[ST_DONE] = 1;
+    signal_done(d);
+  }
+}
+
+// opt-in (BH_ROUND_SOLO=1): measured slower than k_round2 at C2 (DESIGN.md
+// section 5, "One resident workgroup"), kept as the measured alternative
+bool round_solo_eligible(const Dev &d) {
+  const char *e = getenv("BH_ROUND_SOLO");  // (read per loop: the tests switch it)
+  return d.fd_cols != 0 && d.n <= SOLO_N && e && atoi(e);
+}
+
+void launch_round_solo(const Dev &d, hipStream_t s) {
+  const size_t lds = (size_t)d.n * 32 * d.npad * 4;
+  k_round_solo<<<1, 1024, lds, s>>>(d);
+}
+
 // Resuming the loop after a prefix run (segments).  A
 // prefix of the DAG in insertion order is closed under ancestry, so its
 // rows' lastAncestors are final; a candidate beyond the prefix cannot be
@@ -945,6 +1136,7 @@ void configure_round_kernels() {
   CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
   CFG((k_round2<4, true>)); CFG((k_round2<8, true>)); CFG((k_round2<4, false>)); CFG((k_round2<8, false>));
+  CFG(k_round_solo);
 #undef CFG
 }
 

@@ -560,3 +560,17 @@ def test_segment_pipeline_schedule(monkeypatch):
                          d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi])
         hg.run_consensus()
         _compare(o, hg, f"segments, after [0, {hi})")
+
+
+@pytest.mark.parametrize("n,N,seed,lag,K", [(4, 10_000, 0xBABB1E01, 0, 1), (9, 8_000, 14, 3, 1), (32, 60_000, 15, 0, 3),
+                                            (17, 40_000, 31, 5, 4)])
+def test_round_solo_parity(monkeypatch, n, N, seed, lag, K):
+    """The opt-in resident round loop (k_round_solo, BH_ROUND_SOLO=1: one
+    workgroup runs every round, n <= 32) against the oracle, alone and as
+    the loop of the segment pipeline; its windows that miss SM continue from
+    global memory (the wild DAG)."""
+    monkeypatch.setenv("BH_ROUND_SOLO", "1")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    _random_parity(n, N, seed, lag)
+    if K == 1:
+        _wild_parity(24, 30_000, 73, 20_000)
