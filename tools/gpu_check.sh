@@ -19,7 +19,7 @@ step() {  # name timeout cmd...
 }
 for s in "$@"; do
   case $s in
-    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    tests) step pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf ;;
     treset) step pytest_reset 600 python -u -m pytest tests/test_gpu_reset.py -m gpu -v --timeout 120 --timeout-method thread -rf ;;
     twide) step pytest_wide 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rf -k "wide or 512 or 300 or c4 or C4 or floww" ;;
     tfloww) step pytest_floww 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 300 --timeout-method thread -rf -x -k "floww" ;;
