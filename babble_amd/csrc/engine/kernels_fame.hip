@@ -237,7 +237,7 @@ __device__ __forceinline__ uint32_t fame_ballot_word(const unsigned long long *b
 template <int NW>
 struct FameLds {
   static constexpr int MAXN = 32 * NW;
-  uint32_t V[2][MAXN][NW];  // votes: [cur][x chain][word over W(j-1) chains]
+  uint32_t V[2][NW][MAXN];  // votes: [cur][word over W(j-1) chains][x chain] (lanes = consecutive x)
   uint32_t S[MAXN][NW];     // stronglySee rows of W(j), restricted to W(j-1)
   uint32_t wx[NW], wp[NW], wc[NW];  // W(r), W(j-1), W(j)
   int32_t dec[MAXN], nd[MAXN], yev[MAXN], xev[MAXN], xk[MAXN];
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
           if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
           if (d.la[(int64_t)L.yev[y] * npad + xc] >= L.xk[xc]) v |= 1u << b;
         }
-        L.V[0][x][h * HW_ + k] = v;
+        L.V[0][h * HW_ + k][x] = v;
       }
     }
     __syncthreads();
@@ -321,6 +321,10 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
       const bool normal = (diff % n) != 0;
       if (isx && !L.dec[x]) {
         int decide = 0;
+        // x's votes in registers: they are read for every voter y
+        uint32_t vx[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w) vx[w] = L.V[cur][w][x];
         for (int k = 0; k < HW_; ++k) {
           uint32_t v = 0;
           for (int b = 0; b < 32; ++b) {
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
             int yays = 0, tot = 0;
 #pragma unroll
             for (int w = 0; w < NW; ++w) {
-              yays += __popc(L.S[y][w] & L.V[cur][x][w]);
+              yays += __popc(L.S[y][w] & vx[w]);
               tot += __popc(L.S[y][w]);
             }
             const int nays = tot - yays;
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
             }
             if (vote) v |= 1u << b;
           }
-          L.V[cur ^ 1][x][h * HW_ + k] = v;
+          L.V[cur ^ 1][h * HW_ + k][x] = v;
         }
         if (decide) atomicOr(&L.nd[x], decide);
       }

@@ -83,6 +83,30 @@ __device__ __forceinline__ int32_t block_min(int32_t v, int32_t *sh) {
   return *sh;
 }
 
+// LDS histogram add for one wave: lanes with equal bins are grouped by
+// ballots (a block's events span a few frames, so a wave has one to a few
+// distinct bins), and one lane per group adds the group's count -- per-lane
+// atomics on one bin serialise in the LDS (16 conflict cycles per LDS
+// instruction, profiles/pmc_sq.json round 3).  Returns each lane's rank
+// among the block's events of its bin (the old value of the group's add
+// plus its rank within the group); b < 0: no bin
+__device__ __forceinline__ int32_t wave_hist_add(int32_t *hist, int32_t b) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pending = __ballot(b >= 0);
+  int32_t rank = -1;
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const int32_t bl = __shfl(b, leader);
+    const unsigned long long same = __ballot(b == bl) & pending;
+    int32_t old = 0;
+    if (lane == leader) old = atomicAdd(&hist[bl], __popcll(same));
+    old = __shfl(old, leader);
+    if (b == bl) rank = old + __popcll(same & ((1ull << lane) - 1));
+    pending &= ~same;
+  }
+  return rank;
+}
+
 __global__ __launch_bounds__(256) void k_frame_count(Dev d) {
   __shared__ int32_t hist[HB], rmin_s;
   const int t = threadIdx.x;
@@ -102,10 +126,9 @@ __global__ __launch_bounds__(256) void k_frame_count(Dev d) {
   const int32_t rmin = block_min(lo, &rmin_s);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    if (rr[u] < 0) continue;
-    const int32_t b = rr[u] - rmin;
-    if (b < HB) atomicAdd(&hist[b], 1);
-    else atomicAdd(&d.frame_cnt[rr[u]], 1);
+    const int32_t b = rr[u] < 0 ? -1 : rr[u] - rmin;
+    (void)wave_hist_add(hist, b < HB ? b : -1);
+    if (b >= HB) atomicAdd(&d.frame_cnt[rr[u]], 1);
   }
   __syncthreads();
   if (t < HB && hist[t]) atomicAdd(&d.frame_cnt[rmin + t], hist[t]);
@@ -160,11 +183,9 @@ __global__ __launch_bounds__(256) void k_frame_scatter(Dev d, int32_t P0) {
   const int32_t rmin = block_min(lo, &rmin_s);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    slot[u] = -1;
-    if (rr[u] < 0) continue;
-    const int32_t b = rr[u] - rmin;
-    if (b < HB) slot[u] = atomicAdd(&hist[b], 1);                          // rank in the block
-    else slot[u] = d.frame_ofs[rr[u]] + atomicAdd(&d.frame_cur[rr[u]], 1);  // absolute (rare)
+    const int32_t b = rr[u] < 0 ? -1 : rr[u] - rmin;
+    slot[u] = wave_hist_add(hist, b < HB ? b : -1);                                   // rank in the block
+    if (b >= HB) slot[u] = d.frame_ofs[rr[u]] + atomicAdd(&d.frame_cur[rr[u]], 1);  // absolute (rare)
   }
   __syncthreads();
   if (t < HB) basev[t] = hist[t] ? d.frame_ofs[rmin + t] + atomicAdd(&d.frame_cur[rmin + t], hist[t]) : 0;
