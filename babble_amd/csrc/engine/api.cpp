@@ -1221,7 +1221,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.rspan = (int32_t)R1;
   if (d.fd_cols) {
     A(&d.ssm, R1 * n * 16);
-    d.round_lpc = d.npad <= 64 ? 4 : 8;
+    d.round_lpc = 8;  // k_round2: 8 lanes per candidate at every n <= 128
   } else {
     // chain-major 32-bit FD rows (fd) are allocated on first use (ensure_fd):
     // only the 32-bit wide loop, n > 512 fame and the chunked sweep's

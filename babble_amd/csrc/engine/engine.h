@@ -118,7 +118,7 @@ struct Dev {
   // does not pay for the rounds below it
   unsigned long long *ssm;
   int32_t rbase, rspan;
-  int32_t round_lpc;  // LPC of k_round2 (4 or 8)
+  int32_t round_lpc;  // lanes per candidate of k_round2 (8), the layout of its ssm ballots
   int32_t round_p8;   // k_round_wide<*, true>: 8-bit window-relative rows where the window's LA spread is at most this
                       // (P8_XMAX; BH_ROUND_P8=<x> lowers it to force the 16-bit fallback, 0: off)
   // [n][rspan][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):

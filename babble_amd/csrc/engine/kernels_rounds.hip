@@ -603,9 +603,14 @@ __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
 // per probe.  Same compares per probe; the groups of a wave read different
 // rows, so each group starts its four 128-B chunks at chunk (q & 3): the
 // four groups of a ds_read_b128 lane set then hit distinct banks.
-template <int LPC, bool TQ>
+// 8 lanes per candidate, PPL 16-B pieces of its FD row per lane (LPC * PPL *
+// 4 >= npad columns), 8 npad threads (rounded up to whole waves): the
+// workgroup is as wide as its candidates need -- at n = 32 four waves of one
+// piece per lane instead of sixteen waves of four pieces, most of them idle
+// rows of nonexistent candidates (C2 search 2.5 us -> see DESIGN.md)
+template <int PPL, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
-  constexpr int PPL = 4;  // pieces per lane: LPC * PPL >= npad / 4
+  constexpr int LPC = 8;
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
   __shared__ int32_t cntk[16];
   __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
@@ -789,9 +794,11 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     }
     // fame's input for the new candidate y = (c, result): SS(y, q) over
     // the candidates q of round r = the ballots of the probe that verified
-    // y's row.  Raw ballots, one aligned 8-B word per wave (fame packs the
-    // LPC-strided bits), chain-major [c][round]; issued last, since a later
-    // vmcnt wait would include them
+    // y's row.  Raw ballots, one aligned 8-B word per wave (candidate q at
+    // bit 8 (q % 8) of word q / 8; fame packs the LPC-strided bits and masks
+    // the words of chains >= n, which fewer waves leave unwritten),
+    // chain-major [c][round]; issued last, since a later vmcnt wait would
+    // include them
     if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
   }
   if (dg) {
@@ -847,8 +854,8 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
 //     the ballot of the probe that verified it is fame's S_j;
 //   * the one dependent load of a round -- the new candidate's FD row -- is
 //     issued together with the next window's LA rows, and the round's outputs
-//     (B history, ssm ballots in k_round2<4>'s raw layout: word k holds
-//     candidates 16k + b at bit 4b) are stored after them, so no wait for the
+//     (B history, ssm ballots in k_round2's raw layout: word k holds
+//     candidates 8k + b at bit 8b) are stored after them, so no wait for the
 //     loads waits for the stores.
 // Windows that do not reach SM continue from global memory (rare).
 // Termination: each round ends the loop (no candidates, or a full round
@@ -971,10 +978,10 @@ __global__ __launch_bounds__(1024) void k_round_solo(Dev d) {
     load_ring(from, to, lv);
     const bool hand = cv && result < len;
     const int32_t v = (hand && q < n) ? d.fdt[fdt_pos((int64_t)cs + result, q, npad)] : FD_NONE;
-    if (hand && q < 2) {  // fame's S_j of the new candidate (k_round2<4>'s ballot layout)
-      const uint32_t bits = (uint32_t)((ssb >> hs) >> (16 * q)) & 0xFFFFu;
+    if (hand && q < 4) {  // fame's S_j of the new candidate (k_round2's ballot layout, 8 lanes per candidate)
+      const uint32_t bits = (uint32_t)((ssb >> hs) >> (8 * q)) & 0xFFu;
       unsigned long long w = 0;
-      for (int k = 0; k < 16; ++k) w |= (unsigned long long)((bits >> k) & 1u) << (4 * k);
+      for (int k = 0; k < 8; ++k) w |= (unsigned long long)((bits >> k) & 1u) << (8 * k);
       d.ssm[ballot_row(d, c, r + 1) * 16 + q] = w;
     } else if (hand && q < 16) {
       d.ssm[ballot_row(d, c, r + 1) * 16 + q] = 0ull;
@@ -1135,7 +1142,8 @@ void configure_round_kernels() {
   CFG((k_round_wide<1, false>)); CFG((k_round_wide<2, false>)); CFG((k_round_wide<4, false>));
   CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
-  CFG((k_round2<4, true>)); CFG((k_round2<8, true>)); CFG((k_round2<4, false>)); CFG((k_round2<8, false>));
+  CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
+  CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG(k_round_solo);
 #undef CFG
 }
@@ -1145,12 +1153,15 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
     const size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
     static const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));
+    const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);  // 8 lanes per candidate
     if (rows_search) {
-      if (d.npad <= 64) k_round2<4, false><<<d.n, 1024, lds, s>>>(d, p);
-      else k_round2<8, false><<<d.n, 1024, lds, s>>>(d, p);
+      if (d.npad <= 32) k_round2<1, false><<<d.n, nt, lds, s>>>(d, p);
+      else if (d.npad <= 64) k_round2<2, false><<<d.n, nt, lds, s>>>(d, p);
+      else k_round2<4, false><<<d.n, nt, lds, s>>>(d, p);
     } else {
-      if (d.npad <= 64) k_round2<4, true><<<d.n, 1024, lds, s>>>(d, p);
-      else k_round2<8, true><<<d.n, 1024, lds, s>>>(d, p);
+      if (d.npad <= 32) k_round2<1, true><<<d.n, nt, lds, s>>>(d, p);
+      else if (d.npad <= 64) k_round2<2, true><<<d.n, nt, lds, s>>>(d, p);
+      else k_round2<4, true><<<d.n, nt, lds, s>>>(d, p);
     }
     return;
   }
