@@ -1152,7 +1152,7 @@ void configure_round_kernels() {
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
     const size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
-    static const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));
+    const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));  // (read per capture: the tests switch it)
     const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);  // 8 lanes per candidate
     if (rows_search) {
       if (d.npad <= 32) k_round2<1, false><<<d.n, nt, lds, s>>>(d, p);

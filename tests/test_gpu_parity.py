@@ -574,3 +574,19 @@ def test_round_solo_parity(monkeypatch, n, N, seed, lag, K):
     _random_parity(n, N, seed, lag)
     if K == 1:
         _wild_parity(24, 30_000, 73, 20_000)
+
+
+@pytest.mark.parametrize("variant", ["tq", "rows"])
+@pytest.mark.parametrize("n,N,seed,lag,K", [(4, 10_000, 0xBABB1E01, 0, 1), (9, 8_000, 14, 3, 2), (32, 60_000, 15, 0, 3),
+                                            (17, 40_000, 31, 5, 4), (48, 40_000, 37, 6, 2)])
+def test_small_n_round_kernels(monkeypatch, variant, n, N, seed, lag, K):
+    """k_round2 at n <= 64 (8 lanes per candidate, one or two pieces each,
+    8 npad threads): the per-candidate T_q search and the row-probe search
+    (BH_ROUND_ROWS=1) against the oracle, alone and inside the segment
+    pipeline; the wild DAG's windows that miss SM continue window by window."""
+    if variant == "rows":
+        monkeypatch.setenv("BH_ROUND_ROWS", "1")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    _random_parity(n, N, seed, lag)
+    if K == 1:
+        _wild_parity(24, 30_000, 73, 20_000)
