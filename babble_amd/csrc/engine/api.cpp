@@ -608,7 +608,9 @@ bool segments_eligible(const bh_handle *h) {
 // 316 ms with 8, profiles/r3_c4_segments.log); its incremental calls still
 // run as one more segment of the same machinery
 int segments_for(const Dev &d, int64_t events) {
-  int K = !d.fd_cols ? 1 : events >= 4000000 ? 8 : events >= 1000000 ? 4 : 1;
+  // (round 3: C5, 2M events, 79.0M events/s at 4 segments, 87.0M at 8,
+  // 88.1M at 12; C2, 1M events, 48.6M at 4, 48.3M at 8; C3 equal at 8 and 12)
+  int K = !d.fd_cols ? 1 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
 }
