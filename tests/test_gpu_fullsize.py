@@ -9,7 +9,7 @@ resume at the last round segment s fixed and the incremental layout are all
 on the path these checks cover:
 
   * C2 (32 peers, 1M events: 4 segments) and C5 (64 peers with 21 lagging,
-    2M events: 4 segments), whole;
+    2M events: 8 segments), whole;
   * C3's DAG (128 peers, the bench's 10M-event DAG) on its first 2.5M
     events with 5 segments of 500k events -- every chain resumes 4 times at
     real chain lengths (the oracle needs about 25 s for them);
@@ -54,7 +54,7 @@ def test_c2_whole_dag():
 @pytest.mark.timeout(600)
 def test_c5_whole_dag():
     hg = _whole(5)
-    assert hg.pipeline()[0] == 4
+    assert hg.pipeline()[0] == 8  # the default from 1.5M events
 
 
 @pytest.mark.timeout(900)
