@@ -49,6 +49,7 @@ void free_all(bh_handle *h) {
   if (h->sha_buf) (void)hipFree(h->sha_buf);
   if (h->q_buf) (void)hipFree(h->q_buf);
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
+  if (h->graph_s) (void)hipGraphExecDestroy(h->graph_s);
   for (auto &e : h->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto &e : h->ev_sweep)
@@ -58,6 +59,8 @@ void free_all(bh_handle *h) {
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   for (auto &g : h->seg_graph)
+    if (g) (void)hipGraphExecDestroy(g);
+  for (auto &g : h->seg_graph_s)
     if (g) (void)hipGraphExecDestroy(g);
   for (auto &e : h->seg_ev)
     if (e) (void)hipEventDestroy(e);
@@ -151,9 +154,9 @@ int set_chain_tables(bh_handle *h) {
   return BH_OK;
 }
 
-// the round loop's iterations as one graph of ITER_BATCH launches for the
-// view v, cached per slot (kernel arguments are captured by value)
-int build_graph(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_dev) {
+// the round loop's iterations as one graph of `iters` (even) launches for
+// the view v, cached per slot (kernel arguments are captured by value)
+int build_graph(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_dev, int iters) {
   if (*graph && memcmp(graph_dev, &v, sizeof(Dev)) == 0) return BH_OK;
   if (*graph) {
     (void)hipGraphExecDestroy(*graph);
@@ -161,7 +164,7 @@ int build_graph(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_de
   }
   hipGraph_t g;
   HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-  for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(v, i & 1, h->stream);
+  for (int i = 0; i < iters; ++i) bh::launch_round_iteration(v, i & 1, h->stream);
   HIPCHK(h, hipStreamEndCapture(h->stream, &g));
   HIPCHK(h, hipGraphInstantiate(graph, g, nullptr, nullptr, 0));
   (void)hipGraphDestroy(g);
@@ -171,8 +174,12 @@ int build_graph(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_de
 
 // the round loop on h->stream for view v, its inputs set up already:
 // replays batches of iterations, checking completion one batch behind so
-// the device never idles on the host round trip.  Returns the loop state.
-int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_dev, int32_t *st) {
+// the device never idles on the host round trip.  The first two batches
+// are ITER_FIRST iterations (graph_s), the rest ITER_BATCH: a loop that ends
+// within a few rounds -- an incremental call's -- runs 8 launches rather
+// than 64, most of them no-ops behind the done flag.  Returns the loop state.
+int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph_dev, hipGraphExec_t *graph_s,
+                   Dev *graph_dev_s, int32_t *st) {
   int rc;
   hipStream_t s = h->stream;
   // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
@@ -191,7 +198,8 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
     return BH_OK;
   }
-  if (!no_graph && (rc = build_graph(h, v, graph, graph_dev))) return rc;
+  if (!no_graph && (rc = build_graph(h, v, graph, graph_dev, ITER_BATCH))) return rc;
+  if (!no_graph && (rc = build_graph(h, v, graph_s, graph_dev_s, ITER_FIRST))) return rc;
   hipEvent_t done_ev[2];
   HIPCHK(h, hipEventCreateWithFlags(&done_ev[0], hipEventDisableTiming));
   HIPCHK(h, hipEventCreateWithFlags(&done_ev[1], hipEventDisableTiming));
@@ -201,13 +209,14 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   bool done = false;
   // the loop's own device time (bh_get_stage_ms entry 7; BH_LOOP_TIMING=0: off, A/B)
   if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));  // (after any wait queued on s: loop time only)
-  const int64_t max_batches = (int64_t)v.R_cap / ITER_BATCH + 2;
+  const int64_t max_batches = (int64_t)v.R_cap / ITER_BATCH + 4;
   for (int64_t b = 0; b < max_batches && !done; ++b) {
+    const bool first = b < 2;
     if (no_graph) {
-      for (int i = 0; i < ITER_BATCH; ++i) bh::launch_round_iteration(v, i & 1, s);
+      for (int i = 0; i < (first ? ITER_FIRST : ITER_BATCH); ++i) bh::launch_round_iteration(v, i & 1, s);
       HIPCHK(h, hipGetLastError());
     } else {
-      HIPCHK(h, hipGraphLaunch(*graph, s));
+      HIPCHK(h, hipGraphLaunch(first ? *graph_s : *graph, s));
     }
     HIPCHK(h, hipEventRecord(done_ev[b & 1], s));
     if (b > 0) {
@@ -216,12 +225,11 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     }
   }
   if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
-  HIPCHK(h, hipStreamSynchronize(s));
+  HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));  // (one synchronisation)
   float lms = 0;
   if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
   (void)hipEventDestroy(done_ev[0]);
   (void)hipEventDestroy(done_ev[1]);
-  HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
   if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
   if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
   return BH_OK;
@@ -533,7 +541,7 @@ int rounds_loop(bh_handle *h) {
   } else {
     bh::launch_round_init(d, s);
   }
-  if ((rc = run_round_loop(h, d, &h->graph, &h->graph_dev, st))) return rc;
+  if ((rc = run_round_loop(h, d, &h->graph, &h->graph_dev, &h->graph_s, &h->graph_dev_s, st))) return rc;
   bh::launch_resume_point(d, st[bh::ST_ROUNDS], nullptr, s);  // each chain's resume round (rq) for the next call
   if ((rc = rounds_tail(h, st, 0))) return rc;
   if (h->reset_on && !h->fdt_lost) {
@@ -758,7 +766,8 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
       }
       bh::launch_round_resume(rv, sr);
     }
-    if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], st))) {
+    if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], &h->seg_graph_s[k & 1],
+                             &h->seg_graph_dev_s[k & 1], st))) {
       (void)hipEventDestroy(sr_mark);
       return rc;
     }
@@ -899,13 +908,16 @@ int fame_finish(bh_handle *h) {
     bh::launch_fame_scatter_range(h->d, h->wofs_h[(size_t)h->P], h->wofs_h[(size_t)h->R], h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
+  // the decided flags of PendingRounds' rounds [P, R) only (the rest are
+  // final) and the error word, behind one synchronisation
   h->decided_h.assign((size_t)h->R, 0);
-  if (h->R > 0)
-    HIPCHK(h, hipMemcpyAsync(h->decided_h.data(), h->d.decided, (size_t)h->R, hipMemcpyDeviceToHost, h->stream));
+  if (h->R > h->P)
+    HIPCHK(h, hipMemcpyAsync(h->decided_h.data() + h->P, h->d.decided + h->P, (size_t)(h->R - h->P),
+                             hipMemcpyDeviceToHost, h->stream));
+  int32_t *err = h->pinned_state + bh::ST_COUNT + 3;  // pinned staging word
+  HIPCHK(h, hipMemcpyAsync(err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  int32_t err = 0;
-  HIPCHK(h, copy_sync(h->stream, &err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost));
-  if (err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
+  if (*err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
   // updatePendingRounds (hashgraph.go:689-695): set, never cleared
   for (int32_t r = h->P; r < h->R; ++r)
     if (h->decided_h[(size_t)r]) h->pend_dec[(size_t)r] = 1;
@@ -1011,26 +1023,31 @@ int order_finish(bh_handle *h) {
   bh::launch_trap_processed(d, h->P, P1, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[5], s));
-  HIPCHK(h, hipStreamSynchronize(s));
-  int32_t st[bh::ST_COUNT];
-  HIPCHK(h, copy_sync(s, st, d.state, sizeof st, hipMemcpyDeviceToHost));
+  // the state and the frames this call processed, [P0, P1), behind one
+  // synchronisation: earlier frames, their blocks and their counts are
+  // final, so a call reads back only its own (O(new frames), not O(every
+  // frame so far) -- a long-running node's calls stay flat)
   const int32_t P0 = h->P;
+  const size_t k = (size_t)std::max(0, P1 - P0);
+  int32_t st[bh::ST_COUNT];
+  std::vector<int32_t> cnt(k), ofs(k), ld(k);
+  std::vector<int64_t> ntx(k);
+  HIPCHK(h, hipMemcpyAsync(st, d.state, sizeof st, hipMemcpyDeviceToHost, s));
+  if (k) {
+    HIPCHK(h, hipMemcpyAsync(cnt.data(), d.frame_cnt + P0, k * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(ofs.data(), d.frame_ofs + P0, k * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(ntx.data(), d.frame_ntx + P0, k * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(ld.data(), d.frame_loaded + P0, k * 4, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(h, hipStreamSynchronize(s));
   const int64_t ncons0 = h->ncons;
   h->P = P1;
   h->ncons = st[bh::ST_NCONS];
-  h->cons_txs = h->cons_loaded = 0;
-  h->blocks.clear();
-  if (h->P > 0) {
-    std::vector<int32_t> cnt(h->P), ofs(h->P), ld(h->P);
-    std::vector<int64_t> ntx(h->P);
-    HIPCHK(h, hipMemcpyAsync(cnt.data(), d.frame_cnt, h->P * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(ofs.data(), d.frame_ofs, h->P * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(ntx.data(), d.frame_ntx, h->P * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, copy_sync(s, ld.data(), d.frame_loaded, h->P * 4, hipMemcpyDeviceToHost));
-    for (int32_t r = 0; r < h->P; ++r) {
-      if (cnt[r] > 0) h->blocks.push_back(Block{r, ofs[r], cnt[r], ntx[r]});
-      h->cons_txs += ntx[r];
-      h->cons_loaded += ld[r];
+  if (k) {
+    for (size_t i = 0; i < k; ++i) {
+      if (cnt[i] > 0) h->blocks.push_back(Block{P0 + (int32_t)i, ofs[i], cnt[i], ntx[i]});
+      h->cons_txs += ntx[i];
+      h->cons_loaded += ld[i];
     }
   }
   if (h->frames_on && P1 > P0) {

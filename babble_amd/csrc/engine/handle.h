@@ -19,6 +19,7 @@ using bh::Dev;
 namespace bh {
 
 constexpr int ITER_BATCH = 32;  // round-loop iterations per graph replay
+constexpr int ITER_FIRST = 4;   // ... for the first two replays of a loop (an incremental call needs a few rounds)
 constexpr int NSTAGE = 5;
 
 struct Block {
@@ -30,6 +31,7 @@ struct Block {
 
 using bh::Block;
 using bh::ITER_BATCH;
+using bh::ITER_FIRST;
 using bh::NSTAGE;
 
 struct bh_handle {
@@ -77,8 +79,8 @@ struct bh_handle {
   int64_t ncons = 0, cons_txs = 0, cons_loaded = 0;
   std::vector<Block> blocks;
   // round-loop graph
-  hipGraphExec_t graph = nullptr;
-  Dev graph_dev{};
+  hipGraphExec_t graph = nullptr, graph_s = nullptr;  // ITER_BATCH / ITER_FIRST iterations
+  Dev graph_dev{}, graph_dev_s{};
   int32_t *pinned_state = nullptr;
   uint8_t *sha_buf = nullptr;  // bh_hash_bodies scratch
   uint8_t *q_buf = nullptr;    // bh_query_events scratch
@@ -99,8 +101,8 @@ struct bh_handle {
   int32_t *seg_zero = nullptr;   // [n] zeros: seg_lo of a one-segment view
   int32_t *segbuf = nullptr;     // [2 parities][lo, len][n]
   int32_t *seg_stage = nullptr;  // pinned staging of segbuf, same layout
-  hipGraphExec_t seg_graph[2] = {nullptr, nullptr};
-  Dev seg_graph_dev[2]{};
+  hipGraphExec_t seg_graph[2] = {nullptr, nullptr}, seg_graph_s[2] = {nullptr, nullptr};
+  Dev seg_graph_dev[2]{}, seg_graph_dev_s[2]{};
   std::vector<hipEvent_t> seg_ev;  // per segment: coordinates done, k_flow32 start / end
   int32_t segments_used = 1;
   int32_t *tlist = nullptr, *tlist_stage = nullptr;  // [2 parities][tlist_cap] segment tile lists

@@ -1148,7 +1148,8 @@ void configure_round_kernels() {
 #undef CFG
 }
 
-// iteration parity p = round & 1 (ITER_BATCH is even, rounds start at 0)
+// iteration parity p: the loop state alternates by iteration (every graph
+// batch -- ITER_FIRST, ITER_BATCH -- is even, so each starts at parity 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
     const size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
