@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.rq, d.candfd, d.opdesc, d.lt_row, d.ssm, d.ssw,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
                   d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
@@ -1252,6 +1252,15 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.rq, (size_t)n);
   A(&d.candfd, (size_t)2 * n * d.npad);
   d.cand16 = !d.fd_cols && n <= 512 ? reinterpret_cast<uint32_t *>(d.candfd) : nullptr;  // (npad + 7) / 8 * 4 <= npad dwords a row
+  d.round2_p8 = getenv("BH_ROUND2_P8") && atoi(getenv("BH_ROUND2_P8"));
+  d.round_p8g = getenv("BH_ROUND_P8G") ? std::clamp(atoi(getenv("BH_ROUND_P8G")), 0, 64) : bh::P8G_DELTA;
+  if (d.cand16 || (d.fd_cols && d.npad > 64 && d.round2_p8)) {  // k_round_wide<*, true> / k_round2<4, true>
+    A(&d.cand8, (size_t)2 * n * ((d.npad + 15) / 16 * 16));
+    A(&d.c8tag, (size_t)2 * n);
+    A(&d.Bq, (size_t)2 * d.npad);
+    if (rc == BH_OK && hipMemset(d.c8tag, 0xFF, (size_t)2 * n * 4) != hipSuccess) rc = BH_ERR_DEVICE;
+    if (rc == BH_OK && hipMemset(d.Bq, 0, (size_t)2 * d.npad * 4) != hipSuccess) rc = BH_ERR_DEVICE;
+  }
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);

@@ -26,6 +26,7 @@ namespace bh {
 constexpr int32_t UNSET = INT32_MIN;    // Go nil
 constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
 constexpr int32_t P16_MAXLEN = 65000;  // longest chain the 16-bit round loop takes
+constexpr int P8G_DELTA = 20;  // k_round_wide's shared 8-bit base: B[r-1][i] - 20
 constexpr int P8_XMAX = 126;  // largest window-relative LA of k_round_wide's 8-bit rows (bit 7 is the compare's)
 constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 8192;     // frames sorted in LDS up to this size (96 KiB)
@@ -121,6 +122,17 @@ struct Dev {
   int32_t round_lpc;  // lanes per candidate of k_round2 (8), the layout of its ssm ballots
   int32_t round_p8;   // k_round_wide<*, true>: 8-bit window-relative rows where the window's LA spread is at most this
                       // (P8_XMAX; BH_ROUND_P8=<x> lowers it to force the 16-bit fallback, 0: off)
+  // round-based 8-bit candidate rows (k_round_wide<*, true>):
+  // iteration r's byte columns are relative to base_i = max(B[r-1][i] -
+  // round_p8g, 0), a base every workgroup of the iteration shares, so the
+  // workgroup that hands a candidate over converts its row once (cand8)
+  // instead of every workgroup converting every candidate.  c8tag[p][c] = r
+  // when cand8[p][c] was written for iteration r (-1: convert from cand16)
+  uint8_t *cand8;     // [2][n][(npad + 15) / 16 * 16] bytes
+  int32_t *c8tag;     // [2][n]
+  int32_t *Bq;        // [2][npad] k_round2 bytes: B[r - 1] for the iteration of parity p (written by iteration r - 1)
+  int32_t round_p8g;  // base offset below B[r-1] (P8G_DELTA; BH_ROUND_P8G=0 turns the shared base off)
+  int32_t round2_p8;  // k_round2<4, true> on byte rows too (BH_ROUND2_P8=1; off by default: no gain measured at C3)
   // [n][rspan][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
   // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])
   unsigned long long *ssw;

@@ -132,6 +132,39 @@ __device__ __forceinline__ uint32_t pack8(uint32_t lo, uint32_t hi) {
   return __builtin_amdgcn_perm(hi, lo, 0x06040200u);
 }
 
+// k_round_wide's hand-off of the new candidate (c, row) for iteration r + 1:
+// its cand16 row (gather_cand16's layout) and, with the shared base on, its
+// cand8 row -- byte i = min(max(FD + 1 - base_i, 0), 127) with base_i =
+// max(B[r][i] - round_p8g, 0) from Bcur = B[r] (the base iteration r + 1
+// reads back from the B history), 127 past column n -- then the row's tag.
+// Four columns per thread; every thread of the workgroup calls it.
+__device__ __forceinline__ void handoff_wide(const Dev &d, int64_t row, int p1, int c, const int32_t *Bcur,
+                                             int32_t rnext) {
+  const int npad = d.npad, n = d.n, w16 = (npad + 7) / 8 * 4, w8 = (npad + 15) / 16 * 16;
+  uint32_t *dst16 = d.cand16 + ((int64_t)p1 * n + c) * w16;
+  const bool g = d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;
+  uint32_t *dst8 = g ? reinterpret_cast<uint32_t *>(d.cand8 + ((int64_t)p1 * n + c) * w8) : nullptr;
+  for (int j = threadIdx.x; j < w8 / 4; j += blockDim.x) {
+    uint32_t h[4], b8 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = 4 * j + k;
+      const int32_t v = i < n ? d.fdt[fdt_pos(row, i, npad)] : FD_NONE;
+      h[k] = min((uint32_t)v + 1u, 0xFFFFu);  // FD_NONE + 1 wraps to 2^31
+      if (g) {
+        const int32_t base = i < n ? max(Bcur[i] - d.round_p8g, 0) : 0;
+        const uint32_t f = i < n ? min((uint32_t)max((int32_t)h[k] - base, 0), 127u) : 127u;
+        b8 |= f << (8 * k);
+      }
+    }
+    if (2 * j < w16) dst16[2 * j] = h[0] | (h[1] << 16);
+    if (2 * j + 1 < w16) dst16[2 * j + 1] = h[2] | (h[3] << 16);
+    if (g) dst8[j] = b8;
+  }
+  // read by the next launch only (the kernel boundary orders it after the row)
+  if (g && threadIdx.x == 0) d.c8tag[(int64_t)p1 * n + c] = rnext;
+}
+
 template <int LPC>
 __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
@@ -300,8 +333,10 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   __shared__ int32_t hist[WROWS + 1];
   __shared__ int32_t sh_res, sh_nc;
   __shared__ int8_t tq_s[512];  // T_q of every candidate in the current window (ssw, n <= 512)
-  __shared__ uint32_t wbase2[256];  // P8: base of columns 2j, 2j + 1 as 16-bit pairs
+  __shared__ uint32_t wbase2[256];  // P8: base of columns 2j, 2j + 1 as 16-bit pairs (the window's first row)
+  __shared__ uint32_t gbase2[256];  // P8: the same from the shared base max(B[r-1][i] - round_p8g, 0)
   __shared__ int32_t sh_wide;       // P8: some column's LA spread exceeds P8_XMAX (16-bit window)
+  __shared__ int32_t sh_gbad;       // P8: the window does not fit the shared base
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
@@ -333,27 +368,43 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   for (;;) {
     const int wrows = min(WROWS, len - wk0);
     if (wrows <= 0) break;
-    bool p8 = false;
+    bool p8 = false, p8g = false;
     if constexpr (P16) {
       if (d.round_p8) {
         // P8 when every column's spread down the window fits (first row: the
-        // base, last row: the largest LA)
-        if (t == 0) sh_wide = 0;
+        // base, last row: the largest LA).  The first window of an iteration
+        // whose previous round's boundaries are known also tries the shared
+        // base (B[r-1][i] - round_p8g): then every candidate whose row its
+        // producer already converted (c8tag) needs no conversion here
+        const bool tryg = d.cand8 != nullptr && d.round_p8g > 0 && r > d.r0 && wk0 == Bp[c];
+        if (t == 0) { sh_wide = 0; sh_gbad = !tryg; }
         __syncthreads();
         const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
-        bool bad = false;
+        const int32_t *Bprev = d.B + (int64_t)(r - 1) * n;
+        bool bad = false, gbad = false;
         for (int j = t; j < 256; j += 256) {
           const int i0 = 2 * j, i1 = 2 * j + 1;
-          const int32_t b0 = i0 < npad ? max(r0p[i0], 0) : 0, b1 = i1 < npad ? max(r0p[i1], 0) : 0;
+          const int32_t a0 = i0 < npad ? r0p[i0] : 0, a1 = i1 < npad ? r0p[i1] : 0;
+          const int32_t z0 = i0 < npad ? r1p[i0] : 0, z1 = i1 < npad ? r1p[i1] : 0;
+          const int32_t b0 = max(a0, 0), b1 = max(a1, 0);
           wbase2[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
-          if (i0 < npad) bad |= r1p[i0] + 1 - b0 > d.round_p8;
-          if (i1 < npad) bad |= r1p[i1] + 1 - b1 > d.round_p8;
+          bad |= z0 + 1 - b0 > d.round_p8 || z1 + 1 - b1 > d.round_p8;
+          if (tryg) {
+            // columns past n keep the window base (their candidate bytes are 127 either way)
+            const int32_t g0 = i0 < n ? max(Bprev[i0] - d.round_p8g, 0) : b0;
+            const int32_t g1 = i1 < n ? max(Bprev[i1] - d.round_p8g, 0) : b1;
+            gbase2[j] = (uint32_t)g0 | ((uint32_t)g1 << 16);
+            gbad |= a0 + 1 < g0 || a1 + 1 < g1 || z0 + 1 - g0 > d.round_p8 || z1 + 1 - g1 > d.round_p8;
+          }
         }
         if (__any(bad) && lane == 0) sh_wide = 1;
+        if (__any(gbad) && lane == 0) sh_gbad = 1;
         __syncthreads();
-        p8 = !sh_wide;
+        p8g = !sh_gbad;
+        p8 = p8g || !sh_wide;
       }
     }
+    const uint32_t *wb2 = p8g ? gbase2 : wbase2;
     __syncthreads();
     if (p8) {
       // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
@@ -368,7 +419,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
           uint32_t v = 0x80808080u;
           if (col < npad) {
             const int4 a = src[row * q4 + col / 4];
-            const uint32_t b01 = wbase2[col / 2], b23 = wbase2[col / 2 + 1];
+            const uint32_t b01 = wb2[col / 2], b23 = wb2[col / 2 + 1];
             const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
             const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
             v = (x0 | (x1 << 8) | (x2 << 16) | (x3 << 24)) | 0x80808080u;
@@ -404,20 +455,36 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       int tw = WROWS;
       if (p8) {
         // the candidate's 16-bit FD row, window-relative 8-bit (fd8x2 / pack8)
-        const int f16q = (npad + 7) / 8;
-        const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
-        const int nvalid = f16q - part * PP;
-        const uint4 *bb = reinterpret_cast<const uint4 *>(wbase2) + part * PP;
         uint32_t f8[4 * PP8];
+        if (p8g && act && d.c8tag[(int64_t)p * n + q] == r) {
+          // converted by its producer against the same shared base (handoff_wide)
+          const int w8q = (npad + 15) / 16;  // 16-B pieces per cand8 row
+          const int4 *fr = reinterpret_cast<const int4 *>(d.cand8) + ((int64_t)p * n + q) * w8q;
 #pragma unroll
-        for (int u = 0; u < PP; ++u) {
-          const int4 v = fr[min(u, max(nvalid - 1, 0))];
-          const uint4 b = bb[u];
-          const bool ok = u < nvalid;
-          const uint32_t e0 = fd8x2(ok ? (uint32_t)v.x : 0xFFFFFFFFu, b.x), e1 = fd8x2(ok ? (uint32_t)v.y : 0xFFFFFFFFu, b.y);
-          const uint32_t e2 = fd8x2(ok ? (uint32_t)v.z : 0xFFFFFFFFu, b.z), e3 = fd8x2(ok ? (uint32_t)v.w : 0xFFFFFFFFu, b.w);
-          f8[2 * u] = pack8(e0, e1);
-          f8[2 * u + 1] = pack8(e2, e3);
+          for (int u = 0; u < PP8; ++u) {
+            const int pc = part * PP8 + u;
+            const int4 v = fr[min(pc, w8q - 1)];  // (in the row: the pieces past it are 127s)
+            const bool ok = pc < w8q;
+            f8[4 * u] = ok ? (uint32_t)v.x : 0x7F7F7F7Fu;
+            f8[4 * u + 1] = ok ? (uint32_t)v.y : 0x7F7F7F7Fu;
+            f8[4 * u + 2] = ok ? (uint32_t)v.z : 0x7F7F7F7Fu;
+            f8[4 * u + 3] = ok ? (uint32_t)v.w : 0x7F7F7F7Fu;
+          }
+        } else {
+          const int f16q = (npad + 7) / 8;
+          const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
+          const int nvalid = f16q - part * PP;
+          const uint4 *bb = reinterpret_cast<const uint4 *>(wb2) + part * PP;
+#pragma unroll
+          for (int u = 0; u < PP; ++u) {
+            const int4 v = fr[min(u, max(nvalid - 1, 0))];
+            const uint4 b = bb[u];
+            const bool ok = u < nvalid;
+            const uint32_t e0 = fd8x2(ok ? (uint32_t)v.x : 0xFFFFFFFFu, b.x), e1 = fd8x2(ok ? (uint32_t)v.y : 0xFFFFFFFFu, b.y);
+            const uint32_t e2 = fd8x2(ok ? (uint32_t)v.z : 0xFFFFFFFFu, b.z), e3 = fd8x2(ok ? (uint32_t)v.w : 0xFFFFFFFFu, b.w);
+            f8[2 * u] = pack8(e0, e1);
+            f8[2 * u + 1] = pack8(e2, e3);
+          }
         }
         const int4 *xb8 = win4 + part * (PP8 + 1);
         auto ss8 = [&](int row) -> bool {
@@ -537,8 +604,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     }
   }
   // the hand-off: the new candidate's FD row for the next iteration
-  if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap)
-    gather_cand16(d, (int64_t)cs + result, d.cand16 + ((int64_t)(p ^ 1) * n + c) * ((npad + 7) / 8 * 4));
+  if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
   if (t == 0) {
     if (sh_nc == 0) {
       if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
@@ -588,6 +654,7 @@ __device__ __forceinline__ int group_sum(int v) {
 __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
   const int c = blockIdx.x, q4 = d.npad / 4;
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  if (threadIdx.x == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
   if (len == 0) return;
   (void)q4;
   // candidate (c, 0): its FD row gathered from the FDT columns
@@ -608,12 +675,30 @@ __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
 // workgroup is as wide as its candidates need -- at n = 32 four waves of one
 // piece per lane instead of sixteen waves of four pieces, most of them idle
 // rows of nonexistent candidates (C2 search 2.5 us -> see DESIGN.md)
+//
+// 8-bit rows (opt-in, BH_ROUND2_P8=1: measured a wash at C3, the search's
+// savings spent again in the prologue and the hand-off -- DESIGN.md 5)
+// (npad > 64, PPL = 4, TQ): iteration r compares
+// bytes relative to the shared base base_i = max(B[r-1][i] - round_p8g, 0),
+// as k_round_wide does.  The workgroup that hands candidate c over writes its
+// row as npad bytes (cand8, min(max(FD + 1 - base_i, 0), 127), 127 past n)
+// beside the 32-bit candfd row, with a tag (c8tag = r); the window's LA is x =
+// LA + 1 - base_i in [0, round_p8] (x | 0x80 in LDS), so LA >= FD <=> x >= f
+// and a probe is four dword compares per lane (16 columns) instead of 16.  A
+// workgroup whose window does not fit the base, or one of whose candidates
+// has no tag for r (the first iteration after a resume), takes the 32-bit
+// rows, loading candfd then.  The window sits in LDS twice, 128 B apart on
+// 256-B rows, and lane groups (g >> 1) & 1 read the second copy: the four
+// groups of a ds_read_b128 lane set then hit 16 distinct bank slots whatever
+// rows their searches probe.
 template <int PPL, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   constexpr int LPC = 8;
+  constexpr bool P8 = PPL == 4 && TQ;
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
   __shared__ int32_t cntk[16];
   __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
+  __shared__ int32_t bad8[16];      // P8: a wave's window columns or candidates do not fit the byte rows
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
@@ -639,13 +724,40 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   int32_t bq = 0, lq = 0;
   if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; }
   int4 f[PPL];
-  {
+  auto load_f = [&]() {
     const int4 *cf = reinterpret_cast<const int4 *>(d.candfd) + ((int64_t)p * n + min(q, n - 1)) * q4;
 #pragma unroll
     for (int u = 0; u < PPL; ++u) {
       const int pc = part + LPC * ((u + rot) & (PPL - 1));
       f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
     }
+  };
+  // P8: try the byte rows (decided by the whole workgroup after staging)
+  // (no load here depends on the state word r: the base row comes from Bq
+  // by parity, and the tags are compared with r only at staging)
+  const bool g8 = P8 && d.round2_p8 && d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;  // byte rows handed over and used
+  const bool try8 = g8;
+  const int s8 = (npad + 15) / 16 * 16;  // bytes per cand8 row
+  int4 f8 = make_int4(0, 0, 0, 0);
+  bool ok8 = try8;
+  int32_t tag8 = r;
+  int32_t bnext = 0;  // P8 hand-off: B[r][t], the base of column t for iteration r + 1
+  int4 gb = make_int4(0, 0, 0, 0);  // P8: the shared base of this thread's four window columns
+  if (g8 && t < s8) bnext = t < n ? Bp[t] : 0;
+  if (g8 && t == 0) d.Bq[(int64_t)(p ^ 1) * npad + c] = k0;  // B[r] for iteration r + 1 (read after this launch)
+  if (try8) {
+    const int w8q = s8 / 16;  // 16-B pieces per byte row (npad = 128: 8, one per lane)
+    if (q < n) {
+      tag8 = d.c8tag[(int64_t)p * n + q];  // (checked at staging for live candidates only)
+      f8 = reinterpret_cast<const int4 *>(d.cand8)[((int64_t)p * n + q) * w8q + min(part, w8q - 1)];
+      if (part >= w8q) f8 = make_int4(0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F);
+    }
+    // B[r - 1] of this thread's four window columns (written by iteration r - 1)
+    const int4 bv = reinterpret_cast<const int4 *>(d.Bq + (int64_t)p * npad)[t % q4];
+    gb = make_int4(max(bv.x - d.round_p8g, 0), max(bv.y - d.round_p8g, 0), max(bv.z - d.round_p8g, 0),
+                   max(bv.w - d.round_p8g, 0));
+  } else {
+    load_f();
   }
   const int rows = min(HW, max(0, len - k0));
   const int4 wv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
@@ -661,7 +773,34 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   if (t < rows * q4) win[t] = wv;
   if (t < 16) cntk[t] = 0;
   if (TQ && t <= HW) hist[t] = 0;
-  __syncthreads();
+  // P8 window: [HW][2 copies][npad bytes] after the 32-bit window (the
+  // hand-off's fdw, which overlaps its first rows, is written only after the
+  // search's last barrier)
+  uint32_t *win8 = reinterpret_cast<uint32_t *>(sm4 + HW * q4);
+  bool p8 = false;
+  if (try8) {
+    if (q < n && bq < lq && tag8 != r) ok8 = false;  // a chain at its end hands nothing over
+    if (t < rows * q4) {
+      const int row = t / q4, col = 4 * (t % q4);
+      // x = LA + 1 - base; columns >= n have base 0 and LA -1 (x = 0, candidate bytes 127)
+      const uint32_t x0 = (uint32_t)(wv.x + 1 - gb.x), x1 = (uint32_t)(wv.y + 1 - gb.y);
+      const uint32_t x2 = (uint32_t)(wv.z + 1 - gb.z), x3 = (uint32_t)(wv.w + 1 - gb.w);
+      const uint32_t lim = (uint32_t)d.round_p8;  // unsigned: x < 0 fails too
+      if ((x0 > lim) | (x1 > lim) | (x2 > lim) | (x3 > lim)) ok8 = false;
+      const uint32_t w = (x0 | x1 << 8 | x2 << 16 | x3 << 24) | 0x80808080u;
+      win8[row * 64 + col / 4] = w;
+      win8[row * 64 + 32 + col / 4] = w;
+    }
+    for (int i = t; i < rows * 32; i += blockDim.x)  // columns npad .. 127: x = 0 (no byte borrows)
+      if ((i & 31) >= q4) win8[(i >> 5) * 64 + (i & 31)] = win8[(i >> 5) * 64 + 32 + (i & 31)] = 0x80808080u;
+    const bool bad = __any(!ok8);
+    if (lane == 0) bad8[wave] = bad;  // every wave writes its own flag: no initialisation to order
+    __syncthreads();
+    p8 = !__any(lane < (int)(blockDim.x >> 6) && bad8[lane & 15]);
+    if (!p8) load_f();  // (rare: the 32-bit rows after all)
+  } else {
+    __syncthreads();
+  }
   const unsigned long long ts1 = dg ? stamp() : 0;
   const unsigned long long rt1 = dg ? __builtin_amdgcn_s_memrealtime() : 0;  // loads landed
   // count(row) into slot: groups whose candidate `row` strongly sees
@@ -688,12 +827,22 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   int slot = 1;
   int32_t res = -1;  // window row of B[r+1][c], or -1
   unsigned long long ssb = 0;  // this wave's ballot of the probe that verified the answer row
+  // P8: does window row `row` strongly see this group's candidate (its bytes f8)?
+  const int4 *w8b = reinterpret_cast<const int4 *>(win8) + ((q >> 1) & 1) * 8 + part;
+  auto ss_row8 = [&](int row) {
+    const int4 x = w8b[row * 16];
+    int ge = __builtin_popcount(((uint32_t)x.x - (uint32_t)f8.x) & 0x80808080u);
+    ge += __builtin_popcount(((uint32_t)x.y - (uint32_t)f8.y) & 0x80808080u);
+    ge += __builtin_popcount(((uint32_t)x.z - (uint32_t)f8.z) & 0x80808080u);
+    ge += __builtin_popcount(((uint32_t)x.w - (uint32_t)f8.w) & 0x80808080u);
+    return group_sum<LPC>(ge) >= sm;
+  };
   if (TQ && rows > 0) {
     // T_q by a per-group binary search over [0, rows] (rows = none in the window)
     int lo = 0, hi = rows;
     while (__any(lo < hi)) {
       const int mid = (lo + hi) >> 1;
-      const bool s = ss_row(win + min(mid, rows - 1) * q4);
+      const bool s = P8 && p8 ? ss_row8(min(mid, rows - 1)) : ss_row(win + min(mid, rows - 1) * q4);
       if (lo < hi) {
         hi = s ? mid : hi;
         lo = s ? lo : mid + 1;
@@ -751,6 +900,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   } else if (nc > 0 && rows == HW) {
     // SM not reached in the handed-over window (rare): later windows of
     // chain c, loaded directly (slot counters are reused per row tested)
+    if (P8 && p8) load_f();
     int4 *x4 = win;  // rows in LDS: row i of the current window at x4[i * q4]
     for (int32_t wk = k0 + HW; wk < len && result == len; wk += HW) {
       const int wr = min(HW, len - wk);
@@ -785,12 +935,26 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     const int32_t off = result - k0;
     int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
     const int frel = (int)(cs + result - rb);  // row of the candidate in fdw
+    int32_t fdv = FD_NONE;
     if (off < HW && frel < HW) {  // both from the rows staged during the search
       if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
       __syncthreads();
-      if (t < npad) cf[t] = t < n ? fdw[t * FDS + frel] : FD_NONE;
+      if (t < n) fdv = fdw[t * FDS + frel];
     } else {
-      if (t < npad) cf[t] = t < n ? d.fdt[fdt_pos(cs + result, t, npad)] : FD_NONE;
+      if (t < n) fdv = d.fdt[fdt_pos(cs + result, t, npad)];
+    }
+    if (t < npad) cf[t] = fdv;
+    if (g8) {
+      // the byte row for iteration r + 1 (base B[r][t] - round_p8g), then its tag
+      if (t < s8) {  // (s8 <= 128: waves 0 and 1, four lanes per dword)
+        const int32_t b = max(bnext - d.round_p8g, 0);
+        const int32_t fx = t >= n || fdv == FD_NONE ? 127 : min(max(fdv + 1 - b, 0), 127);
+        uint32_t v = (uint32_t)fx << (8 * (t & 3));
+        v |= (uint32_t)__shfl_xor((int)v, 1);
+        v |= (uint32_t)__shfl_xor((int)v, 2);
+        if ((t & 3) == 0) reinterpret_cast<uint32_t *>(d.cand8 + ((int64_t)(p ^ 1) * n + c) * s8)[t >> 2] = v;
+      }
+      if (t == 0) d.c8tag[(int64_t)(p ^ 1) * n + c] = r + 1;
     }
     // fame's input for the new candidate y = (c, result): SS(y, q) over
     // the candidates q of round r = the ballots of the probe that verified
@@ -1072,7 +1236,10 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
   const int c = blockIdx.x;
   const int32_t r0 = d.state[ST_RESUME];
   const int32_t b = d.B[(int64_t)r0 * d.n + c], len = d.chain_len[c], cs = d.chain_start[c];
-  if (threadIdx.x == 0) d.Bp[c] = b;
+  if (threadIdx.x == 0) {
+    d.Bp[c] = b;
+    if (d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;  // cand8 rows of an earlier loop are stale
+  }
   if (b < len) {
     if (d.fd_cols) {
       int32_t *cf = d.candfd + (int64_t)c * d.npad;
@@ -1121,6 +1288,7 @@ bool round_p16(const Dev &d) { return d.cand16 != nullptr && d.max_chain_len <= 
 // candidate (c, 0) of every chain for the 16-bit wide loop
 __global__ __launch_bounds__(256) void k_cand16_init(Dev d) {
   const int c = blockIdx.x;
+  if (threadIdx.x == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
   if (d.chain_len[c] > 0) gather_cand16(d, d.chain_start[c], d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
 }
 
@@ -1152,7 +1320,8 @@ void configure_round_kernels() {
 // batch -- ITER_FIRST, ITER_BATCH -- is even, so each starts at parity 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
-    const size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
+    size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
+    if (d.npad > 64 && d.round2_p8) lds = std::max(lds, (size_t)HW * (d.npad / 4) * 16 + (size_t)HW * 256);  // + the P8 window
     const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));  // (read per capture: the tests switch it)
     const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);  // 8 lanes per candidate
     if (rows_search) {

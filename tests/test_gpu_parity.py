@@ -358,15 +358,24 @@ def test_chunk_sweep_wild(monkeypatch):
     _wild_parity(8, 30_000, 41, 25_000)
 
 
-@pytest.mark.parametrize("rows", ["p8", "p8_mixed", "p16", "p32"])
+@pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p16", "p32"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
-    over 8-bit window-relative rows (the default where a window's LA spread
-    fits; p8_mixed lowers the spread limit so windows alternate with the
-    16-bit fallback), over 16-bit rows (fd16; n = 300 has a half-filled last
-    piece) and over the 32-bit rows (BH_NO_P16, the path for chains beyond
-    P16_MAXLEN)."""
+    over 8-bit rows -- the default: relative to the shared base B[r-1][i] -
+    20 with the candidates' bytes converted once by the workgroup that hands
+    them over (cand8); p8_window: relative to each window's first row only
+    (BH_ROUND_P8G=0); p8g_tight: a shared base 2 below B[r-1], which many
+    windows do not fit, so they fall back to their own base beside windows
+    that take the shared one; p8_mixed: a lower spread limit, so windows also
+    alternate with the 16-bit fallback -- over 16-bit rows (fd16; n = 300
+    has a half-filled last piece) and over the 32-bit rows (BH_NO_P16, the
+    path for chains beyond P16_MAXLEN).  n = 160 / 300 leave the last lanes
+    of a candidate's group past the end of its byte row."""
+    if rows == "p8_window":
+        monkeypatch.setenv("BH_ROUND_P8G", "0")
+    if rows == "p8g_tight":
+        monkeypatch.setenv("BH_ROUND_P8G", "2")
     if rows == "p8_mixed":
         monkeypatch.setenv("BH_ROUND_P8", "40")
     if rows == "p16":
@@ -590,3 +599,33 @@ def test_small_n_round_kernels(monkeypatch, variant, n, N, seed, lag, K):
     _random_parity(n, N, seed, lag)
     if K == 1:
         _wild_parity(24, 30_000, 73, 20_000)
+
+
+@pytest.mark.parametrize("variant", ["bytes", "p32", "tight", "mixed", "rows"])
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xB8, 0, 1), (100, 50_000, 0xB9, 4, 3),
+                                            (97, 40_000, 0xBA, 0, 2), (72, 30_000, 0xBB, 3, 1)])
+def test_round2_byte_rows(monkeypatch, variant, n, N, seed, lag, K):
+    """k_round2 at 64 < npad <= 128 over byte rows relative to the shared
+    base B[r-1][i] - 20 (bytes: candidates' bytes written once by the
+    workgroup that hands them over, cand8 + c8tag), against the oracle; p32:
+    the 32-bit rows (the default); tight: a base 2 below B[r-1], so
+    many windows do not fit and their workgroups load the 32-bit rows after
+    staging; mixed: a lower spread limit (BH_ROUND_P8=40); rows: the
+    row-probe search (32-bit).  npad = 100 / 72 leave byte columns past npad
+    in the 16-B pieces; lagging peers, and segments whose first iteration
+    after a resume has no byte rows yet.  (The byte rows are opt-in,
+    BH_ROUND2_P8=1: at C3 they measured no faster than the 32-bit rows.)"""
+    if variant in ("bytes", "tight", "mixed"):
+        monkeypatch.setenv("BH_ROUND2_P8", "1")
+    if variant == "p32":
+        monkeypatch.setenv("BH_ROUND_P8G", "0")
+    if variant == "tight":
+        monkeypatch.setenv("BH_ROUND_P8G", "2")
+    if variant == "mixed":
+        monkeypatch.setenv("BH_ROUND_P8", "40")
+    if variant == "rows":
+        monkeypatch.setenv("BH_ROUND_ROWS", "1")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    _random_parity(n, N, seed, lag)
+    if n == 128 and K == 1:
+        _wild_parity(128, 40_000, 0xBC, 35_000)

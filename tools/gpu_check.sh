@@ -29,6 +29,8 @@ for s in "$@"; do
     serial) step serial 600 env BH_SEG_SERIAL=1 BH_SEG_DEBUG=1 python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     serialrows) step serial_rows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_SEG_DEBUG=1 python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     tl) step tl 600 env BH_DIAG=1 BH_TIMELINE=gpurun_out/tl.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    tlg0) step tlg0 600 env BH_ROUND_P8G=0 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlg0.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    bench3qb) step bench_c3b 900 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     tlser) step tlser 600 env BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlser.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     tlrows) step tlrows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlrows.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench) step bench 900 python bench.py ;;
@@ -44,6 +46,11 @@ for s in "$@"; do
     bench5) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 ;;
     bench4) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 ;;
     bench4q) step bench_c4 1100 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    bench3g0) step bench_c3_g0 900 env BH_ROUND_P8G=0 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench2g0) step bench_c2_g0 600 env BH_ROUND_P8G=0 python bench.py --cfg 2 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench3q) step bench_c3 900 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench4g0) step bench_c4_g0 1100 env BH_ROUND_P8G=0 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
+    tround) step pytest_round 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_schedule.py tests/test_gpu_fullsize.py -m gpu -v --timeout 300 --timeout-method thread -rf ;;
     diag4) step diag_c4 900 env BH_DIAG=1 python bench.py --cfg 4 --steps 1 --warmup 0 --cpu-sample 0 ;;
     diag4old) step diag_c4_old 900 env BH_DIAG=1 BH_FLOWW=1 python bench.py --cfg 4 --steps 1 --warmup 0 --cpu-sample 0 ;;
     diag3) step diag_c3 600 env BH_DIAG=1 python bench.py --cfg 3 --steps 1 --warmup 1 --cpu-sample 0 ;;
