@@ -1252,6 +1252,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.rq, (size_t)n);
   A(&d.candfd, (size_t)2 * n * d.npad);
   d.cand16 = !d.fd_cols && n <= 512 ? reinterpret_cast<uint32_t *>(d.candfd) : nullptr;  // (npad + 7) / 8 * 4 <= npad dwords a row
+  d.round_ilp2 = getenv("BH_ROUND_ILP2") ? atoi(getenv("BH_ROUND_ILP2")) != 0 : 1;
   d.round2_p8 = getenv("BH_ROUND2_P8") && atoi(getenv("BH_ROUND2_P8"));
   d.round_p8g = getenv("BH_ROUND_P8G") ? std::clamp(atoi(getenv("BH_ROUND_P8G")), 0, 64) : bh::P8G_DELTA;
   if (d.cand16 || (d.fd_cols && d.npad > 64 && d.round2_p8)) {  // k_round_wide<*, true> / k_round2<4, true>

@@ -132,6 +132,7 @@ struct Dev {
   int32_t *c8tag;     // [2][n]
   int32_t *Bq;        // [2][npad] k_round2 bytes: B[r - 1] for the iteration of parity p (written by iteration r - 1)
   int32_t round_p8g;  // base offset below B[r-1] (P8G_DELTA; BH_ROUND_P8G=0 turns the shared base off)
+  int32_t round_ilp2;  // k_round_wide byte rows: two candidates' searches interleaved per lane group (BH_ROUND_ILP2=0: one)
   int32_t round2_p8;  // k_round2<4, true> on byte rows too (BH_ROUND2_P8=1; off by default: no gain measured at C3)
   // [n][rspan][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
   // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])

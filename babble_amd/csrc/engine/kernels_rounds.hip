@@ -447,6 +447,104 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     }
     if (t <= WROWS) hist[t] = 0;
     __syncthreads();
+    if (p8 && d.round_ilp2) {
+      // byte rows, two candidates per lane group at once (passes pass and
+      // pass + 1): their binary searches interleave, so each probe's LDS
+      // reads and compares overlap the other's (two waves per SIMD hide
+      // little of a lone search's LDS latency)
+      auto load_f8 = [&](int q, bool act, uint32_t (&f8)[4 * PP8]) {
+        if (p8g && act && d.c8tag[(int64_t)p * n + q] == r) {
+          const int w8q = (npad + 15) / 16;
+          const int4 *fr = reinterpret_cast<const int4 *>(d.cand8) + ((int64_t)p * n + q) * w8q;
+#pragma unroll
+          for (int u = 0; u < PP8; ++u) {
+            const int pc = part * PP8 + u;
+            const int4 v = fr[min(pc, w8q - 1)];
+            const bool ok = pc < w8q;
+            f8[4 * u] = ok ? (uint32_t)v.x : 0x7F7F7F7Fu;
+            f8[4 * u + 1] = ok ? (uint32_t)v.y : 0x7F7F7F7Fu;
+            f8[4 * u + 2] = ok ? (uint32_t)v.z : 0x7F7F7F7Fu;
+            f8[4 * u + 3] = ok ? (uint32_t)v.w : 0x7F7F7F7Fu;
+          }
+        } else {
+          const int f16q = (npad + 7) / 8;
+          const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
+          const int nvalid = f16q - part * PP;
+          const uint4 *bb = reinterpret_cast<const uint4 *>(wb2) + part * PP;
+#pragma unroll
+          for (int u = 0; u < PP; ++u) {
+            const int4 v = fr[min(u, max(nvalid - 1, 0))];
+            const uint4 b = bb[u];
+            const bool ok = u < nvalid;
+            const uint32_t e0 = fd8x2(ok ? (uint32_t)v.x : 0xFFFFFFFFu, b.x), e1 = fd8x2(ok ? (uint32_t)v.y : 0xFFFFFFFFu, b.y);
+            const uint32_t e2 = fd8x2(ok ? (uint32_t)v.z : 0xFFFFFFFFu, b.z), e3 = fd8x2(ok ? (uint32_t)v.w : 0xFFFFFFFFu, b.w);
+            f8[2 * u] = pack8(e0, e1);
+            f8[2 * u + 1] = pack8(e2, e3);
+          }
+        }
+      };
+      const int4 *xb8 = win4 + part * (PP8 + 1);
+      for (int pass = 0; pass < npass; pass += 2) {
+        const int qa = pass * CPP + t / LPC, qb = qa + CPP;
+        int32_t ba = 0, la_ = 0, bb_ = 0, lb = 0;
+        if (qa < n) { ba = Bp[qa]; la_ = d.chain_len[qa]; }
+        if (qb < n) { bb_ = Bp[qb]; lb = d.chain_len[qb]; }
+        const bool acta = qa < n && ba < la_, actb = qb < n && bb_ < lb;
+        uint32_t fa[4 * PP8], fb[4 * PP8];
+        load_f8(qa, acta, fa);
+        load_f8(qb, actb, fb);
+        auto ss2 = [&](int ra, int rb, bool &sa, bool &sb) {
+          const int4 *xa4 = xb8 + ra * WRS8, *xb4 = xb8 + rb * WRS8;
+          int4 xa[PP8], xb[PP8];
+#pragma unroll
+          for (int u = 0; u < PP8; ++u) { xa[u] = xa4[u]; xb[u] = xb4[u]; }
+          int ga = 0, gb = 0;
+#pragma unroll
+          for (int u = 0; u < PP8; ++u) {
+            ga += __builtin_popcount(((uint32_t)xa[u].x - fa[4 * u]) & 0x80808080u);
+            gb += __builtin_popcount(((uint32_t)xb[u].x - fb[4 * u]) & 0x80808080u);
+            ga += __builtin_popcount(((uint32_t)xa[u].y - fa[4 * u + 1]) & 0x80808080u);
+            gb += __builtin_popcount(((uint32_t)xb[u].y - fb[4 * u + 1]) & 0x80808080u);
+            ga += __builtin_popcount(((uint32_t)xa[u].z - fa[4 * u + 2]) & 0x80808080u);
+            gb += __builtin_popcount(((uint32_t)xb[u].z - fb[4 * u + 2]) & 0x80808080u);
+            ga += __builtin_popcount(((uint32_t)xa[u].w - fa[4 * u + 3]) & 0x80808080u);
+            gb += __builtin_popcount(((uint32_t)xb[u].w - fb[4 * u + 3]) & 0x80808080u);
+          }
+          sa = group_total<LPC>(ga) >= sm;
+          sb = group_total<LPC>(gb) >= sm;
+        };
+        // binary search over [0, wrows - 1] without probing the last row
+        // first: that row is probed afterwards only where no probe came out
+        // true (the candidate is seen at the last row, or not at all -- few);
+        // a short window's spare iterations probe lo == hi itself
+        int loa = 0, hia = wrows - 1, lob = 0, hib = wrows - 1;
+        bool va = false, vb = false;
+#pragma unroll
+        for (int it = 0; it < 5; ++it) {
+          const int mida = (loa + hia) >> 1, midb = (lob + hib) >> 1;  // (<= hi, also once lo = hi + 1)
+          bool ta, tb;
+          ss2(mida, midb, ta, tb);
+          if (loa <= hia) {
+            if (ta) { hia = mida; va = true; } else { loa = mida + 1; }
+          }
+          if (lob <= hib) {
+            if (tb) { hib = midb; vb = true; } else { lob = midb + 1; }
+          }
+        }
+        const bool ua = !va && loa < wrows, ub = !vb && lob < wrows;  // lo = hi = wrows - 1, unverified
+        if (__any(ua || ub)) {
+          bool ta, tb;
+          ss2(wrows - 1, wrows - 1, ta, tb);
+          va = va || (ua && ta);
+          vb = vb || (ub && tb);
+        }
+        const int twa = va ? loa : WROWS, twb = vb ? lob : WROWS;
+        if (acta && part == 0 && twa < WROWS) atomicAdd(&hist[twa], 1);
+        if (actb && part == 0 && twb < WROWS) atomicAdd(&hist[twb], 1);
+        if (d.ssw && part == 0 && qa < n) tq_s[qa] = (int8_t)(acta ? twa : WROWS);
+        if (d.ssw && part == 0 && qb < n) tq_s[qb] = (int8_t)(actb ? twb : WROWS);
+      }
+    } else
     for (int pass = 0; pass < npass; ++pass) {
       const int q = pass * CPP + t / LPC;
       int32_t bq = 0, lq = 0, sq = 0;

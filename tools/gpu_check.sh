@@ -49,6 +49,7 @@ for s in "$@"; do
     bench3g0) step bench_c3_g0 900 env BH_ROUND_P8G=0 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench2g0) step bench_c2_g0 600 env BH_ROUND_P8G=0 python bench.py --cfg 2 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench3q) step bench_c3 900 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench4i0) step bench_c4_i0 1100 env BH_ROUND_ILP2=0 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     bench4g0) step bench_c4_g0 1100 env BH_ROUND_P8G=0 python bench.py --cfg 4 --steps 1 --warmup 1 --cpu-sample 0 ;;
     tround) step pytest_round 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fuzz.py tests/test_gpu_schedule.py tests/test_gpu_fullsize.py -m gpu -v --timeout 300 --timeout-method thread -rf ;;
     diag4) step diag_c4 900 env BH_DIAG=1 python bench.py --cfg 4 --steps 1 --warmup 0 --cpu-sample 0 ;;
