@@ -30,6 +30,8 @@ for s in "$@"; do
     serialrows) step serial_rows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_SEG_DEBUG=1 python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     tl) step tl 600 env BH_DIAG=1 BH_TIMELINE=gpurun_out/tl.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     tlg0) step tlg0 600 env BH_ROUND_P8G=0 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlg0.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
+    bench2q) step bench_c2 600 python bench.py --cfg 2 --steps 3 --warmup 1 --cpu-sample 0 ;;
+    bench5q) step bench_c5 600 python bench.py --cfg 5 --steps 3 --warmup 1 --cpu-sample 0 ;;
     bench3qb) step bench_c3b 900 python bench.py --cfg 3 --steps 3 --warmup 1 --cpu-sample 0 ;;
     tlser) step tlser 600 env BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlser.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
     tlrows) step tlrows 600 env BH_ROUND_ROWS=1 BH_SEG_SERIAL=1 BH_DIAG=1 BH_TIMELINE=gpurun_out/tlrows.bin python bench.py --steps 1 --warmup 1 --cpu-sample 0 ;;
