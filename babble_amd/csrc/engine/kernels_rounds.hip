@@ -452,21 +452,25 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       // pass + 1): their binary searches interleave, so each probe's LDS
       // reads and compares overlap the other's (two waves per SIMD hide
       // little of a lone search's LDS latency)
-      auto load_f8 = [&](int q, bool act, uint32_t (&f8)[4 * PP8]) {
-        if (p8g && act && d.c8tag[(int64_t)p * n + q] == r) {
-          const int w8q = (npad + 15) / 16;
-          const int4 *fr = reinterpret_cast<const int4 *>(d.cand8) + ((int64_t)p * n + q) * w8q;
+      // a candidate's byte row, its tag and its chain's B / length are loaded
+      // together, none waiting on another (the tag decides only afterwards
+      // whether the bytes are used or the 16-bit row is converted)
+      const int w8q = (npad + 15) / 16;
+      auto raw_f8 = [&](int q, uint32_t (&f8)[4 * PP8]) {
+        const int4 *fr = reinterpret_cast<const int4 *>(d.cand8) + ((int64_t)p * n + min(q, n - 1)) * w8q;
 #pragma unroll
-          for (int u = 0; u < PP8; ++u) {
-            const int pc = part * PP8 + u;
-            const int4 v = fr[min(pc, w8q - 1)];
-            const bool ok = pc < w8q;
-            f8[4 * u] = ok ? (uint32_t)v.x : 0x7F7F7F7Fu;
-            f8[4 * u + 1] = ok ? (uint32_t)v.y : 0x7F7F7F7Fu;
-            f8[4 * u + 2] = ok ? (uint32_t)v.z : 0x7F7F7F7Fu;
-            f8[4 * u + 3] = ok ? (uint32_t)v.w : 0x7F7F7F7Fu;
-          }
-        } else {
+        for (int u = 0; u < PP8; ++u) {
+          const int pc = part * PP8 + u;
+          const int4 v = fr[min(pc, w8q - 1)];
+          const bool ok = pc < w8q;
+          f8[4 * u] = ok ? (uint32_t)v.x : 0x7F7F7F7Fu;
+          f8[4 * u + 1] = ok ? (uint32_t)v.y : 0x7F7F7F7Fu;
+          f8[4 * u + 2] = ok ? (uint32_t)v.z : 0x7F7F7F7Fu;
+          f8[4 * u + 3] = ok ? (uint32_t)v.w : 0x7F7F7F7Fu;
+        }
+      };
+      auto load_f8 = [&](int q, bool act, int32_t tag, uint32_t (&f8)[4 * PP8]) {
+        if (!(p8g && act && tag == r)) {
           const int f16q = (npad + 7) / 8;
           const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
           const int nvalid = f16q - part * PP;
@@ -486,13 +490,15 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       const int4 *xb8 = win4 + part * (PP8 + 1);
       for (int pass = 0; pass < npass; pass += 2) {
         const int qa = pass * CPP + t / LPC, qb = qa + CPP;
-        int32_t ba = 0, la_ = 0, bb_ = 0, lb = 0;
-        if (qa < n) { ba = Bp[qa]; la_ = d.chain_len[qa]; }
-        if (qb < n) { bb_ = Bp[qb]; lb = d.chain_len[qb]; }
-        const bool acta = qa < n && ba < la_, actb = qb < n && bb_ < lb;
+        const int qa1 = min(qa, n - 1), qb1 = min(qb, n - 1);
+        const int32_t ba = Bp[qa1], la_ = d.chain_len[qa1], bb_ = Bp[qb1], lb = d.chain_len[qb1];
+        const int32_t taga = d.c8tag[(int64_t)p * n + qa1], tagb = d.c8tag[(int64_t)p * n + qb1];
         uint32_t fa[4 * PP8], fb[4 * PP8];
-        load_f8(qa, acta, fa);
-        load_f8(qb, actb, fb);
+        raw_f8(qa, fa);
+        raw_f8(qb, fb);
+        const bool acta = qa < n && ba < la_, actb = qb < n && bb_ < lb;
+        load_f8(qa, acta, taga, fa);
+        load_f8(qb, actb, tagb, fb);
         auto ss2 = [&](int ra, int rb, bool &sa, bool &sb) {
           const int4 *xa4 = xb8 + ra * WRS8, *xb4 = xb8 + rb * WRS8;
           int4 xa[PP8], xb[PP8];
