@@ -732,9 +732,23 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     HIPCHK(h, hipEventCreate(&lt0));
     HIPCHK(h, hipEventCreate(&lt1));
   }
+  bool wd_fired = false;
   for (int k = 0; k < K; ++k) {
     HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * k], 0));
     if (serial) HIPCHK(h, hipStreamSynchronize(sr));
+    if (wide) {
+      // k_floww2's watchdog (ST_FLOWOVF = 2) is read before a loop runs on
+      // the segment: a loop over unfinished coordinates could fail ("did not
+      // terminate", capacity) before the fallback below is reached.  One
+      // host synchronisation per segment; a wide batch runs one segment
+      int32_t *ovf = h->pinned_state + bh::ST_COUNT + 4;
+      HIPCHK(h, hipMemcpyAsync(ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, sr));
+      HIPCHK(h, hipStreamSynchronize(sr));
+      if (*ovf == 2) {
+        wd_fired = true;
+        break;
+      }
+    }
     if (k + 1 < K) {
       // segment k + 1 reuses the segbuf parity of k - 1, last read by its
       // resume point on the loop stream
@@ -794,7 +808,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   if (lt0) (void)hipEventDestroy(lt0);
   if (lt1) (void)hipEventDestroy(lt1);
   (void)hipEventDestroy(sr_mark);
-  if (wide && st[bh::ST_FLOWOVF] == 2) {
+  if (wide && (wd_fired || st[bh::ST_FLOWOVF] == 2)) {
     // k_floww2's watchdog left a segment's coordinates unfinished: the whole
     // DAG again through the unpipelined passes (they fall back to the
     // chunked sweep)
@@ -1196,8 +1210,9 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.n = n;
   d.npad = (n + 3) & ~3;
   d.sm = 2 * n / 3 + 1;  // hashgraph.go:54
-  d.ring_log2 = n < 256 ? 14 : 12;
-  d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;  // sweep LDS: one workgroup per CU below 256 columns
+  d.ring_log2 = n < 256 ? 14 : 12;  // sweep LDS: one workgroup per CU below 256 columns
+  d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;
+  d.flow_wd = getenv("BH_FLOWW_WATCHDOG") ? atoi(getenv("BH_FLOWW_WATCHDOG")) : (1 << 20);
   d.N = 0;
   d.col0 = 0;
   d.ncol = n;
@@ -1679,6 +1694,7 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   // installed Roots (each Root's entries: unique keys sorted by key hash,
   // Go's encoding/json map order; a Go map holds one entry per key)
   bh::Frames nf{};
+  size_t json_cap = 0, bjson_cap = 0;
   if (h->frames_on) {
     const int32_t K = rt->n_others;
     std::vector<int32_t> ord((size_t)K), ofs((size_t)n + 1, 0);
@@ -1719,6 +1735,9 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
     up(nf.ro_round, rd.data(), (size_t)K * 4);
     up(nf.ro_ofs, ofs.data(), ((size_t)n + 1) * 4);
     up(nf.ro_list, ord.data(), ord.size() * 4);
+    // the initial contents and the JSON buffers too: nothing of the
+    // projection can fail after the commit below
+    if (rcf == BH_OK) rcf = frames_prepare(h, nf, (int64_t)R_cap + 1, &json_cap, &bjson_cap);
     if (rcf != BH_OK) {
       frames_free_tables(nf);
       t.free_all();
@@ -1748,6 +1767,10 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   if (h->frames_on) {
     frames_free_tables(h->fr);
     h->fr = nf;
+    h->json_cap = json_cap;
+    h->bjson_cap = bjson_cap;
+    h->arena_cap = h->arena_len = 0;
+    h->others_total = 0;
   }
   for (void *p : {(void *)d.chain_base, (void *)d.lt_seed, (void *)d.root_next, (void *)d.root_sp_round, (void *)d.rflag,
                   (void *)d.ext_lt, (void *)d.fw})
@@ -1770,7 +1793,6 @@ int bh_reset(bh_handle *h, const bh_roots *rt) {
   h->reset_F = F;
   h->P = rt->round_received;  // rounds below LastConsensusRound are never queued (hashgraph.go:809-815)
   h->inc_valid = false;
-  if (h->frames_on) return frames_init(h);
   return BH_OK;
 }
 

@@ -90,6 +90,7 @@ struct Dev {
   int64_t ntiles;
   int32_t *hdone;  // mapped pinned host word: set when the round loop is done
   int32_t flow_ltclamp;  // k_flow32 LT limit (2^21 - 256; BH_FLOW_LTCLAMP lowers it to test the fallback)
+  int32_t flow_wd;       // k_floww / k_floww2 watchdog: stalled headers before it gives up (BH_FLOWW_WATCHDOG; -1 fires at once)
   uint8_t *depth, *chunk_maxd;
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
   // rounds

@@ -201,20 +201,34 @@ void frames_free_tables(bh::Frames &fr) {
   fr = bh::Frames{};
 }
 
-// the tables' initial contents (no event bytes, nothing projected)
-int frames_init(bh_handle *h) {
-  bh::Frames &fr = h->fr;
+// the initial contents of a table set for R1 rounds (no event bytes,
+// nothing projected) and its 1 MiB JSON buffers: every step that can fail,
+// so that bh_reset can prepare a new set before it commits to it
+int frames_prepare(bh_handle *h, bh::Frames &fr, int64_t R1, size_t *json_cap, size_t *bjson_cap) {
   const int64_t n = h->d.n, C = std::max<int64_t>(h->cap, 1);
   HIPCHK(h, hipMemcpy(fr.pids, h->pids.data(), (size_t)n * 8, hipMemcpyHostToDevice));
   HIPCHK(h, hipMemset(fr.body_len, 0xff, (size_t)C * 4));
   HIPCHK(h, hipMemset(fr.sig_len, 0xff, (size_t)C * 4));
   if (fr.oth_of) HIPCHK(h, hipMemset(fr.oth_of, 0xff, (size_t)C * 4));
-  h->json_cap = h->bjson_cap = 0;
-  h->arena_cap = h->arena_len = 0;
-  frames_reset(h);
+  HIPCHK(h, hipMemset(fr.last_pos, 0xff, (size_t)n * 4));
+  HIPCHK(h, hipMemset(fr.oofs, 0, 8));
+  HIPCHK(h, hipMemset(fr.fvalid, 0, (size_t)R1));
+  HIPCHK(h, hipMemset(fr.fhash, 0, (size_t)R1 * 32));
+  HIPCHK(h, hipMemset(fr.bhash, 0, (size_t)R1 * 32));
+  const size_t cap = (1 << 20) + 128;
+  *json_cap = *bjson_cap = 0;
   int rc;
-  if ((rc = ensure_buf(h, &fr.json, &h->json_cap, 1 << 20))) return rc;
-  return ensure_buf(h, &fr.bjson, &h->bjson_cap, 1 << 20);
+  if (!fr.json && (rc = dalloc(h, &fr.json, cap))) return rc;
+  if (!fr.bjson && (rc = dalloc(h, &fr.bjson, cap))) return rc;
+  *json_cap = *bjson_cap = cap;
+  return BH_OK;
+}
+
+// the handle's tables' initial contents
+int frames_init(bh_handle *h) {
+  h->arena_cap = h->arena_len = 0;
+  h->others_total = 0;
+  return frames_prepare(h, h->fr, (int64_t)h->d.R_cap + 1, &h->json_cap, &h->bjson_cap);
 }
 
 int frames_alloc(bh_handle *h) {

@@ -206,6 +206,7 @@ void frames_free(bh_handle *h);
 int frames_alloc_tables(bh_handle *h, bh::Frames &fr, int64_t R1, int64_t K, bool reset);
 void frames_free_tables(bh::Frames &fr);
 int frames_init(bh_handle *h);
+int frames_prepare(bh_handle *h, bh::Frames &fr, int64_t R1, size_t *json_cap, size_t *bjson_cap);
 void frames_reset(bh_handle *h);
 // roots, FrameHash and block hashes of the frames [P0, P1) just processed
 // (consensus positions [i0, i1))

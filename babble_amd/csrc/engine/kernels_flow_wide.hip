@@ -62,7 +62,6 @@ struct FlowLdsW {
 // a compute wave none of whose lanes advanced for this many headers (~0.6 s;
 // a run takes tens of ms) leaves, the workgroup with it, and flags
 // ST_FLOWOVF = 2: the host recomputes the coordinates with the chunked sweep
-constexpr int32_t FW_WATCHDOG = 1 << 20;
 
 typedef __attribute__((address_space(3))) volatile int lds_vint_w;
 
@@ -201,7 +200,7 @@ __device__ __forceinline__ void floww_body(const Dev &d, FlowLdsW &L) {
     }
     if (!__any(k < len)) break;
     stall = __any(k != k2) ? 0 : stall + 1;
-    if (stall > FW_WATCHDOG || *abort_) {
+    if (stall > d.flow_wd || *abort_) {
       if (lane == 0) {
         *abort_ = 1;
         atomicMax(&d.state[ST_FLOWOVF], 2);
@@ -514,7 +513,7 @@ __device__ __forceinline__ void floww2_body(const Dev &d, FlowLdsW2 &L, int colA
     }
     if (!__any(k < len)) break;
     stall = __any(k != k2) ? 0 : stall + 1;
-    if (stall > FW_WATCHDOG || *abort_) {
+    if (stall > d.flow_wd || *abort_) {
       if (lane == 0) {
         *abort_ = 1;
         atomicMax(&d.state[ST_FLOWOVF], 2);

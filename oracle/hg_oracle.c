@@ -22,6 +22,28 @@
 #define UNSET INT32_MIN
 #define FD_NONE INT32_MAX /* math.MaxInt32, hashgraph.go:447 */
 
+/* Storage of the coordinate vectors.  The default keeps each Index as an
+ * int32.  -DHGO_COORD16 (liboracle16.so, for whole-DAG digests of C4:
+ * 512 x 20M events x 2 vectors would need 82 GB as int32) stores them as
+ * uint16 -- LA as index + 1 (so -1 is 0), FD as the index or 0xFFFF for
+ * MaxInt32 -- and aborts on an index it cannot hold.  Only the storage
+ * changes; every comparison sees the decoded int32 values. */
+#ifdef HGO_COORD16
+typedef uint16_t coord_t;
+#define COORD_MAX_INDEX 65533
+static inline int32_t la_get(const coord_t *r, int32_t i) { return (int32_t)r[i] - 1; }
+static inline void la_put(coord_t *r, int32_t i, int32_t v) { r[i] = (coord_t)(v + 1); }
+static inline int32_t fd_get(const coord_t *r, int32_t i) { return r[i] == 0xFFFF ? FD_NONE : (int32_t)r[i]; }
+static inline void fd_put(coord_t *r, int32_t i, int32_t v) { r[i] = v == FD_NONE ? (coord_t)0xFFFF : (coord_t)v; }
+#else
+typedef int32_t coord_t;
+#define COORD_MAX_INDEX INT32_MAX
+static inline int32_t la_get(const coord_t *r, int32_t i) { return r[i]; }
+static inline void la_put(coord_t *r, int32_t i, int32_t v) { r[i] = v; }
+static inline int32_t fd_get(const coord_t *r, int32_t i) { return r[i]; }
+static inline void fd_put(coord_t *r, int32_t i, int32_t v) { r[i] = v; }
+#endif
+
 enum { TRI_UNDEFINED = 0, TRI_TRUE = 1, TRI_FALSE = 2 }; /* roundInfo.go:10-16 */
 
 typedef struct {
@@ -50,8 +72,9 @@ struct hgo {
   /* event bodies */
   int32_t *creator, *index, *sp, *op, *ntx;
   uint8_t *hash, *sigr;
-  /* coordinates: lastAncestors / firstDescendants indexes, [N][n] */
-  int32_t *la, *fd;
+  /* coordinates: lastAncestors / firstDescendants indexes, [N][n]
+   * (coord_t: see the storage note below) */
+  coord_t *la, *fd;
   /* memo caches (hashgraph.go:36-40) */
   int32_t *round_memo, *lt_memo;
   /* Event private fields (event.go:107-116): nil == UNSET */
@@ -160,8 +183,8 @@ hgo *hgo_create(int32_t n, const int64_t *participant_ids, int64_t capacity) {
   h->ntx = (int32_t *)xcalloc(C, 4);
   h->hash = (uint8_t *)xcalloc(C, 32);
   h->sigr = (uint8_t *)xcalloc(C, 32);
-  h->la = (int32_t *)xcalloc(C * (size_t)n, 4);
-  h->fd = (int32_t *)xcalloc(C * (size_t)n, 4);
+  h->la = (coord_t *)xcalloc(C * (size_t)n, sizeof(coord_t));
+  h->fd = (coord_t *)xcalloc(C * (size_t)n, sizeof(coord_t));
   h->round_memo = (int32_t *)xcalloc(C, 4);
   h->lt_memo = (int32_t *)xcalloc(C, 4);
   h->ev_round = (int32_t *)xcalloc(C, 4);
@@ -314,20 +337,20 @@ static int ri_witnesses_decided(const round_info *ri) {
 /* ------------------------------------------------------------------------ */
 /* ancestry primitives                                                       */
 
-static inline int32_t *LA(const hgo *h, int32_t e) { return h->la + (size_t)e * h->n; }
-static inline int32_t *FD(const hgo *h, int32_t e) { return h->fd + (size_t)e * h->n; }
+static inline coord_t *LA(const hgo *h, int32_t e) { return h->la + (size_t)e * h->n; }
+static inline coord_t *FD(const hgo *h, int32_t e) { return h->fd + (size_t)e * h->n; }
 
 /* _ancestor / see (hashgraph.go:92-117, 152-157) */
 static int see(const hgo *h, int32_t x, int32_t y) {
   if (x == y) return 1;
-  return LA(h, x)[h->creator[y]] >= h->index[y];
+  return la_get(LA(h, x), h->creator[y]) >= h->index[y];
 }
 
 /* _stronglySee (hashgraph.go:172-191) */
 static int strongly_see(const hgo *h, int32_t x, int32_t y) {
-  const int32_t *lx = LA(h, x), *fy = FD(h, y);
+  const coord_t *lx = LA(h, x), *fy = FD(h, y);
   int c = 0;
-  for (int32_t i = 0; i < h->n; i++) c += lx[i] >= fy[i];
+  for (int32_t i = 0; i < h->n; i++) c += la_get(lx, i) >= fd_get(fy, i);
   return c >= h->sm;
 }
 
@@ -463,6 +486,10 @@ int hgo_insert_ext(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t o
    * indexes (caches.go / common/rolling_index.go:58-96); chains start at the
    * Root's SelfParent.Index + 1 */
   if (index != h->r_sp_index[creator] + 1 + clen) return HGO_ERR_SELF_PARENT;
+  if (index > COORD_MAX_INDEX) {
+    fprintf(stderr, "hg_oracle: index %d exceeds this build's coordinate storage\n", index);
+    abort();
+  }
 
   int32_t x = (int32_t)h->N++;
   h->creator[x] = creator; h->index[x] = index; h->sp[x] = sp; h->op[x] = op;
@@ -477,33 +504,36 @@ int hgo_insert_ext(hgo *h, int32_t creator, int32_t index, int32_t sp, int32_t o
 
   /* initEventCoordinates (hashgraph.go:439-507) */
   int32_t n = h->n;
-  int32_t *la = LA(h, x), *fd = FD(h, x);
-  for (int32_t i = 0; i < n; i++) fd[i] = FD_NONE;
+  coord_t *la = LA(h, x), *fd = FD(h, x);
+  for (int32_t i = 0; i < n; i++) fd_put(fd, i, FD_NONE);
   /* parents the Store does not hold (Roots, Root.Others) contribute nothing */
   if (sp < 0 && op < 0) {
-    for (int32_t i = 0; i < n; i++) la[i] = -1;
+    for (int32_t i = 0; i < n; i++) la_put(la, i, -1);
   } else if (sp < 0) {
-    memcpy(la, LA(h, op), (size_t)n * 4);
+    memcpy(la, LA(h, op), (size_t)n * sizeof(coord_t));
   } else if (op < 0) {
-    memcpy(la, LA(h, sp), (size_t)n * 4);
+    memcpy(la, LA(h, sp), (size_t)n * sizeof(coord_t));
   } else {
-    const int32_t *a = LA(h, sp), *b = LA(h, op);
-    for (int32_t i = 0; i < n; i++) la[i] = a[i] < b[i] ? b[i] : a[i];
+    const coord_t *a = LA(h, sp), *b = LA(h, op);
+    for (int32_t i = 0; i < n; i++) {
+      const int32_t u = la_get(a, i), v = la_get(b, i);
+      la_put(la, i, u < v ? v : u);
+    }
   }
-  fd[creator] = index;
-  la[creator] = index;
+  fd_put(fd, creator, index);
+  la_put(la, creator, index);
   chain_push(h, creator, x); /* Store.SetEvent -> addParticipantEvent */
 
   /* updateAncestorFirstDescendant (hashgraph.go:510-544): walk each last
    * ancestor's self-parent chain while its firstDescendant is unset */
   for (int32_t i = 0; i < n; i++) {
     const int32_t base = h->r_sp_index[i] + 1; /* Index of chain i's first event */
-    int32_t k = la[i];
+    int32_t k = la_get(la, i);
     while (k >= base) {
       int32_t a = h->chain[i][k - base];
-      int32_t *fa = FD(h, a);
-      if (fa[creator] != FD_NONE) break;
-      fa[creator] = index;
+      coord_t *fa = FD(h, a);
+      if (fd_get(fa, creator) != FD_NONE) break;
+      fd_put(fa, creator, index);
       k--; /* a.SelfParent(); the Root is not an event -> GetEvent fails -> break */
     }
   }
@@ -1160,8 +1190,10 @@ int32_t hgo_pending_rounds(const hgo *h, int32_t *index, int8_t *decided, int32_
 }
 
 void hgo_coordinates(const hgo *h, int32_t id, int32_t *la, int32_t *fd) {
-  if (la) memcpy(la, LA(h, id), (size_t)h->n * 4);
-  if (fd) memcpy(fd, FD(h, id), (size_t)h->n * 4);
+  for (int32_t i = 0; i < h->n; i++) {
+    if (la) la[i] = la_get(LA(h, id), i);
+    if (fd) fd[i] = fd_get(FD(h, id), i);
+  }
 }
 
 int64_t hgo_undetermined(const hgo *h, int32_t *ids, int64_t cap) {

@@ -180,19 +180,12 @@ def test_empty_and_tiny():
     assert hg.last_consensus_round is None
 
 
-def test_large_properties():
-    """C2 size (1M events, 32 peers): size-independent properties of the
-    whole-DAG run -- the Lamport recurrence, round monotonicity along both
-    parents, the witness definition, the frame sort key order and the
-    block / transaction conservation.  (Bit-exact parity at full sizes is
-    test_full_size_prefix_parity.)"""
-    from babble_amd.dag import Dag
-    from babble_amd import Hashgraph
-    n, N = 32, 1_000_000
-    d = Dag(n, N, 0xBABB1E02, sig_mode=0)
-    hg = Hashgraph(d.participant_ids, N)
-    hg.insert_dag(d)
-    hg.run_consensus()
+def invariants(d, hg, ordered=0.95):
+    """Size-independent properties of a whole-DAG run: the Lamport
+    recurrence (hashgraph.go:325-379), round monotonicity along both parents
+    (_round :205-278), the witness definition (:281-296), the frame sort key
+    order (ByLamportTimestamp, event.go:328-347) and block / transaction
+    conservation (ProcessDecidedRounds :1041-1122)."""
     res = hg.results()
     lt = res["lamport"]
     sp, op = d.self_parent, d.other_parent
@@ -210,10 +203,26 @@ def test_large_properties():
     assert np.all(np.diff(key_rr) >= 0)
     same = np.diff(key_rr) == 0
     assert np.all(np.diff(lt[order])[same] >= 0)
+    assert np.all(rr[order] > rnd[order])  # received in a later round
     b = hg.blocks()
     assert b["count"].sum() == len(order)
     assert b["ntx"].sum() == d.ntx[order].sum() == hg.consensus_transactions
-    assert len(order) > 0.95 * N
+    assert len(order) > ordered * d.N
+    return res
+
+
+def test_large_properties():
+    """C2 size (1M events, 32 peers): the invariants of a whole-DAG run
+    (bit-exact whole-DAG parity at full sizes: test_gpu_fullsize.py,
+    test_gpu_whole.py)."""
+    from babble_amd.dag import Dag
+    from babble_amd import Hashgraph
+    n, N = 32, 1_000_000
+    d = Dag(n, N, 0xBABB1E02, sig_mode=0)
+    hg = Hashgraph(d.participant_ids, N)
+    hg.insert_dag(d)
+    hg.run_consensus()
+    invariants(d, hg)
 
 
 def test_wide_512_parity():
@@ -358,7 +367,8 @@ def test_chunk_sweep_wild(monkeypatch):
     _wild_parity(8, 30_000, 41, 25_000)
 
 
-@pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p16", "p32"])
+@pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p8_single", "p8g_tight_single",
+                                  "p16", "p32"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -370,8 +380,13 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     that take the shared one; p8_mixed: a lower spread limit, so windows also
     alternate with the 16-bit fallback -- over 16-bit rows (fd16; n = 300
     has a half-filled last piece) and over the 32-bit rows (BH_NO_P16, the
-    path for chains beyond P16_MAXLEN).  n = 160 / 300 leave the last lanes
-    of a candidate's group past the end of its byte row."""
+    path for chains beyond P16_MAXLEN).  *_single: one candidate's search per
+    lane group instead of two interleaved (BH_ROUND_ILP2=0, its own tag check
+    and cand8 read).  n = 160 / 300 leave the last lanes of a candidate's
+    group past the end of its byte row."""
+    if rows.endswith("_single"):
+        monkeypatch.setenv("BH_ROUND_ILP2", "0")
+        rows = rows[:-len("_single")]
     if rows == "p8_window":
         monkeypatch.setenv("BH_ROUND_P8G", "0")
     if rows == "p8g_tight":
@@ -443,6 +458,36 @@ def test_floww_parity_and_lt_fallback(monkeypatch, kernel):
     monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
     hg = _random_parity(160, 20_000, 77, 2)
     assert hg.results()["lamport"].max() > 300
+
+
+@pytest.mark.parametrize("segments", [None, 4])
+def test_floww_watchdog_fallback(monkeypatch, segments):
+    """k_floww2's watchdog fires (BH_FLOWW_WATCHDOG=-1: at its first header,
+    every launch): the segment pipeline must see the flag before any round
+    loop reads the unfinished coordinates and recompute the call through the
+    chunked sweep -- in one segment and in four, for a batch and for the
+    incremental calls after it."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_FLOWW_WATCHDOG", "-1")  # read at handle creation
+    if segments:
+        monkeypatch.setenv("BH_SEGMENTS", str(segments))
+    n, N = 160, 30_000
+    d = Dag(n, N, 79, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    for lo, hi in ((0, 20_000), (20_000, 25_000), (25_000, N)):
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi],
+                                    opi[lo:hi], d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi]).any()
+        hg.run_consensus()
+        _compare(o, hg, f"watchdog fallback, events [0, {hi})")
+        assert hg.profile_kernel() == "k_la_sweep"
 
 
 def test_flow64_parity(monkeypatch):

@@ -202,11 +202,14 @@ def test_reset_high_round_silent_peer(n, N, seed, silent, join):
     assert (o2.results()["round"][hg.stats().n_events - 1]) > rs.round_received
 
 
-def test_reset_allocation_failure(monkeypatch):
+@pytest.mark.parametrize("frames", [False, True])
+def test_reset_allocation_failure(monkeypatch, frames):
     """A bh_reset whose k-th device allocation fails (BH_TEST_FAIL_ALLOC=k,
     for every k up to the call's last allocation) returns the error and
     leaves the handle a fresh one: the same handle then takes the Reset and
-    the events and matches the oracle."""
+    the events and matches the oracle.  With the block projection on, its
+    tables and JSON buffers are among the allocations (all made before the
+    call commits)."""
     from babble_amd import Hashgraph
     from babble_amd.hashgraph import HashgraphError
     d = DagArrays(Dag(8, 4000, 0xBA8))
@@ -216,12 +219,13 @@ def test_reset_allocation_failure(monkeypatch):
     args = (rs.round_received, rs.block_index, rs.next_round, rs.sp_index, rs.sp_lt, rs.sp_round,
             rs.oth_root, rs.oth_key, pid[np.asarray(rs.oth_creator, np.int64)] if rs.oth_creator else [],
             rs.oth_index, rs.oth_lt, rs.oth_round, rs.oth_hash)
+    kw = dict(self_parent_hash=rs.sp_hash) if frames else {}
     failures = 0
     for k in range(1, 64):
-        hg = Hashgraph(pid, len(d.creator) + 64)
+        hg = Hashgraph(pid, len(d.creator) + 64, frames=frames)
         monkeypatch.setenv("BH_TEST_FAIL_ALLOC", str(k))
         try:
-            hg.reset(*args)
+            hg.reset(*args, **kw)
             ok = True
         except HashgraphError as e:
             assert e.kind == "Device", e
@@ -230,7 +234,7 @@ def test_reset_allocation_failure(monkeypatch):
         if ok:
             break
         failures += 1
-        hg.reset(*args)  # the failed call changed nothing: the handle takes the Reset now
+        hg.reset(*args, **kw)  # the failed call changed nothing: the handle takes the Reset now
         o2 = Oracle(d.n, d.participant_ids, capacity=len(d.creator) + 64)
         rs2 = ResetInputs(o, d, 4)
         o2.reset(rs2)
@@ -240,7 +244,7 @@ def test_reset_allocation_failure(monkeypatch):
         hg.run_consensus()
         _compare(o2, hg, f"after an injected failure at allocation {k}")
         hg.close()
-    assert failures >= 10  # every allocation of the call was covered
+    assert failures >= (30 if frames else 10)  # every allocation of the call was covered
 
 
 def _event_bytes(g):
