@@ -428,6 +428,7 @@ int rounds_coords(bh_handle *h) {
   h->segments_used = 1;
   h->inc_valid = false;
   h->fdt_lost = false;
+  h->rows_stale = false;  // (rounds_loop transposes)
   if ((rc = set_chain_tables(h))) return rc;
   d.rows = h->layout_rows;
   hipStream_t s = h->stream;
@@ -631,6 +632,13 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   const int n = d.n;
   const bool wide = !d.fd_cols;  // k_floww2 + k_round_wide (cand16 from FDT)
   if (wide) d.fd_rows = 0;
+  // n <= 128: k_round2 and fame read only the dataflow's column-major LA, so
+  // the segments skip the row-major LA and FDT (the transpose; 21 GB of the
+  // C3 step's HBM traffic) -- queries build them on demand (ensure_coords).
+  // A Reset hashgraph's fiat pass and the resident loop (BH_ROUND_SOLO) read
+  // them; BH_EAGER_ROWS=1 builds them anyway (A/B)
+  static const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
+  const bool eager = wide || h->reset_on || eager_env || bh::round_solo_eligible(d);
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
   h->fdt_lost = false;
@@ -713,8 +721,12 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
       bh::launch_flow(v, sc);
     }
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
-    bh::launch_flow_transpose(v, sc);
-    bh::launch_fd_idle(v, sc);
+    if (eager) {
+      bh::launch_flow_transpose(v, sc);
+      bh::launch_fd_idle(v, sc);
+    } else {
+      bh::launch_lt_rows(v, sc);
+    }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));  // the coordinate pipeline's end
@@ -819,6 +831,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
     return rounds_loop(h);
   }
   h->coords_for = (int)N;
+  h->rows_stale = !eager;
   float ms = 0;
   h->sweep_ms = 0;
   for (int k = 0; k < K; ++k)
@@ -1268,9 +1281,8 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.candfd, (size_t)2 * n * d.npad);
   d.cand16 = !d.fd_cols && n <= 512 ? reinterpret_cast<uint32_t *>(d.candfd) : nullptr;  // (npad + 7) / 8 * 4 <= npad dwords a row
   d.round_ilp2 = getenv("BH_ROUND_ILP2") ? atoi(getenv("BH_ROUND_ILP2")) != 0 : 1;
-  d.round2_p8 = getenv("BH_ROUND2_P8") && atoi(getenv("BH_ROUND2_P8"));
   d.round_p8g = getenv("BH_ROUND_P8G") ? std::clamp(atoi(getenv("BH_ROUND_P8G")), 0, 64) : bh::P8G_DELTA;
-  if (d.cand16 || (d.fd_cols && d.npad > 64 && d.round2_p8)) {  // k_round_wide<*, true> / k_round2<4, true>
+  if (d.cand16) {  // k_round_wide<*, true>
     A(&d.cand8, (size_t)2 * n * ((d.npad + 15) / 16 * 16));
     A(&d.c8tag, (size_t)2 * n);
     A(&d.Bq, (size_t)2 * d.npad);
@@ -2001,6 +2013,22 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
 static int ensure_coords(bh_handle *h) {
   Dev &d = h->d;
   const int64_t N = (int64_t)h->h_creator.size();
+  if (h->coords_for == N && h->rows_stale) {
+    // the segments left only the column-major LA (rounds_pipelined): the
+    // row-major LA and the complete FDT of every row, as a whole-layout
+    // transpose builds them
+    Dev full = d;
+    full.e0 = 0;
+    full.seg_lo = h->seg_zero;
+    full.tile_list = nullptr;
+    full.rows = h->layout_rows;
+    full.col0 = 0;
+    full.ncol = d.n;
+    bh::launch_flow_transpose(full, h->stream);
+    bh::launch_fd_idle(full, h->stream);
+    HIPCHK(h, hipGetLastError());
+    h->rows_stale = false;
+  }
   if (h->coords_for != N) {
     int rc;
     hipStream_t s = h->stream;
@@ -2058,6 +2086,7 @@ static int ensure_coords(bh_handle *h) {
     if (!keep) h->inc_valid = false;
     HIPCHK(h, hipGetLastError());
     h->coords_for = (int)N;
+    h->rows_stale = false;
     if (h->n_div < N) {
       // the passes that follow (DecideFame, DecideRoundReceived,
       // ProcessDecidedRounds) see the events DivideRounds covered, as Go's

@@ -134,7 +134,6 @@ struct Dev {
   int32_t *Bq;        // [2][npad] k_round2 bytes: B[r - 1] for the iteration of parity p (written by iteration r - 1)
   int32_t round_p8g;  // base offset below B[r-1] (P8G_DELTA; BH_ROUND_P8G=0 turns the shared base off)
   int32_t round_ilp2;  // k_round_wide byte rows: two candidates' searches interleaved per lane group (BH_ROUND_ILP2=0: one)
-  int32_t round2_p8;  // k_round2<4, true> on byte rows too (BH_ROUND2_P8=1; off by default: no gain measured at C3)
   // [n][rspan][8] k_round_wide's stronglySee masks (n <= 512, !fd_cols):
   // word w bit b = candidate (64 w + b, B[r-1]) is strongly seen by (c, B[r][c])
   unsigned long long *ssw;
@@ -192,6 +191,16 @@ struct Dev {
   int32_t frame_lo;  // frames below it are never emitted (Reset: LastConsensusRound's, hashgraph.go:1063-1065)
   int32_t blk_base;  // Block.Index of the first block this handle makes (LastBlockIndex()+1: after a Reset block.Index()+1)
 };
+
+__host__ __device__ inline int64_t la_col_stride(const Dev &d) { return d.la_rows + 64; }
+
+// LA[row][col] of chain-major row `row`.  n <= 128 (fd_cols): the dataflow's
+// column-major copy, which every coordinate path writes; the pipelined path
+// builds the row-major `la` (and FDT) only when a query asks for them.
+// Wider: the row-major table (la_col may share FDT's memory there).
+__device__ __forceinline__ int32_t la_at(const Dev &d, int64_t row, int col) {
+  return d.fd_cols ? d.la_col[(int64_t)col * la_col_stride(d) + row] : d.la[row * d.npad + col];
+}
 // row of (chain c, round r) in the ballot tables ssm / ssw
 __host__ __device__ inline int64_t ballot_row(const Dev &d, int c, int r) {
   return (int64_t)c * d.rspan + (r - d.rbase);
@@ -311,6 +320,10 @@ void launch_round_resume(const Dev &d, hipStream_t s);
 void launch_resume_point(const Dev &d, int32_t R, const int32_t *next_len, hipStream_t s);
 // FD entries of a segment's new rows for chains with no event in the segment
 void launch_fd_idle(const Dev &d, hipStream_t s);
+// Lamport timestamps of the segment's events [e0, N) from the chain-major
+// LT rows (what the transpose does beside LA / FDT, for a segment whose
+// row-major LA and FDT are left unbuilt: n <= 128)
+void launch_lt_rows(const Dev &d, hipStream_t s);
 void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_round
 // n <= 32 on the chain dataflow: the whole loop in one resident workgroup
 // (k_round_solo; opt-in with BH_ROUND_SOLO=1, measured A/B)

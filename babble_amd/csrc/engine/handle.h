@@ -117,6 +117,7 @@ struct bh_handle {
   // of the current layout; lens_coord their chain lengths
   bool inc_valid = false;
   bool fdt_lost = false;  // the wide LT fallback's sweep overwrote FDT (no resume from it)
+  bool rows_stale = false;  // n <= 128 segments built la_col only: row-major LA / FDT wait for a query
   int64_t n_coord = 0;
   int64_t inc_calls = 0;  // DivideRounds calls that resumed (statistics)
   std::vector<int32_t> lens_coord;

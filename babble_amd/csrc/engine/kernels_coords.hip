@@ -293,7 +293,11 @@ __global__ __launch_bounds__(256) void k_permute(Dev d) {
   const int n = d.n, npad = d.npad;
   const int64_t stride = d.la_rows + 64;
   const int32_t *src = d.la_ev + e;
-  int4 *dst = reinterpret_cast<int4 *>(d.la + (int64_t)d.epos[e] * npad);
+  const int64_t row = d.epos[e];
+  int4 *dst = reinterpret_cast<int4 *>(d.la + row * npad);
+  // n <= 128: the column-major copy too (k_round2 and fame read it; its
+  // own allocation there -- wider groups' la_col may be the slabs themselves)
+  int32_t *col = d.fd_cols ? d.la_col + row : nullptr;
   int c = 0;
   for (; c + 32 <= n; c += 32) {
     int32_t v[32];
@@ -301,12 +305,18 @@ __global__ __launch_bounds__(256) void k_permute(Dev d) {
     for (int u = 0; u < 32; ++u) v[u] = __builtin_nontemporal_load(src + (int64_t)(c + u) * stride);
 #pragma unroll
     for (int u = 0; u < 8; ++u) dst[c / 4 + u] = make_int4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
+    if (col)
+#pragma unroll
+      for (int u = 0; u < 32; ++u) col[(int64_t)(c + u) * stride] = v[u];
   }
   for (; c < npad; c += 4) {
     int32_t v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = c + u < n ? src[(int64_t)(c + u) * stride] : -1;
     dst[c / 4] = make_int4(v[0], v[1], v[2], v[3]);
+    if (col)
+      for (int u = 0; u < 4; ++u)
+        if (c + u < n) col[(int64_t)(c + u) * stride] = v[u];
   }
 }
 

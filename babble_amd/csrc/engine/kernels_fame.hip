@@ -296,7 +296,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
         for (int b = 0; b < 32; ++b) {
           const int y = h * HY + k * 32 + b;
           if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
-          if (d.la[(int64_t)L.yev[y] * npad + xc] >= L.xk[xc]) v |= 1u << b;
+          if (la_at(d, L.yev[y], xc) >= L.xk[xc]) v |= 1u << b;
         }
         L.V[0][h * HW_ + k][x] = v;
       }
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   const int nf = L.nfam_s;
   for (int c = t; c < npad; c += nt) {
     int32_t m = INT32_MAX;
-    for (int i = 0; i < nf; ++i) m = min(m, d.la[(int64_t)L.frow[i] * npad + c]);
+    for (int i = 0; i < nf; ++i) m = min(m, c < n ? la_at(d, L.frow[i], c) : -1);
     d.minla[(int64_t)r * npad + c] = m;
     if (c == 0) d.nfam[r] = nf;
   }

@@ -801,6 +801,19 @@ void launch_flow_transpose(const Dev &d, hipStream_t s) {
   k_flow_transpose<64, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 66 * 4, s>>>(d);
 }
 
+// Lamport timestamps of the events [e0, N) from the chain-major LT rows:
+// the transpose's side job, for segments that do without it (n <= 128)
+__global__ __launch_bounds__(256) void k_lt_rows(Dev d) {
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  d.lt[e] = d.lt_row[(int64_t)d.chain_start[d.creator[e]] + d.index[e]];
+}
+
+void launch_lt_rows(const Dev &d, hipStream_t s) {
+  if (d.N <= d.e0) return;
+  k_lt_rows<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+}
+
 void launch_flow_coordinates(const Dev &d, hipStream_t s) {
   launch_flow_desc(d, s);
   launch_flow(d, s);

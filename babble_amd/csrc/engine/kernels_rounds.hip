@@ -754,16 +754,65 @@ __device__ __forceinline__ int group_sum(int v) {
   return v;
 }
 
-// per-chain hand-off for round 0 (B[0] = 0)
-__global__ __launch_bounds__(256) void k_round2_init(Dev d) {
-  const int c = blockIdx.x, q4 = d.npad / 4;
-  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
-  if (threadIdx.x == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
-  if (len == 0) return;
-  (void)q4;
-  // candidate (c, 0): its FD row gathered from the FDT columns
+// The first row j of chain i at or after row `lo` (of [lo, hi)) whose LA
+// in column c is >= k, or hi if none: firstDescendants read from the
+// column-major LA (FD[(c, k)][i] = min{j : LA[(i, j)][c]
+// >= k}, and LA[(i, j)][c] is non-decreasing in j).  `col` = LA[.][c] from
+// chain i's first row.  Found by the 16 lanes of every aligned lane group
+// with `on` set (col, lo, hi, k uniform over the group); every lane of the
+// wave calls it.  One dependent load per pass: a first pass over the 1024
+// rows after lo (16 probes 64 apart, when `near`), then 16-ary narrowing,
+// spans of <= 64 rows finished with 4 rows a lane.
+__device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, int32_t hi, int32_t k, bool on,
+                                              bool near) {
+  const int lane = threadIdx.x & 63, g = lane & 15, gb = lane & 48;
+  while (__any(on)) {
+    if (on) {
+      if (hi - lo <= 64) {
+        const int32_t x = lo + 4 * g;
+        int cnt = 0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          cnt += __popc((uint32_t)(__ballot(x + v < hi && col[x + v] < k) >> gb) & 0xFFFFu);
+        lo += cnt;
+        on = false;
+      } else {
+        const int32_t lim = near ? min(hi, lo + 1024) : hi;
+        const int32_t s = (lim - lo + 15) >> 4;
+        const int32_t pr = min(lo + (g + 1) * s, lim) - 1;
+        const uint32_t m = (uint32_t)(__ballot(col[pr] >= k) >> gb) & 0xFFFFu;
+        if (m) {
+          const int f = __builtin_ctz(m);
+          hi = min(lo + (f + 1) * s, lim);
+          lo += f * s;
+        } else {
+          lo = lim;
+          on = lim < hi;
+        }
+        near = false;
+      }
+    }
+  }
+  return lo;
+}
+
+// candidates' FD rows for the first iteration of a loop (parity 0): round 0
+// (B = 0) or the resume round ST_RESUME (B[r0]), searched in la_col -- one
+// workgroup per candidate chain c, a 16-lane group per chain i
+__global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int32_t b = from_resume ? d.B[(int64_t)d.state[ST_RESUME] * d.n + c] : 0;
+  if (t == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
+  if (b >= d.chain_len[c]) return;  // no candidate on chain c
+  const int32_t *colc = d.la_col + (int64_t)c * la_col_stride(d);
   int32_t *cf = d.candfd + (int64_t)c * d.npad;
-  for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs, i, d.npad)] : FD_NONE;
+  for (int i0 = 0; i0 < d.npad; i0 += blockDim.x >> 4) {  // (uniform trip count)
+    const int i = i0 + (t >> 4);
+    const bool on = i < d.n;
+    const int32_t cs = on ? d.chain_start[i] : 0, len = on ? d.chain_len[i] : 0;
+    const int32_t j = first_ge16(colc + cs, 0, len, b, on && len > 0, false);
+    if ((t & 15) == 0 && i < d.npad) cf[i] = on && j < len ? j : FD_NONE;
+  }
 }
 
 // TQ (default): every lane group binary-searches its own T_q (the first
@@ -772,48 +821,50 @@ __global__ __launch_bounds__(256) void k_round2_init(Dev d) {
 // #{q : T_q <= row} reaches SM.  !TQ (BH_ROUND_ROWS=1, A/B): the row-probe
 // search -- the workgroup binary-searches count(row) together, one barrier
 // per probe.  Same compares per probe; the groups of a wave read different
-// rows, so each group starts its four 128-B chunks at chunk (q & 3): the
-// four groups of a ds_read_b128 lane set then hit distinct banks.
+// rows, so each group starts its four 128-B chunks at chunk (q & 3).
 // 8 lanes per candidate, PPL 16-B pieces of its FD row per lane (LPC * PPL *
 // 4 >= npad columns), 8 npad threads (rounded up to whole waves): the
 // workgroup is as wide as its candidates need -- at n = 32 four waves of one
-// piece per lane instead of sixteen waves of four pieces, most of them idle
-// rows of nonexistent candidates (C2 search 2.5 us -> see DESIGN.md)
+// piece per lane instead of sixteen waves of four pieces.
 //
-// 8-bit rows (opt-in, BH_ROUND2_P8=1: measured a wash at C3, the search's
-// savings spent again in the prologue and the hand-off -- DESIGN.md 5)
-// (npad > 64, PPL = 4, TQ): iteration r compares
-// bytes relative to the shared base base_i = max(B[r-1][i] - round_p8g, 0),
-// as k_round_wide does.  The workgroup that hands candidate c over writes its
-// row as npad bytes (cand8, min(max(FD + 1 - base_i, 0), 127), 127 past n)
-// beside the 32-bit candfd row, with a tag (c8tag = r); the window's LA is x =
-// LA + 1 - base_i in [0, round_p8] (x | 0x80 in LDS), so LA >= FD <=> x >= f
-// and a probe is four dword compares per lane (16 columns) instead of 16.  A
-// workgroup whose window does not fit the base, or one of whose candidates
-// has no tag for r (the first iteration after a resume), takes the 32-bit
-// rows, loading candfd then.  The window sits in LDS twice, 128 B apart on
-// 256-B rows, and lane groups (g >> 1) & 1 read the second copy: the four
-// groups of a ds_read_b128 lane set then hit 16 distinct bank slots whatever
-// rows their searches probe.
+// Round 4: the loop reads only the dataflow's column-major LA (la_col); no
+// row-major LA and no firstDescendants table are built for it.
+//   * The window: HWL = 36 rows of every column from rb = the window's first
+//     row rounded down to 4, one aligned 16-B piece (4 rows of one column)
+//     per thread, stored transposed into the row-major LDS window; the search
+//     runs over its rows off .. off + 31 (off = the alignment offset).
+//   * The hand-off: the new candidate (c, B[r+1][c])'s FD row.  FD[(c, k)][i]
+//     is non-decreasing in k, so it starts at the previous candidate's entry
+//     j0 = FD[(c, B[r][c])][i] (its row, candfd[p][c]).  At the start of the
+//     iteration every 16-lane group loads FDB = 64 rows of LA[.][c] on chain
+//     i from j0 (rounded down to 4); once the boundary is known, the entry is
+//     j0 + #{rows < the boundary index} -- one count and a group sum, no
+//     dependent load.  A group whose 64 rows all stay below (a jump of more
+//     than ~60 rows, e.g. a lagging chain's candidate) searches on
+//     (first_ge16: usually two more loads).  Entries beyond the view's chain
+//     lengths are MaxInt32, as the prefix semantics need (section 4.9).
+constexpr int HWL = HW + 4;  // staged window rows
+constexpr int WP = HWL / 4;  // 16-B pieces per column of the window
+constexpr int FDB = 64;      // LA rows per chain loaded for the hand-off
+
+// the first iteration's candidate rows (round 0, or the resume round)
+void launch_cand_rows(const Dev &d, int from_resume, hipStream_t s) {
+  k_cand_rows<<<d.n, 1024, 0, s>>>(d, from_resume);
+}
+
 template <int PPL, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   constexpr int LPC = 8;
-  constexpr bool P8 = PPL == 4 && TQ;
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
   __shared__ int32_t cntk[16];
   __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
-  __shared__ int32_t bad8[16];      // P8: a wave's window columns or candidates do not fit the byte rows
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
-  int4 *win = sm4;              // [HW][q4]: LA rows k0 .. k0 + 31
-  // [npad][FDS]: FD rows rb .. rb + 31 by column, for the hand-off after the
-  // search -- the window's space (every read of it is behind the search's
-  // last barrier), so the workgroup's LDS (18 KiB at n = 128) fits beside a
-  // k_flow32 workgroup (133 KiB) on one compute unit: the segment pipeline
-  // runs both at once
-  int32_t *fdw = reinterpret_cast<int32_t *>(sm4);
-  constexpr int FDS = HW + 4;
+  const int rs4 = q4 + 1, rs = 4 * rs4;  // window row stride (one spare piece: staging stores spread over banks)
+  const int64_t stride = la_col_stride(d);
+  int4 *win = sm4;  // [HWL][rs4]: LA rows rb .. rb + HWL - 1
+  int32_t *win32 = reinterpret_cast<int32_t *>(sm4);
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   const bool dg = d.diag != nullptr && t == 0;
   const unsigned long long ts0 = dg ? stamp() : 0;
@@ -828,86 +879,71 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   int32_t bq = 0, lq = 0;
   if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; }
   int4 f[PPL];
-  auto load_f = [&]() {
+  {
     const int4 *cf = reinterpret_cast<const int4 *>(d.candfd) + ((int64_t)p * n + min(q, n - 1)) * q4;
 #pragma unroll
     for (int u = 0; u < PPL; ++u) {
       const int pc = part + LPC * ((u + rot) & (PPL - 1));
       f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
     }
-  };
-  // P8: try the byte rows (decided by the whole workgroup after staging)
-  // (no load here depends on the state word r: the base row comes from Bq
-  // by parity, and the tags are compared with r only at staging)
-  const bool g8 = P8 && d.round2_p8 && d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;  // byte rows handed over and used
-  const bool try8 = g8;
-  const int s8 = (npad + 15) / 16 * 16;  // bytes per cand8 row
-  int4 f8 = make_int4(0, 0, 0, 0);
-  bool ok8 = try8;
-  int32_t tag8 = r;
-  int32_t bnext = 0;  // P8 hand-off: B[r][t], the base of column t for iteration r + 1
-  int4 gb = make_int4(0, 0, 0, 0);  // P8: the shared base of this thread's four window columns
-  if (g8 && t < s8) bnext = t < n ? Bp[t] : 0;
-  if (g8 && t == 0) d.Bq[(int64_t)(p ^ 1) * npad + c] = k0;  // B[r] for iteration r + 1 (read after this launch)
-  if (try8) {
-    const int w8q = s8 / 16;  // 16-B pieces per byte row (npad = 128: 8, one per lane)
-    if (q < n) {
-      tag8 = d.c8tag[(int64_t)p * n + q];  // (checked at staging for live candidates only)
-      f8 = reinterpret_cast<const int4 *>(d.cand8)[((int64_t)p * n + q) * w8q + min(part, w8q - 1)];
-      if (part >= w8q) f8 = make_int4(0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F);
-    }
-    // B[r - 1] of this thread's four window columns (written by iteration r - 1)
-    const int4 bv = reinterpret_cast<const int4 *>(d.Bq + (int64_t)p * npad)[t % q4];
-    gb = make_int4(max(bv.x - d.round_p8g, 0), max(bv.y - d.round_p8g, 0), max(bv.z - d.round_p8g, 0),
-                   max(bv.w - d.round_p8g, 0));
-  } else {
-    load_f();
   }
-  const int rows = min(HW, max(0, len - k0));
-  const int4 wv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
-  if (done) return;
-  const bool act = q < n && bq < lq;
-  // ---- loads for the hand-off (consumed after the search) ----
-  // FD rows rb .. rb + 31 (rb = the window's first row rounded down to 4)
-  // from the FDT tiles: 16 B = 4 rows of one column per thread, 8 threads
-  // per column
+  // the hand-off's inputs: chain i = (t + u nt) / 16 of this thread, its
+  // view length and the previous candidate's entry FD[(c, k0)][i]
+  const int32_t *colc = d.la_col + (int64_t)c * stride;  // LA[.][c]
+  const int32_t *cfc = d.candfd + ((int64_t)p * n + c) * npad;
+  int32_t hj0[2], hcs[2], hlen[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = (t + u * nt) >> 4;
+    hj0[u] = FD_NONE;
+    hcs[u] = 0;
+    hlen[u] = 0;
+    if (i < n && k0 < len) {
+      hj0[u] = cfc[i];
+      hcs[u] = d.chain_start[i];
+      hlen[u] = d.chain_len[i];
+    }
+  }
+  // the window's pieces: item j = column j / WP, rows rb + 4 (j % WP) .. + 3
   const int64_t rb = (int64_t)(cs + k0) & ~(int64_t)3;
-  const int fi = min(t >> 3, n - 1), fp = (t & 7) * 4;
-  const int4 fv = *reinterpret_cast<const int4 *>(d.fdt + fdt_pos(rb + fp, fi, npad));
-  if (t < rows * q4) win[t] = wv;
+  const int off = (int)(cs + k0 - rb);
+  int4 wv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = t + u * nt;
+    wv[u] = j < WP * n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)(j / WP) * stride + rb + 4 * (j % WP))
+                       : make_int4(-1, -1, -1, -1);
+  }
+  if (done) return;
+  // the hand-off's 64 rows of LA[.][c] per chain i (depend on j0 only)
+  int4 fb[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int piece = (t + u * nt) & 15;
+    const bool live = hj0[u] != FD_NONE;
+    const int64_t a = live ? ((int64_t)hcs[u] + hj0[u]) & ~(int64_t)3 : 0;
+    fb[u] = live ? *reinterpret_cast<const int4 *>(colc + a + 4 * piece) : make_int4(0, 0, 0, 0);
+  }
+  const bool act = q < n && bq < lq;
+  const int rows = min(HW, max(0, len - k0));
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = t + u * nt;
+    if (j < WP * n) {
+      const int i = j / WP, r4 = 4 * (j - i * WP);
+      win32[(r4 + 0) * rs + i] = wv[u].x;
+      win32[(r4 + 1) * rs + i] = wv[u].y;
+      win32[(r4 + 2) * rs + i] = wv[u].z;
+      win32[(r4 + 3) * rs + i] = wv[u].w;
+    }
+  }
+  if (npad > n)  // columns past n: LA -1 (never >= an FD)
+    for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
   if (t < 16) cntk[t] = 0;
   if (TQ && t <= HW) hist[t] = 0;
-  // P8 window: [HW][2 copies][npad bytes] after the 32-bit window (the
-  // hand-off's fdw, which overlaps its first rows, is written only after the
-  // search's last barrier)
-  uint32_t *win8 = reinterpret_cast<uint32_t *>(sm4 + HW * q4);
-  bool p8 = false;
-  if (try8) {
-    if (q < n && bq < lq && tag8 != r) ok8 = false;  // a chain at its end hands nothing over
-    if (t < rows * q4) {
-      const int row = t / q4, col = 4 * (t % q4);
-      // x = LA + 1 - base; columns >= n have base 0 and LA -1 (x = 0, candidate bytes 127)
-      const uint32_t x0 = (uint32_t)(wv.x + 1 - gb.x), x1 = (uint32_t)(wv.y + 1 - gb.y);
-      const uint32_t x2 = (uint32_t)(wv.z + 1 - gb.z), x3 = (uint32_t)(wv.w + 1 - gb.w);
-      const uint32_t lim = (uint32_t)d.round_p8;  // unsigned: x < 0 fails too
-      if ((x0 > lim) | (x1 > lim) | (x2 > lim) | (x3 > lim)) ok8 = false;
-      const uint32_t w = (x0 | x1 << 8 | x2 << 16 | x3 << 24) | 0x80808080u;
-      win8[row * 64 + col / 4] = w;
-      win8[row * 64 + 32 + col / 4] = w;
-    }
-    for (int i = t; i < rows * 32; i += blockDim.x)  // columns npad .. 127: x = 0 (no byte borrows)
-      if ((i & 31) >= q4) win8[(i >> 5) * 64 + (i & 31)] = win8[(i >> 5) * 64 + 32 + (i & 31)] = 0x80808080u;
-    const bool bad = __any(!ok8);
-    if (lane == 0) bad8[wave] = bad;  // every wave writes its own flag: no initialisation to order
-    __syncthreads();
-    p8 = !__any(lane < (int)(blockDim.x >> 6) && bad8[lane & 15]);
-    if (!p8) load_f();  // (rare: the 32-bit rows after all)
-  } else {
-    __syncthreads();
-  }
+  __syncthreads();
   const unsigned long long ts1 = dg ? stamp() : 0;
   const unsigned long long rt1 = dg ? __builtin_amdgcn_s_memrealtime() : 0;  // loads landed
-  // count(row) into slot: groups whose candidate `row` strongly sees
   // does window row x4 strongly see this group's candidate?
   auto ss_row = [&](const int4 *x4) {
     int4 x[PPL];  // all reads first: one LDS round trip per probe
@@ -928,25 +964,16 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     const unsigned long long m = __ballot(act && part == 0);
     if (lane == 0 && m) atomicAdd(&cntk[0], __popcll(m));
   }
+  const int4 *w0 = win + off * rs4;  // window row 0 = row k0 of chain c
   int slot = 1;
   int32_t res = -1;  // window row of B[r+1][c], or -1
   unsigned long long ssb = 0;  // this wave's ballot of the probe that verified the answer row
-  // P8: does window row `row` strongly see this group's candidate (its bytes f8)?
-  const int4 *w8b = reinterpret_cast<const int4 *>(win8) + ((q >> 1) & 1) * 8 + part;
-  auto ss_row8 = [&](int row) {
-    const int4 x = w8b[row * 16];
-    int ge = __builtin_popcount(((uint32_t)x.x - (uint32_t)f8.x) & 0x80808080u);
-    ge += __builtin_popcount(((uint32_t)x.y - (uint32_t)f8.y) & 0x80808080u);
-    ge += __builtin_popcount(((uint32_t)x.z - (uint32_t)f8.z) & 0x80808080u);
-    ge += __builtin_popcount(((uint32_t)x.w - (uint32_t)f8.w) & 0x80808080u);
-    return group_sum<LPC>(ge) >= sm;
-  };
   if (TQ && rows > 0) {
     // T_q by a per-group binary search over [0, rows] (rows = none in the window)
     int lo = 0, hi = rows;
     while (__any(lo < hi)) {
       const int mid = (lo + hi) >> 1;
-      const bool s = P8 && p8 ? ss_row8(min(mid, rows - 1)) : ss_row(win + min(mid, rows - 1) * q4);
+      const bool s = ss_row(w0 + min(mid, rows - 1) * rs4);
       if (lo < hi) {
         hi = s ? mid : hi;
         lo = s ? lo : mid + 1;
@@ -957,9 +984,9 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     if (wave == 0) {
       int h = lane < rows ? hist[lane] : 0;
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(h, off);
-        h += lane >= off ? o : 0;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int x = __shfl_up(h, o);
+        h += lane >= o ? x : 0;
       }
       const unsigned long long hit = __ballot(lane < rows && h >= sm);
       if (lane == 0) hist[HW] = hit ? (int)__builtin_ctzll(hit) : -1;
@@ -975,7 +1002,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     bool hi_ok = false;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      const unsigned long long m = probe(win + mid * q4, slot);
+      const unsigned long long m = probe(w0 + mid * rs4, slot);
       __syncthreads();
       if (cntk[slot] >= sm) {
         hi = mid;
@@ -987,7 +1014,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       ++slot;
     }
     if (!hi_ok) {
-      ssb = probe(win + hi * q4, slot);
+      ssb = probe(w0 + hi * rs4, slot);
       __syncthreads();
       hi_ok = cntk[slot] >= sm;
     }
@@ -1002,18 +1029,24 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   if (res >= 0) {
     result = k0 + res;
   } else if (nc > 0 && rows == HW) {
-    // SM not reached in the handed-over window (rare): later windows of
-    // chain c, loaded directly (slot counters are reused per row tested)
-    if (P8 && p8) load_f();
-    int4 *x4 = win;  // rows in LDS: row i of the current window at x4[i * q4]
+    // SM not reached in the window (rare): the next windows of chain c,
+    // staged the same way (slot counters are reused per row tested)
     for (int32_t wk = k0 + HW; wk < len && result == len; wk += HW) {
       const int wr = min(HW, len - wk);
+      const int64_t rb2 = (int64_t)(cs + wk) & ~(int64_t)3;
       __syncthreads();
-      for (int i = t; i < wr * q4; i += blockDim.x)
-        x4[i] = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + wk) * q4 + i];
+      for (int j = t; j < WP * n; j += nt) {
+        const int i = j / WP, r4 = 4 * (j - i * WP);
+        const int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)i * stride + rb2 + r4);
+        win32[(r4 + 0) * rs + i] = v.x;
+        win32[(r4 + 1) * rs + i] = v.y;
+        win32[(r4 + 2) * rs + i] = v.z;
+        win32[(r4 + 3) * rs + i] = v.w;
+      }
       if (t < 16) cntk[t] = 0;
       __syncthreads();
-      const unsigned long long ml = probe(x4 + (wr - 1) * q4, 1);
+      const int4 *x4 = win + (int)(cs + wk - rb2) * rs4;
+      const unsigned long long ml = probe(x4 + (wr - 1) * rs4, 1);
       __syncthreads();
       if (cntk[1] < sm) continue;
       int lo = 0, hi = wr - 1, sl = 1;
@@ -1021,7 +1054,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         ++sl;
-        const unsigned long long m = probe(x4 + mid * q4, sl);
+        const unsigned long long m = probe(x4 + mid * rs4, sl);
         __syncthreads();
         if (cntk[sl] >= sm) {
           hi = mid;
@@ -1034,31 +1067,45 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     }
     __syncthreads();
   }
-  // ---- hand-off for the next iteration ----
+  // ---- hand-off for the next iteration: FD[(c, result)][i] ----
   if (nc > 0 && r + 1 < d.R_cap && result < len) {
-    const int32_t off = result - k0;
     int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
-    const int frel = (int)(cs + result - rb);  // row of the candidate in fdw
-    int32_t fdv = FD_NONE;
-    if (off < HW && frel < HW) {  // both from the rows staged during the search
-      if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
-      __syncthreads();
-      if (t < n) fdv = fdw[t * FDS + frel];
-    } else {
-      if (t < n) fdv = d.fdt[fdt_pos(cs + result, t, npad)];
-    }
-    if (t < npad) cf[t] = fdv;
-    if (g8) {
-      // the byte row for iteration r + 1 (base B[r][t] - round_p8g), then its tag
-      if (t < s8) {  // (s8 <= 128: waves 0 and 1, four lanes per dword)
-        const int32_t b = max(bnext - d.round_p8g, 0);
-        const int32_t fx = t >= n || fdv == FD_NONE ? 127 : min(max(fdv + 1 - b, 0), 127);
-        uint32_t v = (uint32_t)fx << (8 * (t & 3));
-        v |= (uint32_t)__shfl_xor((int)v, 1);
-        v |= (uint32_t)__shfl_xor((int)v, 2);
-        if ((t & 3) == 0) reinterpret_cast<uint32_t *>(d.cand8 + ((int64_t)(p ^ 1) * n + c) * s8)[t >> 2] = v;
+    int32_t fdv[2], mlo[2];
+    bool miss[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = t + u * nt, i = j >> 4, piece = j & 15;
+      const bool live = hj0[u] != FD_NONE;
+      const int64_t a = (int64_t)hcs[u] + hj0[u];  // the previous candidate's entry (absolute row)
+      const int64_t ab = a & ~(int64_t)3, end = (int64_t)hcs[u] + hlen[u];
+      const int64_t x0 = ab + 4 * piece;
+      int cnt = 0;
+      if (live) {
+        cnt += x0 >= a && x0 < end && fb[u].x < result;
+        cnt += x0 + 1 >= a && x0 + 1 < end && fb[u].y < result;
+        cnt += x0 + 2 >= a && x0 + 2 < end && fb[u].z < result;
+        cnt += x0 + 3 >= a && x0 + 3 < end && fb[u].w < result;
       }
-      if (t == 0) d.c8tag[(int64_t)(p ^ 1) * n + c] = r + 1;
+      cnt = group_total<16>(cnt);
+      const int64_t jn = a + cnt, bend = min(ab + FDB, end);
+      fdv[u] = FD_NONE;
+      miss[u] = false;
+      mlo[u] = 0;
+      if (live) {
+        if (i == c) fdv[u] = result;  // an event is its own first descendant
+        else if (jn < bend) fdv[u] = (int32_t)(jn - hcs[u]);
+        else if (bend < end) { miss[u] = true; mlo[u] = (int32_t)(bend - hcs[u]); }
+        // else: no row of chain i in this view sees the candidate
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (__any(miss[u])) {  // (rare) the entry lies beyond the 64 rows loaded
+        const int32_t jm = first_ge16(colc + hcs[u], mlo[u], hlen[u], result, miss[u], true);
+        if (miss[u]) fdv[u] = jm < hlen[u] ? jm : FD_NONE;
+      }
+      const int j = t + u * nt;
+      if ((j & 15) == 0 && (j >> 4) < npad) cf[j >> 4] = fdv[u];
     }
     // fame's input for the new candidate y = (c, result): SS(y, q) over
     // the candidates q of round r = the ballots of the probe that verified
@@ -1164,7 +1211,7 @@ __global__ __launch_bounds__(1024) void k_round_solo(Dev d) {
       if (cv && row < to) ring[(row & 31) * q4 + (it - (it / q4) * q4)] = lv[j];
     }
   };
-  int r = d.state[ST_CUR0];  // parity-0 buffers: k_round2_init / k_round_resume
+  int r = d.state[ST_CUR0];  // parity-0 buffers: k_cand_rows (after k_round_resume)
   if (t < n) bsh[0][t] = d.Bp[t];
   for (int i = t; i < n * npad; i += blockDim.x) cand[0][i / npad][i % npad] = d.candfd[i];
   int32_t k0 = cv ? d.Bp[c] : 0;
@@ -1344,14 +1391,9 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
     d.Bp[c] = b;
     if (d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;  // cand8 rows of an earlier loop are stale
   }
-  if (b < len) {
-    if (d.fd_cols) {
-      int32_t *cf = d.candfd + (int64_t)c * d.npad;
-      for (int i = threadIdx.x; i < d.npad; i += blockDim.x) cf[i] = i < d.n ? d.fdt[fdt_pos(cs + b, i, d.npad)] : FD_NONE;
-    } else if (d.cand16 && !d.fd_rows) {
-      gather_cand16(d, (int64_t)cs + b, d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
-    }
-  }
+  // (n <= 128: the candidates' rows are searched in la_col, k_cand_rows)
+  if (b < len && !d.fd_cols && d.cand16 && !d.fd_rows)
+    gather_cand16(d, (int64_t)cs + b, d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
   if (c == 0 && threadIdx.x == 0) {
     d.state[ST_CUR0] = r0;
     d.state[ST_CUR0 + 1] = 0;
@@ -1362,7 +1404,10 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
   }
 }
 
-void launch_round_resume(const Dev &d, hipStream_t s) { k_round_resume<<<d.n, 256, 0, s>>>(d); }
+void launch_round_resume(const Dev &d, hipStream_t s) {
+  k_round_resume<<<d.n, 256, 0, s>>>(d);
+  if (d.fd_cols) launch_cand_rows(d, 1, s);
+}
 
 // A chain with no event in the segment has no last-row tile to write
 // "never seen" (MaxInt32) into the new rows of the other chains: done here
@@ -1397,7 +1442,7 @@ __global__ __launch_bounds__(256) void k_cand16_init(Dev d) {
 }
 
 void launch_round_init(const Dev &d, hipStream_t s) {
-  if (round2_eligible(d)) k_round2_init<<<d.n, 256, 0, s>>>(d);
+  if (round2_eligible(d)) launch_cand_rows(d, 0, s);
   else if (d.cand16 && !d.fd_rows) k_cand16_init<<<d.n, 256, 0, s>>>(d);
 }
 
@@ -1424,8 +1469,7 @@ void configure_round_kernels() {
 // batch -- ITER_FIRST, ITER_BATCH -- is even, so each starts at parity 0)
 void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   if (round2_eligible(d)) {
-    size_t lds = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
-    if (d.npad > 64 && d.round2_p8) lds = std::max(lds, (size_t)HW * (d.npad / 4) * 16 + (size_t)HW * 256);  // + the P8 window
+    const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;  // the staged window
     const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));  // (read per capture: the tests switch it)
     const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);  // 8 lanes per candidate
     if (rows_search) {

@@ -646,31 +646,57 @@ def test_small_n_round_kernels(monkeypatch, variant, n, N, seed, lag, K):
         _wild_parity(24, 30_000, 73, 20_000)
 
 
-@pytest.mark.parametrize("variant", ["bytes", "p32", "tight", "mixed", "rows"])
+@pytest.mark.parametrize("variant", ["tq", "rows", "eager"])
 @pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xB8, 0, 1), (100, 50_000, 0xB9, 4, 3),
                                             (97, 40_000, 0xBA, 0, 2), (72, 30_000, 0xBB, 3, 1)])
-def test_round2_byte_rows(monkeypatch, variant, n, N, seed, lag, K):
-    """k_round2 at 64 < npad <= 128 over byte rows relative to the shared
-    base B[r-1][i] - 20 (bytes: candidates' bytes written once by the
-    workgroup that hands them over, cand8 + c8tag), against the oracle; p32:
-    the 32-bit rows (the default); tight: a base 2 below B[r-1], so
-    many windows do not fit and their workgroups load the 32-bit rows after
-    staging; mixed: a lower spread limit (BH_ROUND_P8=40); rows: the
-    row-probe search (32-bit).  npad = 100 / 72 leave byte columns past npad
-    in the 16-B pieces; lagging peers, and segments whose first iteration
-    after a resume has no byte rows yet.  (The byte rows are opt-in,
-    BH_ROUND2_P8=1: at C3 they measured no faster than the 32-bit rows.)"""
-    if variant in ("bytes", "tight", "mixed"):
-        monkeypatch.setenv("BH_ROUND2_P8", "1")
-    if variant == "p32":
-        monkeypatch.setenv("BH_ROUND_P8G", "0")
-    if variant == "tight":
-        monkeypatch.setenv("BH_ROUND_P8G", "2")
-    if variant == "mixed":
-        monkeypatch.setenv("BH_ROUND_P8", "40")
+def test_round2_la_col(monkeypatch, variant, n, N, seed, lag, K):
+    """k_round2 at 64 < npad <= 128 reading only the column-major LA (round
+    4): the window staged from la_col 4-row pieces (npad = 100 / 72 leave
+    padding columns), the candidates' FD rows searched in la_col at each
+    hand-off, lagging peers (hand-offs whose FD entries jump past the 64
+    rows loaded), segments resumed at candidates searched from scratch;
+    rows: the row-probe search; eager: the segments also build the row-major
+    LA and FDT (BH_EAGER_ROWS=1, the round-3 pipeline)."""
     if variant == "rows":
         monkeypatch.setenv("BH_ROUND_ROWS", "1")
+    if variant == "eager":
+        monkeypatch.setenv("BH_EAGER_ROWS", "1")
     monkeypatch.setenv("BH_SEGMENTS", str(K))
     _random_parity(n, N, seed, lag)
     if n == 128 and K == 1:
         _wild_parity(128, 40_000, 0xBC, 35_000)
+
+
+@pytest.mark.parametrize("n,N,seed,lag,K", [(64, 40_000, 0xBD, 21, 4), (128, 60_000, 0xBE, 40, 3)])
+def test_lazy_rows_queries(monkeypatch, n, N, seed, lag, K):
+    """After a pipelined run that left only the column-major LA, the
+    coordinates (LA and FD of every event) and the pair predicates are built
+    on demand and equal the oracle's; the next incremental call still
+    resumes."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    d = Dag(n, N, seed, lagging=lag, sig_mode=0)
+    half = N // 2
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    rng = np.random.default_rng(seed)
+    for lo, hi in ((0, half), (half, N)):
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi], opi[lo:hi],
+                                    d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi]).any()
+        hg.run_consensus()
+        _compare(o, hg, f"lazy rows, events [0, {hi})")
+        for e in rng.integers(0, hi, 40).tolist():
+            la, fd = hg.coordinates(e)
+            ola, ofd = o.coordinates(e)
+            assert la.tolist() == ola.tolist() and fd.tolist() == ofd.tolist(), e
+        x, y = rng.integers(0, hi, 300), rng.integers(0, hi, 300)
+        got = hg.query("strongly_see", x, y)
+        assert [bool(v) for v in got] == [o.strongly_see(int(a), int(b)) for a, b in zip(x, y)]
+    assert hg.pipeline()[1] >= 1
