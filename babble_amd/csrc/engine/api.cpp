@@ -70,6 +70,9 @@ void free_all(bh_handle *h) {
   if (h->tlist) (void)hipFree(h->tlist);
   if (h->tlist_stage) (void)hipHostFree(h->tlist_stage);
   if (h->comm) (void)ncclCommDestroy(h->comm);
+  if (h->xbuf) (void)hipFree(h->xbuf);
+  if (h->xseg) (void)hipFree(h->xseg);
+  if (h->xbase) (void)hipFree(h->xbase);
 }
 
 // upload events inserted since the last upload
@@ -624,9 +627,179 @@ int segments_for(const Dev &d, int64_t events) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
 }
 
+// ---------------------------------------------------------------------------
+// the coordinate split (kernels_split.hip): shard 0 of
+// a group runs the round loop, fame and order and computes no coordinates;
+// shards 1 .. G-1 run the chain dataflow for a range of LA columns each
+// (rank 1 also the Lamport timestamps) and ship every segment's rows of
+// them to shard 0, packed as 16-bit offsets, over xGMI (peer copies in
+// process, ncclSend / ncclRecv across processes)
+
+// the LA columns of coordinate shard `rank` (>= 1) of a split group
+inline void split_cols(const bh_handle *h, int32_t rank, int64_t *c0, int64_t *c1) {
+  shard_range(h->d.n, h->world - 1, rank - 1, c0, c1);
+}
+
+// the split runs on the n <= 128 chain dataflow (k_flow32 + k_round2);
+// every shard decides it alike from its (identical) host tables
+bool split_active(const bh_handle *h) {
+  return h->split && !h->reset_on && h->d.N > 0 && bh::flow_eligible(h->d) && bh::flow32_eligible(h->d) &&
+         !(getenv("BH_SWEEP") && !strcmp(getenv("BH_SWEEP"), "chunk"));
+}
+
+// per-chain prefix lengths at an insertion-order boundary (ids of a chain
+// ascend with its index)
+void chain_lens_at(const bh_handle *h, int64_t bound, int32_t *out) {
+  for (int c = 0; c < h->d.n; ++c) {
+    const auto &ch = h->chain[(size_t)c];
+    out[c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)std::min<int64_t>(bound, INT32_MAX)) - ch.begin());
+  }
+}
+
+// one call's segments, alike on every shard: boundaries, each segment's
+// chain ranges [lo, hi) and packing tables P (rows before chain c) and Q
+// (64-row chunks before chain c), the blocks' sizes
+struct SplitPlan {
+  int K = 0;
+  int64_t base = 0;
+  std::vector<int64_t> Ns, S, NQ;
+  std::vector<int32_t> tab;  // [K][lo, hi][n], then [K][P, Q][n + 1]
+  const int32_t *dview(const bh_handle *h, int k) const { return h->xseg + (size_t)k * 2 * h->d.n; }
+  const int32_t *dpq(const bh_handle *h, int k) const {
+    return h->xseg + (size_t)K * 2 * h->d.n + (size_t)k * 2 * (h->d.n + 1);
+  }
+  size_t block_bytes(const bh_handle *h, int k, int32_t rank) const {
+    int64_t c0, c1;
+    split_cols(h, rank, &c0, &c1);
+    return bh::split_layout((int)(c1 - c0), S[(size_t)k], NQ[(size_t)k], rank == 1, nullptr, nullptr);
+  }
+  bh::SplitBlock block(const bh_handle *h, int k, int32_t rank, uint8_t *at) const {
+    int64_t c0, c1;
+    split_cols(h, rank, &c0, &c1);
+    bh::SplitBlock b;
+    bh::split_layout((int)(c1 - c0), S[(size_t)k], NQ[(size_t)k], rank == 1, &b, at);
+    b.c0 = (int32_t)c0;
+    const char *e = getenv("BH_SPLIT_RANGE");  // (read per block: the tests switch it)
+    b.range = e ? std::clamp(atoi(e), 0, 65535) : 65535;
+    return b;
+  }
+};
+
+SplitPlan split_plan(const bh_handle *h, int K, int64_t base) {
+  const int n = h->d.n;
+  const int64_t N = h->d.N;
+  SplitPlan p;
+  p.K = K;
+  p.base = base;
+  p.Ns.assign((size_t)K + 1, base);
+  for (int k = 1; k <= K; ++k) p.Ns[(size_t)k] = base + (N - base) * k / K;
+  p.tab.assign((size_t)K * 2 * n + (size_t)K * 2 * (n + 1), 0);
+  p.S.assign((size_t)K, 0);
+  p.NQ.assign((size_t)K, 0);
+  for (int k = 0; k < K; ++k) {
+    int32_t *lo = p.tab.data() + (size_t)k * 2 * n, *hi = lo + n;
+    chain_lens_at(h, p.Ns[(size_t)k], lo);
+    chain_lens_at(h, p.Ns[(size_t)k + 1], hi);
+    int32_t *P = p.tab.data() + (size_t)K * 2 * n + (size_t)k * 2 * (n + 1), *Q = P + n + 1;
+    P[0] = Q[0] = 0;
+    for (int c = 0; c < n; ++c) {
+      P[c + 1] = P[c] + (hi[c] - lo[c]);
+      Q[c + 1] = Q[c] + (hi[c] - lo[c] + 63) / 64;
+    }
+    p.S[(size_t)k] = P[n];
+    p.NQ[(size_t)k] = Q[n];
+  }
+  return p;
+}
+
+// the plan's tables on x's device (one upload), its segment events, and
+// `bytes` of block buffer
+int split_prepare(bh_handle *x, const SplitPlan &p, size_t bytes) {
+  if (p.K > x->xseg_k) {
+    if (x->xseg) (void)hipFree(x->xseg);
+    x->xseg = nullptr;
+    x->xseg_k = 0;
+    HIPCHK(x, hipMalloc((void **)&x->xseg, p.tab.size() * 4));
+    x->xseg_k = p.K;
+  }
+  HIPCHK(x, copy_sync(x->stream, x->xseg, p.tab.data(), p.tab.size() * 4, hipMemcpyHostToDevice));
+  if (bytes > x->xcap) {
+    HIPCHK(x, hipStreamSynchronize(x->stream2));
+    if (x->xbuf) (void)hipFree(x->xbuf);
+    x->xbuf = nullptr;
+    x->xcap = 0;
+    const size_t cap = bytes + bytes / 4;
+    HIPCHK(x, hipMalloc((void **)&x->xbuf, cap));
+    x->xcap = cap;
+  }
+  while ((int)x->seg_ev.size() < 4 * p.K) {
+    hipEvent_t e;
+    HIPCHK(x, hipEventCreate(&e));
+    x->seg_ev.push_back(e);
+  }
+  return BH_OK;
+}
+
+// a coordinate shard's part of the call, enqueued on its stream2: per
+// segment the descriptors, k_flow32 over its columns (+ LT on rank 1), the
+// packed block, then its send (ncclSend to rank 0, or an event rank 0's
+// peer copy waits for)
+int split_coords(bh_handle *x, const SplitPlan &p) {
+  Dev dv = x->d;
+  const int n = dv.n;
+  int64_t c0, c1;
+  split_cols(x, x->rank, &c0, &c1);
+  dv.col0 = (int32_t)c0;
+  dv.ncol = (int32_t)(c1 - c0);
+  dv.flow_lt = x->rank == 1;
+  size_t bytes = 0;
+  for (int k = 0; k < p.K; ++k) bytes += p.block_bytes(x, k, x->rank);
+  int rc;
+  if ((rc = split_prepare(x, p, bytes))) return rc;
+  hipStream_t sc = x->stream2;
+  x->segments_used = p.K;
+  if (p.base == 0) bh::launch_prep(dv, sc);
+  else bh::launch_chain_scatter(dv, p.base, sc);
+  HIPCHK(x, hipMemsetAsync(dv.state + bh::ST_FLOWOVF, 0, 4, sc));
+  size_t off = 0;
+  for (int k = 0; k < p.K; ++k) {
+    Dev v = dv;
+    v.seg_lo = const_cast<int32_t *>(p.dview(x, k));
+    v.chain_len = v.seg_lo + n;
+    v.N = p.Ns[(size_t)k + 1];
+    v.e0 = p.Ns[(size_t)k];
+    v.rows = x->layout_rows;
+    v.tile_list = nullptr;
+    bh::launch_flow_desc(v, sc);
+    if (dv.ncol > 0 || dv.flow_lt) bh::launch_flow(v, sc);
+    const bh::SplitBlock b = p.block(x, k, x->rank, x->xbuf + off);
+    bh::launch_split_pack(v, p.dpq(x, k), b, sc);
+    const size_t bb = p.block_bytes(x, k, x->rank);
+    if (x->comm) {
+      if (ncclSend(x->xbuf + off, bb, ncclChar, 0, x->comm, sc) != ncclSuccess)
+        return x->fail(BH_ERR_DEVICE, "ncclSend (segment %d)", k);
+    } else {
+      HIPCHK(x, hipEventRecord(x->seg_ev[(size_t)k], sc));
+    }
+    off += bb;
+  }
+  HIPCHK(x, hipGetLastError());
+  // bookkeeping alike on every shard (the next call's base is rank 0's anyway)
+  x->coords_for = (int)dv.N;
+  x->n_coord = dv.N;
+  x->lens_coord = x->lens_h;
+  x->inc_valid = true;
+  x->rows_stale = true;
+  x->sweep_kernel = "k_flow32";
+  return BH_OK;
+}
+
 // base > 0: an incremental call -- events [0, base) hold coordinates and
-// the round loop left its resume point (ST_RESUME) for that prefix
-int rounds_pipelined(bh_handle *h, int K, int64_t base) {
+// the round loop left its resume point (ST_RESUME) for that prefix.  sp: the
+// coordinate split -- shard 0's segments arrive from the coordinate shards
+// (grp: the in-process group, else over h->comm) instead of being computed
+int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nullptr,
+                     const std::vector<bh_handle *> *grp = nullptr) {
   int rc;
   Dev &d = h->d;  // the whole prefix: every segment's view derives from it
   const int n = d.n;
@@ -638,7 +811,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   // A Reset hashgraph's fiat pass and the resident loop (BH_ROUND_SOLO) read
   // them; BH_EAGER_ROWS=1 builds them anyway (A/B)
   static const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
-  const bool eager = wide || h->reset_on || eager_env || bh::round_solo_eligible(d);
+  const bool eager = !sp && (wide || h->reset_on || eager_env || bh::round_solo_eligible(d));
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
   h->fdt_lost = false;
@@ -680,16 +853,63 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
       out[c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)std::min<int64_t>(bound, INT32_MAX)) - ch.begin());
     }
   };
+  if (sp) {  // the plan's tables and the receive buffer (every segment's blocks)
+    size_t bytes = 0;
+    for (int k = 0; k < K; ++k)
+      for (int r = 1; r < h->world; ++r) bytes += sp->block_bytes(h, k, r);
+    if ((rc = split_prepare(h, *sp, bytes))) return rc;
+  }
   auto view = [&](int k) {  // segment k: events [Ns[k], Ns[k + 1])
     Dev v = d;
-    v.seg_lo = h->segbuf + (size_t)(k & 1) * 2 * n;
+    v.seg_lo = sp ? const_cast<int32_t *>(sp->dview(h, k)) : h->segbuf + (size_t)(k & 1) * 2 * n;
     v.chain_len = v.seg_lo + n;
     v.N = Ns[(size_t)k + 1];
     v.e0 = Ns[(size_t)k];
     v.rows = h->layout_rows;
     return v;
   };
+  size_t xoff = 0;  // the receive buffer's next block
+  auto receive = [&](int k) -> int {  // the split: segment k's columns from the coordinate shards
+    Dev v = view(k);
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sc));
+    if (grp) {  // peer copies (xGMI between devices, a device copy on a shared one)
+      for (int r = 1; r < h->world; ++r) HIPCHK(h, hipStreamWaitEvent(sc, (*grp)[(size_t)r]->seg_ev[(size_t)k], 0));
+    }
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
+    std::vector<bh::SplitBlock> blk((size_t)h->world);
+    if (grp) {
+      for (int r = 1; r < h->world; ++r) {
+        const bh_handle *x = (*grp)[(size_t)r];
+        size_t soff = 0;  // x's block of segment k in its send buffer
+        for (int j = 0; j < k; ++j) soff += sp->block_bytes(h, j, r);
+        const size_t bb = sp->block_bytes(h, k, r);
+        blk[(size_t)r] = sp->block(h, k, r, h->xbuf + xoff);
+        HIPCHK(h, hipMemcpyPeerAsync(h->xbuf + xoff, h->device, x->xbuf + soff, x->device, bb, sc));
+        xoff += bb;
+      }
+    } else {
+      if (ncclGroupStart() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupStart");
+      for (int r = 1; r < h->world; ++r) {
+        const size_t bb = sp->block_bytes(h, k, r);
+        blk[(size_t)r] = sp->block(h, k, r, h->xbuf + xoff);
+        if (ncclRecv(h->xbuf + xoff, bb, ncclChar, r, h->comm, sc) != ncclSuccess) {
+          (void)ncclGroupEnd();
+          return h->fail(BH_ERR_DEVICE, "ncclRecv (segment %d, rank %d)", k, r);
+        }
+        xoff += bb;
+      }
+      if (ncclGroupEnd() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupEnd");
+    }
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
+    for (int r = 1; r < h->world; ++r) bh::launch_split_unpack(v, sp->dpq(h, k), blk[(size_t)r], sc);
+    bh::launch_lt_rows(v, sc);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));
+    if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));
+    return BH_OK;
+  };
   auto coords = [&](int k) -> int {
+    if (sp) return receive(k);
     Dev v = view(k);
     int32_t *stg = h->seg_stage + (size_t)(k & 1) * 2 * n;
     lens_at(Ns[(size_t)k], stg);
@@ -748,8 +968,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   for (int k = 0; k < K; ++k) {
     HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * k], 0));
     if (serial) HIPCHK(h, hipStreamSynchronize(sr));
-    if (wide) {
-      // k_floww2's watchdog (ST_FLOWOVF = 2) is read before a loop runs on
+    if (wide || sp) {
+      // k_floww2's watchdog (ST_FLOWOVF = 2; the split: a block that ran out
+      // of overflow slots) is read before a loop runs on
       // the segment: a loop over unfinished coordinates could fail ("did not
       // terminate", capacity) before the fallback below is reached.  One
       // host synchronisation per segment; a wide batch runs one segment
@@ -820,10 +1041,11 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   if (lt0) (void)hipEventDestroy(lt0);
   if (lt1) (void)hipEventDestroy(lt1);
   (void)hipEventDestroy(sr_mark);
-  if (wide && (wd_fired || st[bh::ST_FLOWOVF] == 2)) {
-    // k_floww2's watchdog left a segment's coordinates unfinished: the whole
-    // DAG again through the unpipelined passes (they fall back to the
-    // chunked sweep)
+  if ((wide || sp) && (wd_fired || st[bh::ST_FLOWOVF] == 2)) {
+    // k_floww2's watchdog left a segment's coordinates unfinished (or a
+    // split block could not carry its columns): the whole DAG again through
+    // the unpipelined passes on this shard (they fall back to the chunked
+    // sweep)
     h->inc_valid = false;
     h->segments_used = 1;
     HIPCHK(h, hipStreamSynchronize(sc));
@@ -837,6 +1059,10 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base) {
   for (int k = 0; k < K; ++k)
     if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
   h->sweep_kernel = wide ? bh::floww_kernel(d) : "k_flow32";
+  if (sp) {  // the coordinate time is the coordinate shards'; the receive windows are the exchange
+    h->xchg_ms = h->sweep_ms;
+    h->sweep_ms = 0;
+  }
   if (h->reset_on && base > 0) h->fiat_max = h->pinned_state[bh::ST_COUNT + 2];
   if ((rc = rounds_tail(h, st, base))) return rc;
   h->n_coord = N;
@@ -881,10 +1107,85 @@ int rounds_segmented(bh_handle *h, bool *used) {
   return rounds_pipelined(h, h->reset_on ? 1 : segments_for(d, d.N - base), base);
 }
 
+// DivideRounds of a split group: this process's
+// shards -- the whole group in process, or this rank -- each in its role.
+// Rank 0 decides the call's base (its own resume state; broadcast across
+// processes), so every shard cuts the same segments.
+int rounds_split_stage(bh_handle *h) {
+  int rc;
+  std::vector<bh_handle *> sh = local_shards(h);
+  for (bh_handle *x : sh) {
+    HIPCHK(x, hipSetDevice(x->device));
+    x->d.N = (int64_t)x->h_creator.size();
+    x->xchg_ms = 0;
+    if ((rc = upload(x))) return rc;
+    if ((rc = set_chain_tables(x))) return rc;
+  }
+  (void)hipSetDevice(h->device);
+  bh_handle *h0 = sh[0]->rank == 0 ? sh[0] : nullptr;  // the loop shard, if this process drives it
+  const int64_t N = sh[0]->d.N;
+  int64_t base = 0;
+  if (h0) base = (!h0->layout_changed && h0->inc_valid && N >= h0->n_coord) ? h0->n_coord : 0;
+  if (h->comm) {  // across processes: rank 0's base
+    if (!h->xbase) HIPCHK(h, hipMalloc((void **)&h->xbase, 8));
+    int64_t *pin = reinterpret_cast<int64_t *>(h->pinned_state + bh::ST_COUNT + 6);  // (8-B aligned pinned words)
+    *pin = base;
+    HIPCHK(h, hipMemcpyAsync(h->xbase, pin, 8, hipMemcpyHostToDevice, h->stream));
+    if (ncclBroadcast(h->xbase, h->xbase, 1, ncclInt64, 0, h->comm, h->stream) != ncclSuccess)
+      return h->fail(BH_ERR_DEVICE, "ncclBroadcast (base)");
+    HIPCHK(h, copy_sync(h->stream, pin, h->xbase, 8, hipMemcpyDeviceToHost));
+    base = *pin;
+  }
+  if (!split_active(sh[0])) {
+    // n > 128, chains beyond k_flow32's limits, or nothing inserted: shard 0
+    // alone takes the unsplit path; the coordinate shards start over when
+    // the split applies again
+    for (bh_handle *x : sh)
+      if (x->rank > 0) x->inc_valid = false;
+    if (!h0) return BH_OK;
+    bool used = false;
+    if ((rc = rounds_segmented(h0, &used))) return rc;
+    if (used) return BH_OK;
+    if ((rc = rounds_coords(h0))) return rc;
+    return rounds_loop(h0);
+  }
+  if (base == N) {  // nothing new to divide
+    if (h0) h0->stage = std::max(h0->stage, 1);
+    return BH_OK;
+  }
+  const SplitPlan plan = split_plan(sh[0], segments_for(sh[0]->d, N - base), base);
+  // the coordinate shards' work first: shard 0's receive waits on it
+  for (bh_handle *x : sh) {
+    if (x->rank == 0) continue;
+    HIPCHK(x, hipSetDevice(x->device));
+    if ((rc = split_coords(x, plan))) {
+      if (x != h) h->err = "shard " + std::to_string(x->rank) + ": " + x->err;
+      (void)hipSetDevice(h->device);
+      return rc;
+    }
+  }
+  (void)hipSetDevice(h->device);
+  if (h0) {
+    h0->d.rows = h0->layout_rows;
+    h0->d.e0 = 0;
+    h0->d.seg_lo = h0->seg_zero;
+    h0->inc_calls += base > 0;
+    rc = rounds_pipelined(h0, plan.K, base, &plan, h->comm ? nullptr : &sh);
+  }
+  for (bh_handle *x : sh) {  // the sends / copies of this call are done
+    if (x->rank == 0) continue;
+    HIPCHK(x, hipSetDevice(x->device));
+    HIPCHK(x, hipStreamSynchronize(x->stream2));
+  }
+  (void)hipSetDevice(h->device);
+  return rc;
+}
+
 int stage_rounds(bh_handle *h) {
   int rc;
   h->xchg_ms = 0;
   for (bh_handle *x : local_shards(h)) x->loop_ms_acc = 0;
+  if (h->split) return rounds_split_stage(h);
   if (!h->shard_cols) {
     // every shard holds the whole DAG and computes the same coordinates and
     // rounds: each runs the segment pipeline on its own device (one host
@@ -919,12 +1220,22 @@ int stage_rounds(bh_handle *h) {
 // ---------------------------------------------------------------------------
 // stage 2: DecideFame -- this shard's rounds, then exchanged
 
+// the shards the passes after DivideRounds split between: every shard, or
+// with the coordinate split shard 0 alone (it holds the rounds)
+inline int32_t pass_world(const bh_handle *h) { return h->split ? 1 : h->world; }
+
+template <class F>
+int run_pass(bh_handle *h, F fn) {
+  if (!h->split) return run_local(h, fn);
+  return h->rank == 0 ? fn(h) : BH_OK;  // (in process, h is shard 0)
+}
+
 // only PendingRounds' rounds [P, R): a processed round's witnesses are
 // decided for good (or trapped), DecideFame never visits it again
 int fame_local(bh_handle *h) {
   if (h->stage < 1) return h->fail(BH_ERR_STATE, "DecideFame before DivideRounds");
   int64_t r0, r1;
-  shard_range(std::max(0, h->R - h->P), h->world, h->rank, &r0, &r1);
+  shard_range(std::max(0, h->R - h->P), pass_world(h), h->split ? 0 : h->rank, &r0, &r1);
   if (r1 > r0) bh::launch_fame(h->d, h->R, (int32_t)(h->P + r0), (int32_t)(h->P + r1), h->stream);
   HIPCHK(h, hipGetLastError());
   return BH_OK;
@@ -954,8 +1265,8 @@ int fame_finish(bh_handle *h) {
 
 int stage_fame(bh_handle *h) {
   int rc;
-  if ((rc = run_local(h, fame_local))) return rc;
-  if (h->world > 1) {
+  if ((rc = run_pass(h, fame_local))) return rc;
+  if (pass_world(h) > 1) {
     const int64_t R = h->R - h->P, P = h->P;
     const int npad = h->d.npad;
     struct {
@@ -974,7 +1285,7 @@ int stage_fame(bh_handle *h) {
         return rc;
     }
   }
-  return run_local(h, fame_finish);
+  return run_pass(h, fame_finish);
 }
 
 // ---------------------------------------------------------------------------
@@ -1006,7 +1317,7 @@ int stage_rr_local(bh_handle *h) {
   return BH_OK;
 }
 
-int stage_rr(bh_handle *h) { return run_local(h, stage_rr_local); }
+int stage_rr(bh_handle *h) { return run_pass(h, stage_rr_local); }
 
 // ---------------------------------------------------------------------------
 // stage 4: ProcessDecidedRounds -- frames sorted by range, then exchanged
@@ -1029,10 +1340,10 @@ int order_local(bh_handle *h) {
   // frames [P, P1): rounds this call processes (earlier frames are final)
   bh::launch_order_buckets(d, h->R, h->P, s);
   int64_t f0, f1;
-  shard_range(P1 - h->P, h->world, h->rank, &f0, &f1);
+  shard_range(P1 - h->P, pass_world(h), h->split ? 0 : h->rank, &f0, &f1);
   bh::launch_order_sort(d, (int32_t)(h->P + f0), (int32_t)(h->P + f1), s);
   HIPCHK(h, hipGetLastError());
-  if (h->world > 1) {  // frame offsets: the order exchange's ranges
+  if (pass_world(h) > 1) {  // frame offsets: the order exchange's ranges
     h->fofs_h.resize((size_t)P1 + 1);
     if (P1 > 0) HIPCHK(h, hipMemcpyAsync(h->fofs_h.data(), d.frame_ofs, (size_t)P1 * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(h->fofs_h.data() + P1, d.state + bh::ST_NCONS, 4, hipMemcpyDeviceToHost, s));
@@ -1045,7 +1356,7 @@ int order_finish(bh_handle *h) {
   Dev &d = h->d;
   hipStream_t s = h->stream;
   const int32_t P1 = next_prefix(h);
-  if (h->world > 1)  // frames sorted by other shards arrived
+  if (pass_world(h) > 1)  // frames sorted by other shards arrived
     bh::launch_cons_pos(d, h->fofs_h[(size_t)h->P], h->fofs_h[(size_t)P1], s);
   bh::launch_trap_processed(d, h->P, P1, s);
   HIPCHK(h, hipGetLastError());
@@ -1114,8 +1425,8 @@ int order_finish(bh_handle *h) {
 
 int stage_order(bh_handle *h) {
   int rc;
-  if ((rc = run_local(h, order_local))) return rc;
-  if (h->world > 1) {
+  if ((rc = run_pass(h, order_local))) return rc;
+  if (pass_world(h) > 1) {
     const int32_t P0 = h->P, F = next_prefix(h) - h->P;
     // order: frame f's sorted events at [frame_ofs[f], frame_ofs[f + 1])
     if ((rc = exchange(h, [](bh_handle *x) -> void * { return x->d.order; },
@@ -1128,7 +1439,7 @@ int stage_order(bh_handle *h) {
                        range_bytes(h, F, 4, false, nullptr, P0), range_bytes(h, F, 4, true, nullptr, P0))))
       return rc;
   }
-  return run_local(h, order_finish);
+  return run_pass(h, order_finish);
 }
 
 }  // namespace
@@ -1139,6 +1450,20 @@ extern "C" {
 static int create_one(const bh_config *cfg, int device, bh_handle **out);
 
 void bh_destroy(bh_handle *h);
+
+// How a group shares the coordinates (BH_SHARD_COORDS):
+//   split (2, the default where it applies: n <= 128) -- shard 0 runs the
+//     round loop, fame and order; the other shards compute LA columns and
+//     ship them to it per segment (kernels_split.hip);
+//   columns (1) -- every shard computes a range of LA columns, all-gathered;
+//   replicate (0, the default above n = 128) -- every shard computes all of
+//     it; fame rounds and frame sorts are split.
+static int shard_mode(int n) {
+  const char *e = getenv("BH_SHARD_COORDS");
+  if (e && !strcmp(e, "columns")) return 1;
+  if (e && !strcmp(e, "replicate")) return 0;
+  return n <= bh::FL_MAXN ? 2 : 0;
+}
 
 int bh_create(const bh_config *cfg, bh_handle **out) {
   if (!cfg || !out || cfg->n_participants < 1 || cfg->max_events < 0 || !cfg->participant_ids)
@@ -1156,19 +1481,15 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
       return rc;
     }
   }
-  // BH_SHARD_COORDS=columns splits the coordinate dataflow's LA columns
-  // between shards and all-gathers them; by default every shard runs the
-  // whole dataflow (it is bound by the DAG's critical path, not by its
-  // columns, so splitting saves no time and the gather costs (G-1)/G of LA)
-  const char *sc = getenv("BH_SHARD_COORDS");
-  const bool cols = sc && !strcmp(sc, "columns");
+  const int mode = shard_mode(cfg->n_participants);
   for (int r = 0; r < G; ++r) {
     bh_handle *x = g[(size_t)r];
     x->rank = r;
     x->world = G;
-    x->shard_cols = cols;
+    x->shard_cols = mode == 1;
+    x->split = mode == 2;
     int64_t c0 = 0, c1 = x->d.n;
-    if (cols) shard_range(x->d.n, G, r, &c0, &c1);
+    if (x->shard_cols) shard_range(x->d.n, G, r, &c0, &c1);
     x->d.col0 = (int32_t)c0;
     x->d.ncol = (int32_t)(c1 - c0);
     // peer access between the group's devices (xGMI); same-device pairs need none
@@ -1226,6 +1547,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.ring_log2 = n < 256 ? 14 : 12;  // sweep LDS: one workgroup per CU below 256 columns
   d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;
   d.flow_wd = getenv("BH_FLOWW_WATCHDOG") ? atoi(getenv("BH_FLOWW_WATCHDOG")) : (1 << 20);
+  d.flow_lt = 1;
   d.N = 0;
   d.col0 = 0;
   d.ncol = n;
@@ -1832,8 +2154,9 @@ int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id) {
   }
   h->rank = rank;
   h->world = world;
-  const char *sc = getenv("BH_SHARD_COORDS");  // see bh_create
-  h->shard_cols = sc && !strcmp(sc, "columns");
+  const int mode = world > 1 ? shard_mode(h->d.n) : 0;  // see bh_create
+  h->shard_cols = mode == 1;
+  h->split = mode == 2;
   int64_t c0 = 0, c1 = h->d.n;
   if (h->shard_cols) shard_range(h->d.n, world, rank, &c0, &c1);
   h->d.col0 = (int32_t)c0;

@@ -90,6 +90,7 @@ struct Dev {
   int64_t ntiles;
   int32_t *hdone;  // mapped pinned host word: set when the round loop is done
   int32_t flow_ltclamp;  // k_flow32 LT limit (2^21 - 256; BH_FLOW_LTCLAMP lowers it to test the fallback)
+  int32_t flow_lt;       // k_flow32 runs the LT workgroup beside its columns (0: a coordinate shard without it)
   int32_t flow_wd;       // k_floww / k_floww2 watchdog: stalled headers before it gives up (BH_FLOWW_WATCHDOG; -1 fires at once)
   uint8_t *depth, *chunk_maxd;
   int4 *desc;  // [N] packed sweep descriptors (kernels_coords.hip)
@@ -320,6 +321,25 @@ void launch_round_resume(const Dev &d, hipStream_t s);
 void launch_resume_point(const Dev &d, int32_t R, const int32_t *next_len, hipStream_t s);
 // FD entries of a segment's new rows for chains with no event in the segment
 void launch_fd_idle(const Dev &d, hipStream_t s);
+// the coordinate split's packed blocks (kernels_split.hip): one per
+// coordinate shard and segment
+constexpr int SPLIT_OV_CAP = 64;  // raw 64-row chunks per block (columns whose chunk spans > 65535)
+struct SplitBlock {
+  int64_t S = 0, NQ = 0;  // the segment's events; its 64-row chunks per column
+  int32_t c0 = 0, ncol = 0;
+  int32_t range = 65535;  // largest 16-bit offset (BH_SPLIT_RANGE lowers it to test the overflow slots)
+  bool lt_on = false;     // the block carries the segment's LT rows (the LT shard)
+  int32_t *hdr = nullptr;
+  uint16_t *pay = nullptr;
+  int32_t *ovf_count = nullptr, *err = nullptr;  // err[0]: overflow slots exhausted, err[1]: LT clamp (k_flow32)
+  int32_t *ovf = nullptr, *lt = nullptr;
+};
+// byte size of a block (and its pointers from `base` when b is given)
+size_t split_layout(int ncol, int64_t S, int64_t NQ, bool lt, SplitBlock *b, uint8_t *base);
+// pack (coordinate shard) / unpack (shard 0) the segment view v's rows; pq =
+// the segment's [P, Q][n + 1] tables on the device
+void launch_split_pack(const Dev &v, const int32_t *pq, const SplitBlock &b, hipStream_t s);
+void launch_split_unpack(const Dev &v, const int32_t *pq, const SplitBlock &b, hipStream_t s);
 // Lamport timestamps of the segment's events [e0, N) from the chain-major
 // LT rows (what the transpose does beside LA / FDT, for a segment whose
 // row-major LA and FDT are left unbuilt: n <= 128)

@@ -126,6 +126,16 @@ struct bh_handle {
   std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
   ncclComm_t comm = nullptr;       // multi-process group (bh_comm_init)
   bool shard_cols = false;         // split the coordinate dataflow's LA columns (else every shard computes all)
+  // the coordinate split (kernels_split.hip): shard 0
+  // runs the round loop, fame and order; shards 1 .. G-1 the dataflow for a
+  // range of LA columns each, shipped to shard 0 per segment
+  bool split = false;
+  uint8_t *xbuf = nullptr;        // coordinate shard: packed blocks of every segment; shard 0: received blocks
+  size_t xcap = 0;
+  int32_t *xseg = nullptr;        // [K][lo, hi][n] segment views, then [K][P, Q][n + 1] packing tables
+  int32_t xseg_k = 0;             // segments xseg has room for
+  hipEvent_t xev[2]{};            // shard 0: around a segment's receive (exchange time)
+  int32_t *xbase = nullptr;       // multi-process: rank 0's base for the call (broadcast)
   float xchg_ms = 0;               // exchange time of the last pass sequence (host wall, incl. waits)
   std::vector<int32_t> wofs_h;     // [R + 1] witness offsets (fame exchange ranges; launch size)
   std::vector<int32_t> fofs_h;     // [P + 1] frame offsets (order exchange ranges)

@@ -760,7 +760,7 @@ void launch_flow_desc(const Dev &d, hipStream_t s) {
 void launch_flow(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
-  if (flow32_eligible(d)) k_flow32<<<d.ncol + 1, (nw + 2) * 64, 0, s>>>(d);
+  if (flow32_eligible(d)) k_flow32<<<d.ncol + (d.flow_lt ? 1 : 0), (nw + 2) * 64, 0, s>>>(d);
   else k_flow<<<d.ncol + 1, (nw + 2) * 64, 0, s>>>(d, 0);
 }
 

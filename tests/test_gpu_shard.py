@@ -2,8 +2,11 @@
 in-process shard group on ONE device (device_ids = [0, 0] / [0, 0, 0]) runs
 exactly the split kernels and device-to-device exchanges a multi-GPU group
 runs over xGMI, and must match the single-shard engine -- and the oracle --
-bit for bit: LA columns (BH_SHARD_COORDS=columns) or replicated coordinates,
-fame by round ranges, frames sorted by range."""
+bit for bit: the coordinate split (the default at n <= 128: shard 0 runs the
+round loop, fame and order; the other shards compute LA columns and ship
+them per segment), LA columns all-gathered (BH_SHARD_COORDS=columns) or
+replicated coordinates with fame by round ranges and frames sorted by
+range (BH_SHARD_COORDS=replicate)."""
 import numpy as np
 import pytest
 
@@ -27,7 +30,7 @@ def _same_engine(a, b, where):
         assert getattr(sa, f) == getattr(sb, f), f"{where}: stats.{f}"
 
 
-@pytest.mark.parametrize("coords", ["replicate", "columns"])
+@pytest.mark.parametrize("coords", ["replicate", "columns", "split"])
 @pytest.mark.parametrize("n,N,seed,lag,devs", [
     (32, 40_000, 81, 0, [0, 0]),
     (64, 40_000, 82, 21, [0, 0, 0]),
@@ -121,3 +124,56 @@ def test_group_pipelined_incremental(monkeypatch, n, N, step):
         _compare(o, grp, f"group n={n} after [0, {hi})")
         assert grp.pipeline()[0] == 3
     assert grp.pipeline()[1] >= N // step - 2  # (a call whose chains outgrow their slack rows lays out anew)
+
+
+@pytest.mark.parametrize("devs,K", [([0, 0], 3), ([0, 0, 0, 0], 4), ([0, 0, 0], 1)])
+@pytest.mark.parametrize("n,N,seed,lag,step", [(128, 60_000, 91, 0, 20_000), (64, 50_000, 92, 21, 10_000),
+                                               (24, 40_000, 93, 3, 5_000)])
+def test_split_pipeline_incremental(monkeypatch, devs, K, n, N, seed, lag, step):
+    """The coordinate split through the segment pipeline and incremental
+    calls: 2 / 3 / 4 shards on one device, shard 0 receiving every segment's
+    packed LA columns (and rank 1's Lamport timestamps) from the coordinate
+    shards; the state equals the oracle's after every call, the calls after
+    the first resume, and the receive windows (the exchange) are timed."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    from test_gpu_schedule import _wire_batches
+    monkeypatch.setenv("BH_SHARD_COORDS", "split")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    d = Dag(n, N, seed, lagging=lag, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    grp = Hashgraph(d.participant_ids, N, devices=devs)
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not np.asarray(grp.insert_events(*batch(lo, hi))).any()
+        grp.run_consensus()
+        _compare(o, grp, f"split {len(devs)} shards n={n} after [0, {hi})")
+        assert grp.pipeline()[0] == K
+        assert grp.stage_ms()[5] > 0  # the receive windows
+    assert grp.pipeline()[1] >= N // step - 2
+
+
+@pytest.mark.parametrize("rng", [2, 60, 120, 250])
+def test_split_overflow_chunks(monkeypatch, rng):
+    """Chunks whose 64 rows span more than the 16-bit range travel raw in the
+    block's overflow slots (BH_SPLIT_RANGE lowers the range so gossip DAGs
+    have them); a block that runs out of slots sends the call to the unsplit
+    path on shard 0 -- either way the result is the oracle's."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_SHARD_COORDS", "split")
+    monkeypatch.setenv("BH_SEGMENTS", "3")
+    monkeypatch.setenv("BH_SPLIT_RANGE", str(rng))
+    n, N = 32, 30_000
+    d = Dag(n, N, 95, lagging=4, sig_mode=0)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    grp = Hashgraph(d.participant_ids, N, devices=[0, 0, 0])
+    assert not grp.insert_dag(d).any()
+    grp.run_consensus()
+    _compare(o, grp, f"split, range {rng}")
