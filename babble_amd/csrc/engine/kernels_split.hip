@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_split_unpack(Dev v, const int32_t *pq, 
     // unsplit, ST_FLOWOVF = 2 as a dataflow watchdog), LT beyond k_flow32's
     // range (the LT fallback, 1)
     if (b.err[0]) atomicMax(&v.state[ST_FLOWOVF], 2);
-    if (b.err[1]) atomicMax(&v.state[ST_FLOWOVF], b.err[1]);
+    if (b.err[1]) atomicMax(&v.state[ST_FLOWOVF], 1);
   }
   if (x >= b.S) return;
   const int c = split_chain(P, n, x);
@@ -160,7 +160,7 @@ size_t split_layout(int ncol, int64_t S, int64_t NQ, bool lt, SplitBlock *b, uin
 }
 
 void launch_split_pack(const Dev &v, const int32_t *pq, const SplitBlock &b, hipStream_t s) {
-  (void)hipMemsetAsync(b.ovf_count, 0, 8, s);  // (the flags travel even in an empty block)
+  (void)hipMemsetAsync(b.ovf_count, 0, 12, s);  // count, err[0], err[1] (the flags travel even in an empty block)
   if (b.S > 0 && b.ncol > 0) k_split_hdr<<<dim3((unsigned)((b.NQ + 255) / 256), (unsigned)b.ncol), 256, 0, s>>>(v, pq, b);
   const unsigned ny = (unsigned)(b.ncol + (b.lt_on ? 1 : 0));
   if (b.S > 0 && ny) k_split_pack<<<dim3((unsigned)((b.S + 255) / 256), ny), 256, 0, s>>>(v, pq, b);

@@ -5,13 +5,14 @@ A step = one pass of the hot path over the resident DAG: coordinates
 ProcessDecidedRounds (frame sort + blocks), all in libbabble_hip on one GPU.
 The DAG (generation, hashing, signing, H2D copy) is prepared before the timed
 region.  Workload: BASELINE.json's headline config C3 (128 participants,
-10M-event random-gossip DAG).  Multi-GPU: one process per GPU, each orders
-the same DAG as one shard of a group (strong scaling): DecideFame rounds
-and frame sorts are split between the ranks and exchanged with RCCL
-(ncclBroadcast per range, over xGMI); the coordinate dataflow and the
-round loop -- both serial latency chains -- run on every rank
-(BH_SHARD_COORDS=columns splits the LA columns and all-gathers them
-instead).  --mode replicas runs independent DAGs per rank (weak scaling).
+10M-event random-gossip DAG).  Multi-GPU: one process per GPU, the ranks
+order one DAG together (strong scaling).  By default (n <= 128) rank 0
+runs the round loop -- the serial chain of the path -- with fame and the
+order, and ranks 1..N-1 run the coordinate dataflow for ranges of LA
+columns, shipping every pipeline segment's columns to rank 0 (ncclSend /
+ncclRecv over xGMI, 16-bit packed); BH_SHARD_COORDS=replicate / columns
+select the round-3 splits.  --mode replicas runs independent DAGs per rank
+(weak scaling).
 
 usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--events N]
        torchrun ... bench.py --gpus N ...
@@ -61,6 +62,18 @@ def _pmc_table(n, N):
         return {}
     cfg = tab.get(f"n{n}_N{N}", {})
     return cfg if all("hbm_bytes_per_step" in v for v in cfg.values()) else {}
+
+
+def _parallelism(world, n):
+    """the engine's shard mode (BH_SHARD_COORDS; api.cpp shard_mode)"""
+    mode = os.environ.get("BH_SHARD_COORDS") or ("split" if n <= 128 else "replicate")
+    if mode == "split":
+        return (f"{world} shards (RCCL send/recv over xGMI): rank 0 runs the round loop, fame and order; "
+                f"ranks 1..{world - 1} run the coordinate dataflow over LA column ranges and ship every "
+                f"segment's columns to rank 0 (16-bit packed)")
+    if mode == "columns":
+        return f"{world} shards (RCCL broadcast): LA columns, fame rounds and frame sorts split, round loop replicated"
+    return f"{world} shards (RCCL broadcast): fame rounds + frame sorts split, coordinates and round loop replicated"
 
 
 def _cpu_model():
@@ -243,9 +256,7 @@ def main():
                                f"DivideRounds + DecideFame + DecideRoundReceived + ProcessDecidedRounds",
                    "participants": n, "events": N, "events_ordered_per_step": ordered,
                    "rounds": stats.last_round + 1, "blocks": stats.blocks,
-                   "parallelism": (f"{world} shards (RCCL): fame rounds + frame sorts split, coordinates "
-                                   f"{os.environ.get('BH_SHARD_COORDS', 'replicated') if os.environ.get('BH_SHARD_COORDS') == 'columns' else 'replicated'}"
-                                   f", round loop replicated") if sharded else
+                   "parallelism": _parallelism(world, n) if sharded else
                                   (f"replicas x{world}" if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_step,

@@ -152,7 +152,7 @@ def test_split_pipeline_incremental(monkeypatch, devs, K, n, N, seed, lag, step)
         assert not np.asarray(grp.insert_events(*batch(lo, hi))).any()
         grp.run_consensus()
         _compare(o, grp, f"split {len(devs)} shards n={n} after [0, {hi})")
-        assert grp.pipeline()[0] == K
+        assert 1 <= grp.pipeline()[0] <= K  # (segments_for: at most one per 4096 events)
         assert grp.stage_ms()[5] > 0  # the receive windows
     assert grp.pipeline()[1] >= N // step - 2
 
