@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.cla, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
                   d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
@@ -517,6 +517,7 @@ int rounds_loop(bh_handle *h) {
     return BH_OK;
   }
   int32_t st[bh::ST_COUNT];
+  d.use_cla = d.fd_cols && !bh::round_solo_eligible(d);
   if (h->reset_on) {
     // rounds below r0 event by event, then the loop from B[r0]
     HIPCHK(h, hipMemsetAsync(d.rexists, 0, (size_t)d.R_cap + 1, s));
@@ -811,7 +812,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // A Reset hashgraph's fiat pass and the resident loop (BH_ROUND_SOLO) read
   // them; BH_EAGER_ROWS=1 builds them anyway (A/B)
   static const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
-  const bool eager = !sp && (wide || h->reset_on || eager_env || bh::round_solo_eligible(d));
+  const bool eager = !sp && (wide || h->reset_on || eager_env || bh::round_solo_eligible(d) || d.round_src_rows);
+  d.use_cla = d.fd_cols && !bh::round_solo_eligible(d);
+  if (sp) d.round_src_rows = 0;  // the split ships the column-major LA only
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
   h->fdt_lost = false;
@@ -938,17 +941,31 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     } else {
       bh::launch_flow_desc(v, sc);
       HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
-      bh::launch_flow(v, sc);
+      // the LA columns only: n workgroups.  With the Lamport timestamps'
+      // workgroup beside them (n + 1 = 129 at n = 128) one compute unit of
+      // the 256 hosts a column workgroup and a round-loop workgroup at once,
+      // and every loop iteration waits for that slower one (C3: 10.8 against
+      // 9.7 us per iteration); LT, which the loop does not read, follows
+      // once the segment's columns are handed to the loop
+      Dev vc = v;
+      vc.flow_lt = 0;
+      bh::launch_flow(vc, sc);
     }
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
     if (eager) {
-      bh::launch_flow_transpose(v, sc);
+      bh::launch_flow_transpose(v, sc);  // (its LT copy is redone by k_lt_rows below)
       bh::launch_fd_idle(v, sc);
-    } else {
-      bh::launch_lt_rows(v, sc);
     }
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));  // the segment's LA is ready for the loop
+    if (!wide) {  // the segment's Lamport timestamps: one workgroup, beside the loop
+      Dev vl = v;
+      vl.ncol = 0;
+      vl.flow_lt = 1;
+      bh::launch_flow(vl, sc);
+      bh::launch_lt_rows(v, sc);
+      HIPCHK(h, hipGetLastError());
+    }
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));  // the coordinate pipeline's end
     return BH_OK;
   };
@@ -1416,6 +1433,7 @@ int order_finish(bh_handle *h) {
       const double nc = (double)(g[14] ? g[14] : 1);
       fprintf(stderr, "[bh diag] k_round: calls %llu, avg total %.0f cyc: loads %.0f, (unused) %.0f, search %.0f\n",
               g[14], g[13] / nc, g[10] / nc, g[11] / nc, g[12] / nc);
+      fprintf(stderr, "[bh diag] k_round2: hand-off waves past the 64 rows %llu, windows without SM %llu\n", g[21], g[22]);
     }
     (void)hipMemsetAsync(d.diag, 0, bh::DG_COUNT * 8, h->stream);
   }
@@ -1548,6 +1566,8 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;
   d.flow_wd = getenv("BH_FLOWW_WATCHDOG") ? atoi(getenv("BH_FLOWW_WATCHDOG")) : (1 << 20);
   d.flow_lt = 1;
+  d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
+  d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
   d.ncol = n;
@@ -1590,6 +1610,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.rspan = (int32_t)R1;
   if (d.fd_cols) {
     A(&d.ssm, R1 * n * 16);
+    A(&d.cla, R1 * n * d.npad);
     d.round_lpc = 8;  // k_round2: 8 lanes per candidate at every n <= 128
   } else {
     // chain-major 32-bit FD rows (fd) are allocated on first use (ensure_fd):
@@ -1632,10 +1653,20 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
      // the critical path while the coordinate pipeline streams beside it
     int lo_pri = 0, hi_pri = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
-    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi_pri) != hipSuccess)
-      rc = BH_ERR_DEVICE;
-    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
-      rc = BH_ERR_DEVICE;
+    // BH_CU_SPLIT=k (A/B): the loop's stream on CUs [0, k) and the
+    // coordinate stream on the others (hipExtStreamCreateWithCUMask)
+    const int cus = getenv("BH_CU_SPLIT") ? atoi(getenv("BH_CU_SPLIT")) : 0;
+    if (cus > 0) {
+      uint32_t m0[8] = {0}, m1[8] = {0};
+      for (int i = 0; i < 256; ++i) (i < cus ? m0 : m1)[i / 32] |= 1u << (i % 32);
+      if (rc == BH_OK && hipExtStreamCreateWithCUMask(&h->stream, 8, m0) != hipSuccess) rc = BH_ERR_DEVICE;
+      if (rc == BH_OK && hipExtStreamCreateWithCUMask(&h->stream2, 8, m1) != hipSuccess) rc = BH_ERR_DEVICE;
+    } else {
+      if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi_pri) != hipSuccess)
+        rc = BH_ERR_DEVICE;
+      if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
+        rc = BH_ERR_DEVICE;
+    }
   }
   if (rc == BH_OK) rc = dalloc(h, &h->seg_zero, (size_t)n);
   if (rc == BH_OK) rc = dalloc(h, &h->segbuf, (size_t)4 * n);
@@ -1900,6 +1931,7 @@ int bh_reset_consensus(bh_handle *h) {
 // pointer of it.
 struct RoundTables {
   unsigned long long *ssm = nullptr, *ssw = nullptr;
+  int32_t *cla = nullptr;
   int32_t *B = nullptr, *wofs = nullptr, *wcnt = nullptr, *blocked = nullptr, *frame_loaded = nullptr, *nfam = nullptr,
           *minla = nullptr, *frame_cnt = nullptr, *frame_ofs = nullptr, *frame_cur = nullptr, *blk_of_frame = nullptr;
   int8_t *decided = nullptr, *rexists = nullptr;
@@ -1912,6 +1944,7 @@ struct RoundTables {
   void free_all() {
     for (int i = 0; i < 16; ++i)
       if (void *p = all(i)) (void)hipFree(p);
+    if (cla) (void)hipFree(cla);
     *this = RoundTables{};
   }
 };
@@ -1925,6 +1958,7 @@ static int alloc_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int32
     if (rc == BH_OK && hipMemset(*p, 0, std::max<size_t>(cnt, 1) * sizeof(**p)) != hipSuccess) rc = BH_ERR_DEVICE;
   };
   if (ssm) A(&t.ssm, span * n * 16);
+  if (ssm) A(&t.cla, span * n * h->d.npad);
   if (ssw) A(&t.ssw, span * n * 8);
   A(&t.B, R1 * n); A(&t.wofs, R1); A(&t.wcnt, R1); A(&t.blocked, R1); A(&t.frame_loaded, R1);
   A(&t.decided, R1); A(&t.nfam, R1); A(&t.minla, R1 * h->d.npad); A(&t.frame_cnt, R1);
@@ -1941,10 +1975,10 @@ static int alloc_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int32
 static void commit_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int32_t rbase) {
   Dev &d = h->d;
   void *old[] = {d.ssm, d.ssw, d.B, d.wofs, d.wcnt, d.blocked, d.frame_loaded, d.nfam, d.minla, d.frame_cnt,
-                 d.frame_ofs, d.frame_cur, d.blk_of_frame, d.decided, d.rexists, d.frame_ntx};
+                 d.frame_ofs, d.frame_cur, d.blk_of_frame, d.decided, d.rexists, d.frame_ntx, d.cla};
   for (void *p : old)
     if (p) (void)hipFree(p);
-  d.ssm = t.ssm; d.ssw = t.ssw; d.B = t.B; d.wofs = t.wofs; d.wcnt = t.wcnt; d.blocked = t.blocked;
+  d.ssm = t.ssm; d.ssw = t.ssw; d.cla = t.cla; d.B = t.B; d.wofs = t.wofs; d.wcnt = t.wcnt; d.blocked = t.blocked;
   d.frame_loaded = t.frame_loaded; d.nfam = t.nfam; d.minla = t.minla; d.frame_cnt = t.frame_cnt;
   d.frame_ofs = t.frame_ofs; d.frame_cur = t.frame_cur; d.blk_of_frame = t.blk_of_frame; d.decided = t.decided;
   d.rexists = t.rexists; d.frame_ntx = t.frame_ntx;

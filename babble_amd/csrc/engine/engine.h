@@ -120,6 +120,14 @@ struct Dev {
   // starts from (0, or a Reset hashgraph's r0), so a Reset at a high round
   // does not pay for the rounds below it
   unsigned long long *ssm;
+  // k_round2 path: the LA row of each candidate (c, B[r][c]) at row
+  // ballot_row(d, c, r), npad wide, stored by the workgroup that finds it
+  // (from its LDS window) -- fame's first votes and minLA read witnesses'
+  // rows here, whole and coalesced, instead of n scattered column reads
+  int32_t *cla;
+  int32_t use_cla;  // the loop that ran wrote cla (k_round2; not the resident k_round_solo)
+  int32_t round_src_rows;  // k_round2r: windows from the row-major LA, hand-off from FDT (BH_ROUND_SRC=rows, A/B)
+  int32_t round_prio;  // k_round2's wave priority (s_setprio) against co-resident coordinate waves (BH_ROUND_PRIO)
   int32_t rbase, rspan;
   int32_t round_lpc;  // lanes per candidate of k_round2 (8), the layout of its ssm ballots
   int32_t round_p8;   // k_round_wide<*, true>: 8-bit window-relative rows where the window's LA spread is at most this
@@ -274,6 +282,7 @@ enum DiagSlot {
   DG_SW_MEM_PREF, DG_SW_MEM_STORE, DG_SW_MEM_IDLE,
   DG_RD_B = 10, DG_RD_LOAD, DG_RD_COMP, DG_RD_TOTAL, DG_RD_CALLS,
   DG_FL_STEPS = 16, DG_FL_CYC, DG_FL_ADV, DG_FL_FAR, DG_FL_WAITD,
+  DG_RD_HMISS = 21, DG_RD_WMISS,  // k_round2: waves whose hand-off searched past its 64 rows; windows without SM
   DG_TL = 32,  // k_round2 timeline: rounds TL_R0 .. TL_R0+TL_NR, [r][c][4] realtime stamps
   DG_COUNT = 32 + 64 * 128 * 4
 };

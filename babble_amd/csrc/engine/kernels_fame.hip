@@ -272,7 +272,9 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
       const int32_t b0 = d.B[(int64_t)r * n + q];
       if (b0 < d.chain_len[q]) L.xev[q] = d.chain_ids[d.chain_start[q] + b0];
       L.xk[q] = b0;
-      if (r + 1 < R) L.yev[q] = d.chain_start[q] + min(d.B[(int64_t)(r + 1) * n + q], d.chain_len[q] - 1);
+      if (r + 1 < R)
+        L.yev[q] = d.use_cla ? (int32_t)ballot_row(d, q, r + 1)
+                             : d.chain_start[q] + min(d.B[(int64_t)(r + 1) * n + q], d.chain_len[q] - 1);
     }
   }
   __syncthreads();
@@ -296,7 +298,8 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
         for (int b = 0; b < 32; ++b) {
           const int y = h * HY + k * 32 + b;
           if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
-          if (la_at(d, L.yev[y], xc) >= L.xk[xc]) v |= 1u << b;
+          const int32_t a = d.use_cla ? d.cla[(int64_t)L.yev[y] * npad + xc] : la_at(d, L.yev[y], xc);
+          if (a >= L.xk[xc]) v |= 1u << b;
         }
         L.V[0][h * HW_ + k][x] = v;
       }
@@ -375,7 +378,8 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
     if (L.misc[1]) d.state[ST_ERR] = 2;
     int m = 0;
     for (int q = 0; q < n; ++q)
-      if (((L.wx[q >> 5] >> (q & 31)) & 1u) && L.dec[q] == 1) L.frow[m++] = d.chain_start[q] + d.B[(int64_t)r * n + q];
+      if (((L.wx[q >> 5] >> (q & 31)) & 1u) && L.dec[q] == 1)
+        L.frow[m++] = d.use_cla ? (int32_t)ballot_row(d, q, r) : d.chain_start[q] + d.B[(int64_t)r * n + q];
     L.nfam_s = m;
   }
   __syncthreads();
@@ -383,7 +387,10 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   const int nf = L.nfam_s;
   for (int c = t; c < npad; c += nt) {
     int32_t m = INT32_MAX;
-    for (int i = 0; i < nf; ++i) m = min(m, c < n ? la_at(d, L.frow[i], c) : -1);
+    if (d.use_cla)
+      for (int i = 0; i < nf; ++i) m = min(m, d.cla[(int64_t)L.frow[i] * npad + c]);
+    else
+      for (int i = 0; i < nf; ++i) m = min(m, c < n ? la_at(d, L.frow[i], c) : -1);
     d.minla[(int64_t)r * npad + c] = m;
     if (c == 0) d.nfam[r] = nf;
   }

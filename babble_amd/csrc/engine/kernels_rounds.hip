@@ -801,9 +801,13 @@ __device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, in
 // workgroup per candidate chain c, a 16-lane group per chain i
 __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
   const int c = blockIdx.x, t = threadIdx.x;
-  const int32_t b = from_resume ? d.B[(int64_t)d.state[ST_RESUME] * d.n + c] : 0;
+  const int32_t r = from_resume ? d.state[ST_RESUME] : 0;
+  const int32_t b = from_resume ? d.B[(int64_t)r * d.n + c] : 0;
   if (t == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
   if (b >= d.chain_len[c]) return;  // no candidate on chain c
+  if (d.cla && t < d.npad)  // the candidate's LA row (fame)
+    d.cla[ballot_row(d, c, r) * d.npad + t] =
+        t < d.n ? d.la_col[(int64_t)t * la_col_stride(d) + d.chain_start[c] + b] : -1;
   const int32_t *colc = d.la_col + (int64_t)c * la_col_stride(d);
   int32_t *cf = d.candfd + (int64_t)c * d.npad;
   for (int i0 = 0; i0 < d.npad; i0 += blockDim.x >> 4) {  // (uniform trip count)
@@ -860,6 +864,15 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x;
+  // a loop workgroup placed on a compute unit beside a k_flow32 workgroup
+  // (the segment pipeline: 129 + 128 workgroups on 256 CUs) loses VALU
+  // arbitration to those older waves; a higher priority takes it back
+  switch (d.round_prio) {
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: break;
+  }
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int rs4 = q4 + 1, rs = 4 * rs4;  // window row stride (one spare piece: staging stores spread over banks)
   const int64_t stride = la_col_stride(d);
@@ -1026,11 +1039,14 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const unsigned long long ts2 = dg ? stamp() : 0;
   const unsigned long long rt2 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
   int32_t result = len;
+  int lrow = 0;  // the LDS window row holding the result's LA row
   if (res >= 0) {
     result = k0 + res;
+    lrow = off + res;
   } else if (nc > 0 && rows == HW) {
     // SM not reached in the window (rare): the next windows of chain c,
     // staged the same way (slot counters are reused per row tested)
+    if (d.diag && t == 0) atomicAdd(&d.diag[DG_RD_WMISS], 1ull);
     for (int32_t wk = k0 + HW; wk < len && result == len; wk += HW) {
       const int wr = min(HW, len - wk);
       const int64_t rb2 = (int64_t)(cs + wk) & ~(int64_t)3;
@@ -1064,6 +1080,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
         }
       }
       result = wk + lo;
+      lrow = (int)(cs + wk - rb2) + lo;
     }
     __syncthreads();
   }
@@ -1101,11 +1118,246 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (__any(miss[u])) {  // (rare) the entry lies beyond the 64 rows loaded
+        if (d.diag && lane == 0) atomicAdd(&d.diag[DG_RD_HMISS], 1ull);
         const int32_t jm = first_ge16(colc + hcs[u], mlo[u], hlen[u], result, miss[u], true);
         if (miss[u]) fdv[u] = jm < hlen[u] ? jm : FD_NONE;
       }
       const int j = t + u * nt;
       if ((j & 15) == 0 && (j >> 4) < npad) cf[j >> 4] = fdv[u];
+    }
+    // fame's inputs for the new candidate y = (c, result): its LA row (from
+    // the window in LDS) and SS(y, q) over the candidates q of round r = the
+    // ballots of the probe that verified y's row.  Raw ballots, one aligned
+    // 8-B word per wave (candidate q at bit 8 (q % 8) of word q / 8; fame
+    // packs the LPC-strided bits and masks the words of chains >= n, which
+    // fewer waves leave unwritten), chain-major [c][round]; issued last,
+    // since a later vmcnt wait would include them
+    if (t < npad) d.cla[ballot_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
+    if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
+  }
+  if (dg) {
+    const unsigned long long te = stamp();
+    if (r >= TL_R0 && r < TL_R0 + TL_NR && c < 128) {
+      unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
+      const unsigned long long fl = (unsigned long long)(min(result - k0, 255) & 255) |
+                                    (unsigned long long)(res < 0) << 8 | (unsigned long long)(nc > 0) << 9;
+      tl[0] = rt0 | fl << 52; tl[1] = rt2; tl[2] = rt1; tl[3] = __builtin_amdgcn_s_memrealtime();
+    } else if (r < TL_R0 - 64 || r >= TL_R0 + TL_NR + 64) {
+      // phase counters (device-scope atomics from every workgroup: they
+      // stretch the round by several us, so none near the timeline window)
+      atomicAdd(&d.diag[DG_RD_B], ts1 - ts0);
+      atomicAdd(&d.diag[DG_RD_LOAD], 0ull);
+      atomicAdd(&d.diag[DG_RD_COMP], ts2 - ts1);
+      atomicAdd(&d.diag[DG_RD_TOTAL], te - ts0);
+      atomicAdd(&d.diag[DG_RD_CALLS], 1ull);
+    }
+  }
+  if (t == 0) {
+    if (nc == 0) {  // no candidates: R = r
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
+      return;
+    }
+    if (r + 1 >= d.R_cap) {
+      if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
+      return;
+    }
+    d.Bp[(int64_t)(p ^ 1) * n + c] = result;
+    d.B[(int64_t)(r + 1) * n + c] = result;
+    if (c == 0) {
+      d.state[ST_CUR0 + (p ^ 1)] = r + 1;
+      d.state[ST_ITERS] = r + 1;
+    }
+  }
+}
+
+// k_round2r (BH_ROUND_SRC=rows, A/B): the round-3 iteration, reading its
+// window from the row-major LA and its hand-off from the FDT tiles that the
+// segments' transpose builds (eager rows); k_round2 reads only la_col
+template <int PPL, bool TQ>
+__global__ __launch_bounds__(1024) void k_round2r(Dev d, int p) {
+  constexpr int LPC = 8;
+  extern __shared__ __attribute__((aligned(16))) int4 sm4[];
+  __shared__ int32_t cntk[16];
+  __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int c = blockIdx.x;
+  const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
+  int4 *win = sm4;              // [HW][q4]: LA rows k0 .. k0 + 31
+  // [npad][FDS]: FD rows rb .. rb + 31 by column, for the hand-off after the
+  // search -- the window's space (every read of it is behind the search's
+  // last barrier), so the workgroup's LDS (18 KiB at n = 128) fits beside a
+  // k_flow32 workgroup (133 KiB) on one compute unit: the segment pipeline
+  // runs both at once
+  int32_t *fdw = reinterpret_cast<int32_t *>(sm4);
+  constexpr int FDS = HW + 4;
+  const int32_t *Bp = d.Bp + (int64_t)p * n;
+  const bool dg = d.diag != nullptr && t == 0;
+  const unsigned long long ts0 = dg ? stamp() : 0;
+  const unsigned long long rt0 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
+  // ---- independent loads ----
+  const int done = d.state[ST_DONE];
+  const int r = d.state[ST_CUR0 + p];
+  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  const int32_t k0 = Bp[c];
+  const int q = t / LPC, part = t % LPC;
+  const int rot = TQ ? (q & (PPL - 1)) : 0;  // piece order of this group (bank spread)
+  int32_t bq = 0, lq = 0;
+  if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; }
+  int4 f[PPL];
+  {
+    const int4 *cf = reinterpret_cast<const int4 *>(d.candfd) + ((int64_t)p * n + min(q, n - 1)) * q4;
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) {
+      const int pc = part + LPC * ((u + rot) & (PPL - 1));
+      f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+    }
+  }
+  const int rows = min(HW, max(0, len - k0));
+  const int4 wv = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + k0) * q4 + min(t, max(rows * q4 - 1, 0))];
+  if (done) return;
+  const bool act = q < n && bq < lq;
+  // ---- loads for the hand-off (consumed after the search) ----
+  // FD rows rb .. rb + 31 (rb = the window's first row rounded down to 4)
+  // from the FDT tiles: 16 B = 4 rows of one column per thread, 8 threads
+  // per column
+  const int64_t rb = (int64_t)(cs + k0) & ~(int64_t)3;
+  const int fi = min(t >> 3, n - 1), fp = (t & 7) * 4;
+  const int4 fv = *reinterpret_cast<const int4 *>(d.fdt + fdt_pos(rb + fp, fi, npad));
+  if (t < rows * q4) win[t] = wv;
+  if (t < 16) cntk[t] = 0;
+  if (TQ && t <= HW) hist[t] = 0;
+  __syncthreads();
+  const unsigned long long ts1 = dg ? stamp() : 0;
+  const unsigned long long rt1 = dg ? __builtin_amdgcn_s_memrealtime() : 0;  // loads landed
+  // count(row) into slot: groups whose candidate `row` strongly sees
+  // does window row x4 strongly see this group's candidate?
+  auto ss_row = [&](const int4 *x4) {
+    int4 x[PPL];  // all reads first: one LDS round trip per probe
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * ((u + rot) & (PPL - 1)), q4 - 1)];
+    int lt = 0;
+#pragma unroll
+    for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
+    return LPC * PPL * 4 - group_sum<LPC>(lt) >= sm;
+  };
+  auto probe = [&](const int4 *x4, int slot) {
+    const bool s = ss_row(x4);
+    const unsigned long long m = __ballot(act && part == 0 && s);
+    if (lane == 0 && m) atomicAdd(&cntk[slot], __popcll(m));
+    return m;  // this wave's candidates the row strongly sees (fame's S_j)
+  };
+  {
+    const unsigned long long m = __ballot(act && part == 0);
+    if (lane == 0 && m) atomicAdd(&cntk[0], __popcll(m));
+  }
+  int slot = 1;
+  int32_t res = -1;  // window row of B[r+1][c], or -1
+  unsigned long long ssb = 0;  // this wave's ballot of the probe that verified the answer row
+  if (TQ && rows > 0) {
+    // T_q by a per-group binary search over [0, rows] (rows = none in the window)
+    int lo = 0, hi = rows;
+    while (__any(lo < hi)) {
+      const int mid = (lo + hi) >> 1;
+      const bool s = ss_row(win + min(mid, rows - 1) * q4);
+      if (lo < hi) {
+        hi = s ? mid : hi;
+        lo = s ? lo : mid + 1;
+      }
+    }
+    if (act && part == 0 && lo < rows) atomicAdd(&hist[lo], 1);
+    __syncthreads();
+    if (wave == 0) {
+      int h = lane < rows ? hist[lane] : 0;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(h, off);
+        h += lane >= off ? o : 0;
+      }
+      const unsigned long long hit = __ballot(lane < rows && h >= sm);
+      if (lane == 0) hist[HW] = hit ? (int)__builtin_ctzll(hit) : -1;
+    }
+    __syncthreads();
+    res = hist[HW];
+    // fame's S_j for the new candidate: the candidates whose T_q is at most its row
+    ssb = __ballot(act && part == 0 && res >= 0 && lo <= res);
+  } else if (rows > 0) {
+    // binary search assuming the window's last row reaches SM (count is
+    // monotone); that row is probed only if the search ends on it unverified
+    int lo = 0, hi = rows - 1;
+    bool hi_ok = false;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const unsigned long long m = probe(win + mid * q4, slot);
+      __syncthreads();
+      if (cntk[slot] >= sm) {
+        hi = mid;
+        hi_ok = true;
+        ssb = m;
+      } else {
+        lo = mid + 1;
+      }
+      ++slot;
+    }
+    if (!hi_ok) {
+      ssb = probe(win + hi * q4, slot);
+      __syncthreads();
+      hi_ok = cntk[slot] >= sm;
+    }
+    if (hi_ok) res = lo;
+  } else {
+    __syncthreads();
+  }
+  const int nc = cntk[0];
+  const unsigned long long ts2 = dg ? stamp() : 0;
+  const unsigned long long rt2 = dg ? __builtin_amdgcn_s_memrealtime() : 0;
+  int32_t result = len;
+  if (res >= 0) {
+    result = k0 + res;
+  } else if (nc > 0 && rows == HW) {
+    // SM not reached in the handed-over window (rare): later windows of
+    // chain c, loaded directly (slot counters are reused per row tested)
+    int4 *x4 = win;  // rows in LDS: row i of the current window at x4[i * q4]
+    for (int32_t wk = k0 + HW; wk < len && result == len; wk += HW) {
+      const int wr = min(HW, len - wk);
+      __syncthreads();
+      for (int i = t; i < wr * q4; i += blockDim.x)
+        x4[i] = reinterpret_cast<const int4 *>(d.la)[(int64_t)(cs + wk) * q4 + i];
+      if (t < 16) cntk[t] = 0;
+      __syncthreads();
+      const unsigned long long ml = probe(x4 + (wr - 1) * q4, 1);
+      __syncthreads();
+      if (cntk[1] < sm) continue;
+      int lo = 0, hi = wr - 1, sl = 1;
+      ssb = ml;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        ++sl;
+        const unsigned long long m = probe(x4 + mid * q4, sl);
+        __syncthreads();
+        if (cntk[sl] >= sm) {
+          hi = mid;
+          ssb = m;
+        } else {
+          lo = mid + 1;
+        }
+      }
+      result = wk + lo;
+    }
+    __syncthreads();
+  }
+  // ---- hand-off for the next iteration ----
+  if (nc > 0 && r + 1 < d.R_cap && result < len) {
+    const int32_t off = result - k0;
+    int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
+    const int frel = (int)(cs + result - rb);  // row of the candidate in fdw
+    // the candidate's LA row for fame (cla), before fdw overwrites the window
+    if (t < npad) d.cla[ballot_row(d, c, r + 1) * npad + t] = d.la[(int64_t)(cs + result) * npad + t];
+    if (off < HW && frel < HW) {  // both from the rows staged during the search
+      if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
+      __syncthreads();
+      if (t < npad) cf[t] = t < n ? fdw[t * FDS + frel] : FD_NONE;
+    } else {
+      if (t < npad) cf[t] = t < n ? d.fdt[fdt_pos(cs + result, t, npad)] : FD_NONE;
     }
     // fame's input for the new candidate y = (c, result): SS(y, q) over
     // the candidates q of round r = the ballots of the probe that verified
@@ -1461,6 +1713,7 @@ void configure_round_kernels() {
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
+  CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
   CFG(k_round_solo);
 #undef CFG
 }
@@ -1472,7 +1725,12 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
     const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;  // the staged window
     const bool rows_search = getenv("BH_ROUND_ROWS") && atoi(getenv("BH_ROUND_ROWS"));  // (read per capture: the tests switch it)
     const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);  // 8 lanes per candidate
-    if (rows_search) {
+    if (d.round_src_rows) {
+      const size_t lds2 = std::max((size_t)HW * (d.npad / 4) * 16, (size_t)d.npad * (HW + 4) * 4);
+      if (d.npad <= 32) k_round2r<1, true><<<d.n, nt, lds2, s>>>(d, p);
+      else if (d.npad <= 64) k_round2r<2, true><<<d.n, nt, lds2, s>>>(d, p);
+      else k_round2r<4, true><<<d.n, nt, lds2, s>>>(d, p);
+    } else if (rows_search) {
       if (d.npad <= 32) k_round2<1, false><<<d.n, nt, lds, s>>>(d, p);
       else if (d.npad <= 64) k_round2<2, false><<<d.n, nt, lds, s>>>(d, p);
       else k_round2<4, false><<<d.n, nt, lds, s>>>(d, p);
