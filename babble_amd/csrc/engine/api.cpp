@@ -911,6 +911,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));
     return BH_OK;
   };
+  static const bool lt_combined = getenv("BH_LT_COMBINED") && atoi(getenv("BH_LT_COMBINED"));  // (A/B: LT beside the columns)
   auto coords = [&](int k) -> int {
     if (sp) return receive(k);
     Dev v = view(k);
@@ -948,7 +949,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       // 9.7 us per iteration); LT, which the loop does not read, follows
       // once the segment's columns are handed to the loop
       Dev vc = v;
-      vc.flow_lt = 0;
+      vc.flow_lt = lt_combined ? 1 : 0;
       bh::launch_flow(vc, sc);
     }
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
@@ -958,7 +959,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));  // the segment's LA is ready for the loop
-    if (!wide) {  // the segment's Lamport timestamps: one workgroup, beside the loop
+    if (!wide && lt_combined) {
+      bh::launch_lt_rows(v, sc);
+    } else if (!wide) {  // the segment's Lamport timestamps: one workgroup, beside the loop
       Dev vl = v;
       vl.ncol = 0;
       vl.flow_lt = 1;
@@ -1069,6 +1072,10 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if ((rc = rounds_coords(h))) return rc;
     return rounds_loop(h);
   }
+  // the last segment's Lamport timestamps run after its LA columns were
+  // handed to the loop (coords): the passes after DivideRounds (the frame
+  // order reads LT) wait for the coordinate stream's end
+  HIPCHK(h, hipStreamWaitEvent(sr, h->ev[1], 0));
   h->coords_for = (int)N;
   h->rows_stale = !eager;
   float ms = 0;
