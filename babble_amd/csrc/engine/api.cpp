@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.cla, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.cla, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw, d.pbar,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
                   d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
@@ -198,6 +198,19 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     float lms = 0;
     if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
     if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
+    if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
+    return BH_OK;
+  }
+  if (bh::round_persist_eligible(v)) {  // one launch, a grid barrier per iteration (k_round2p)
+    if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));
+    bh::launch_round_persist(v, s);
+    HIPCHK(h, hipGetLastError());
+    if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
+    HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
+    float lms = 0;
+    if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
+    if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
+    if (st[bh::ST_ERR] == 3) return h->fail(BH_ERR_DEVICE, "the persistent round loop's grid barrier gave up");
     if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
     return BH_OK;
   }
@@ -517,6 +530,7 @@ int rounds_loop(bh_handle *h) {
     return BH_OK;
   }
   int32_t st[bh::ST_COUNT];
+  d.wide_cols = 0;  // (the wide loop over FDT: rows were transposed above)
   d.use_cla = d.fd_cols && !bh::round_solo_eligible(d);
   if (h->reset_on) {
     // rounds below r0 event by event, then the loop from B[r0]
@@ -636,6 +650,21 @@ int segments_for(const Dev &d, int64_t events) {
 // them to shard 0, packed as 16-bit offsets, over xGMI (peer copies in
 // process, ncclSend / ncclRecv across processes)
 
+// segment boundaries of a K-segment pipeline over events [base, N): the
+// first segment is short (1/(4K) of the events; BH_SEG_FIRST=<permille>
+// sets it), the rest equal.  The loop waits for the first segment's
+// coordinates only: the dataflow then stays ahead of it (C3: 57 ms of
+// coordinates against 62 ms of loop), so a short first segment starts the
+// loop ~5 ms earlier than K equal ones would
+static void segment_bounds(int64_t base, int64_t N, int K, int64_t *Ns) {
+  Ns[0] = base;
+  if (K <= 1) { Ns[1] = N; return; }
+  static const int pm = getenv("BH_SEG_FIRST") ? std::clamp(atoi(getenv("BH_SEG_FIRST")), 1, 1000) : 0;
+  const int64_t first = pm ? (N - base) * pm / 1000 : (N - base) / (4 * K);
+  Ns[1] = base + std::max<int64_t>(first, 1);
+  for (int k = 2; k <= K; ++k) Ns[k] = Ns[1] + (N - Ns[1]) * (k - 1) / (K - 1);
+}
+
 // the LA columns of coordinate shard `rank` (>= 1) of a split group
 inline void split_cols(const bh_handle *h, int32_t rank, int64_t *c0, int64_t *c1) {
   shard_range(h->d.n, h->world - 1, rank - 1, c0, c1);
@@ -693,7 +722,7 @@ SplitPlan split_plan(const bh_handle *h, int K, int64_t base) {
   p.K = K;
   p.base = base;
   p.Ns.assign((size_t)K + 1, base);
-  for (int k = 1; k <= K; ++k) p.Ns[(size_t)k] = base + (N - base) * k / K;
+  segment_bounds(base, N, K, p.Ns.data());
   p.tab.assign((size_t)K * 2 * n + (size_t)K * 2 * (n + 1), 0);
   p.S.assign((size_t)K, 0);
   p.NQ.assign((size_t)K, 0);
@@ -811,9 +840,16 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // C3 step's HBM traffic) -- queries build them on demand (ensure_coords).
   // A Reset hashgraph's fiat pass and the resident loop (BH_ROUND_SOLO) read
   // them; BH_EAGER_ROWS=1 builds them anyway (A/B)
+  // 128 < n <= 512: the 16-bit wide loop reads la_col as well (window,
+  // candidates' FD rows, fame's LA rows; k_round_wide<*, true, true>) --
+  // BH_WIDE_ROWS=1 keeps the FDT / row-major LA loop (A/B)
   static const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
-  const bool eager = !sp && (wide || h->reset_on || eager_env || bh::round_solo_eligible(d) || d.round_src_rows);
-  d.use_cla = d.fd_cols && !bh::round_solo_eligible(d);
+  static const bool wide_rows_env = !getenv("BH_WIDE_COLS") || !atoi(getenv("BH_WIDE_COLS")) ||
+                                    (getenv("BH_WIDE_ROWS") && atoi(getenv("BH_WIDE_ROWS")));  // (off until verified)
+  d.wide_cols = wide && !sp && !h->reset_on && !wide_rows_env && !eager_env && bh::round_p16(d) && d.cla && d.n <= 512;
+  const bool eager = !sp && ((wide && !d.wide_cols) || h->reset_on || eager_env || bh::round_solo_eligible(d) ||
+                             d.round_src_rows);
+  d.use_cla = (d.fd_cols || d.wide_cols) && !bh::round_solo_eligible(d);
   if (sp) d.round_src_rows = 0;  // the split ships the column-major LA only
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
@@ -848,7 +884,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, sc));
   const int64_t N = d.N;
   std::vector<int64_t> Ns((size_t)K + 1, base);
-  for (int k = 1; k <= K; ++k) Ns[(size_t)k] = base + (N - base) * k / K;
+  segment_bounds(base, N, K, Ns.data());
   // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
   auto lens_at = [&](int64_t bound, int32_t *out) {
     for (int c = 0; c < n; ++c) {
@@ -966,6 +1002,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       vl.ncol = 0;
       vl.flow_lt = 1;
       bh::launch_flow(vl, sc);
+      bh::launch_lt_rows(v, sc);
+      HIPCHK(h, hipGetLastError());
+    } else if (!eager) {  // wide: k_floww2 wrote lt_row; per-event LT (the transpose copies it otherwise)
       bh::launch_lt_rows(v, sc);
       HIPCHK(h, hipGetLastError());
     }
@@ -1574,6 +1613,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.flow_wd = getenv("BH_FLOWW_WATCHDOG") ? atoi(getenv("BH_FLOWW_WATCHDOG")) : (1 << 20);
   d.flow_lt = 1;
   d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
+  d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 0;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
@@ -1615,9 +1655,10 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   // ballot tables: every round from 0 (bh_reset moves the base up)
   d.rbase = 0;
   d.rspan = (int32_t)R1;
+  d.cla_span = (int32_t)std::min<size_t>(R1, std::max<size_t>(64, bh::CLA_BYTES / ((size_t)n * d.npad * 4)));
   if (d.fd_cols) {
     A(&d.ssm, R1 * n * 16);
-    A(&d.cla, R1 * n * d.npad);
+    A(&d.cla, (size_t)d.cla_span * n * d.npad);
     d.round_lpc = 8;  // k_round2: 8 lanes per candidate at every n <= 128
   } else {
     // chain-major 32-bit FD rows (fd) are allocated on first use (ensure_fd):
@@ -1625,6 +1666,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
     // queries read them; the 16-bit loop reads the complete FDT
     d.fd = nullptr;
     if (n <= 512) A(&d.ssw, R1 * n * 8);  // k_round_wide's masks for k_fame_masks<16>
+    if (n <= 512) A(&d.cla, (size_t)d.cla_span * n * d.npad);  // and its candidates' LA rows (wide_cols)
   }
   A(&d.last_la, (size_t)(n + 1) * d.npad);
   A(&d.rq, (size_t)n);
@@ -1642,7 +1684,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
-  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT);
+  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 64);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C); A(&d.trapped, C); A(&d.blocked, R1);
   A(&d.wfame, (size_t)d.W_cap); A(&d.frame_loaded, R1);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
@@ -1939,6 +1981,7 @@ int bh_reset_consensus(bh_handle *h) {
 struct RoundTables {
   unsigned long long *ssm = nullptr, *ssw = nullptr;
   int32_t *cla = nullptr;
+  int32_t cla_span = 0;
   int32_t *B = nullptr, *wofs = nullptr, *wcnt = nullptr, *blocked = nullptr, *frame_loaded = nullptr, *nfam = nullptr,
           *minla = nullptr, *frame_cnt = nullptr, *frame_ofs = nullptr, *frame_cur = nullptr, *blk_of_frame = nullptr;
   int8_t *decided = nullptr, *rexists = nullptr;
@@ -1965,7 +2008,10 @@ static int alloc_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int32
     if (rc == BH_OK && hipMemset(*p, 0, std::max<size_t>(cnt, 1) * sizeof(**p)) != hipSuccess) rc = BH_ERR_DEVICE;
   };
   if (ssm) A(&t.ssm, span * n * 16);
-  if (ssm) A(&t.cla, span * n * h->d.npad);
+  if (ssm || ssw) {
+    t.cla_span = (int32_t)std::min<size_t>(span, std::max<size_t>(64, bh::CLA_BYTES / ((size_t)n * h->d.npad * 4)));
+    A(&t.cla, (size_t)t.cla_span * n * h->d.npad);
+  }
   if (ssw) A(&t.ssw, span * n * 8);
   A(&t.B, R1 * n); A(&t.wofs, R1); A(&t.wcnt, R1); A(&t.blocked, R1); A(&t.frame_loaded, R1);
   A(&t.decided, R1); A(&t.nfam, R1); A(&t.minla, R1 * h->d.npad); A(&t.frame_cnt, R1);
@@ -1985,7 +2031,7 @@ static void commit_round_tables(bh_handle *h, RoundTables &t, int32_t R_cap, int
                  d.frame_ofs, d.frame_cur, d.blk_of_frame, d.decided, d.rexists, d.frame_ntx, d.cla};
   for (void *p : old)
     if (p) (void)hipFree(p);
-  d.ssm = t.ssm; d.ssw = t.ssw; d.cla = t.cla; d.B = t.B; d.wofs = t.wofs; d.wcnt = t.wcnt; d.blocked = t.blocked;
+  d.ssm = t.ssm; d.ssw = t.ssw; d.cla = t.cla; d.cla_span = t.cla_span; d.B = t.B; d.wofs = t.wofs; d.wcnt = t.wcnt; d.blocked = t.blocked;
   d.frame_loaded = t.frame_loaded; d.nfam = t.nfam; d.minla = t.minla; d.frame_cnt = t.frame_cnt;
   d.frame_ofs = t.frame_ofs; d.frame_cur = t.frame_cur; d.blk_of_frame = t.blk_of_frame; d.decided = t.decided;
   d.rexists = t.rexists; d.frame_ntx = t.frame_ntx;

@@ -125,7 +125,11 @@ struct Dev {
   // (from its LDS window) -- fame's first votes and minLA read witnesses'
   // rows here, whole and coalesced, instead of n scattered column reads
   int32_t *cla;
+  int32_t cla_span;  // rounds cla holds: a ring over rounds (cla_row), rounds > R - cla_span intact
   int32_t use_cla;  // the loop that ran wrote cla (k_round2; not the resident k_round_solo)
+  int32_t wide_cols;  // the 16-bit wide loop reads la_col (k_round_wide<*, true, true>; no FDT)
+  int32_t round_persist;  // BH_ROUND_PERSIST=1: k_round2p, the whole n <= 128 loop in one launch (A/B)
+  int32_t *pbar;          // k_round2p's grid-barrier counter
   int32_t round_src_rows;  // k_round2r: windows from the row-major LA, hand-off from FDT (BH_ROUND_SRC=rows, A/B)
   int32_t round_prio;  // k_round2's wave priority (s_setprio) against co-resident coordinate waves (BH_ROUND_PRIO)
   int32_t rbase, rspan;
@@ -208,11 +212,17 @@ __host__ __device__ inline int64_t la_col_stride(const Dev &d) { return d.la_row
 // builds the row-major `la` (and FDT) only when a query asks for them.
 // Wider: the row-major table (la_col may share FDT's memory there).
 __device__ __forceinline__ int32_t la_at(const Dev &d, int64_t row, int col) {
-  return d.fd_cols ? d.la_col[(int64_t)col * la_col_stride(d) + row] : d.la[row * d.npad + col];
+  return d.fd_cols || d.wide_cols ? d.la_col[(int64_t)col * la_col_stride(d) + row] : d.la[row * d.npad + col];
 }
 // row of (chain c, round r) in the ballot tables ssm / ssw
 __host__ __device__ inline int64_t ballot_row(const Dev &d, int c, int r) {
   return (int64_t)c * d.rspan + (r - d.rbase);
+}
+// row of (chain c, round r) in cla: a ring of cla_span rounds (at most
+// CLA_BYTES; C4's 512 x 512 rows would take 61 GB over R_cap = C / SM rounds)
+constexpr size_t CLA_BYTES = (size_t)8 << 30;
+__host__ __device__ inline int64_t cla_row(const Dev &d, int c, int r) {
+  return (int64_t)c * d.cla_span + (r - d.rbase) % d.cla_span;
 }
 constexpr int32_t RR_DROP = INT32_MIN + 1;  // left UndeterminedEvents with no round received (hashgraph.go:970-977)
 
@@ -357,6 +367,9 @@ void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_roun
 // n <= 32 on the chain dataflow: the whole loop in one resident workgroup
 // (k_round_solo; opt-in with BH_ROUND_SOLO=1, measured A/B)
 bool round_solo_eligible(const Dev &d);
+bool round2_eligible(const Dev &d);
+bool round_persist_eligible(const Dev &d);
+void launch_round_persist(const Dev &d, hipStream_t s);
 void launch_round_solo(const Dev &d, hipStream_t s);
 // Reset hashgraphs: coordinates of events [0, d.N) one event at a time (the
 // batch whose other-parents only Root.Others knows), and the rounds below r0

@@ -261,6 +261,9 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   FameLds<NW> &L = *reinterpret_cast<FameLds<NW> *>(fsm_);
   const int r = r0 + (int)blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const int n = d.n, npad = d.npad, sm = d.sm;
+  // cla rows of rounds r + 1 (first votes) and r (minLA), unless a later
+  // round of this loop reused their ring slot: then la_at
+  const bool cy = d.use_cla && r + 1 > R - d.cla_span, cx = d.use_cla && r > R - d.cla_span;
   if (t < NW) L.wx[t] = fame_wmask_word(d, r, t);
   for (int q = t; q < MAXN; q += nt) {
     L.dec[q] = 0;
@@ -273,7 +276,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
       if (b0 < d.chain_len[q]) L.xev[q] = d.chain_ids[d.chain_start[q] + b0];
       L.xk[q] = b0;
       if (r + 1 < R)
-        L.yev[q] = d.use_cla ? (int32_t)ballot_row(d, q, r + 1)
+        L.yev[q] = cy ? (int32_t)cla_row(d, q, r + 1)
                              : d.chain_start[q] + min(d.B[(int64_t)(r + 1) * n + q], d.chain_len[q] - 1);
     }
   }
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
         for (int b = 0; b < 32; ++b) {
           const int y = h * HY + k * 32 + b;
           if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
-          const int32_t a = d.use_cla ? d.cla[(int64_t)L.yev[y] * npad + xc] : la_at(d, L.yev[y], xc);
+          const int32_t a = cy ? d.cla[(int64_t)L.yev[y] * npad + xc] : la_at(d, L.yev[y], xc);
           if (a >= L.xk[xc]) v |= 1u << b;
         }
         L.V[0][h * HW_ + k][x] = v;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
     int m = 0;
     for (int q = 0; q < n; ++q)
       if (((L.wx[q >> 5] >> (q & 31)) & 1u) && L.dec[q] == 1)
-        L.frow[m++] = d.use_cla ? (int32_t)ballot_row(d, q, r) : d.chain_start[q] + d.B[(int64_t)r * n + q];
+        L.frow[m++] = cx ? (int32_t)cla_row(d, q, r) : d.chain_start[q] + d.B[(int64_t)r * n + q];
     L.nfam_s = m;
   }
   __syncthreads();
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   const int nf = L.nfam_s;
   for (int c = t; c < npad; c += nt) {
     int32_t m = INT32_MAX;
-    if (d.use_cla)
+    if (cx)
       for (int i = 0; i < nf; ++i) m = min(m, d.cla[(int64_t)L.frow[i] * npad + c]);
     else
       for (int i = 0; i < nf; ++i) m = min(m, c < n ? la_at(d, L.frow[i], c) : -1);

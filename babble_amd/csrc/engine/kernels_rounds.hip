@@ -165,6 +165,114 @@ __device__ __forceinline__ void handoff_wide(const Dev &d, int64_t row, int p1, 
   if (g && threadIdx.x == 0) d.c8tag[(int64_t)p1 * n + c] = rnext;
 }
 
+// The first j in [lo, hi) with col[j] >= k (col non-decreasing), or hi:
+// the whole wave searches (lo, hi, k uniform), 64 probes per pass.
+__device__ __forceinline__ int32_t first_ge_wave(const int32_t *col, int32_t lo, int32_t hi, int32_t k) {
+  const int lane = threadIdx.x & 63;
+  while (hi - lo > 64) {
+    const int32_t s = (hi - lo + 63) >> 6;
+    const unsigned long long m = __ballot(col[min(lo + (lane + 1) * s, hi) - 1] >= k);
+    if (!m) return hi;
+    const int f = __builtin_ctzll(m);
+    hi = min(lo + (f + 1) * s, hi);
+    lo += f * s;
+  }
+  const unsigned long long m = __ballot(lo + lane < hi && col[lo + lane] >= k);
+  return m ? lo + __builtin_ctzll(m) : hi;
+}
+
+// k_round_wide<*, true, COLS>'s hand-off of the new candidate (c, row) for
+// iteration r + 1 from the dataflow's column-major LA (no FDT):
+// FD[(c, row)][i] = min{j : LA[(i, j)][c] >= row} is non-decreasing in the
+// candidate's row, so chain i's entry starts at the previous candidate's
+// (cand16[p][c]); 4 lanes per chain count the rows below `row` among the 48
+// from there (rounded down to 4), 64 chains per pass.  An entry beyond them
+// (an advance of more than ~45 rows) is searched by the wave
+// (first_ge_wave).  Writes cand16 (16-bit FD + 1), cand8 against the shared
+// base (as handoff_wide) and the candidate's LA row into cla (fame).
+__device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, int32_t row, const int32_t *Bcur,
+                                                  int32_t rnext) {
+  constexpr int K = 8, HR = 48;  // chains per thread (n <= 512), rows per chain
+  const int t = threadIdx.x, lane = t & 63, l4 = t & 3;
+  const int n = d.n, npad = d.npad, w16 = (npad + 7) / 8 * 4, w8 = (npad + 15) / 16 * 16;
+  const int64_t stride = la_col_stride(d);
+  const int32_t *colc = d.la_col + (int64_t)c * stride;
+  const uint16_t *prev = reinterpret_cast<const uint16_t *>(d.cand16 + ((int64_t)p * n + c) * w16);
+  uint16_t *dst16 = reinterpret_cast<uint16_t *>(d.cand16 + ((int64_t)(p ^ 1) * n + c) * w16);
+  const bool g = d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;
+  uint8_t *dst8 = g ? d.cand8 + ((int64_t)(p ^ 1) * n + c) * w8 : nullptr;
+  const int64_t crow = (int64_t)d.chain_start[c] + row;
+  int32_t la[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = t + 256 * k;
+    la[k] = i < n ? d.la_col[(int64_t)i * stride + crow] : -1;
+  }
+  int32_t a[K], cs[K], end[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = (t >> 2) + 64 * k;
+    const uint32_t h = i < n ? prev[i] : 0xFFFFu;
+    cs[k] = i < n ? d.chain_start[i] : 0;
+    end[k] = i < n ? cs[k] + d.chain_len[i] : 0;
+    a[k] = h == 0xFFFFu ? -1 : cs[k] + (int32_t)h - 1;  // the previous entry (absolute row), -1: none
+  }
+  int4 v[K][3];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      v[k][u] = a[k] >= 0 ? *reinterpret_cast<const int4 *>(colc + ((a[k] & ~3) + 12 * l4 + 4 * u)) : make_int4(0, 0, 0, 0);
+  if (t < npad) d.cla[cla_row(d, c, rnext) * npad + t] = la[0];
+  if (t + 256 < npad) d.cla[cla_row(d, c, rnext) * npad + t + 256] = la[1];
+  int32_t fd[K];
+  bool miss[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = (t >> 2) + 64 * k;
+    const int32_t ab = a[k] & ~3, x0 = ab + 12 * l4, elo = a[k] - x0, ehi = end[k] - x0;
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      cnt += (4 * u + 0 >= elo) & (4 * u + 0 < ehi) & (v[k][u].x < row);
+      cnt += (4 * u + 1 >= elo) & (4 * u + 1 < ehi) & (v[k][u].y < row);
+      cnt += (4 * u + 2 >= elo) & (4 * u + 2 < ehi) & (v[k][u].z < row);
+      cnt += (4 * u + 3 >= elo) & (4 * u + 3 < ehi) & (v[k][u].w < row);
+    }
+    cnt = group_total<4>(cnt);
+    const int32_t jn = a[k] + cnt, bend = min(ab + HR, end[k]);
+    fd[k] = FD_NONE;
+    miss[k] = false;
+    if (a[k] >= 0) {
+      if (i == c) fd[k] = row;  // an event is its own first descendant
+      else if (jn < bend) fd[k] = jn - cs[k];
+      else if (bend < end[k]) miss[k] = true;
+      // else: no row of chain i in this view sees the candidate
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    unsigned long long mm = __ballot(miss[k] && l4 == 0);
+    while (mm) {  // (rare) beyond the 48 rows: the wave searches each such chain
+      const int src = __builtin_ctzll(mm);
+      mm &= mm - 1;
+      const int32_t lo = __shfl(min((a[k] & ~3) + HR, end[k]), src), hi = __shfl(end[k], src), b = __shfl(cs[k], src);
+      const int32_t j = first_ge_wave(colc, lo, hi, row);
+      if (lane == src) fd[k] = j < hi ? j - b : FD_NONE;
+    }
+    const int i = (t >> 2) + 64 * k;
+    if (l4 == 0 && i < 2 * w16) {
+      const uint32_t h = i < n ? min((uint32_t)fd[k] + 1u, 0xFFFFu) : 0xFFFFu;  // FD_NONE + 1 wraps to 2^31
+      dst16[i] = (uint16_t)h;
+      if (g && i < w8) {
+        const int32_t base = i < n ? max(Bcur[i] - d.round_p8g, 0) : 0;
+        dst8[i] = (uint8_t)(i < n ? min((uint32_t)max((int32_t)h - base, 0), 127u) : 127u);
+      }
+    }
+  }
+  if (g && t == 0) d.c8tag[(int64_t)(p ^ 1) * n + c] = rnext;
+}
+
 template <int LPC>
 __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
   extern __shared__ __attribute__((aligned(16))) int32_t ssm[];
@@ -325,7 +433,7 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // P16: the same search over 16-bit rows (cand16, LA converted while staged):
 // lane `part` owns 8 pieces of 8 columns, half the LDS reads and 3/5 of the
 // compare work per probe.
-template <int LPC, bool P16>
+template <int LPC, bool P16, bool COLS = false>
 __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU
   extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
   constexpr int PP = P16 ? 8 : PIECES;  // 16-B pieces per lane
@@ -368,6 +476,25 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   for (;;) {
     const int wrows = min(WROWS, len - wk0);
     if (wrows <= 0) break;
+    // COLS: the window's 36 aligned rows of every column from la_col, issued
+    // before the fit check below reads its two rows
+    constexpr int CQ = LPC * 16, CT = 256 / CQ, CNP = (9 + CT - 1) / CT;  // column quads, threads per quad, pieces per thread
+    const int cg = t % CQ, ch = t / CQ;
+    const int32_t crb = (cs + wk0) & ~3;
+    const int coff = cs + wk0 - crb;
+    int4 cpv[COLS ? CNP : 1][4];
+    if constexpr (COLS) {
+#pragma unroll
+      for (int u = 0; u < CNP; ++u) {
+        const int pc = ch + u * CT;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int col = 4 * cg + k;
+          cpv[u][k] = pc < 9 && col < n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)col * la_col_stride(d) + (crb + 4 * pc))
+                                        : make_int4(-1, -1, -1, -1);
+        }
+      }
+    }
     bool p8 = false, p8g = false;
     if constexpr (P16) {
       if (d.round_p8) {
@@ -381,11 +508,19 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
         __syncthreads();
         const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
         const int32_t *Bprev = d.B + (int64_t)(r - 1) * n;
+        // LA of column i at the window's first / last row (-1 past n, 0 past npad)
+        auto la_w = [&](int i, int last) -> int32_t {
+          if (i >= npad) return 0;
+          if constexpr (COLS)
+            return i < n ? d.la_col[(int64_t)i * la_col_stride(d) + cs + wk0 + (last ? wrows - 1 : 0)] : -1;
+          else
+            return (last ? r1p : r0p)[i];
+        };
         bool bad = false, gbad = false;
         for (int j = t; j < 256; j += 256) {
           const int i0 = 2 * j, i1 = 2 * j + 1;
-          const int32_t a0 = i0 < npad ? r0p[i0] : 0, a1 = i1 < npad ? r0p[i1] : 0;
-          const int32_t z0 = i0 < npad ? r1p[i0] : 0, z1 = i1 < npad ? r1p[i1] : 0;
+          const int32_t a0 = la_w(i0, 0), a1 = la_w(i1, 0);
+          const int32_t z0 = la_w(i0, 1), z1 = la_w(i1, 1);
           const int32_t b0 = max(a0, 0), b1 = max(a1, 0);
           wbase2[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
           bad |= z0 + 1 - b0 > d.round_p8 || z1 + 1 - b1 > d.round_p8;
@@ -406,7 +541,42 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     }
     const uint32_t *wb2 = p8g ? gbase2 : wbase2;
     __syncthreads();
-    if (p8) {
+    if constexpr (COLS) {
+      // quad cg's 4 columns, 4 rows per piece: P8 one dword per row (bytes
+      // x | 0x80, as below), P16 two (16-bit LA + 1 pairs); window row = the
+      // piece's row - coff, rows outside [0, wrows) skipped
+      uint32_t *w32 = reinterpret_cast<uint32_t *>(win4);
+      uint32_t bs[4] = {0, 0, 0, 0};
+      if (p8) {
+        const uint32_t b01 = wb2[2 * cg], b23 = wb2[2 * cg + 1];
+        bs[0] = b01 & 0xFFFFu; bs[1] = b01 >> 16; bs[2] = b23 & 0xFFFFu; bs[3] = b23 >> 16;
+      }
+      const int pc8 = cg >> 2, pc16 = cg >> 1;
+      const int o8 = (pc8 + pc8 / PP8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
+#pragma unroll
+      for (int u = 0; u < CNP; ++u) {
+        const int pc = ch + u * CT;
+        if (pc >= 9) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int wr = 4 * pc + e - coff;
+          if (wr < 0 || wr >= wrows) continue;
+          auto el = [&](int k) -> int32_t {
+            const int4 v = cpv[u][k];
+            return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+          };
+          if (p8) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x |= ((uint32_t)(el(k) + 1 - (int32_t)bs[k]) & 0xFFu) << (8 * k);
+            w32[wr * WRS8 * 4 + o8] = x | 0x80808080u;
+          } else {
+            w32[wr * WRS4 * 4 + o16] = pack_la16(el(0), el(1));
+            w32[wr * WRS4 * 4 + o16 + 1] = pack_la16(el(2), el(3));
+          }
+        }
+      }
+    } else if (p8) {
       // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
       constexpr int RP8 = LPC * PP8;
       const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
@@ -662,8 +832,8 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
 #pragma unroll
           for (int u = 0; u < PP; ++u) lt += lt4(x[u], f[u]);
         }
-        constexpr int COLS = LPC * PP * (P16 ? 8 : 4);  // columns per group, padding included
-        return COLS - group_total<LPC>(lt) >= sm;
+        constexpr int NCOL = LPC * PP * (P16 ? 8 : 4);  // columns per group, padding included
+        return NCOL - group_total<LPC>(lt) >= sm;
       };
       if (ss(wrows - 1)) {
         int lo = 0, hi = wrows - 1;
@@ -708,7 +878,10 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     }
   }
   // the hand-off: the new candidate's FD row for the next iteration
-  if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
+  if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
+    if constexpr (COLS) handoff_wide_cols(d, p, c, result, Bp, r + 1);
+    else handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
+  }
   if (t == 0) {
     if (sh_nc == 0) {
       if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
@@ -806,16 +979,25 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
   if (t == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
   if (b >= d.chain_len[c]) return;  // no candidate on chain c
   if (d.cla && t < d.npad)  // the candidate's LA row (fame)
-    d.cla[ballot_row(d, c, r) * d.npad + t] =
+    d.cla[cla_row(d, c, r) * d.npad + t] =
         t < d.n ? d.la_col[(int64_t)t * la_col_stride(d) + d.chain_start[c] + b] : -1;
   const int32_t *colc = d.la_col + (int64_t)c * la_col_stride(d);
   int32_t *cf = d.candfd + (int64_t)c * d.npad;
-  for (int i0 = 0; i0 < d.npad; i0 += blockDim.x >> 4) {  // (uniform trip count)
+  // the wide loop's rows (wide_cols): 16-bit FD + 1 (0xFFFF: none), the
+  // entries up to npad rounded to 8 (cand16's row)
+  const int w16 = (d.npad + 7) / 8 * 4;
+  uint16_t *c16 = d.wide_cols ? reinterpret_cast<uint16_t *>(d.cand16 + (int64_t)c * w16) : nullptr;
+  const int nrow = c16 ? 2 * w16 : d.npad;
+  for (int i0 = 0; i0 < nrow; i0 += blockDim.x >> 4) {  // (uniform trip count)
     const int i = i0 + (t >> 4);
     const bool on = i < d.n;
     const int32_t cs = on ? d.chain_start[i] : 0, len = on ? d.chain_len[i] : 0;
     const int32_t j = first_ge16(colc + cs, 0, len, b, on && len > 0, false);
-    if ((t & 15) == 0 && i < d.npad) cf[i] = on && j < len ? j : FD_NONE;
+    const int32_t f = on && j < len ? j : FD_NONE;
+    if ((t & 15) == 0 && i < nrow) {
+      if (c16) c16[i] = (uint16_t)min((uint32_t)f + 1u, 0xFFFFu);
+      else cf[i] = f;
+    }
   }
 }
 
@@ -833,10 +1015,13 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
 //
 // Round 4: the loop reads only the dataflow's column-major LA (la_col); no
 // row-major LA and no firstDescendants table are built for it.
-//   * The window: HWL = 36 rows of every column from rb = the window's first
+//   * The window: HWL = 32 rows of every column from rb = the window's first
 //     row rounded down to 4, one aligned 16-B piece (4 rows of one column)
-//     per thread, stored transposed into the row-major LDS window; the search
-//     runs over its rows off .. off + 31 (off = the alignment offset).
+//     per thread (one load instruction per lane), stored transposed into the
+//     row-major LDS window; the search runs over its rows off .. 31 (off =
+//     the alignment offset, 29 to 32 rows: on the C3 DAG B[r+1][c] - B[r][c]
+//     is 12 on average and at most 28; a later row is found by the fallback,
+//     window by window).
 //   * The hand-off: the new candidate (c, B[r+1][c])'s FD row.  FD[(c, k)][i]
 //     is non-decreasing in k, so it starts at the previous candidate's entry
 //     j0 = FD[(c, B[r][c])][i] (its row, candfd[p][c]).  At the start of the
@@ -847,8 +1032,7 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
 //     than ~60 rows, e.g. a lagging chain's candidate) searches on
 //     (first_ge16: usually two more loads).  Entries beyond the view's chain
 //     lengths are MaxInt32, as the prefix semantics need (section 4.9).
-constexpr int HWL = HW + 4;  // staged window rows
-constexpr int WP = HWL / 4;  // 16-B pieces per column of the window
+constexpr int HWL = HW;     // staged window rows (8 aligned 16-B pieces per column)
 constexpr int FDB = 64;      // LA rows per chain loaded for the hand-off
 
 // the first iteration's candidate rows (round 0, or the resume round)
@@ -917,16 +1101,12 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       hlen[u] = d.chain_len[i];
     }
   }
-  // the window's pieces: item j = column j / WP, rows rb + 4 (j % WP) .. + 3
-  const int64_t rb = (int64_t)(cs + k0) & ~(int64_t)3;
-  const int off = (int)(cs + k0 - rb);
-  int4 wv[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = t + u * nt;
-    wv[u] = j < WP * n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)(j / WP) * stride + rb + 4 * (j % WP))
-                       : make_int4(-1, -1, -1, -1);
-  }
+  // the window's pieces: thread t stages column t / 8, rows rb + 4 (t % 8) .. + 3
+  const int32_t rb = (cs + k0) & ~3;
+  const int off = cs + k0 - rb;
+  const int wi = t >> 3, wr4 = 4 * (t & 7);
+  const int4 wv = wi < n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
+                         : make_int4(-1, -1, -1, -1);
   if (done) return;
   // the hand-off's 64 rows of LA[.][c] per chain i (depend on j0 only)
   int4 fb[2];
@@ -934,21 +1114,16 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   for (int u = 0; u < 2; ++u) {
     const int piece = (t + u * nt) & 15;
     const bool live = hj0[u] != FD_NONE;
-    const int64_t a = live ? ((int64_t)hcs[u] + hj0[u]) & ~(int64_t)3 : 0;
-    fb[u] = live ? *reinterpret_cast<const int4 *>(colc + a + 4 * piece) : make_int4(0, 0, 0, 0);
+    const int32_t a = live ? (hcs[u] + hj0[u]) & ~3 : 0;
+    fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 4 * piece)) : make_int4(0, 0, 0, 0);
   }
   const bool act = q < n && bq < lq;
-  const int rows = min(HW, max(0, len - k0));
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = t + u * nt;
-    if (j < WP * n) {
-      const int i = j / WP, r4 = 4 * (j - i * WP);
-      win32[(r4 + 0) * rs + i] = wv[u].x;
-      win32[(r4 + 1) * rs + i] = wv[u].y;
-      win32[(r4 + 2) * rs + i] = wv[u].z;
-      win32[(r4 + 3) * rs + i] = wv[u].w;
-    }
+  const int rows = min(HWL - off, max(0, len - k0));  // (the window's rows off .. HWL - 1)
+  if (wi < n) {
+    win32[(wr4 + 0) * rs + wi] = wv.x;
+    win32[(wr4 + 1) * rs + wi] = wv.y;
+    win32[(wr4 + 2) * rs + wi] = wv.z;
+    win32[(wr4 + 3) * rs + wi] = wv.w;
   }
   if (npad > n)  // columns past n: LA -1 (never >= an FD)
     for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
@@ -1043,25 +1218,25 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   if (res >= 0) {
     result = k0 + res;
     lrow = off + res;
-  } else if (nc > 0 && rows == HW) {
+  } else if (nc > 0 && rows == HWL - off) {
     // SM not reached in the window (rare): the next windows of chain c,
     // staged the same way (slot counters are reused per row tested)
     if (d.diag && t == 0) atomicAdd(&d.diag[DG_RD_WMISS], 1ull);
-    for (int32_t wk = k0 + HW; wk < len && result == len; wk += HW) {
-      const int wr = min(HW, len - wk);
-      const int64_t rb2 = (int64_t)(cs + wk) & ~(int64_t)3;
+    for (int32_t wk = k0 + rows, wr = 0; wk < len && result == len; wk += wr) {
+      const int32_t rb2 = (cs + wk) & ~3;
+      const int off2 = cs + wk - rb2;
+      wr = min(HWL - off2, len - wk);
       __syncthreads();
-      for (int j = t; j < WP * n; j += nt) {
-        const int i = j / WP, r4 = 4 * (j - i * WP);
-        const int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)i * stride + rb2 + r4);
-        win32[(r4 + 0) * rs + i] = v.x;
-        win32[(r4 + 1) * rs + i] = v.y;
-        win32[(r4 + 2) * rs + i] = v.z;
-        win32[(r4 + 3) * rs + i] = v.w;
+      if (wi < n) {
+        const int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb2 + wr4));
+        win32[(wr4 + 0) * rs + wi] = v.x;
+        win32[(wr4 + 1) * rs + wi] = v.y;
+        win32[(wr4 + 2) * rs + wi] = v.z;
+        win32[(wr4 + 3) * rs + wi] = v.w;
       }
       if (t < 16) cntk[t] = 0;
       __syncthreads();
-      const int4 *x4 = win + (int)(cs + wk - rb2) * rs4;
+      const int4 *x4 = win + off2 * rs4;
       const unsigned long long ml = probe(x4 + (wr - 1) * rs4, 1);
       __syncthreads();
       if (cntk[1] < sm) continue;
@@ -1080,7 +1255,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
         }
       }
       result = wk + lo;
-      lrow = (int)(cs + wk - rb2) + lo;
+      lrow = off2 + lo;
     }
     __syncthreads();
   }
@@ -1093,25 +1268,26 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     for (int u = 0; u < 2; ++u) {
       const int j = t + u * nt, i = j >> 4, piece = j & 15;
       const bool live = hj0[u] != FD_NONE;
-      const int64_t a = (int64_t)hcs[u] + hj0[u];  // the previous candidate's entry (absolute row)
-      const int64_t ab = a & ~(int64_t)3, end = (int64_t)hcs[u] + hlen[u];
-      const int64_t x0 = ab + 4 * piece;
+      // rows a .. end - 1 of the 16 B at ab + 4 piece (a = the first row
+      // seeing (c, k0), end = the chain's view)
+      const int32_t a = hcs[u] + hj0[u], ab = a & ~3, end = hcs[u] + hlen[u];
+      const int32_t x0 = ab + 4 * piece, elo = a - x0, ehi = end - x0;
       int cnt = 0;
       if (live) {
-        cnt += x0 >= a && x0 < end && fb[u].x < result;
-        cnt += x0 + 1 >= a && x0 + 1 < end && fb[u].y < result;
-        cnt += x0 + 2 >= a && x0 + 2 < end && fb[u].z < result;
-        cnt += x0 + 3 >= a && x0 + 3 < end && fb[u].w < result;
+        cnt += (0 >= elo) & (0 < ehi) & (fb[u].x < result);
+        cnt += (1 >= elo) & (1 < ehi) & (fb[u].y < result);
+        cnt += (2 >= elo) & (2 < ehi) & (fb[u].z < result);
+        cnt += (3 >= elo) & (3 < ehi) & (fb[u].w < result);
       }
       cnt = group_total<16>(cnt);
-      const int64_t jn = a + cnt, bend = min(ab + FDB, end);
+      const int32_t jn = a + cnt, bend = min(ab + FDB, end);
       fdv[u] = FD_NONE;
       miss[u] = false;
       mlo[u] = 0;
       if (live) {
         if (i == c) fdv[u] = result;  // an event is its own first descendant
-        else if (jn < bend) fdv[u] = (int32_t)(jn - hcs[u]);
-        else if (bend < end) { miss[u] = true; mlo[u] = (int32_t)(bend - hcs[u]); }
+        else if (jn < bend) fdv[u] = jn - hcs[u];
+        else if (bend < end) { miss[u] = true; mlo[u] = bend - hcs[u]; }
         // else: no row of chain i in this view sees the candidate
       }
     }
@@ -1132,7 +1308,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
     // packs the LPC-strided bits and masks the words of chains >= n, which
     // fewer waves leave unwritten), chain-major [c][round]; issued last,
     // since a later vmcnt wait would include them
-    if (t < npad) d.cla[ballot_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
+    if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
     if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
   }
   if (dg) {
@@ -1173,6 +1349,296 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
 // k_round2r (BH_ROUND_SRC=rows, A/B): the round-3 iteration, reading its
 // window from the row-major LA and its hand-off from the FDT tiles that the
 // segments' transpose builds (eager rows); k_round2 reads only la_col
+// ---------------------------------------------------------------------------
+// k_round2p: the n <= 128 round loop as ONE launch of n workgroups, one per
+// chain (BH_ROUND_PERSIST=1, the A/B against one k_round2 launch per
+// iteration).  Each iteration is k_round2's (TQ search, hand-off counted
+// from 64 LA rows per chain); a grid barrier replaces the kernel boundary.
+// What crosses it -- each candidate's FD row (candfd) and boundary (Bp) --
+// is stored sc1; every workgroup then adds to one agent-scope counter after
+// its stores have drained, polls the counter with sc1 loads and reads the
+// rows back with sc1 loads (MI355X_MICROARCH.md, the hand-off table's first
+// row: no L2 write-back or invalidate).  What a workgroup needs of its own
+// chain -- the next window (rows from its new boundary) and the LA rows its
+// next hand-off counts from (its new FD row is in registers) -- is issued
+// before the barrier wait and lands during it.  Every workgroup sees the
+// same candidate count, so each decides the loop's end itself.  The spin is
+// bounded (ST_ERR = 3: the barrier gave up).
+constexpr int PBAR_SPIN_LIMIT = 1 << 24;
+
+template <int PPL>
+__global__ __launch_bounds__(1024) void k_round2p(Dev d) {
+  constexpr int LPC = 8;
+  extern __shared__ __attribute__((aligned(16))) int4 sm4[];
+  __shared__ int32_t cntk[16];
+  __shared__ int32_t hist[HW + 1];
+  __shared__ int32_t sh_fail;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
+  const int c = blockIdx.x, G = gridDim.x;
+  const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
+  const int rs4 = q4 + 1, rs = 4 * rs4;
+  const int64_t stride = la_col_stride(d);
+  int4 *win = sm4;
+  int32_t *win32 = reinterpret_cast<int32_t *>(sm4);
+  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  const int q = t / LPC, part = t % LPC, rot = q & (PPL - 1);
+  const int32_t lq = q < n ? d.chain_len[q] : 0;
+  const int32_t *colc = d.la_col + (int64_t)c * stride;
+  const __amdgpu_buffer_rsrc_t cfr = __builtin_amdgcn_make_buffer_rsrc(d.candfd, (short)0, 0x7fffffff, 0x00020000);
+  int32_t r = d.state[ST_CUR0];  // the first iteration has parity 0
+  int32_t k0 = d.Bp[c];
+  int32_t hcs[2], hlen[2], hj0[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = (t + u * nt) >> 4;
+    hcs[u] = i < n ? d.chain_start[i] : 0;
+    hlen[u] = i < n ? d.chain_len[i] : 0;
+    hj0[u] = i < n && k0 < len ? d.candfd[(int64_t)c * npad + i] : FD_NONE;
+  }
+  const int wi = t >> 3, wr4 = 4 * (t & 7);
+  int4 wv, fb[2];
+  auto own_loads = [&]() {  // chain c's window from k0 and its hand-off rows from hj0
+    const int32_t rb = (cs + k0) & ~3;
+    wv = wi < n && k0 < len ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
+                            : make_int4(-1, -1, -1, -1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int piece = (t + u * nt) & 15;
+      const bool live = hj0[u] != FD_NONE;
+      const int32_t a = live ? (hcs[u] + hj0[u]) & ~3 : 0;
+      fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 4 * piece)) : make_int4(0, 0, 0, 0);
+    }
+  };
+  own_loads();
+  if (t == 0) sh_fail = 0;
+  if (npad > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
+    for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
+  int p = 0;
+  for (int it = 0;; ++it) {
+    // round r's candidates: boundaries and FD rows, stored by other workgroups
+    const int32_t bq = q < n ? __hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    int4 f[PPL];
+    {
+      const int32_t row0 = (int32_t)(((int64_t)p * n + min(q, n - 1)) * npad * 4);
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) {
+        const int pc = part + LPC * ((u + rot) & (PPL - 1));
+        f[u] = pc < q4 ? __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * pc, 0, 16))
+                       : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+      }
+    }
+    const bool act = q < n && bq < lq;
+    const int off = (cs + k0) & 3;
+    const int rows = min(HWL - off, max(0, len - k0));
+    if (wi < n) {
+      win32[(wr4 + 0) * rs + wi] = wv.x;
+      win32[(wr4 + 1) * rs + wi] = wv.y;
+      win32[(wr4 + 2) * rs + wi] = wv.z;
+      win32[(wr4 + 3) * rs + wi] = wv.w;
+    }
+    if (t < 16) cntk[t] = 0;
+    if (t <= HW) hist[t] = 0;
+    __syncthreads();
+    auto ss_row = [&](const int4 *x4) {
+      int4 x[PPL];
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * ((u + rot) & (PPL - 1)), q4 - 1)];
+      int lt = 0;
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
+      return LPC * PPL * 4 - group_sum<LPC>(lt) >= sm;
+    };
+    auto probe = [&](const int4 *x4, int slot) {
+      const bool sv = ss_row(x4);
+      const unsigned long long m = __ballot(act && part == 0 && sv);
+      if (lane == 0 && m) atomicAdd(&cntk[slot], __popcll(m));
+      return m;
+    };
+    {
+      const unsigned long long m = __ballot(act && part == 0);
+      if (lane == 0 && m) atomicAdd(&cntk[0], __popcll(m));
+    }
+    const int4 *w0 = win + off * rs4;
+    int32_t res = -1;
+    unsigned long long ssb = 0;
+    if (rows > 0) {  // T_q per lane group, then the histogram (k_round2's TQ search)
+      int lo = 0, hi = rows;
+      while (__any(lo < hi)) {
+        const int mid = (lo + hi) >> 1;
+        const bool sv = ss_row(w0 + min(mid, rows - 1) * rs4);
+        if (lo < hi) {
+          hi = sv ? mid : hi;
+          lo = sv ? lo : mid + 1;
+        }
+      }
+      if (act && part == 0 && lo < rows) atomicAdd(&hist[lo], 1);
+      __syncthreads();
+      if (wave == 0) {
+        int h = lane < rows ? hist[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int x = __shfl_up(h, o);
+          h += lane >= o ? x : 0;
+        }
+        const unsigned long long hit = __ballot(lane < rows && h >= sm);
+        if (lane == 0) hist[HW] = hit ? (int)__builtin_ctzll(hit) : -1;
+      }
+      __syncthreads();
+      res = hist[HW];
+      ssb = __ballot(act && part == 0 && res >= 0 && lo <= res);
+    } else {
+      __syncthreads();
+    }
+    const int nc = cntk[0];
+    int32_t result = len;
+    int lrow = 0;
+    if (res >= 0) {
+      result = k0 + res;
+      lrow = off + res;
+    } else if (nc > 0 && rows == HWL - off) {
+      // SM not reached in the window (rare): the next windows, staged alike
+      for (int32_t wk = k0 + rows, wr = 0; wk < len && result == len; wk += wr) {
+        const int32_t rb2 = (cs + wk) & ~3;
+        const int off2 = cs + wk - rb2;
+        wr = min(HWL - off2, len - wk);
+        __syncthreads();
+        if (wi < n) {
+          const int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb2 + wr4));
+          win32[(wr4 + 0) * rs + wi] = v.x;
+          win32[(wr4 + 1) * rs + wi] = v.y;
+          win32[(wr4 + 2) * rs + wi] = v.z;
+          win32[(wr4 + 3) * rs + wi] = v.w;
+        }
+        if (t < 16) cntk[t] = 0;
+        __syncthreads();
+        const int4 *x4 = win + off2 * rs4;
+        const unsigned long long ml = probe(x4 + (wr - 1) * rs4, 1);
+        __syncthreads();
+        if (cntk[1] < sm) continue;
+        int lo = 0, hi = wr - 1, sl = 1;
+        ssb = ml;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          ++sl;
+          const unsigned long long m = probe(x4 + mid * rs4, sl);
+          __syncthreads();
+          if (cntk[sl] >= sm) {
+            hi = mid;
+            ssb = m;
+          } else {
+            lo = mid + 1;
+          }
+        }
+        result = wk + lo;
+        lrow = off2 + lo;
+      }
+      __syncthreads();
+    }
+    // the loop's end, the same in every workgroup: no candidates (R = r), or
+    // the round table's capacity
+    if (nc == 0 || r + 1 >= d.R_cap) {
+      if (c == 0 && t == 0) {
+        if (nc > 0) d.state[ST_ERR] = 1;
+        d.state[ST_ROUNDS] = r;
+        d.state[ST_ITERS] = r;
+        d.state[ST_DONE] = 1;
+        signal_done(d);
+      }
+      break;
+    }
+    // ---- hand-off: FD[(c, result)][i] (k_round2's count) ----
+    int32_t fdv[2] = {FD_NONE, FD_NONE};
+    if (result < len) {
+      int32_t mlo[2];
+      bool miss[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j = t + u * nt, i = j >> 4, piece = j & 15;
+        const bool live = hj0[u] != FD_NONE;
+        const int32_t a = hcs[u] + hj0[u], ab = a & ~3, end = hcs[u] + hlen[u];
+        const int32_t x0 = ab + 4 * piece, elo = a - x0, ehi = end - x0;
+        int cnt = 0;
+        if (live) {
+          cnt += (0 >= elo) & (0 < ehi) & (fb[u].x < result);
+          cnt += (1 >= elo) & (1 < ehi) & (fb[u].y < result);
+          cnt += (2 >= elo) & (2 < ehi) & (fb[u].z < result);
+          cnt += (3 >= elo) & (3 < ehi) & (fb[u].w < result);
+        }
+        cnt = group_total<16>(cnt);
+        const int32_t jn = a + cnt, bend = min(ab + FDB, end);
+        miss[u] = false;
+        mlo[u] = 0;
+        if (live) {
+          if (i == c) fdv[u] = result;
+          else if (jn < bend) fdv[u] = jn - hcs[u];
+          else if (bend < end) { miss[u] = true; mlo[u] = bend - hcs[u]; }
+        }
+      }
+      int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (__any(miss[u])) {
+          const int32_t jm = first_ge16(colc + hcs[u], mlo[u], hlen[u], result, miss[u], true);
+          if (miss[u]) fdv[u] = jm < hlen[u] ? jm : FD_NONE;
+        }
+        const int j = t + u * nt;
+        if ((j & 15) == 0 && (j >> 4) < npad)
+          __hip_atomic_store(cf + (j >> 4), fdv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
+      if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
+    }
+    if (t == 0) {
+      __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, result, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      d.B[(int64_t)(r + 1) * n + c] = result;
+    }
+    // ---- grid barrier ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ++r;
+    p ^= 1;
+    k0 = result;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) hj0[u] = result < len ? fdv[u] : FD_NONE;
+    own_loads();  // lands during the wait
+    if (t == 0) {
+      const int32_t target = (it + 1) * G;
+      int spins = 0;
+      while (__hip_atomic_load(d.pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > PBAR_SPIN_LIMIT) {
+          sh_fail = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (sh_fail) {
+      if (t == 0) {
+        d.state[ST_ERR] = 3;
+        d.state[ST_ROUNDS] = r;
+        d.state[ST_DONE] = 1;
+        if (c == 0) signal_done(d);
+      }
+      break;
+    }
+  }
+}
+
+bool round_persist_eligible(const Dev &d) {
+  return d.round_persist && round2_eligible(d) && !d.round_src_rows && d.pbar != nullptr && d.n <= 256;
+}
+
+void launch_round_persist(const Dev &d, hipStream_t s) {
+  const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
+  const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
+  (void)hipMemsetAsync(d.pbar, 0, 4, s);
+  if (d.npad <= 32) k_round2p<1><<<d.n, nt, lds, s>>>(d);
+  else if (d.npad <= 64) k_round2p<2><<<d.n, nt, lds, s>>>(d);
+  else k_round2p<4><<<d.n, nt, lds, s>>>(d);
+}
+
 template <int PPL, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2r(Dev d, int p) {
   constexpr int LPC = 8;
@@ -1351,7 +1817,7 @@ __global__ __launch_bounds__(1024) void k_round2r(Dev d, int p) {
     int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
     const int frel = (int)(cs + result - rb);  // row of the candidate in fdw
     // the candidate's LA row for fame (cla), before fdw overwrites the window
-    if (t < npad) d.cla[ballot_row(d, c, r + 1) * npad + t] = d.la[(int64_t)(cs + result) * npad + t];
+    if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = d.la[(int64_t)(cs + result) * npad + t];
     if (off < HW && frel < HW) {  // both from the rows staged during the search
       if (t < n * 8) *reinterpret_cast<int4 *>(fdw + fi * FDS + fp) = fv;
       __syncthreads();
@@ -1644,7 +2110,7 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
     if (d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;  // cand8 rows of an earlier loop are stale
   }
   // (n <= 128: the candidates' rows are searched in la_col, k_cand_rows)
-  if (b < len && !d.fd_cols && d.cand16 && !d.fd_rows)
+  if (b < len && !d.fd_cols && !d.wide_cols && d.cand16 && !d.fd_rows)
     gather_cand16(d, (int64_t)cs + b, d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
   if (c == 0 && threadIdx.x == 0) {
     d.state[ST_CUR0] = r0;
@@ -1658,7 +2124,7 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
 
 void launch_round_resume(const Dev &d, hipStream_t s) {
   k_round_resume<<<d.n, 256, 0, s>>>(d);
-  if (d.fd_cols) launch_cand_rows(d, 1, s);
+  if (d.fd_cols || d.wide_cols) launch_cand_rows(d, 1, s);
 }
 
 // A chain with no event in the segment has no last-row tile to write
@@ -1694,7 +2160,7 @@ __global__ __launch_bounds__(256) void k_cand16_init(Dev d) {
 }
 
 void launch_round_init(const Dev &d, hipStream_t s) {
-  if (round2_eligible(d)) launch_cand_rows(d, 0, s);
+  if (round2_eligible(d) || d.wide_cols) launch_cand_rows(d, 0, s);
   else if (d.cand16 && !d.fd_rows) k_cand16_init<<<d.n, 256, 0, s>>>(d);
 }
 
@@ -1711,9 +2177,11 @@ void configure_round_kernels() {
   CFG((k_round_wide<1, false>)); CFG((k_round_wide<2, false>)); CFG((k_round_wide<4, false>));
   CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
+  CFG((k_round_wide<4, true, true>)); CFG((k_round_wide<8, true, true>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
+  CFG(k_round2p<1>); CFG(k_round2p<2>); CFG(k_round2p<4>);
   CFG(k_round_solo);
 #undef CFG
 }
@@ -1745,8 +2213,13 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   const bool wide = d.n > 256 / lpc;
   if (wide && round_p16(d) && !d.fd_rows && (lpc == 4 || lpc == 8)) {
     const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
-    if (lpc == 4) k_round_wide<4, true><<<d.n, 256, wb16, s>>>(d, p);
-    else k_round_wide<8, true><<<d.n, 256, wb16, s>>>(d, p);
+    if (d.wide_cols) {
+      if (lpc == 4) k_round_wide<4, true, true><<<d.n, 256, wb16, s>>>(d, p);
+      else k_round_wide<8, true, true><<<d.n, 256, wb16, s>>>(d, p);
+    } else {
+      if (lpc == 4) k_round_wide<4, true><<<d.n, 256, wb16, s>>>(d, p);
+      else k_round_wide<8, true><<<d.n, 256, wb16, s>>>(d, p);
+    }
     return;
   }
   const size_t wbytes = wide ? (size_t)WROWS * lpc * (PIECES + 1) * 16 : (size_t)WROWS * (d.npad + SCAN_PAD) * 4;

@@ -368,7 +368,7 @@ def test_chunk_sweep_wild(monkeypatch):
 
 
 @pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p8_single", "p8g_tight_single",
-                                  "p16", "p32"])
+                                  "p16", "p32", "fdt_p8", "fdt_p16"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -383,7 +383,13 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     path for chains beyond P16_MAXLEN).  *_single: one candidate's search per
     lane group instead of two interleaved (BH_ROUND_ILP2=0, its own tag check
     and cand8 read).  n = 160 / 300 leave the last lanes of a candidate's
-    group past the end of its byte row."""
+    group past the end of its byte row.  The default loop reads its windows,
+    its candidates' FD rows (searched from the previous candidate's) and
+    fame's LA rows from the dataflow's column-major LA; fdt_*: the loop over
+    the transposed row-major LA and the complete FDT (BH_WIDE_ROWS=1)."""
+    if rows.startswith("fdt_"):
+        monkeypatch.setenv("BH_WIDE_ROWS", "1")
+        rows = rows[len("fdt_"):]
     if rows.endswith("_single"):
         monkeypatch.setenv("BH_ROUND_ILP2", "0")
         rows = rows[:-len("_single")]
@@ -665,6 +671,41 @@ def test_round2_la_col(monkeypatch, variant, n, N, seed, lag, K):
     _random_parity(n, N, seed, lag)
     if n == 128 and K == 1:
         _wild_parity(128, 40_000, 0xBC, 35_000)
+
+
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xC0, 0, 1), (100, 50_000, 0xC1, 4, 3),
+                                            (32, 40_000, 0xC2, 0, 4), (7, 5_000, 0xC3, 2, 2), (64, 40_000, 0xC4, 21, 1)])
+def test_round2_persistent(monkeypatch, n, N, seed, lag, K):
+    """The n <= 128 round loop as one launch (k_round2p, BH_ROUND_PERSIST=1):
+    a grid barrier per iteration, candidates' FD rows and boundaries handed
+    over through sc1 stores and loads, every workgroup ending the loop by
+    itself -- through segments (resumed candidates), lagging peers, padding
+    columns (npad > n) and a 7-chain grid; then incremental calls."""
+    monkeypatch.setenv("BH_ROUND_PERSIST", "1")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    _random_parity(n, N, seed, lag)
+    if n == 128 and K == 1:
+        _wild_parity(128, 40_000, 0xC5, 35_000)
+
+
+def test_round2_persistent_incremental(monkeypatch):
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    from test_gpu_schedule import _wire_batches
+    monkeypatch.setenv("BH_ROUND_PERSIST", "1")
+    n, N, step = 96, 40_000, 5_000
+    d = Dag(n, N, 0xC6, lagging=3, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not np.asarray(hg.insert_events(*batch(lo, hi))).any()
+        hg.run_consensus()
+        _compare(o, hg, f"persistent after [0, {hi})")
 
 
 @pytest.mark.parametrize("n,N,seed,lag,K", [(64, 40_000, 0xBD, 21, 4), (128, 60_000, 0xBE, 40, 3)])
