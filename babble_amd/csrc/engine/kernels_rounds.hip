@@ -1040,6 +1040,64 @@ void launch_cand_rows(const Dev &d, int from_resume, hipStream_t s) {
   k_cand_rows<<<d.n, 1024, 0, s>>>(d, from_resume);
 }
 
+// The hand-off's per-lane inputs (k_round2 / k_round2p): chain i = t / 8
+// (8 lanes per chain, n <= 128 = nt / 8), its first row and view length,
+// the previous candidate's entry j0 = FD[(c, B[r][c])][i], and the lane's
+// 8 rows of LA[.][c] on chain i: 2 aligned 16-B pieces at ab + 8 (t % 8)
+// (ab = chain i's row of j0 rounded down to 4; FDB = 64 rows per chain).
+struct HandIn {
+  int32_t j0, cs, len;
+  int4 fb[2];
+};
+
+__device__ __forceinline__ void hand_load(const int32_t *colc, HandIn &h) {
+  const int l8 = threadIdx.x & 7;
+  const bool live = h.j0 != FD_NONE;
+  const int32_t a = live ? (h.cs + h.j0) & ~3 : 0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    h.fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 8 * l8 + 4 * u)) : make_int4(0, 0, 0, 0);
+}
+
+// FD[(c, row)][i] for the lane's chain i: j0 + #{rows from j0 below `row`}
+// among the 64 loaded (a count and a group sum); an entry beyond them (rare)
+// is searched by the wave, chain by chain (first_ge_wave).  Every lane of
+// the chain's group returns it; FD_NONE if no row of the view sees (c, row)
+__device__ __forceinline__ int32_t hand_entry(const int32_t *colc, const HandIn &h, int i, int c, int32_t row) {
+  const int lane = threadIdx.x & 63, l8 = lane & 7;
+  const bool live = h.j0 != FD_NONE;
+  const int32_t a = h.cs + h.j0, ab = a & ~3, end = h.cs + h.len;
+  const int32_t x0 = ab + 8 * l8, elo = a - x0, ehi = end - x0;  // rows a .. end - 1 of the lane's 8
+  int cnt = 0;
+  if (live) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      cnt += (4 * u + 0 >= elo) & (4 * u + 0 < ehi) & (h.fb[u].x < row);
+      cnt += (4 * u + 1 >= elo) & (4 * u + 1 < ehi) & (h.fb[u].y < row);
+      cnt += (4 * u + 2 >= elo) & (4 * u + 2 < ehi) & (h.fb[u].z < row);
+      cnt += (4 * u + 3 >= elo) & (4 * u + 3 < ehi) & (h.fb[u].w < row);
+    }
+  }
+  cnt = group_total<8>(cnt);
+  const int32_t jn = a + cnt, bend = min(ab + FDB, end);
+  int32_t fd = FD_NONE;
+  bool miss = false;
+  if (live) {
+    if (i == c) fd = row;  // an event is its own first descendant
+    else if (jn < bend) fd = jn - h.cs;
+    else miss = bend < end;  // (else: no row of chain i in this view sees the candidate)
+  }
+  unsigned long long mm = __ballot(miss && l8 == 0);
+  while (mm) {  // (rare) the entry lies beyond the 64 rows loaded
+    const int src = __builtin_ctzll(mm);
+    mm &= mm - 1;
+    const int32_t lo = __shfl(bend, src), hi = __shfl(end, src), b = __shfl(h.cs, src);
+    const int32_t j = first_ge_wave(colc, lo, hi, row);
+    if ((lane >> 3) == (src >> 3)) fd = j < hi ? j - b : FD_NONE;
+  }
+  return fd;
+}
+
 template <int PPL, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   constexpr int LPC = 8;
@@ -1084,21 +1142,15 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
       f[u] = pc < q4 ? cf[pc] : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
     }
   }
-  // the hand-off's inputs: chain i = (t + u nt) / 16 of this thread, its
-  // view length and the previous candidate's entry FD[(c, k0)][i]
+  // the hand-off's inputs (HandIn): chain t / 8 of this lane
   const int32_t *colc = d.la_col + (int64_t)c * stride;  // LA[.][c]
-  const int32_t *cfc = d.candfd + ((int64_t)p * n + c) * npad;
-  int32_t hj0[2], hcs[2], hlen[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = (t + u * nt) >> 4;
-    hj0[u] = FD_NONE;
-    hcs[u] = 0;
-    hlen[u] = 0;
+  HandIn hin{FD_NONE, 0, 0, {}};
+  {
+    const int i = t >> 3;
     if (i < n && k0 < len) {
-      hj0[u] = cfc[i];
-      hcs[u] = d.chain_start[i];
-      hlen[u] = d.chain_len[i];
+      hin.j0 = d.candfd[((int64_t)p * n + c) * npad + i];
+      hin.cs = d.chain_start[i];
+      hin.len = d.chain_len[i];
     }
   }
   // the window's pieces: thread t stages column t / 8, rows rb + 4 (t % 8) .. + 3
@@ -1108,15 +1160,7 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   const int4 wv = wi < n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
                          : make_int4(-1, -1, -1, -1);
   if (done) return;
-  // the hand-off's 64 rows of LA[.][c] per chain i (depend on j0 only)
-  int4 fb[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int piece = (t + u * nt) & 15;
-    const bool live = hj0[u] != FD_NONE;
-    const int32_t a = live ? (hcs[u] + hj0[u]) & ~3 : 0;
-    fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 4 * piece)) : make_int4(0, 0, 0, 0);
-  }
+  hand_load(colc, hin);  // the hand-off's 64 rows of LA[.][c] per chain (depend on j0 only)
   const bool act = q < n && bq < lq;
   const int rows = min(HWL - off, max(0, len - k0));  // (the window's rows off .. HWL - 1)
   if (wi < n) {
@@ -1261,46 +1305,8 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
   // ---- hand-off for the next iteration: FD[(c, result)][i] ----
   if (nc > 0 && r + 1 < d.R_cap && result < len) {
-    int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
-    int32_t fdv[2], mlo[2];
-    bool miss[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int j = t + u * nt, i = j >> 4, piece = j & 15;
-      const bool live = hj0[u] != FD_NONE;
-      // rows a .. end - 1 of the 16 B at ab + 4 piece (a = the first row
-      // seeing (c, k0), end = the chain's view)
-      const int32_t a = hcs[u] + hj0[u], ab = a & ~3, end = hcs[u] + hlen[u];
-      const int32_t x0 = ab + 4 * piece, elo = a - x0, ehi = end - x0;
-      int cnt = 0;
-      if (live) {
-        cnt += (0 >= elo) & (0 < ehi) & (fb[u].x < result);
-        cnt += (1 >= elo) & (1 < ehi) & (fb[u].y < result);
-        cnt += (2 >= elo) & (2 < ehi) & (fb[u].z < result);
-        cnt += (3 >= elo) & (3 < ehi) & (fb[u].w < result);
-      }
-      cnt = group_total<16>(cnt);
-      const int32_t jn = a + cnt, bend = min(ab + FDB, end);
-      fdv[u] = FD_NONE;
-      miss[u] = false;
-      mlo[u] = 0;
-      if (live) {
-        if (i == c) fdv[u] = result;  // an event is its own first descendant
-        else if (jn < bend) fdv[u] = jn - hcs[u];
-        else if (bend < end) { miss[u] = true; mlo[u] = bend - hcs[u]; }
-        // else: no row of chain i in this view sees the candidate
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (__any(miss[u])) {  // (rare) the entry lies beyond the 64 rows loaded
-        if (d.diag && lane == 0) atomicAdd(&d.diag[DG_RD_HMISS], 1ull);
-        const int32_t jm = first_ge16(colc + hcs[u], mlo[u], hlen[u], result, miss[u], true);
-        if (miss[u]) fdv[u] = jm < hlen[u] ? jm : FD_NONE;
-      }
-      const int j = t + u * nt;
-      if ((j & 15) == 0 && (j >> 4) < npad) cf[j >> 4] = fdv[u];
-    }
+    const int32_t fdv = hand_entry(colc, hin, t >> 3, c, result);
+    if ((t & 7) == 0 && (t >> 3) < npad) d.candfd[((int64_t)(p ^ 1) * n + c) * npad + (t >> 3)] = fdv;
     // fame's inputs for the new candidate y = (c, result): its LA row (from
     // the window in LDS) and SS(y, q) over the candidates q of round r = the
     // ballots of the probe that verified y's row.  Raw ballots, one aligned
@@ -1387,27 +1393,19 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   const __amdgpu_buffer_rsrc_t cfr = __builtin_amdgcn_make_buffer_rsrc(d.candfd, (short)0, 0x7fffffff, 0x00020000);
   int32_t r = d.state[ST_CUR0];  // the first iteration has parity 0
   int32_t k0 = d.Bp[c];
-  int32_t hcs[2], hlen[2], hj0[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = (t + u * nt) >> 4;
-    hcs[u] = i < n ? d.chain_start[i] : 0;
-    hlen[u] = i < n ? d.chain_len[i] : 0;
-    hj0[u] = i < n && k0 < len ? d.candfd[(int64_t)c * npad + i] : FD_NONE;
+  HandIn hin{FD_NONE, 0, 0, {}};  // chain t / 8's hand-off inputs
+  if ((t >> 3) < n) {
+    hin.cs = d.chain_start[t >> 3];
+    hin.len = d.chain_len[t >> 3];
+    if (k0 < len) hin.j0 = d.candfd[(int64_t)c * npad + (t >> 3)];
   }
   const int wi = t >> 3, wr4 = 4 * (t & 7);
-  int4 wv, fb[2];
-  auto own_loads = [&]() {  // chain c's window from k0 and its hand-off rows from hj0
+  int4 wv;
+  auto own_loads = [&]() {  // chain c's window from k0 and its hand-off rows from j0
     const int32_t rb = (cs + k0) & ~3;
     wv = wi < n && k0 < len ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
                             : make_int4(-1, -1, -1, -1);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int piece = (t + u * nt) & 15;
-      const bool live = hj0[u] != FD_NONE;
-      const int32_t a = live ? (hcs[u] + hj0[u]) & ~3 : 0;
-      fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 4 * piece)) : make_int4(0, 0, 0, 0);
-    }
+    hand_load(colc, hin);
   };
   own_loads();
   if (t == 0) sh_fail = 0;
@@ -1546,45 +1544,13 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       }
       break;
     }
-    // ---- hand-off: FD[(c, result)][i] (k_round2's count) ----
-    int32_t fdv[2] = {FD_NONE, FD_NONE};
+    // ---- hand-off: FD[(c, result)][i] ----
+    int32_t fdv = FD_NONE;
     if (result < len) {
-      int32_t mlo[2];
-      bool miss[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int j = t + u * nt, i = j >> 4, piece = j & 15;
-        const bool live = hj0[u] != FD_NONE;
-        const int32_t a = hcs[u] + hj0[u], ab = a & ~3, end = hcs[u] + hlen[u];
-        const int32_t x0 = ab + 4 * piece, elo = a - x0, ehi = end - x0;
-        int cnt = 0;
-        if (live) {
-          cnt += (0 >= elo) & (0 < ehi) & (fb[u].x < result);
-          cnt += (1 >= elo) & (1 < ehi) & (fb[u].y < result);
-          cnt += (2 >= elo) & (2 < ehi) & (fb[u].z < result);
-          cnt += (3 >= elo) & (3 < ehi) & (fb[u].w < result);
-        }
-        cnt = group_total<16>(cnt);
-        const int32_t jn = a + cnt, bend = min(ab + FDB, end);
-        miss[u] = false;
-        mlo[u] = 0;
-        if (live) {
-          if (i == c) fdv[u] = result;
-          else if (jn < bend) fdv[u] = jn - hcs[u];
-          else if (bend < end) { miss[u] = true; mlo[u] = bend - hcs[u]; }
-        }
-      }
-      int32_t *cf = d.candfd + ((int64_t)(p ^ 1) * n + c) * npad;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (__any(miss[u])) {
-          const int32_t jm = first_ge16(colc + hcs[u], mlo[u], hlen[u], result, miss[u], true);
-          if (miss[u]) fdv[u] = jm < hlen[u] ? jm : FD_NONE;
-        }
-        const int j = t + u * nt;
-        if ((j & 15) == 0 && (j >> 4) < npad)
-          __hip_atomic_store(cf + (j >> 4), fdv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      fdv = hand_entry(colc, hin, t >> 3, c, result);
+      if ((t & 7) == 0 && (t >> 3) < npad)
+        __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + (t >> 3), fdv, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
       if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
     }
@@ -1599,8 +1565,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     ++r;
     p ^= 1;
     k0 = result;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) hj0[u] = result < len ? fdv[u] : FD_NONE;
+    hin.j0 = result < len ? fdv : FD_NONE;
     own_loads();  // lands during the wait
     if (t == 0) {
       const int32_t target = (it + 1) * G;
