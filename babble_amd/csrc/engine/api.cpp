@@ -844,8 +844,8 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // candidates' FD rows, fame's LA rows; k_round_wide<*, true, true>) --
   // BH_WIDE_ROWS=1 keeps the FDT / row-major LA loop (A/B)
   static const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
-  static const bool wide_rows_env = !getenv("BH_WIDE_COLS") || !atoi(getenv("BH_WIDE_COLS")) ||
-                                    (getenv("BH_WIDE_ROWS") && atoi(getenv("BH_WIDE_ROWS")));  // (off until verified)
+  const bool wide_rows_env = !getenv("BH_WIDE_COLS") || !atoi(getenv("BH_WIDE_COLS")) ||
+                             (getenv("BH_WIDE_ROWS") && atoi(getenv("BH_WIDE_ROWS")));  // (off until verified; read per call: the tests switch it)
   d.wide_cols = wide && !sp && !h->reset_on && !wide_rows_env && !eager_env && bh::round_p16(d) && d.cla && d.n <= 512;
   const bool eager = !sp && ((wide && !d.wide_cols) || h->reset_on || eager_env || bh::round_solo_eligible(d) ||
                              d.round_src_rows);

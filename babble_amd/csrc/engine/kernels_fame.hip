@@ -262,8 +262,11 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   const int r = r0 + (int)blockIdx.x, t = threadIdx.x, nt = blockDim.x;
   const int n = d.n, npad = d.npad, sm = d.sm;
   // cla rows of rounds r + 1 (first votes) and r (minLA), unless a later
-  // round of this loop reused their ring slot: then la_at
-  const bool cy = d.use_cla && r + 1 > R - d.cla_span, cx = d.use_cla && r > R - d.cla_span;
+  // round of this loop reused their ring slot, or the round lies below the
+  // loop's first round (a Reset hashgraph's fiat rounds < r0 = rbase, which
+  // no loop wrote and the ring does not hold): then la_at
+  const bool cy = d.use_cla && r + 1 >= d.r0 && r + 1 > R - d.cla_span;
+  const bool cx = d.use_cla && r >= d.r0 && r > R - d.cla_span;
   if (t < NW) L.wx[t] = fame_wmask_word(d, r, t);
   for (int q = t; q < MAXN; q += nt) {
     L.dec[q] = 0;

@@ -190,9 +190,10 @@ __device__ __forceinline__ int32_t first_ge_wave(const int32_t *col, int32_t lo,
 // (an advance of more than ~45 rows) is searched by the wave
 // (first_ge_wave).  Writes cand16 (16-bit FD + 1), cand8 against the shared
 // base (as handoff_wide) and the candidate's LA row into cla (fame).
+template <int NT>
 __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, int32_t row, const int32_t *Bcur,
                                                   int32_t rnext) {
-  constexpr int K = 8, HR = 48;  // chains per thread (n <= 512), rows per chain
+  constexpr int K = 2048 / NT, HR = 48, KL = 512 / NT;  // chains per thread (n <= 512), rows per chain, LA values per thread
   const int t = threadIdx.x, lane = t & 63, l4 = t & 3;
   const int n = d.n, npad = d.npad, w16 = (npad + 7) / 8 * 4, w8 = (npad + 15) / 16 * 16;
   const int64_t stride = la_col_stride(d);
@@ -202,16 +203,16 @@ __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, in
   const bool g = d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;
   uint8_t *dst8 = g ? d.cand8 + ((int64_t)(p ^ 1) * n + c) * w8 : nullptr;
   const int64_t crow = (int64_t)d.chain_start[c] + row;
-  int32_t la[2];
+  int32_t la[KL];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int i = t + 256 * k;
+  for (int k = 0; k < KL; ++k) {
+    const int i = t + NT * k;
     la[k] = i < n ? d.la_col[(int64_t)i * stride + crow] : -1;
   }
   int32_t a[K], cs[K], end[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int i = (t >> 2) + 64 * k;
+    const int i = (t >> 2) + (NT / 4) * k;
     const uint32_t h = i < n ? prev[i] : 0xFFFFu;
     cs[k] = i < n ? d.chain_start[i] : 0;
     end[k] = i < n ? cs[k] + d.chain_len[i] : 0;
@@ -223,13 +224,14 @@ __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, in
 #pragma unroll
     for (int u = 0; u < 3; ++u)
       v[k][u] = a[k] >= 0 ? *reinterpret_cast<const int4 *>(colc + ((a[k] & ~3) + 12 * l4 + 4 * u)) : make_int4(0, 0, 0, 0);
-  if (t < npad) d.cla[cla_row(d, c, rnext) * npad + t] = la[0];
-  if (t + 256 < npad) d.cla[cla_row(d, c, rnext) * npad + t + 256] = la[1];
+#pragma unroll
+  for (int k = 0; k < KL; ++k)
+    if (t + NT * k < npad) d.cla[cla_row(d, c, rnext) * npad + t + NT * k] = la[k];
   int32_t fd[K];
   bool miss[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int i = (t >> 2) + 64 * k;
+    const int i = (t >> 2) + (NT / 4) * k;
     const int32_t ab = a[k] & ~3, x0 = ab + 12 * l4, elo = a[k] - x0, ehi = end[k] - x0;
     int cnt = 0;
 #pragma unroll
@@ -260,7 +262,7 @@ __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, in
       const int32_t j = first_ge_wave(colc, lo, hi, row);
       if (lane == src) fd[k] = j < hi ? j - b : FD_NONE;
     }
-    const int i = (t >> 2) + 64 * k;
+    const int i = (t >> 2) + (NT / 4) * k;
     if (l4 == 0 && i < 2 * w16) {
       const uint32_t h = i < n ? min((uint32_t)fd[k] + 1u, 0xFFFFu) : 0xFFFFu;  // FD_NONE + 1 wraps to 2^31
       dst16[i] = (uint16_t)h;
@@ -433,8 +435,8 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // P16: the same search over 16-bit rows (cand16, LA converted while staged):
 // lane `part` owns 8 pieces of 8 columns, half the LDS reads and 3/5 of the
 // compare work per probe.
-template <int LPC, bool P16, bool COLS = false>
-__global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU
+template <int LPC, bool P16, bool COLS = false, int NT = 256>
+__global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU (NT / 128 waves per SIMD)
   extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
   constexpr int PP = P16 ? 8 : PIECES;  // 16-B pieces per lane
   constexpr int WRS4 = LPC * (PP + 1);
@@ -454,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   const int r = d.state[ST_CUR0 + p];
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
   if (done) return;
-  constexpr int CPP = 256 / LPC;
+  constexpr int CPP = NT / LPC;
   const int part = t % LPC;
   const int npass = (n + CPP - 1) / CPP;
   if (t == 0) sh_nc = 0;
@@ -478,7 +480,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     if (wrows <= 0) break;
     // COLS: the window's 36 aligned rows of every column from la_col, issued
     // before the fit check below reads its two rows
-    constexpr int CQ = LPC * 16, CT = 256 / CQ, CNP = (9 + CT - 1) / CT;  // column quads, threads per quad, pieces per thread
+    constexpr int CQ = LPC * 16, CT = NT / CQ, CNP = (9 + CT - 1) / CT;  // column quads, threads per quad, pieces per thread
     const int cg = t % CQ, ch = t / CQ;
     const int32_t crb = (cs + wk0) & ~3;
     const int coff = cs + wk0 - crb;
@@ -580,7 +582,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
       // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
       constexpr int RP8 = LPC * PP8;
       const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-      for (int i = t; i < wrows * RP8; i += 256) {
+      for (int i = t; i < wrows * RP8; i += NT) {
         const int row = i / RP8, pc = i - row * RP8;
         uint32_t w[4];
 #pragma unroll
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
     } else {
       constexpr int RP = LPC * PP;  // pieces per padded row
       const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-      for (int i = t; i < wrows * RP; i += 256) {
+      for (int i = t; i < wrows * RP; i += NT) {
         const int row = i / RP, pc = i - row * RP;
         if constexpr (P16) {  // columns 8pc .. 8pc + 7 (npad is a multiple of 4)
           const int4 a = src[row * q4 + min(2 * pc, q4 - 1)];
@@ -645,8 +647,10 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
           const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
           const int nvalid = f16q - part * PP;
           const uint4 *bb = reinterpret_cast<const uint4 *>(wb2) + part * PP;
+          // (rare: in halves, so the 512-thread variant's 128 registers hold it)
 #pragma unroll
           for (int u = 0; u < PP; ++u) {
+            if (NT > 256 && u == PP / 2) __builtin_amdgcn_sched_barrier(0);
             const int4 v = fr[min(u, max(nvalid - 1, 0))];
             const uint4 b = bb[u];
             const bool ok = u < nvalid;
@@ -871,7 +875,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   // most y's row (stronglySee is monotone along the chain)
   if (d.ssw && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
     const int res = sh_res;
-    for (int q0 = 0; q0 < 512; q0 += 256) {
+    for (int q0 = 0; q0 < 512; q0 += NT) {
       const int q = q0 + t;
       const unsigned long long m = __ballot(q < n && tq_s[q] <= res);
       if (lane == 0) d.ssw[ballot_row(d, c, r + 1) * 8 + (q0 >> 6) + wave] = m;
@@ -879,7 +883,7 @@ __global__ __launch_bounds__(256, 2) void k_round_wide(Dev d, int p) {  // 2 wor
   }
   // the hand-off: the new candidate's FD row for the next iteration
   if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
-    if constexpr (COLS) handoff_wide_cols(d, p, c, result, Bp, r + 1);
+    if constexpr (COLS) handoff_wide_cols<NT>(d, p, c, result, Bp, r + 1);
     else handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
   }
   if (t == 0) {
@@ -2143,6 +2147,8 @@ void configure_round_kernels() {
   CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
   CFG((k_round_wide<4, true, true>)); CFG((k_round_wide<8, true, true>));
+  CFG((k_round_wide<4, true, false, 512>)); CFG((k_round_wide<8, true, false, 512>));
+  CFG((k_round_wide<4, true, true, 512>)); CFG((k_round_wide<8, true, true, 512>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
@@ -2178,7 +2184,18 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   const bool wide = d.n > 256 / lpc;
   if (wide && round_p16(d) && !d.fd_rows && (lpc == 4 || lpc == 8)) {
     const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
-    if (d.wide_cols) {
+    // BH_WIDE_NT=512: 512-thread workgroups (4 waves per SIMD at 2 per CU,
+    // registers capped at 128) -- the A/B against 256 threads, 2 waves per SIMD
+    const int nt = getenv("BH_WIDE_NT") && atoi(getenv("BH_WIDE_NT")) == 512 ? 512 : 256;  // (read per capture)
+    if (nt == 512) {
+      if (d.wide_cols) {
+        if (lpc == 4) k_round_wide<4, true, true, 512><<<d.n, 512, wb16, s>>>(d, p);
+        else k_round_wide<8, true, true, 512><<<d.n, 512, wb16, s>>>(d, p);
+      } else {
+        if (lpc == 4) k_round_wide<4, true, false, 512><<<d.n, 512, wb16, s>>>(d, p);
+        else k_round_wide<8, true, false, 512><<<d.n, 512, wb16, s>>>(d, p);
+      }
+    } else if (d.wide_cols) {
       if (lpc == 4) k_round_wide<4, true, true><<<d.n, 256, wb16, s>>>(d, p);
       else k_round_wide<8, true, true><<<d.n, 256, wb16, s>>>(d, p);
     } else {
