@@ -847,7 +847,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   const bool wide_rows_env = !getenv("BH_WIDE_COLS") || !atoi(getenv("BH_WIDE_COLS")) ||
                              (getenv("BH_WIDE_ROWS") && atoi(getenv("BH_WIDE_ROWS")));  // (off until verified; read per call: the tests switch it)
   d.wide_cols = wide && !sp && !h->reset_on && !wide_rows_env && !eager_env && bh::round_p16(d) && d.cla && d.n <= 512;
-  const bool eager = !sp && ((wide && !d.wide_cols) || h->reset_on || eager_env || bh::round_solo_eligible(d) ||
+  // BH_WIDE_COLS=2 (A/B): the window from the transposed row-major LA, the hand-off from la_col
+  if (d.wide_cols && atoi(getenv("BH_WIDE_COLS")) == 2) d.wide_cols = 2;
+  const bool eager = !sp && ((wide && d.wide_cols != 1) || h->reset_on || eager_env || bh::round_solo_eligible(d) ||
                              d.round_src_rows);
   d.use_cla = (d.fd_cols || d.wide_cols) && !bh::round_solo_eligible(d);
   if (sp) d.round_src_rows = 0;  // the split ships the column-major LA only

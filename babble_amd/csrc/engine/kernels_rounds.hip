@@ -181,7 +181,7 @@ __device__ __forceinline__ int32_t first_ge_wave(const int32_t *col, int32_t lo,
   return m ? lo + __builtin_ctzll(m) : hi;
 }
 
-// k_round_wide<*, true, COLS>'s hand-off of the new candidate (c, row) for
+// k_round_wide<*, true, 1 / 2>'s hand-off of the new candidate (c, row) for
 // iteration r + 1 from the dataflow's column-major LA (no FDT):
 // FD[(c, row)][i] = min{j : LA[(i, j)][c] >= row} is non-decreasing in the
 // candidate's row, so chain i's entry starts at the previous candidate's
@@ -435,7 +435,10 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // P16: the same search over 16-bit rows (cand16, LA converted while staged):
 // lane `part` owns 8 pieces of 8 columns, half the LDS reads and 3/5 of the
 // compare work per probe.
-template <int LPC, bool P16, bool COLS = false, int NT = 256>
+// COLS: 0 = window rows from the row-major LA, candidates' FD rows gathered
+// from FDT (handoff_wide); 1 = both from the column-major LA (no transpose);
+// 2 = window rows from the row-major LA, hand-off from la_col (A/B)
+template <int LPC, bool P16, int COLS = 0, int NT = 256>
 __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU (NT / 128 waves per SIMD)
   extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
   constexpr int PP = P16 ? 8 : PIECES;  // 16-B pieces per lane
@@ -484,8 +487,8 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     const int cg = t % CQ, ch = t / CQ;
     const int32_t crb = (cs + wk0) & ~3;
     const int coff = cs + wk0 - crb;
-    int4 cpv[COLS ? CNP : 1][4];
-    if constexpr (COLS) {
+    int4 cpv[COLS == 1 ? CNP : 1][4];
+    if constexpr (COLS == 1) {
 #pragma unroll
       for (int u = 0; u < CNP; ++u) {
         const int pc = ch + u * CT;
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
         // LA of column i at the window's first / last row (-1 past n, 0 past npad)
         auto la_w = [&](int i, int last) -> int32_t {
           if (i >= npad) return 0;
-          if constexpr (COLS)
+          if constexpr (COLS == 1)
             return i < n ? d.la_col[(int64_t)i * la_col_stride(d) + cs + wk0 + (last ? wrows - 1 : 0)] : -1;
           else
             return (last ? r1p : r0p)[i];
@@ -543,7 +546,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     }
     const uint32_t *wb2 = p8g ? gbase2 : wbase2;
     __syncthreads();
-    if constexpr (COLS) {
+    if constexpr (COLS == 1) {
       // quad cg's 4 columns, 4 rows per piece: P8 one dword per row (bytes
       // x | 0x80, as below), P16 two (16-bit LA + 1 pairs); window row = the
       // piece's row - coff, rows outside [0, wrows) skipped
@@ -647,10 +650,8 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
           const int nvalid = f16q - part * PP;
           const uint4 *bb = reinterpret_cast<const uint4 *>(wb2) + part * PP;
-          // (rare: in halves, so the 512-thread variant's 128 registers hold it)
 #pragma unroll
           for (int u = 0; u < PP; ++u) {
-            if (NT > 256 && u == PP / 2) __builtin_amdgcn_sched_barrier(0);
             const int4 v = fr[min(u, max(nvalid - 1, 0))];
             const uint4 b = bb[u];
             const bool ok = u < nvalid;
@@ -883,7 +884,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   }
   // the hand-off: the new candidate's FD row for the next iteration
   if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
-    if constexpr (COLS) handoff_wide_cols<NT>(d, p, c, result, Bp, r + 1);
+    if constexpr (COLS != 0) handoff_wide_cols<NT>(d, p, c, result, Bp, r + 1);
     else handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
   }
   if (t == 0) {
@@ -2146,9 +2147,8 @@ void configure_round_kernels() {
   CFG((k_round_wide<1, false>)); CFG((k_round_wide<2, false>)); CFG((k_round_wide<4, false>));
   CFG((k_round_wide<8, false>)); CFG((k_round_wide<16, false>));
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
-  CFG((k_round_wide<4, true, true>)); CFG((k_round_wide<8, true, true>));
-  CFG((k_round_wide<4, true, false, 512>)); CFG((k_round_wide<8, true, false, 512>));
-  CFG((k_round_wide<4, true, true, 512>)); CFG((k_round_wide<8, true, true, 512>));
+  CFG((k_round_wide<4, true, 1>)); CFG((k_round_wide<8, true, 1>));
+  CFG((k_round_wide<4, true, 2>)); CFG((k_round_wide<8, true, 2>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
@@ -2184,20 +2184,12 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
   const bool wide = d.n > 256 / lpc;
   if (wide && round_p16(d) && !d.fd_rows && (lpc == 4 || lpc == 8)) {
     const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
-    // BH_WIDE_NT=512: 512-thread workgroups (4 waves per SIMD at 2 per CU,
-    // registers capped at 128) -- the A/B against 256 threads, 2 waves per SIMD
-    const int nt = getenv("BH_WIDE_NT") && atoi(getenv("BH_WIDE_NT")) == 512 ? 512 : 256;  // (read per capture)
-    if (nt == 512) {
-      if (d.wide_cols) {
-        if (lpc == 4) k_round_wide<4, true, true, 512><<<d.n, 512, wb16, s>>>(d, p);
-        else k_round_wide<8, true, true, 512><<<d.n, 512, wb16, s>>>(d, p);
-      } else {
-        if (lpc == 4) k_round_wide<4, true, false, 512><<<d.n, 512, wb16, s>>>(d, p);
-        else k_round_wide<8, true, false, 512><<<d.n, 512, wb16, s>>>(d, p);
-      }
+    if (d.wide_cols == 2) {  // (A/B: window rows from la, hand-off from la_col)
+      if (lpc == 4) k_round_wide<4, true, 2><<<d.n, 256, wb16, s>>>(d, p);
+      else k_round_wide<8, true, 2><<<d.n, 256, wb16, s>>>(d, p);
     } else if (d.wide_cols) {
-      if (lpc == 4) k_round_wide<4, true, true><<<d.n, 256, wb16, s>>>(d, p);
-      else k_round_wide<8, true, true><<<d.n, 256, wb16, s>>>(d, p);
+      if (lpc == 4) k_round_wide<4, true, 1><<<d.n, 256, wb16, s>>>(d, p);
+      else k_round_wide<8, true, 1><<<d.n, 256, wb16, s>>>(d, p);
     } else {
       if (lpc == 4) k_round_wide<4, true><<<d.n, 256, wb16, s>>>(d, p);
       else k_round_wide<8, true><<<d.n, 256, wb16, s>>>(d, p);

@@ -369,7 +369,7 @@ def test_chunk_sweep_wild(monkeypatch):
 
 @pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p8_single", "p8g_tight_single",
                                   "p16", "p32", "fdt_p8", "fdt_p16", "cols_p8", "cols_p8g_tight", "cols_p16",
-                                  "nt512_p8", "nt512_p8g_tight", "nt512_p16", "nt512_cols_p8"])
+                                  "cols2_p8", "cols2_p16"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -388,11 +388,11 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     its candidates' FD rows (searched from the previous candidate's) and
     fame's LA rows from the dataflow's column-major LA; fdt_*: the loop over
     the transposed row-major LA and the complete FDT (BH_WIDE_ROWS=1).
-    nt512_*: 512-thread workgroups (BH_WIDE_NT=512, four waves per SIMD);
-    cols_*: the loop over the column-major LA (BH_WIDE_COLS=1)."""
-    if rows.startswith("nt512_"):
-        monkeypatch.setenv("BH_WIDE_NT", "512")
-        rows = rows[len("nt512_"):]
+    cols_*: the loop over the column-major LA (BH_WIDE_COLS=1); cols2_*: the
+    window from the row-major LA, the hand-off from la_col (BH_WIDE_COLS=2)."""
+    if rows.startswith("cols2_"):
+        monkeypatch.setenv("BH_WIDE_COLS", "2")
+        rows = rows[len("cols2_"):]
     if rows.startswith("cols_"):
         monkeypatch.setenv("BH_WIDE_COLS", "1")
         rows = rows[len("cols_"):]
