@@ -24,7 +24,7 @@ SYMBOLS = (
     "bh_run_consensus", "bh_synchronize", "bh_reset_consensus", "bh_reset", "bh_get_stats", "bh_get_event_meta",
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_round_info", "bh_get_coordinates", "bh_query_events", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
-    "bh_get_pipeline", "bh_hash_bodies", "bh_verify_signatures", "bh_set_event_bytes", "bh_get_frame_roots",
+    "bh_get_pipeline", "bh_get_loop_stats", "bh_hash_bodies", "bh_verify_signatures", "bh_set_event_bytes", "bh_get_frame_roots",
     "bh_get_frame_json", "bh_get_block_hashes", "bh_get_block_json", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
 )
 
@@ -110,6 +110,8 @@ def load():
     L.bh_get_profile_kernel.restype = C.c_char_p
     L.bh_get_pipeline.argtypes = [P, C.POINTER(I32), C.POINTER(I64)]
     L.bh_get_pipeline.restype = C.c_int
+    L.bh_get_loop_stats.argtypes = [P, C.POINTER(I64), C.POINTER(I64)]
+    L.bh_get_loop_stats.restype = C.c_int
     L.bh_hash_bodies.argtypes = [P, VP, VP, I64, VP]
     L.bh_hash_bodies.restype = C.c_int
     L.bh_verify_signatures.argtypes = [P, VP, VP, VP, VP, I64, VP, I32, VP]

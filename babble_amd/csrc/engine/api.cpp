@@ -40,7 +40,7 @@ void free_all(bh_handle *h) {
                   d.wofs, d.wcnt, d.wids, d.wrow, d.state, d.round, d.witness, d.fame,
                   d.decided, d.nfam, d.minla, d.rr, d.frame_cnt, d.frame_ofs, d.frame_cur,
                   d.blk_of_frame, d.order, d.cons_pos, d.frame_ntx, d.counters, d.diag, d.trapped, d.blocked,
-                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.cla, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw, d.pbar,
+                  d.wfame, d.frame_loaded, d.Bp, d.fd, d.fdt, d.cla, d.last_la, d.rq, d.candfd, d.cand8, d.c8tag, d.Bq, d.opdesc, d.lt_row, d.ssm, d.ssw, d.pbar, d.psnap,
                   d.la_col != d.fdt ? d.la_col : nullptr,  // la_ev aliases fdt
                   d.chain_base, d.lt_seed, d.root_next, d.root_sp_round, d.rflag, d.ext_lt, d.fw, d.rexists};
   for (void *p : ptrs)
@@ -202,17 +202,31 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     return BH_OK;
   }
   if (bh::round_persist_eligible(v)) {  // one launch, a grid barrier per iteration (k_round2p)
+    // the loop's inputs, kept: a barrier that gives up (ST_ERR = 3) leaves
+    // them overwritten, and the per-iteration launches below start again from them
+    const int n = v.n;
+    int32_t *snap_bp = v.psnap, *snap_cf = v.psnap + n, *snap_st = v.psnap + n + (size_t)n * v.npad;
+    HIPCHK(h, hipMemcpyAsync(snap_bp, v.Bp, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(snap_cf, v.candfd, (size_t)n * v.npad * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(snap_st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToDevice, s));
     if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));
+    ++h->persist_loops;
     bh::launch_round_persist(v, s);
     HIPCHK(h, hipGetLastError());
     if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
     HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
     float lms = 0;
     if (loop_timing && hipEventElapsedTime(&lms, h->ev_loop[0], h->ev_loop[1]) == hipSuccess) h->loop_ms_acc += lms;
-    if (!st[bh::ST_DONE]) return h->fail(BH_ERR_STATE, "round loop did not terminate");
-    if (st[bh::ST_ERR] == 3) return h->fail(BH_ERR_DEVICE, "the persistent round loop's grid barrier gave up");
-    if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
-    return BH_OK;
+    if (st[bh::ST_DONE] && st[bh::ST_ERR] != 3) {
+      if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
+      return BH_OK;
+    }
+    // the grid barrier gave up (some workgroup was never placed): restore and
+    // take the per-iteration launches (counted in stats.persist_fallbacks)
+    ++h->persist_fallbacks;
+    HIPCHK(h, hipMemcpyAsync(v.Bp, snap_bp, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(v.candfd, snap_cf, (size_t)n * v.npad * 4, hipMemcpyDeviceToDevice, s));
+    HIPCHK(h, hipMemcpyAsync(v.state, snap_st, bh::ST_COUNT * 4, hipMemcpyDeviceToDevice, s));
   }
   if (!no_graph && (rc = build_graph(h, v, graph, graph_dev, ITER_BATCH))) return rc;
   if (!no_graph && (rc = build_graph(h, v, graph_s, graph_dev_s, ITER_FIRST))) return rc;
@@ -1615,7 +1629,8 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.flow_wd = getenv("BH_FLOWW_WATCHDOG") ? atoi(getenv("BH_FLOWW_WATCHDOG")) : (1 << 20);
   d.flow_lt = 1;
   d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
-  d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 0;
+  d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
+  d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
@@ -1687,6 +1702,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 64);
+  if (d.fd_cols) A(&d.psnap, (size_t)n + (size_t)n * d.npad + bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C); A(&d.trapped, C); A(&d.blocked, R1);
   A(&d.wfame, (size_t)d.W_cap); A(&d.frame_loaded, R1);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);
@@ -2601,6 +2617,13 @@ int bh_get_pipeline(bh_handle *h, int32_t *segments, int64_t *incremental_calls)
   if (!h) return BH_ERR_INVALID;
   if (segments) *segments = h->segments_used;
   if (incremental_calls) *incremental_calls = h->inc_calls;
+  return BH_OK;
+}
+
+int bh_get_loop_stats(bh_handle *h, int64_t *persistent_loops, int64_t *persist_fallbacks) {
+  if (!h) return BH_ERR_INVALID;
+  if (persistent_loops) *persistent_loops = h->persist_loops;
+  if (persist_fallbacks) *persist_fallbacks = h->persist_fallbacks;
   return BH_OK;
 }
 

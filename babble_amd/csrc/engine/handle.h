@@ -120,6 +120,7 @@ struct bh_handle {
   bool rows_stale = false;  // n <= 128 segments built la_col only: row-major LA / FDT wait for a query
   int64_t n_coord = 0;
   int64_t inc_calls = 0;  // DivideRounds calls that resumed (statistics)
+  int64_t persist_loops = 0, persist_fallbacks = 0;  // k_round2p loops run / given up (bh_get_loop_stats)
   std::vector<int32_t> lens_coord;
   // sharding
   int32_t rank = 0, world = 1;

@@ -1374,8 +1374,11 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
 // next hand-off counts from (its new FD row is in registers) -- is issued
 // before the barrier wait and lands during it.  Every workgroup sees the
 // same candidate count, so each decides the loop's end itself.  The spin is
-// bounded (ST_ERR = 3: the barrier gave up).
-constexpr int PBAR_SPIN_LIMIT = 1 << 24;
+// bounded (d.pbar_spin polls, ~0.5 s by default; ST_ERR = 3: the barrier
+// gave up -- the host then restores the loop's inputs and runs one launch per
+// iteration instead).  Co-residency: n <= 128 workgroups of 16 waves fit the
+// 256 compute units beside the segment pipeline's n coordinate workgroups,
+// and those never wait for the loop, so every loop workgroup is placed.
 
 template <int PPL>
 __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
@@ -1577,7 +1580,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       int spins = 0;
       while (__hip_atomic_load(d.pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > PBAR_SPIN_LIMIT) {
+        if (++spins > d.pbar_spin) {
           sh_fail = 1;
           break;
         }

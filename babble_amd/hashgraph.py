@@ -321,6 +321,14 @@ class Hashgraph:
         self._check(self._L.bh_get_pipeline(self._h, C.byref(seg), C.byref(inc)))
         return int(seg.value), int(inc.value)
 
+    def loop_stats(self):
+        """(round loops run as one persistent launch, of which the grid
+        barrier gave up and the per-iteration launches ran them)"""
+        pl = C.c_int64()
+        fb = C.c_int64()
+        self._check(self._L.bh_get_loop_stats(self._h, C.byref(pl), C.byref(fb)))
+        return int(pl.value), int(fb.value)
+
     def profile_kernel(self):
         """Name of the coordinate kernel the last run timed."""
         return self._L.bh_get_profile_kernel(self._h).decode()

@@ -226,6 +226,11 @@ const char *bh_get_profile_kernel(const bh_handle *h);
  * DivideRounds calls so far that resumed from the previous call's device
  * state instead of recomputing the whole DAG */
 int bh_get_pipeline(bh_handle *h, int32_t *segments, int64_t *incremental_calls);
+/* how the round loops ran so far (engine introspection, no reference
+ * counterpart): loops run as one persistent launch (k_round2p, n <= 128),
+ * and of those, loops whose grid barrier gave up and that the per-iteration
+ * launches then ran from the same inputs */
+int bh_get_loop_stats(bh_handle *h, int64_t *persistent_loops, int64_t *persist_fallbacks);
 /* SHA-256 of a batch of event bodies on the device:
  * Event.Hash() = SHA-256 of the body's Go-JSON bytes (event.go:50-56), the
  * digest InsertEvent keys, verifies and takes the coin from

@@ -645,14 +645,18 @@ def test_round_solo_parity(monkeypatch, n, N, seed, lag, K):
         _wild_parity(24, 30_000, 73, 20_000)
 
 
-@pytest.mark.parametrize("variant", ["tq", "rows"])
+@pytest.mark.parametrize("variant", ["persist", "tq", "rows"])
 @pytest.mark.parametrize("n,N,seed,lag,K", [(4, 10_000, 0xBABB1E01, 0, 1), (9, 8_000, 14, 3, 2), (32, 60_000, 15, 0, 3),
                                             (17, 40_000, 31, 5, 4), (48, 40_000, 37, 6, 2)])
 def test_small_n_round_kernels(monkeypatch, variant, n, N, seed, lag, K):
     """k_round2 at n <= 64 (8 lanes per candidate, one or two pieces each,
     8 npad threads): the per-candidate T_q search and the row-probe search
     (BH_ROUND_ROWS=1) against the oracle, alone and inside the segment
-    pipeline; the wild DAG's windows that miss SM continue window by window."""
+    pipeline; the wild DAG's windows that miss SM continue window by window.
+    persist: the default one-launch loop (k_round2p); tq / rows: one launch
+    per iteration (BH_ROUND_PERSIST=0)."""
+    if variant != "persist":
+        monkeypatch.setenv("BH_ROUND_PERSIST", "0")
     if variant == "rows":
         monkeypatch.setenv("BH_ROUND_ROWS", "1")
     monkeypatch.setenv("BH_SEGMENTS", str(K))
@@ -661,7 +665,7 @@ def test_small_n_round_kernels(monkeypatch, variant, n, N, seed, lag, K):
         _wild_parity(24, 30_000, 73, 20_000)
 
 
-@pytest.mark.parametrize("variant", ["tq", "rows", "eager"])
+@pytest.mark.parametrize("variant", ["persist", "tq", "rows", "eager"])
 @pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xB8, 0, 1), (100, 50_000, 0xB9, 4, 3),
                                             (97, 40_000, 0xBA, 0, 2), (72, 30_000, 0xBB, 3, 1)])
 def test_round2_la_col(monkeypatch, variant, n, N, seed, lag, K):
@@ -671,7 +675,10 @@ def test_round2_la_col(monkeypatch, variant, n, N, seed, lag, K):
     hand-off, lagging peers (hand-offs whose FD entries jump past the 64
     rows loaded), segments resumed at candidates searched from scratch;
     rows: the row-probe search; eager: the segments also build the row-major
-    LA and FDT (BH_EAGER_ROWS=1, the round-3 pipeline)."""
+    LA and FDT (BH_EAGER_ROWS=1, the round-3 pipeline); persist: the default
+    one-launch loop, the others one launch per iteration (BH_ROUND_PERSIST=0)."""
+    if variant != "persist":
+        monkeypatch.setenv("BH_ROUND_PERSIST", "0")
     if variant == "rows":
         monkeypatch.setenv("BH_ROUND_ROWS", "1")
     if variant == "eager":
@@ -685,16 +692,30 @@ def test_round2_la_col(monkeypatch, variant, n, N, seed, lag, K):
 @pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xC0, 0, 1), (100, 50_000, 0xC1, 4, 3),
                                             (32, 40_000, 0xC2, 0, 4), (7, 5_000, 0xC3, 2, 2), (64, 40_000, 0xC4, 21, 1)])
 def test_round2_persistent(monkeypatch, n, N, seed, lag, K):
-    """The n <= 128 round loop as one launch (k_round2p, BH_ROUND_PERSIST=1):
+    """The n <= 128 round loop as one launch (k_round2p, the default):
     a grid barrier per iteration, candidates' FD rows and boundaries handed
     over through sc1 stores and loads, every workgroup ending the loop by
     itself -- through segments (resumed candidates), lagging peers, padding
     columns (npad > n) and a 7-chain grid; then incremental calls."""
     monkeypatch.setenv("BH_ROUND_PERSIST", "1")
     monkeypatch.setenv("BH_SEGMENTS", str(K))
-    _random_parity(n, N, seed, lag)
+    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
+    assert loops >= 1 and fallbacks == 0
     if n == 128 and K == 1:
         _wild_parity(128, 40_000, 0xC5, 35_000)
+
+
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 30_000, 0xC7, 0, 1), (64, 30_000, 0xC8, 21, 3)])
+def test_round2_persistent_fallback(monkeypatch, n, N, seed, lag, K):
+    """A grid barrier that gives up (BH_PBAR_SPIN=0: at its first poll that
+    finds a workgroup missing) ends the persistent loop with ST_ERR = 3; the
+    host restores the loop's inputs and runs one launch per iteration, and
+    the results are the oracle's."""
+    monkeypatch.setenv("BH_ROUND_PERSIST", "1")
+    monkeypatch.setenv("BH_PBAR_SPIN", "0")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
+    assert loops >= 1 and fallbacks >= 1
 
 
 def test_round2_persistent_incremental(monkeypatch):
