@@ -1631,6 +1631,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
+  d.pbar_mode = getenv("BH_PBAR") && !strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
@@ -1701,7 +1702,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
-  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 64);
+  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 512);
   if (d.fd_cols) A(&d.psnap, (size_t)n + (size_t)n * d.npad + bh::ST_COUNT);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C); A(&d.trapped, C); A(&d.blocked, R1);
   A(&d.wfame, (size_t)d.W_cap); A(&d.frame_loaded, R1);

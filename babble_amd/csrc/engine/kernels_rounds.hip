@@ -459,6 +459,11 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   const int r = d.state[ST_CUR0 + p];
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
   if (done) return;
+  // BH_DIAG timeline (tools/timeline.py): start, first window staged, search
+  // done, end -- chains < 128 of rounds TL_R0 .. TL_R0 + TL_NR
+  const bool dgt = d.diag != nullptr && t == 0 && c < 128 && r >= TL_R0 && r < TL_R0 + TL_NR;
+  const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+  unsigned long long rt1 = 0, rt2 = 0;
   constexpr int CPP = NT / LPC;
   const int part = t % LPC;
   const int npass = (n + CPP - 1) / CPP;
@@ -622,6 +627,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     }
     if (t <= WROWS) hist[t] = 0;
     __syncthreads();
+    if (dgt && !rt1) rt1 = __builtin_amdgcn_s_memrealtime();
     if (p8 && d.round_ilp2) {
       // byte rows, two candidates per lane group at once (passes pass and
       // pass + 1): their binary searches interleave, so each probe's LDS
@@ -856,6 +862,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       if (d.ssw && part == 0 && q < n) tq_s[q] = (int8_t)(act ? tw : WROWS);
     }
     __syncthreads();
+    if (dgt) rt2 = __builtin_amdgcn_s_memrealtime();
     if (sh_nc == 0) break;
     if (wave == 0) {
       int h = lane < wrows ? hist[lane] : 0;
@@ -886,6 +893,13 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
     if constexpr (COLS != 0) handoff_wide_cols<NT>(d, p, c, result, Bp, r + 1);
     else handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
+  }
+  if (dgt) {
+    unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
+    tl[0] = rt0;
+    tl[1] = rt2;
+    tl[2] = rt1;
+    tl[3] = __builtin_amdgcn_s_memrealtime();
   }
   if (t == 0) {
     if (sh_nc == 0) {
@@ -941,24 +955,29 @@ __device__ __forceinline__ int group_sum(int v) {
 // wave calls it.  One dependent load per pass: a first pass over the 1024
 // rows after lo (16 probes 64 apart, when `near`), then 16-ary narrowing,
 // spans of <= 64 rows finished with 4 rows a lane.
-__device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, int32_t hi, int32_t k, bool on,
-                                              bool near) {
-  const int lane = threadIdx.x & 63, g = lane & 15, gb = lane & 48;
+// GL-lane groups (GL = 16 or 8): GL-ary narrowing, spans of <= 4 GL rows
+// finished with 4 rows a lane; `near`: the first pass covers the 64 GL rows
+// after lo only (an entry just past a hand-off's loaded rows)
+template <int GL>
+__device__ __forceinline__ int32_t first_ge_group(const int32_t *col, int32_t lo, int32_t hi, int32_t k, bool on,
+                                                  bool near) {
+  constexpr uint32_t GM = (1u << GL) - 1u;
+  const int lane = threadIdx.x & 63, g = lane & (GL - 1), gb = lane & (64 - GL);
   while (__any(on)) {
     if (on) {
-      if (hi - lo <= 64) {
+      if (hi - lo <= 4 * GL) {
         const int32_t x = lo + 4 * g;
         int cnt = 0;
 #pragma unroll
         for (int v = 0; v < 4; ++v)
-          cnt += __popc((uint32_t)(__ballot(x + v < hi && col[x + v] < k) >> gb) & 0xFFFFu);
+          cnt += __popc((uint32_t)(__ballot(x + v < hi && col[x + v] < k) >> gb) & GM);
         lo += cnt;
         on = false;
       } else {
-        const int32_t lim = near ? min(hi, lo + 1024) : hi;
-        const int32_t s = (lim - lo + 15) >> 4;
+        const int32_t lim = near ? min(hi, lo + 64 * GL) : hi;
+        const int32_t s = (lim - lo + GL - 1) / GL;
         const int32_t pr = min(lo + (g + 1) * s, lim) - 1;
-        const uint32_t m = (uint32_t)(__ballot(col[pr] >= k) >> gb) & 0xFFFFu;
+        const uint32_t m = (uint32_t)(__ballot(col[pr] >= k) >> gb) & GM;
         if (m) {
           const int f = __builtin_ctz(m);
           hi = min(lo + (f + 1) * s, lim);
@@ -972,6 +991,11 @@ __device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, in
     }
   }
   return lo;
+}
+
+__device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, int32_t hi, int32_t k, bool on,
+                                              bool near) {
+  return first_ge_group<16>(col, lo, hi, k, on, near);
 }
 
 // candidates' FD rows for the first iteration of a loop (parity 0): round 0
@@ -1092,13 +1116,12 @@ __device__ __forceinline__ int32_t hand_entry(const int32_t *colc, const HandIn 
     else if (jn < bend) fd = jn - h.cs;
     else miss = bend < end;  // (else: no row of chain i in this view sees the candidate)
   }
-  unsigned long long mm = __ballot(miss && l8 == 0);
-  while (mm) {  // (rare) the entry lies beyond the 64 rows loaded
-    const int src = __builtin_ctzll(mm);
-    mm &= mm - 1;
-    const int32_t lo = __shfl(bend, src), hi = __shfl(end, src), b = __shfl(h.cs, src);
-    const int32_t j = first_ge_wave(colc, lo, hi, row);
-    if ((lane >> 3) == (src >> 3)) fd = j < hi ? j - b : FD_NONE;
+  // the entry lies beyond the 64 rows loaded (a lagging chain's candidate
+  // jumps far): every such chain's 8 lanes search on at once, the first pass
+  // over the 512 rows after them
+  if (__any(miss)) {
+    const int32_t j = first_ge_group<8>(colc, bend, end, row, miss, true);
+    if (miss) fd = j < end ? j - h.cs : FD_NONE;
   }
   return fd;
 }
@@ -1417,6 +1440,24 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   };
   own_loads();
   if (t == 0) sh_fail = 0;
+  // BH_PBAR=xcd (pbar_mode 1): from the second iteration on, an XCD-
+  // hierarchical barrier -- each workgroup adds to its XCD's counter, the
+  // XCD's last arriver adds to the top counter, every workgroup polls the
+  // top one (16 arrivals per counter instead of 128 on one).  The workgroups
+  // count themselves per XCD first (an add whose return is waited for, so it
+  // is performed before this workgroup's first arrival below).  pbar layout
+  // (ints): [0] flat / top counter, [32 (1 + x)] XCD x's counter, [288 + x]
+  // XCD x's workgroups; each on 128-B lines of its own
+  int xcc = 0;
+  if (d.pbar_mode == 1) {
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    xcc &= 7;
+    if (t == 0) {
+      const int32_t o = __hip_atomic_fetch_add(d.pbar + 288 + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (o < 0) sh_fail = 1;  // (never: consumes the returned value)
+    }
+  }
+  int32_t gx = 0, nx = 0;  // workgroups on this XCD, XCDs with workgroups (read after the first barrier)
   if (npad > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
     for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
   int p = 0;
@@ -1569,14 +1610,23 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // ---- grid barrier ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
     __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool hier = d.pbar_mode == 1 && it > 0;
+    if (t == 0) {
+      if (hier) {
+        const int32_t o = __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == it * gx - 1) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     ++r;
     p ^= 1;
     k0 = result;
     hin.j0 = result < len ? fdv : FD_NONE;
     own_loads();  // lands during the wait
     if (t == 0) {
-      const int32_t target = (it + 1) * G;
+      // flat: (it + 1) G arrivals; hierarchical: G after the first barrier, then nx per iteration
+      const int32_t target = hier ? G + it * nx : (it + 1) * G;
       int spins = 0;
       while (__hip_atomic_load(d.pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
@@ -1585,6 +1635,10 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
           break;
         }
       }
+    }
+    if (d.pbar_mode == 1 && it == 0 && t == 0) {  // every workgroup has counted itself by now
+      gx = __hip_atomic_load(d.pbar + 288 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int x = 0; x < 8; ++x) nx += __hip_atomic_load(d.pbar + 288 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0;
     }
     __syncthreads();
     if (sh_fail) {
@@ -1606,7 +1660,7 @@ bool round_persist_eligible(const Dev &d) {
 void launch_round_persist(const Dev &d, hipStream_t s) {
   const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
-  (void)hipMemsetAsync(d.pbar, 0, 4, s);
+  (void)hipMemsetAsync(d.pbar, 0, 2048, s);  // (the counters' lines; 16-B multiple from the allocation's start)
   if (d.npad <= 32) k_round2p<1><<<d.n, nt, lds, s>>>(d);
   else if (d.npad <= 64) k_round2p<2><<<d.n, nt, lds, s>>>(d);
   else k_round2p<4><<<d.n, nt, lds, s>>>(d);

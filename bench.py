@@ -187,6 +187,7 @@ def main():
         hg.run_consensus()
         log(f"warmup {w}: stages_ms={['%.2f' % x for x in hg.stage_ms()]}")
     sweep_ms, stage_tot = [], np.zeros(8)
+    persist0 = hg.loop_stats()[0]
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -199,6 +200,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist)
+    persist_per_step = (hg.loop_stats()[0] - persist0) / args.steps  # persistent loop launches (one per segment)
     stats = hg.stats()
     ordered = stats.consensus_events
     # whole-job events ordered: one DAG per step when sharded, one per rank per step as replicas
@@ -219,16 +221,21 @@ def main():
     B = 12 * n + 96
     achieved = value * B / 1e9
     traffic_step = sum(v["hbm_bytes_per_step"] for v in pmc.values()) if pmc else None
-    # the dominant kernel: the round loop (one launch per round; N / launches
-    # events per launch), timed live by HIP events around its graph replays
-    round_kernel = "k_round2" if npad <= 128 else "k_round_wide"
+    # the dominant kernel: the round loop, timed live by HIP events around it
+    # (stage 7).  n <= 128: the persistent k_round2p, one launch per pipeline
+    # segment running all of that segment's rounds (N / launches events per
+    # launch); else k_round_wide, one launch per round
+    persistent = persist_per_step > 0
+    round_kernel = "k_round2p" if persistent else ("k_round2" if npad <= 128 else "k_round_wide")
     # the loop's own device time (stage 7): with the segment pipeline the
     # rounds stage [1] only counts what runs after the coordinates
     loop_ms = float(stage_tot[7] / args.steps) if len(stage_tot) > 7 else 0.0
     if loop_ms <= 0:  # (BH_LOOP_TIMING=0: the rounds stage instead)
         loop_ms = float(stage_tot[1] / args.steps)
-    round_avg_ms = loop_ms / max(iters, 1)
-    ev_per_launch = N / max(iters, 1)
+    iter_us = 1000.0 * loop_ms / max(iters, 1)
+    launches = persist_per_step if persistent else iters
+    round_avg_ms = loop_ms / max(launches, 1e-9)
+    ev_per_launch = N / max(launches, 1e-9)
     dom_alg = ev_per_launch * B
     dom_achieved = dom_alg / (round_avg_ms * 1e-3) / 1e9
     dom = pmc.get(round_kernel) if pmc else None
@@ -265,13 +272,15 @@ def main():
                      "traffic_total_note": "PMC HBM bytes of every kernel of one step "
                                            "(profiles/pmc_traffic.json; FETCH_SIZE x 2 + WRITE_SIZE)",
                      "dominant_kernel": {
-                         "kernel": round_kernel, "launches": iters, "avg_launch_ms": round_avg_ms,
+                         "kernel": round_kernel, "launches": launches, "avg_launch_ms": round_avg_ms,
+                         "round_iterations": iters, "us_per_iteration": iter_us,
                          "events_per_launch": ev_per_launch, "alg_bytes_per_launch": dom_alg,
                          "achieved": dom_achieved, "frac": dom_achieved / HBM_PEAK_GBS,
                          "traffic": dom["hbm_bytes_per_launch"] if dom else None,
-                         "note": "latency-bound: rounds are a serial chain, one launch each"},
-                     "l2_level": {"kernel": round_kernel, "bytes_per_launch": l2_bytes,
-                                  "GBps": l2_bytes / (round_avg_ms * 1e-3) / 1e9,
+                         "note": "latency-bound: rounds are a serial chain (k_round2p: a grid barrier "
+                                 "per round inside one launch per segment; k_round_wide: one launch per round)"},
+                     "l2_level": {"kernel": round_kernel, "bytes_per_iteration": l2_bytes,
+                                  "GBps": l2_bytes / (iter_us * 1e-6) / 1e9,
                                   "note": "candidate FD rows + LA/FD windows re-read by every workgroup "
                                           "from L2/MALL; not HBM traffic"}},
         "roofline_coordinates": {"kernel": hg.profile_kernel(), "avg_launch_ms": sweep_avg_ms,

@@ -705,6 +705,17 @@ def test_round2_persistent(monkeypatch, n, N, seed, lag, K):
         _wild_parity(128, 40_000, 0xC5, 35_000)
 
 
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xC9, 0, 1), (100, 50_000, 0xCA, 4, 3), (7, 5_000, 0xCB, 2, 2)])
+def test_round2_persistent_xcd_barrier(monkeypatch, n, N, seed, lag, K):
+    """The persistent loop with its XCD-hierarchical grid barrier (BH_PBAR=xcd:
+    per-XCD arrival counters, the XCD's last arriver adds to the top one)."""
+    monkeypatch.setenv("BH_ROUND_PERSIST", "1")
+    monkeypatch.setenv("BH_PBAR", "xcd")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
+    assert loops >= 1 and fallbacks == 0
+
+
 @pytest.mark.parametrize("n,N,seed,lag,K", [(128, 30_000, 0xC7, 0, 1), (64, 30_000, 0xC8, 21, 3)])
 def test_round2_persistent_fallback(monkeypatch, n, N, seed, lag, K):
     """A grid barrier that gives up (BH_PBAR_SPIN=0: at its first poll that
