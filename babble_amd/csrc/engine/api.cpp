@@ -58,6 +58,9 @@ void free_all(bh_handle *h) {
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
+  if (h->stream3) (void)hipStreamDestroy(h->stream3);
+  for (auto &e : h->lt_ev)
+    if (e) (void)hipEventDestroy(e);
   for (auto &g : h->seg_graph)
     if (g) (void)hipGraphExecDestroy(g);
   for (auto &g : h->seg_graph_s)
@@ -963,10 +966,26 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));
     return BH_OK;
   };
-  static const bool lt_combined = getenv("BH_LT_COMBINED") && atoi(getenv("BH_LT_COMBINED"));  // (A/B: LT beside the columns)
+  // where a segment's Lamport timestamps (one more dataflow workgroup, the LT
+  // lane) run: 1 = inside the column launch (n + 1 workgroups) while 2n + 1
+  // fit the compute units, so the loop's n workgroups still find units of
+  // their own; 2 = on a stream of their own once the segment's columns are
+  // done (n = 128: 129 column workgroups would share a unit with a loop
+  // workgroup, which every barrier then waits for), beside the next
+  // segment's columns; 0 = after the columns on the coordinate stream (the
+  // round-4 first form, A/B).  BH_LT_MODE=<0|1|2> overrides
+  const int lt_mode = getenv("BH_LT_MODE") ? std::clamp(atoi(getenv("BH_LT_MODE")), 0, 2)
+                      : (getenv("BH_LT_COMBINED") && atoi(getenv("BH_LT_COMBINED"))) ? 1
+                      : (2 * n + 1 <= h->ncu ? 1 : 2);
+  const bool lt_combined = lt_mode == 1;
+  hipStream_t sl = h->stream3;
   auto coords = [&](int k) -> int {
     if (sp) return receive(k);
     Dev v = view(k);
+    if (h->lt_ev_live[k & 1]) {  // the LT of segment k - 2 still reads this segbuf half
+      HIPCHK(h, hipStreamWaitEvent(sc, h->lt_ev[k & 1], 0));
+      h->lt_ev_live[k & 1] = false;
+    }
     int32_t *stg = h->seg_stage + (size_t)(k & 1) * 2 * n;
     lens_at(Ns[(size_t)k], stg);
     lens_at(Ns[(size_t)k + 1], stg + n);
@@ -1014,12 +1033,23 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if (!wide && lt_combined) {
       bh::launch_lt_rows(v, sc);
     } else if (!wide) {  // the segment's Lamport timestamps: one workgroup, beside the loop
+      hipStream_t st = lt_mode == 2 ? sl : sc;
+      if (lt_mode == 2) HIPCHK(h, hipStreamWaitEvent(sl, h->seg_ev[(size_t)3 * k], 0));  // (after the segment's columns)
       Dev vl = v;
       vl.ncol = 0;
       vl.flow_lt = 1;
-      bh::launch_flow(vl, sc);
-      bh::launch_lt_rows(v, sc);
+      bh::launch_flow(vl, st);
+      bh::launch_lt_rows(v, st);
       HIPCHK(h, hipGetLastError());
+      if (lt_mode == 2) {
+        // segment k + 2 reuses this view's segbuf half: the coordinate
+        // stream waits for this LT first (below, before coords(k + 2))
+        HIPCHK(h, hipEventRecord(h->lt_ev[k & 1], sl));
+        h->lt_ev_live[k & 1] = true;
+        if (k == K - 1) {  // the pipeline's end includes the last LT
+          HIPCHK(h, hipStreamWaitEvent(sc, h->lt_ev[k & 1], 0));
+        }
+      }
     } else if (!eager) {  // wide: k_floww2 wrote lt_row; per-event LT (the transpose copies it otherwise)
       bh::launch_lt_rows(v, sc);
       HIPCHK(h, hipGetLastError());
@@ -1631,7 +1661,9 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
-  d.pbar_mode = getenv("BH_PBAR") && !strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0;
+  // the XCD-hierarchical barrier from 64 workgroups up (C3: 8.4 -> 7.2 us per
+  // iteration; C2's 32 workgroups: 4.3 -> 4.6, one counter stays); BH_PBAR=xcd|flat overrides
+  d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n > 64 ? 1 : 0);
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
@@ -1735,6 +1767,13 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
       if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
         rc = BH_ERR_DEVICE;
     }
+    // the segments' Lamport timestamps (rounds_pipelined, lt_mode 2)
+    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking, lo_pri) != hipSuccess)
+      rc = BH_ERR_DEVICE;
+    for (auto &e : h->lt_ev)
+      if (rc == BH_OK && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = BH_ERR_DEVICE;
+    hipDeviceProp_t prop;
+    if (rc == BH_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) h->ncu = prop.multiProcessorCount;
   }
   if (rc == BH_OK) rc = dalloc(h, &h->seg_zero, (size_t)n);
   if (rc == BH_OK) rc = dalloc(h, &h->segbuf, (size_t)4 * n);
