@@ -204,17 +204,31 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     if (st[bh::ST_ERR]) return h->fail(BH_ERR_CAPACITY, "round table capacity exceeded");
     return BH_OK;
   }
-  if (bh::round_persist_eligible(v)) {  // one launch, a grid barrier per iteration (k_round2p)
+  const bool pers = bh::round_persist_eligible(v), wpers = !pers && bh::round_wide_persist_eligible(v);
+  if (pers || wpers) {  // one launch, a grid barrier per iteration (k_round2p / k_round_wide<..., true>)
     // the loop's inputs, kept: a barrier that gives up (ST_ERR = 3) leaves
-    // them overwritten, and the per-iteration launches below start again from them
+    // them overwritten, and the per-iteration launches below start again
+    // from them -- parity 0's boundaries and candidate rows (candfd, which
+    // the wide loop's cand16 aliases; cand8 and its tags), the state block
     const int n = v.n;
-    int32_t *snap_bp = v.psnap, *snap_cf = v.psnap + n, *snap_st = v.psnap + n + (size_t)n * v.npad;
-    HIPCHK(h, hipMemcpyAsync(snap_bp, v.Bp, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(h, hipMemcpyAsync(snap_cf, v.candfd, (size_t)n * v.npad * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(h, hipMemcpyAsync(snap_st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToDevice, s));
+    const size_t w8 = v.cand8 ? (size_t)n * ((v.npad + 15) / 16 * 16) : 0;
+    struct Piece { void *dev; size_t bytes; } pieces[] = {
+        {v.Bp, (size_t)n * 4}, {v.candfd, (size_t)n * v.npad * 4}, {v.state, bh::ST_COUNT * 4},
+        {v.cand8, wpers ? w8 : 0}, {v.c8tag, wpers && v.c8tag ? (size_t)n * 4 : 0}};
+    auto snapshot = [&](bool restore) -> int {
+      char *sp = reinterpret_cast<char *>(v.psnap);
+      for (const Piece &pc : pieces) {
+        if (!pc.bytes) continue;
+        HIPCHK(h, hipMemcpyAsync(restore ? pc.dev : sp, restore ? sp : pc.dev, pc.bytes, hipMemcpyDeviceToDevice, s));
+        sp += (pc.bytes + 15) & ~(size_t)15;
+      }
+      return BH_OK;
+    };
+    if ((rc = snapshot(false))) return rc;
     if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));
     ++h->persist_loops;
-    bh::launch_round_persist(v, s);
+    if (pers) bh::launch_round_persist(v, s);
+    else bh::launch_round_wide_persist(v, s);
     HIPCHK(h, hipGetLastError());
     if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[1], s));
     HIPCHK(h, copy_sync(s, st, v.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
@@ -227,9 +241,7 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     // the grid barrier gave up (some workgroup was never placed): restore and
     // take the per-iteration launches (counted in stats.persist_fallbacks)
     ++h->persist_fallbacks;
-    HIPCHK(h, hipMemcpyAsync(v.Bp, snap_bp, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(h, hipMemcpyAsync(v.candfd, snap_cf, (size_t)n * v.npad * 4, hipMemcpyDeviceToDevice, s));
-    HIPCHK(h, hipMemcpyAsync(v.state, snap_st, bh::ST_COUNT * 4, hipMemcpyDeviceToDevice, s));
+    if ((rc = snapshot(true))) return rc;
   }
   if (!no_graph && (rc = build_graph(h, v, graph, graph_dev, ITER_BATCH))) return rc;
   if (!no_graph && (rc = build_graph(h, v, graph_s, graph_dev_s, ITER_FIRST))) return rc;
@@ -969,14 +981,15 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // where a segment's Lamport timestamps (one more dataflow workgroup, the LT
   // lane) run: 1 = inside the column launch (n + 1 workgroups) while 2n + 1
   // fit the compute units, so the loop's n workgroups still find units of
-  // their own; 2 = on a stream of their own once the segment's columns are
-  // done (n = 128: 129 column workgroups would share a unit with a loop
-  // workgroup, which every barrier then waits for), beside the next
-  // segment's columns; 0 = after the columns on the coordinate stream (the
-  // round-4 first form, A/B).  BH_LT_MODE=<0|1|2> overrides
+  // their own (C5: 82 -> 101M events/s against 0); 0 = after the segment's
+  // columns on the coordinate stream (n = 128: 129 column workgroups would
+  // share a unit with a loop workgroup, which every barrier then waits for;
+  // C3: 161M with 1); 2 = on a stream of their own after the columns, beside
+  // the next segment's (C3: 176M against 0's 180M: the loop shares more).
+  // BH_LT_MODE=<0|1|2> overrides (profiles/r4_ab_lt.txt)
   const int lt_mode = getenv("BH_LT_MODE") ? std::clamp(atoi(getenv("BH_LT_MODE")), 0, 2)
                       : (getenv("BH_LT_COMBINED") && atoi(getenv("BH_LT_COMBINED"))) ? 1
-                      : (2 * n + 1 <= h->ncu ? 1 : 2);
+                      : (2 * n + 1 <= h->ncu ? 1 : 0);
   const bool lt_combined = lt_mode == 1;
   hipStream_t sl = h->stream3;
   auto coords = [&](int k) -> int {
@@ -1662,8 +1675,9 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
   // the XCD-hierarchical barrier from 64 workgroups up (C3: 8.4 -> 7.2 us per
-  // iteration; C2's 32 workgroups: 4.3 -> 4.6, one counter stays); BH_PBAR=xcd|flat overrides
-  d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n > 64 ? 1 : 0);
+  // iteration, C5: 6.9 -> 6.7; C2's 32 workgroups: 4.3 -> 4.6, one counter
+  // stays); BH_PBAR=xcd|flat overrides
+  d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n >= 64 ? 1 : 0);
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
@@ -1735,7 +1749,9 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
   A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 512);
-  if (d.fd_cols) A(&d.psnap, (size_t)n + (size_t)n * d.npad + bh::ST_COUNT);
+  // the persistent loops' input snapshot (run_round_loop): Bp, candfd, the
+  // state block, cand8 and its tags, each rounded to 16 B
+  A(&d.psnap, (size_t)n + 4 + (size_t)n * d.npad + bh::ST_COUNT + (size_t)n * ((d.npad + 15) / 16 * 4) + n + 4);
   A(&d.round, C); A(&d.witness, C); A(&d.fame, C); A(&d.trapped, C); A(&d.blocked, R1);
   A(&d.wfame, (size_t)d.W_cap); A(&d.frame_loaded, R1);
   A(&d.decided, R1); A(&d.nfam, R1); A(&d.minla, R1 * d.npad); A(&d.rr, C);

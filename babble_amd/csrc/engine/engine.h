@@ -373,6 +373,8 @@ bool round_solo_eligible(const Dev &d);
 bool round2_eligible(const Dev &d);
 bool round_persist_eligible(const Dev &d);
 void launch_round_persist(const Dev &d, hipStream_t s);
+bool round_wide_persist_eligible(const Dev &d);
+void launch_round_wide_persist(const Dev &d, hipStream_t s);
 void launch_round_solo(const Dev &d, hipStream_t s);
 // Reset hashgraphs: coordinates of events [0, d.N) one event at a time (the
 // batch whose other-parents only Root.Others knows), and the rounds below r0

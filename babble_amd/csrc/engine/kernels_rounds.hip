@@ -132,12 +132,78 @@ __device__ __forceinline__ uint32_t pack8(uint32_t lo, uint32_t hi) {
   return __builtin_amdgcn_perm(hi, lo, 0x06040200u);
 }
 
+// Loads and stores of what other workgroups of the same launch store (the
+// persistent loops): sc1, so neither this CU's L1 nor this XCD's L2 can serve
+// a stale line (MI355X_MICROARCH.md, the hand-off table); plain otherwise.
+template <bool SC1>
+__device__ __forceinline__ int32_t ldx(const int32_t *p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool SC1, class T>
+__device__ __forceinline__ void stx(T *p, T v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+// 16-B element `idx` of a buffer whose descriptor is rs (SC1: buffer load
+// with sc1), or of the plain pointer base
+template <bool SC1>
+__device__ __forceinline__ int4 ld128(__amdgpu_buffer_rsrc_t rs, const int4 *base, int64_t idx) {
+  if constexpr (SC1) return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(idx * 16), 0, 16));
+  else return base[idx];
+}
+
+// The persistent loops' grid barrier (thread 0 of each workgroup calls these).
+// pbar layout (ints): [0] the counter (flat) / top counter (hierarchical),
+// [32 (1 + x)] XCD x's arrivals, [288 + x] XCD x's workgroups, each group on
+// 128-B lines of its own.  pbar_mode 1 (XCD-hierarchical) from the second
+// barrier on: a workgroup adds to its XCD's counter, the XCD's last arriver
+// (told by the value its add returns) adds to the top counter, every
+// workgroup polls the top counter -- 16 or 64 arrivals per counter instead
+// of every workgroup's on one.
+__device__ __forceinline__ int pbar_register(const Dev &d) {  // at the start: this workgroup's XCD, counted
+  int xcc = 0;
+  if (d.pbar_mode == 1) {
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    xcc &= 7;
+    // an add whose returned value is used: performed before this workgroup's first arrival
+    if (__hip_atomic_fetch_add(d.pbar + 288 + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) xcc = 0;
+  }
+  return xcc;
+}
+__device__ __forceinline__ void pbar_arrive(const Dev &d, int it, int xcc, int32_t gx) {
+  if (d.pbar_mode == 1 && it > 0) {
+    const int32_t o = __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o == it * gx - 1) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// false: the barrier gave up (d.pbar_spin polls)
+__device__ __forceinline__ bool pbar_wait(const Dev &d, int it, int G, int32_t nx) {
+  const int32_t target = d.pbar_mode == 1 && it > 0 ? G + it * nx : (it + 1) * G;
+  int spins = 0;
+  while (__hip_atomic_load(d.pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > d.pbar_spin) return false;
+  }
+  return true;
+}
+// after the first barrier every workgroup has counted itself
+__device__ __forceinline__ void pbar_counts(const Dev &d, int xcc, int32_t &gx, int32_t &nx) {
+  if (d.pbar_mode != 1) return;
+  gx = __hip_atomic_load(d.pbar + 288 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  nx = 0;
+  for (int x = 0; x < 8; ++x) nx += __hip_atomic_load(d.pbar + 288 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0;
+}
+
 // k_round_wide's hand-off of the new candidate (c, row) for iteration r + 1:
 // its cand16 row (gather_cand16's layout) and, with the shared base on, its
 // cand8 row -- byte i = min(max(FD + 1 - base_i, 0), 127) with base_i =
 // max(B[r][i] - round_p8g, 0) from Bcur = B[r] (the base iteration r + 1
 // reads back from the B history), 127 past column n -- then the row's tag.
 // Four columns per thread; every thread of the workgroup calls it.
+template <bool SC1 = false>
 __device__ __forceinline__ void handoff_wide(const Dev &d, int64_t row, int p1, int c, const int32_t *Bcur,
                                              int32_t rnext) {
   const int npad = d.npad, n = d.n, w16 = (npad + 7) / 8 * 4, w8 = (npad + 15) / 16 * 16;
@@ -152,17 +218,18 @@ __device__ __forceinline__ void handoff_wide(const Dev &d, int64_t row, int p1, 
       const int32_t v = i < n ? d.fdt[fdt_pos(row, i, npad)] : FD_NONE;
       h[k] = min((uint32_t)v + 1u, 0xFFFFu);  // FD_NONE + 1 wraps to 2^31
       if (g) {
-        const int32_t base = i < n ? max(Bcur[i] - d.round_p8g, 0) : 0;
+        const int32_t base = i < n ? max(ldx<SC1>(Bcur + i) - d.round_p8g, 0) : 0;
         const uint32_t f = i < n ? min((uint32_t)max((int32_t)h[k] - base, 0), 127u) : 127u;
         b8 |= f << (8 * k);
       }
     }
-    if (2 * j < w16) dst16[2 * j] = h[0] | (h[1] << 16);
-    if (2 * j + 1 < w16) dst16[2 * j + 1] = h[2] | (h[3] << 16);
-    if (g) dst8[j] = b8;
+    if (2 * j < w16) stx<SC1>(dst16 + 2 * j, h[0] | (h[1] << 16));
+    if (2 * j + 1 < w16) stx<SC1>(dst16 + 2 * j + 1, h[2] | (h[3] << 16));
+    if (g) stx<SC1>(dst8 + j, b8);
   }
-  // read by the next launch only (the kernel boundary orders it after the row)
-  if (g && threadIdx.x == 0) d.c8tag[(int64_t)p1 * n + c] = rnext;
+  // read by the next launch (the kernel boundary orders it after the row),
+  // or after the persistent loop's grid barrier (sc1 stores, drained first)
+  if (g && threadIdx.x == 0) stx<SC1>(d.c8tag + (int64_t)p1 * n + c, rnext);
 }
 
 // The first j in [lo, hi) with col[j] >= k (col non-decreasing), or hi:
@@ -438,7 +505,13 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // COLS: 0 = window rows from the row-major LA, candidates' FD rows gathered
 // from FDT (handoff_wide); 1 = both from the column-major LA (no transpose);
 // 2 = window rows from the row-major LA, hand-off from la_col (A/B)
-template <int LPC, bool P16, int COLS = 0, int NT = 256>
+// PERS (k_round_wide<*, true, 0, 256, true>, the default where it fits): the
+// whole loop in one launch, every round's iteration followed by a grid
+// barrier instead of a kernel boundary (as k_round2p at n <= 128): what the
+// workgroups hand each other -- boundaries (Bp, B), candidates' rows (cand16,
+// cand8) and tags -- goes through sc1 stores and loads.  512 workgroups, two
+// per compute unit, all resident.
+template <int LPC, bool P16, int COLS = 0, int NT = 256, bool PERS = false>
 __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU (NT / 128 waves per SIMD)
   extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
   constexpr int PP = P16 ? 8 : PIECES;  // 16-B pieces per lane
@@ -454,11 +527,19 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int c = blockIdx.x;
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
-  const int32_t *Bp = d.Bp + (int64_t)p * n;
-  const int done = d.state[ST_DONE];
-  const int r = d.state[ST_CUR0 + p];
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
-  if (done) return;
+  if (d.state[ST_DONE]) return;
+  if (PERS) p = 0;  // (the loop's first iteration has parity 0)
+  int r = d.state[ST_CUR0 + p];
+  int32_t own = d.Bp[(int64_t)p * n + c];  // B[r][c]: this workgroup's own boundary
+  // (PERS: sc1 buffer loads of the candidates' rows)
+  const __amdgpu_buffer_rsrc_t rs8 = __builtin_amdgcn_make_buffer_rsrc(d.cand8, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs16 = __builtin_amdgcn_make_buffer_rsrc(d.cand16, (short)0, 0x7fffffff, 0x00020000);
+  int xcc = 0;
+  int32_t gx = 0, nx = 0;
+  if (PERS && t == 0) xcc = pbar_register(d);
+  for (int it = 0;; ++it) {
+  const int32_t *Bp = d.Bp + (int64_t)p * n;
   // BH_DIAG timeline (tools/timeline.py): start, first window staged, search
   // done, end -- chains < 128 of rounds TL_R0 .. TL_R0 + TL_NR
   const bool dgt = d.diag != nullptr && t == 0 && c < 128 && r >= TL_R0 && r < TL_R0 + TL_NR;
@@ -474,13 +555,13 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     // boundary already reached its end has no window at all and must still
     // write B[r + 1] = len (and not read as "no candidates anywhere")
     int nc = 0;
-    for (int q = t; q < n; q += blockDim.x) nc += Bp[q] < d.chain_len[q];
+    for (int q = t; q < n; q += blockDim.x) nc += ldx<PERS>(Bp + q) < d.chain_len[q];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nc += __shfl_xor(nc, off);
     if (lane == 0 && nc) atomicAdd(&sh_nc, nc);
   }
   __syncthreads();
-  int32_t wk0 = Bp[c];
+  int32_t wk0 = own;
   int32_t result = len;
   constexpr int PP8 = PP / 2, WRS8 = LPC * (PP8 + 1);  // P8: 16-B pieces of 16 columns per lane
   for (;;) {
@@ -513,7 +594,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
         // whose previous round's boundaries are known also tries the shared
         // base (B[r-1][i] - round_p8g): then every candidate whose row its
         // producer already converted (c8tag) needs no conversion here
-        const bool tryg = d.cand8 != nullptr && d.round_p8g > 0 && r > d.r0 && wk0 == Bp[c];
+        const bool tryg = d.cand8 != nullptr && d.round_p8g > 0 && r > d.r0 && wk0 == own;
         if (t == 0) { sh_wide = 0; sh_gbad = !tryg; }
         __syncthreads();
         const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
@@ -536,8 +617,8 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           bad |= z0 + 1 - b0 > d.round_p8 || z1 + 1 - b1 > d.round_p8;
           if (tryg) {
             // columns past n keep the window base (their candidate bytes are 127 either way)
-            const int32_t g0 = i0 < n ? max(Bprev[i0] - d.round_p8g, 0) : b0;
-            const int32_t g1 = i1 < n ? max(Bprev[i1] - d.round_p8g, 0) : b1;
+            const int32_t g0 = i0 < n ? max(ldx<PERS>(Bprev + i0) - d.round_p8g, 0) : b0;
+            const int32_t g1 = i1 < n ? max(ldx<PERS>(Bprev + i1) - d.round_p8g, 0) : b1;
             gbase2[j] = (uint32_t)g0 | ((uint32_t)g1 << 16);
             gbad |= a0 + 1 < g0 || a1 + 1 < g1 || z0 + 1 - g0 > d.round_p8 || z1 + 1 - g1 > d.round_p8;
           }
@@ -638,11 +719,11 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       // whether the bytes are used or the 16-bit row is converted)
       const int w8q = (npad + 15) / 16;
       auto raw_f8 = [&](int q, uint32_t (&f8)[4 * PP8]) {
-        const int4 *fr = reinterpret_cast<const int4 *>(d.cand8) + ((int64_t)p * n + min(q, n - 1)) * w8q;
+        const int64_t f0 = ((int64_t)p * n + min(q, n - 1)) * w8q;
 #pragma unroll
         for (int u = 0; u < PP8; ++u) {
           const int pc = part * PP8 + u;
-          const int4 v = fr[min(pc, w8q - 1)];
+          const int4 v = ld128<PERS>(rs8, reinterpret_cast<const int4 *>(d.cand8), f0 + min(pc, w8q - 1));
           const bool ok = pc < w8q;
           f8[4 * u] = ok ? (uint32_t)v.x : 0x7F7F7F7Fu;
           f8[4 * u + 1] = ok ? (uint32_t)v.y : 0x7F7F7F7Fu;
@@ -653,12 +734,12 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       auto load_f8 = [&](int q, bool act, int32_t tag, uint32_t (&f8)[4 * PP8]) {
         if (!(p8g && act && tag == r)) {
           const int f16q = (npad + 7) / 8;
-          const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
+          const int64_t f0 = ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
           const int nvalid = f16q - part * PP;
           const uint4 *bb = reinterpret_cast<const uint4 *>(wb2) + part * PP;
 #pragma unroll
           for (int u = 0; u < PP; ++u) {
-            const int4 v = fr[min(u, max(nvalid - 1, 0))];
+            const int4 v = ld128<PERS>(rs16, reinterpret_cast<const int4 *>(d.cand16), f0 + min(u, max(nvalid - 1, 0)));
             const uint4 b = bb[u];
             const bool ok = u < nvalid;
             const uint32_t e0 = fd8x2(ok ? (uint32_t)v.x : 0xFFFFFFFFu, b.x), e1 = fd8x2(ok ? (uint32_t)v.y : 0xFFFFFFFFu, b.y);
@@ -672,8 +753,8 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       for (int pass = 0; pass < npass; pass += 2) {
         const int qa = pass * CPP + t / LPC, qb = qa + CPP;
         const int qa1 = min(qa, n - 1), qb1 = min(qb, n - 1);
-        const int32_t ba = Bp[qa1], la_ = d.chain_len[qa1], bb_ = Bp[qb1], lb = d.chain_len[qb1];
-        const int32_t taga = d.c8tag[(int64_t)p * n + qa1], tagb = d.c8tag[(int64_t)p * n + qb1];
+        const int32_t ba = ldx<PERS>(Bp + qa1), la_ = d.chain_len[qa1], bb_ = ldx<PERS>(Bp + qb1), lb = d.chain_len[qb1];
+        const int32_t taga = ldx<PERS>(d.c8tag + (int64_t)p * n + qa1), tagb = ldx<PERS>(d.c8tag + (int64_t)p * n + qb1);
         uint32_t fa[4 * PP8], fb[4 * PP8];
         raw_f8(qa, fa);
         raw_f8(qb, fb);
@@ -735,20 +816,20 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     for (int pass = 0; pass < npass; ++pass) {
       const int q = pass * CPP + t / LPC;
       int32_t bq = 0, lq = 0, sq = 0;
-      if (q < n) { bq = Bp[q]; lq = d.chain_len[q]; sq = d.chain_start[q]; }
+      if (q < n) { bq = ldx<PERS>(Bp + q); lq = d.chain_len[q]; sq = d.chain_start[q]; }
       const bool act = q < n && bq < lq;
       int tw = WROWS;
       if (p8) {
         // the candidate's 16-bit FD row, window-relative 8-bit (fd8x2 / pack8)
         uint32_t f8[4 * PP8];
-        if (p8g && act && d.c8tag[(int64_t)p * n + q] == r) {
+        if (p8g && act && ldx<PERS>(d.c8tag + (int64_t)p * n + q) == r) {
           // converted by its producer against the same shared base (handoff_wide)
           const int w8q = (npad + 15) / 16;  // 16-B pieces per cand8 row
-          const int4 *fr = reinterpret_cast<const int4 *>(d.cand8) + ((int64_t)p * n + q) * w8q;
+          const int64_t f0 = ((int64_t)p * n + q) * w8q;
 #pragma unroll
           for (int u = 0; u < PP8; ++u) {
             const int pc = part * PP8 + u;
-            const int4 v = fr[min(pc, w8q - 1)];  // (in the row: the pieces past it are 127s)
+            const int4 v = ld128<PERS>(rs8, reinterpret_cast<const int4 *>(d.cand8), f0 + min(pc, w8q - 1));  // (in the row: the pieces past it are 127s)
             const bool ok = pc < w8q;
             f8[4 * u] = ok ? (uint32_t)v.x : 0x7F7F7F7Fu;
             f8[4 * u + 1] = ok ? (uint32_t)v.y : 0x7F7F7F7Fu;
@@ -757,12 +838,12 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         } else {
           const int f16q = (npad + 7) / 8;
-          const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
+          const int64_t f0 = ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
           const int nvalid = f16q - part * PP;
           const uint4 *bb = reinterpret_cast<const uint4 *>(wb2) + part * PP;
 #pragma unroll
           for (int u = 0; u < PP; ++u) {
-            const int4 v = fr[min(u, max(nvalid - 1, 0))];
+            const int4 v = ld128<PERS>(rs16, reinterpret_cast<const int4 *>(d.cand16), f0 + min(u, max(nvalid - 1, 0)));
             const uint4 b = bb[u];
             const bool ok = u < nvalid;
             const uint32_t e0 = fd8x2(ok ? (uint32_t)v.x : 0xFFFFFFFFu, b.x), e1 = fd8x2(ok ? (uint32_t)v.y : 0xFFFFFFFFu, b.y);
@@ -802,11 +883,11 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       int4 f[PP];
       if constexpr (P16) {
         const int f16q = (npad + 7) / 8;  // 16-B pieces per cand16 row
-        const int4 *fr = reinterpret_cast<const int4 *>(d.cand16) + ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
+        const int64_t f0 = ((int64_t)p * n + (act ? q : 0)) * f16q + part * PP;
         const int nvalid = f16q - part * PP;
 #pragma unroll
         for (int u = 0; u < PP; ++u) {
-          const int4 v = fr[min(u, max(nvalid - 1, 0))];
+          const int4 v = ld128<PERS>(rs16, reinterpret_cast<const int4 *>(d.cand16), f0 + min(u, max(nvalid - 1, 0)));
           f[u] = u < nvalid ? v : make_int4(-1, -1, -1, -1);  // 0xFFFF: never reached
         }
       } else {
@@ -892,7 +973,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // the hand-off: the new candidate's FD row for the next iteration
   if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
     if constexpr (COLS != 0) handoff_wide_cols<NT>(d, p, c, result, Bp, r + 1);
-    else handoff_wide(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
+    else handoff_wide<PERS>(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
   }
   if (dgt) {
     unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
@@ -901,22 +982,46 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     tl[2] = rt1;
     tl[3] = __builtin_amdgcn_s_memrealtime();
   }
+  // the loop's end (the same in every workgroup: the candidate count and
+  // the round are), else this iteration's boundary
+  const bool stop = sh_nc == 0 || r + 1 >= d.R_cap;
   if (t == 0) {
     if (sh_nc == 0) {
-      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
-      return;
-    }
-    if (r + 1 >= d.R_cap) {
+      if (c == 0) { d.state[ST_ROUNDS] = r; d.state[ST_ITERS] = r; d.state[ST_DONE] = 1; signal_done(d); }
+    } else if (r + 1 >= d.R_cap) {
       if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
-      return;
-    }
-    d.Bp[(int64_t)(p ^ 1) * n + c] = result;
-    d.B[(int64_t)(r + 1) * n + c] = result;
-    if (c == 0) {
-      d.state[ST_CUR0 + (p ^ 1)] = r + 1;
-      d.state[ST_ITERS] = r + 1;
+    } else {
+      stx<PERS>(d.Bp + (int64_t)(p ^ 1) * n + c, result);
+      stx<PERS>(d.B + (int64_t)(r + 1) * n + c, result);
+      if (c == 0) {
+        d.state[ST_CUR0 + (p ^ 1)] = r + 1;
+        d.state[ST_ITERS] = r + 1;
+      }
     }
   }
+  if (!PERS || stop) return;
+  // ---- grid barrier (PERS) ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
+  __syncthreads();
+  if (t == 0) {
+    pbar_arrive(d, it, xcc, gx);
+    sh_res = pbar_wait(d, it, gridDim.x, nx) ? 0 : -1;
+    if (it == 0) pbar_counts(d, xcc, gx, nx);
+  }
+  __syncthreads();
+  if (sh_res < 0) {  // the barrier gave up: the host restores the inputs and relaunches per iteration
+    if (t == 0) {
+      d.state[ST_ERR] = 3;
+      d.state[ST_ROUNDS] = r;
+      d.state[ST_DONE] = 1;
+      if (c == 0) signal_done(d);
+    }
+    return;
+  }
+  own = result;
+  ++r;
+  p ^= 1;
+  }  // for (it)
 }
 
 // ---------------------------------------------------------------------------
@@ -1657,6 +1762,42 @@ bool round_persist_eligible(const Dev &d) {
   return d.round_persist && round2_eligible(d) && !d.round_src_rows && d.pbar != nullptr && d.n <= 256;
 }
 
+static int lanes_per_candidate(int npad);
+
+// the wide persistent loop (k_round_wide<*, true, 0, 256, true>): the 16-bit
+// loop over FDT with byte rows searched in pairs, n workgroups that must all
+// be resident at once (two per compute unit at n = 512)
+static int wide_resident(int lpc) {
+  static int slots[2] = {-1, -1};
+  int &s = slots[lpc == 8];
+  if (s < 0) {
+    int nb = 0, cus = 0, dev = 0;
+    const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (lpc == 8) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_round_wide<8, true, 0, 256, true>, 256, wb16);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_round_wide<4, true, 0, 256, true>, 256, wb16);
+    s = std::min(nb, 8) * cus;
+  }
+  return s;
+}
+
+bool round_wide_persist_eligible(const Dev &d) {
+  if (!d.round_persist || d.fd_cols || !d.cand16 || d.fd_rows || d.wide_cols || !d.round_ilp2 || !d.pbar ||
+      !round_p16(d))
+    return false;
+  const int lpc = lanes_per_candidate(d.npad);
+  return d.n > 256 / lpc && (lpc == 4 || lpc == 8) && d.n <= wide_resident(lpc);
+}
+
+void launch_round_wide_persist(const Dev &d, hipStream_t s) {
+  const int lpc = lanes_per_candidate(d.npad);
+  const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
+  (void)hipMemsetAsync(d.pbar, 0, 2048, s);
+  if (lpc == 8) k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  else k_round_wide<4, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+}
+
 void launch_round_persist(const Dev &d, hipStream_t s) {
   const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
@@ -2206,6 +2347,7 @@ void configure_round_kernels() {
   CFG((k_round_wide<4, true>)); CFG((k_round_wide<8, true>));
   CFG((k_round_wide<4, true, 1>)); CFG((k_round_wide<8, true, 1>));
   CFG((k_round_wide<4, true, 2>)); CFG((k_round_wide<8, true, 2>));
+  CFG((k_round_wide<4, true, 0, 256, true>)); CFG((k_round_wide<8, true, 0, 256, true>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));

@@ -369,7 +369,8 @@ def test_chunk_sweep_wild(monkeypatch):
 
 @pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p8_single", "p8g_tight_single",
                                   "p16", "p32", "fdt_p8", "fdt_p16", "cols_p8", "cols_p8g_tight", "cols_p16",
-                                  "cols2_p8", "cols2_p16"])
+                                  "cols2_p8", "cols2_p16", "iter_p8", "iter_p8_mixed", "iter_p8g_tight",
+                                  "fallback_p8"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -389,7 +390,17 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     fame's LA rows from the dataflow's column-major LA; fdt_*: the loop over
     the transposed row-major LA and the complete FDT (BH_WIDE_ROWS=1).
     cols_*: the loop over the column-major LA (BH_WIDE_COLS=1); cols2_*: the
-    window from the row-major LA, the hand-off from la_col (BH_WIDE_COLS=2)."""
+    window from the row-major LA, the hand-off from la_col (BH_WIDE_COLS=2).
+    The default 8-bit loop runs as one persistent launch (a grid barrier per
+    round); iter_*: one launch per round (BH_ROUND_PERSIST=0); fallback_*: the
+    persistent loop's barrier gives up at once (BH_PBAR_SPIN=0), the host
+    restores the loop's inputs and runs the per-round launches."""
+    if rows.startswith("iter_"):
+        monkeypatch.setenv("BH_ROUND_PERSIST", "0")
+        rows = rows[len("iter_"):]
+    if rows.startswith("fallback_"):
+        monkeypatch.setenv("BH_PBAR_SPIN", "0")
+        rows = rows[len("fallback_"):]
     if rows.startswith("cols2_"):
         monkeypatch.setenv("BH_WIDE_COLS", "2")
         rows = rows[len("cols2_"):]
