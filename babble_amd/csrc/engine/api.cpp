@@ -1678,6 +1678,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   // iteration, C5: 6.9 -> 6.7; C2's 32 workgroups: 4.3 -> 4.6, one counter
   // stays); BH_PBAR=xcd|flat overrides
   d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n >= 64 ? 1 : 0);
+  d.prestage = getenv("BH_PRESTAGE") ? atoi(getenv("BH_PRESTAGE")) != 0 : 1;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;
@@ -1748,7 +1749,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
-  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 512);
+  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 1024);
   // the persistent loops' input snapshot (run_round_loop): Bp, candfd, the
   // state block, cand8 and its tags, each rounded to 16 B
   A(&d.psnap, (size_t)n + 4 + (size_t)n * d.npad + bh::ST_COUNT + (size_t)n * ((d.npad + 15) / 16 * 4) + n + 4);

@@ -155,12 +155,14 @@ __device__ __forceinline__ int4 ld128(__amdgpu_buffer_rsrc_t rs, const int4 *bas
 
 // The persistent loops' grid barrier (thread 0 of each workgroup calls these).
 // pbar layout (ints): [0] the counter (flat) / top counter (hierarchical),
-// [32 (1 + x)] XCD x's arrivals, [288 + x] XCD x's workgroups, each group on
-// 128-B lines of its own.  pbar_mode 1 (XCD-hierarchical) from the second
-// barrier on: a workgroup adds to its XCD's counter, the XCD's last arriver
-// (told by the value its add returns) adds to the top counter, every
-// workgroup polls the top counter -- 16 or 64 arrivals per counter instead
-// of every workgroup's on one.
+// [32 (1 + x)] XCD x's arrivals, [288 + x] XCD x's workgroups, [320 + 32 x]
+// XCD x's release generation, each group on 128-B lines of its own.
+// pbar_mode 1 (XCD-hierarchical) from the second barrier on: a workgroup
+// adds to its XCD's counter; the XCD's last arriver (told by the value its
+// add returns) adds to the top counter, polls it until every XCD's leader
+// has added, and releases its XCD by storing the generation its other
+// workgroups poll -- 16 or 64 arrivals per counter and 8 pollers of the top
+// one, instead of every workgroup's adds and polls on one line.
 __device__ __forceinline__ int pbar_register(const Dev &d) {  // at the start: this workgroup's XCD, counted
   int xcc = 0;
   if (d.pbar_mode == 1) {
@@ -171,23 +173,33 @@ __device__ __forceinline__ int pbar_register(const Dev &d) {  // at the start: t
   }
   return xcc;
 }
-__device__ __forceinline__ void pbar_arrive(const Dev &d, int it, int xcc, int32_t gx) {
+// returns whether this workgroup is its XCD's leader for this barrier
+__device__ __forceinline__ bool pbar_arrive(const Dev &d, int it, int xcc, int32_t gx) {
   if (d.pbar_mode == 1 && it > 0) {
     const int32_t o = __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (o == it * gx - 1) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
+    if (o != it * gx - 1) return false;
     __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
   }
+  __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return false;
 }
-// false: the barrier gave up (d.pbar_spin polls)
-__device__ __forceinline__ bool pbar_wait(const Dev &d, int it, int G, int32_t nx) {
-  const int32_t target = d.pbar_mode == 1 && it > 0 ? G + it * nx : (it + 1) * G;
+__device__ __forceinline__ bool pbar_poll(const Dev &d, const int32_t *w, int32_t target) {
   int spins = 0;
-  while (__hip_atomic_load(d.pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     __builtin_amdgcn_s_sleep(1);
     if (++spins > d.pbar_spin) return false;
   }
   return true;
+}
+// false: the barrier gave up (d.pbar_spin polls)
+__device__ __forceinline__ bool pbar_wait(const Dev &d, int it, int G, int32_t nx, int xcc, bool lead) {
+  if (!(d.pbar_mode == 1 && it > 0)) return pbar_poll(d, d.pbar, (it + 1) * G);
+  if (!lead) return pbar_poll(d, d.pbar + 320 + 32 * xcc, it);
+  const bool ok = pbar_poll(d, d.pbar, G + it * nx);
+  // released (or given up: the waiters then give up too, at their own limit)
+  if (ok) __hip_atomic_store(d.pbar + 320 + 32 * xcc, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ok;
 }
 // after the first barrier every workgroup has counted itself
 __device__ __forceinline__ void pbar_counts(const Dev &d, int xcc, int32_t &gx, int32_t &nx) {
@@ -538,6 +550,159 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   int xcc = 0;
   int32_t gx = 0, nx = 0;
   if (PERS && t == 0) xcc = pbar_register(d);
+  bool prestaged = false;  // (PERS) the first window of this round is in LDS already
+  constexpr int PP8 = PP / 2, WRS8 = LPC * (PP8 + 1);  // P8: 16-B pieces of 16 columns per lane
+  // the first window of chain c from row wk0 for round rr (own_: its
+  // boundary): the fit check against the window's own and the shared base,
+  // then the rows staged in LDS (sets p8, p8g, wb2).  PERS: the next round's
+  // is staged while this round's grid barrier is waited for (its rows and
+  // B[r] are known before the barrier)
+  bool p8 = false, p8g = false;
+  const uint32_t *wb2 = wbase2;
+  auto stage = [&](const int32_t wk0, const int wrows, const int rr, const int32_t own_) {
+      // COLS: the window's 36 aligned rows of every column from la_col, issued
+      // before the fit check below reads its two rows
+      constexpr int CQ = LPC * 16, CT = NT / CQ, CNP = (9 + CT - 1) / CT;  // column quads, threads per quad, pieces per thread
+      const int cg = t % CQ, ch = t / CQ;
+      const int32_t crb = (cs + wk0) & ~3;
+      const int coff = cs + wk0 - crb;
+      int4 cpv[COLS == 1 ? CNP : 1][4];
+      if constexpr (COLS == 1) {
+  #pragma unroll
+        for (int u = 0; u < CNP; ++u) {
+          const int pc = ch + u * CT;
+  #pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int col = 4 * cg + k;
+            cpv[u][k] = pc < 9 && col < n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)col * la_col_stride(d) + (crb + 4 * pc))
+                                          : make_int4(-1, -1, -1, -1);
+          }
+        }
+      }
+      p8 = false;
+      p8g = false;
+      if constexpr (P16) {
+        if (d.round_p8) {
+          // P8 when every column's spread down the window fits (first row: the
+          // base, last row: the largest LA).  The first window of an iteration
+          // whose previous round's boundaries are known also tries the shared
+          // base (B[r-1][i] - round_p8g): then every candidate whose row its
+          // producer already converted (c8tag) needs no conversion here
+          const bool tryg = d.cand8 != nullptr && d.round_p8g > 0 && rr > d.r0 && wk0 == own_;
+          if (t == 0) { sh_wide = 0; sh_gbad = !tryg; }
+          __syncthreads();
+          const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
+          const int32_t *Bprev = d.B + (int64_t)(rr - 1) * n;
+          // LA of column i at the window's first / last row (-1 past n, 0 past npad)
+          auto la_w = [&](int i, int last) -> int32_t {
+            if (i >= npad) return 0;
+            if constexpr (COLS == 1)
+              return i < n ? d.la_col[(int64_t)i * la_col_stride(d) + cs + wk0 + (last ? wrows - 1 : 0)] : -1;
+            else
+              return (last ? r1p : r0p)[i];
+          };
+          bool bad = false, gbad = false;
+          for (int j = t; j < 256; j += 256) {
+            const int i0 = 2 * j, i1 = 2 * j + 1;
+            const int32_t a0 = la_w(i0, 0), a1 = la_w(i1, 0);
+            const int32_t z0 = la_w(i0, 1), z1 = la_w(i1, 1);
+            const int32_t b0 = max(a0, 0), b1 = max(a1, 0);
+            wbase2[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
+            bad |= z0 + 1 - b0 > d.round_p8 || z1 + 1 - b1 > d.round_p8;
+            if (tryg) {
+              // columns past n keep the window base (their candidate bytes are 127 either way)
+              const int32_t g0 = i0 < n ? max(ldx<PERS>(Bprev + i0) - d.round_p8g, 0) : b0;
+              const int32_t g1 = i1 < n ? max(ldx<PERS>(Bprev + i1) - d.round_p8g, 0) : b1;
+              gbase2[j] = (uint32_t)g0 | ((uint32_t)g1 << 16);
+              gbad |= a0 + 1 < g0 || a1 + 1 < g1 || z0 + 1 - g0 > d.round_p8 || z1 + 1 - g1 > d.round_p8;
+            }
+          }
+          if (__any(bad) && lane == 0) sh_wide = 1;
+          if (__any(gbad) && lane == 0) sh_gbad = 1;
+          __syncthreads();
+          p8g = !sh_gbad;
+          p8 = p8g || !sh_wide;
+        }
+      }
+      wb2 = p8g ? gbase2 : wbase2;
+      __syncthreads();
+      if constexpr (COLS == 1) {
+        // quad cg's 4 columns, 4 rows per piece: P8 one dword per row (bytes
+        // x | 0x80, as below), P16 two (16-bit LA + 1 pairs); window row = the
+        // piece's row - coff, rows outside [0, wrows) skipped
+        uint32_t *w32 = reinterpret_cast<uint32_t *>(win4);
+        uint32_t bs[4] = {0, 0, 0, 0};
+        if (p8) {
+          const uint32_t b01 = wb2[2 * cg], b23 = wb2[2 * cg + 1];
+          bs[0] = b01 & 0xFFFFu; bs[1] = b01 >> 16; bs[2] = b23 & 0xFFFFu; bs[3] = b23 >> 16;
+        }
+        const int pc8 = cg >> 2, pc16 = cg >> 1;
+        const int o8 = (pc8 + pc8 / PP8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
+  #pragma unroll
+        for (int u = 0; u < CNP; ++u) {
+          const int pc = ch + u * CT;
+          if (pc >= 9) continue;
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int wr = 4 * pc + e - coff;
+            if (wr < 0 || wr >= wrows) continue;
+            auto el = [&](int k) -> int32_t {
+              const int4 v = cpv[u][k];
+              return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+            };
+            if (p8) {
+              uint32_t x = 0;
+  #pragma unroll
+              for (int k = 0; k < 4; ++k) x |= ((uint32_t)(el(k) + 1 - (int32_t)bs[k]) & 0xFFu) << (8 * k);
+              w32[wr * WRS8 * 4 + o8] = x | 0x80808080u;
+            } else {
+              w32[wr * WRS4 * 4 + o16] = pack_la16(el(0), el(1));
+              w32[wr * WRS4 * 4 + o16 + 1] = pack_la16(el(2), el(3));
+            }
+          }
+        }
+      } else if (p8) {
+        // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
+        constexpr int RP8 = LPC * PP8;
+        const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+        for (int i = t; i < wrows * RP8; i += NT) {
+          const int row = i / RP8, pc = i - row * RP8;
+          uint32_t w[4];
+  #pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
+            uint32_t v = 0x80808080u;
+            if (col < npad) {
+              const int4 a = src[row * q4 + col / 4];
+              const uint32_t b01 = wb2[col / 2], b23 = wb2[col / 2 + 1];
+              const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
+              const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
+              v = (x0 | (x1 << 8) | (x2 << 16) | (x3 << 24)) | 0x80808080u;
+            }
+            w[h] = v;
+          }
+          win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+        }
+      } else {
+        constexpr int RP = LPC * PP;  // pieces per padded row
+        const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+        for (int i = t; i < wrows * RP; i += NT) {
+          const int row = i / RP, pc = i - row * RP;
+          if constexpr (P16) {  // columns 8pc .. 8pc + 7 (npad is a multiple of 4)
+            const int4 a = src[row * q4 + min(2 * pc, q4 - 1)];
+            const int4 b = src[row * q4 + min(2 * pc + 1, q4 - 1)];
+            const bool va = 8 * pc < npad, vb = 8 * pc + 4 < npad;  // else -1 (packs to 0)
+            win4[row * WRS4 + pc + pc / PP] =
+                make_int4(va ? (int)pack_la16(a.x, a.y) : 0, va ? (int)pack_la16(a.z, a.w) : 0,
+                          vb ? (int)pack_la16(b.x, b.y) : 0, vb ? (int)pack_la16(b.z, b.w) : 0);
+          } else {
+            win4[row * WRS4 + pc + pc / PP] = pc < q4 ? src[row * q4 + pc] : make_int4(-1, -1, -1, -1);
+          }
+        }
+      }
+      if (t <= WROWS) hist[t] = 0;
+      __syncthreads();
+  };
   for (int it = 0;; ++it) {
   const int32_t *Bp = d.Bp + (int64_t)p * n;
   // BH_DIAG timeline (tools/timeline.py): start, first window staged, search
@@ -563,151 +728,11 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   __syncthreads();
   int32_t wk0 = own;
   int32_t result = len;
-  constexpr int PP8 = PP / 2, WRS8 = LPC * (PP8 + 1);  // P8: 16-B pieces of 16 columns per lane
   for (;;) {
     const int wrows = min(WROWS, len - wk0);
     if (wrows <= 0) break;
-    // COLS: the window's 36 aligned rows of every column from la_col, issued
-    // before the fit check below reads its two rows
-    constexpr int CQ = LPC * 16, CT = NT / CQ, CNP = (9 + CT - 1) / CT;  // column quads, threads per quad, pieces per thread
-    const int cg = t % CQ, ch = t / CQ;
-    const int32_t crb = (cs + wk0) & ~3;
-    const int coff = cs + wk0 - crb;
-    int4 cpv[COLS == 1 ? CNP : 1][4];
-    if constexpr (COLS == 1) {
-#pragma unroll
-      for (int u = 0; u < CNP; ++u) {
-        const int pc = ch + u * CT;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int col = 4 * cg + k;
-          cpv[u][k] = pc < 9 && col < n ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)col * la_col_stride(d) + (crb + 4 * pc))
-                                        : make_int4(-1, -1, -1, -1);
-        }
-      }
-    }
-    bool p8 = false, p8g = false;
-    if constexpr (P16) {
-      if (d.round_p8) {
-        // P8 when every column's spread down the window fits (first row: the
-        // base, last row: the largest LA).  The first window of an iteration
-        // whose previous round's boundaries are known also tries the shared
-        // base (B[r-1][i] - round_p8g): then every candidate whose row its
-        // producer already converted (c8tag) needs no conversion here
-        const bool tryg = d.cand8 != nullptr && d.round_p8g > 0 && r > d.r0 && wk0 == own;
-        if (t == 0) { sh_wide = 0; sh_gbad = !tryg; }
-        __syncthreads();
-        const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
-        const int32_t *Bprev = d.B + (int64_t)(r - 1) * n;
-        // LA of column i at the window's first / last row (-1 past n, 0 past npad)
-        auto la_w = [&](int i, int last) -> int32_t {
-          if (i >= npad) return 0;
-          if constexpr (COLS == 1)
-            return i < n ? d.la_col[(int64_t)i * la_col_stride(d) + cs + wk0 + (last ? wrows - 1 : 0)] : -1;
-          else
-            return (last ? r1p : r0p)[i];
-        };
-        bool bad = false, gbad = false;
-        for (int j = t; j < 256; j += 256) {
-          const int i0 = 2 * j, i1 = 2 * j + 1;
-          const int32_t a0 = la_w(i0, 0), a1 = la_w(i1, 0);
-          const int32_t z0 = la_w(i0, 1), z1 = la_w(i1, 1);
-          const int32_t b0 = max(a0, 0), b1 = max(a1, 0);
-          wbase2[j] = (uint32_t)b0 | ((uint32_t)b1 << 16);
-          bad |= z0 + 1 - b0 > d.round_p8 || z1 + 1 - b1 > d.round_p8;
-          if (tryg) {
-            // columns past n keep the window base (their candidate bytes are 127 either way)
-            const int32_t g0 = i0 < n ? max(ldx<PERS>(Bprev + i0) - d.round_p8g, 0) : b0;
-            const int32_t g1 = i1 < n ? max(ldx<PERS>(Bprev + i1) - d.round_p8g, 0) : b1;
-            gbase2[j] = (uint32_t)g0 | ((uint32_t)g1 << 16);
-            gbad |= a0 + 1 < g0 || a1 + 1 < g1 || z0 + 1 - g0 > d.round_p8 || z1 + 1 - g1 > d.round_p8;
-          }
-        }
-        if (__any(bad) && lane == 0) sh_wide = 1;
-        if (__any(gbad) && lane == 0) sh_gbad = 1;
-        __syncthreads();
-        p8g = !sh_gbad;
-        p8 = p8g || !sh_wide;
-      }
-    }
-    const uint32_t *wb2 = p8g ? gbase2 : wbase2;
-    __syncthreads();
-    if constexpr (COLS == 1) {
-      // quad cg's 4 columns, 4 rows per piece: P8 one dword per row (bytes
-      // x | 0x80, as below), P16 two (16-bit LA + 1 pairs); window row = the
-      // piece's row - coff, rows outside [0, wrows) skipped
-      uint32_t *w32 = reinterpret_cast<uint32_t *>(win4);
-      uint32_t bs[4] = {0, 0, 0, 0};
-      if (p8) {
-        const uint32_t b01 = wb2[2 * cg], b23 = wb2[2 * cg + 1];
-        bs[0] = b01 & 0xFFFFu; bs[1] = b01 >> 16; bs[2] = b23 & 0xFFFFu; bs[3] = b23 >> 16;
-      }
-      const int pc8 = cg >> 2, pc16 = cg >> 1;
-      const int o8 = (pc8 + pc8 / PP8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
-#pragma unroll
-      for (int u = 0; u < CNP; ++u) {
-        const int pc = ch + u * CT;
-        if (pc >= 9) continue;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int wr = 4 * pc + e - coff;
-          if (wr < 0 || wr >= wrows) continue;
-          auto el = [&](int k) -> int32_t {
-            const int4 v = cpv[u][k];
-            return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
-          };
-          if (p8) {
-            uint32_t x = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) x |= ((uint32_t)(el(k) + 1 - (int32_t)bs[k]) & 0xFFu) << (8 * k);
-            w32[wr * WRS8 * 4 + o8] = x | 0x80808080u;
-          } else {
-            w32[wr * WRS4 * 4 + o16] = pack_la16(el(0), el(1));
-            w32[wr * WRS4 * 4 + o16 + 1] = pack_la16(el(2), el(3));
-          }
-        }
-      }
-    } else if (p8) {
-      // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
-      constexpr int RP8 = LPC * PP8;
-      const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-      for (int i = t; i < wrows * RP8; i += NT) {
-        const int row = i / RP8, pc = i - row * RP8;
-        uint32_t w[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
-          uint32_t v = 0x80808080u;
-          if (col < npad) {
-            const int4 a = src[row * q4 + col / 4];
-            const uint32_t b01 = wb2[col / 2], b23 = wb2[col / 2 + 1];
-            const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
-            const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
-            v = (x0 | (x1 << 8) | (x2 << 16) | (x3 << 24)) | 0x80808080u;
-          }
-          w[h] = v;
-        }
-        win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
-      }
-    } else {
-      constexpr int RP = LPC * PP;  // pieces per padded row
-      const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-      for (int i = t; i < wrows * RP; i += NT) {
-        const int row = i / RP, pc = i - row * RP;
-        if constexpr (P16) {  // columns 8pc .. 8pc + 7 (npad is a multiple of 4)
-          const int4 a = src[row * q4 + min(2 * pc, q4 - 1)];
-          const int4 b = src[row * q4 + min(2 * pc + 1, q4 - 1)];
-          const bool va = 8 * pc < npad, vb = 8 * pc + 4 < npad;  // else -1 (packs to 0)
-          win4[row * WRS4 + pc + pc / PP] =
-              make_int4(va ? (int)pack_la16(a.x, a.y) : 0, va ? (int)pack_la16(a.z, a.w) : 0,
-                        vb ? (int)pack_la16(b.x, b.y) : 0, vb ? (int)pack_la16(b.z, b.w) : 0);
-        } else {
-          win4[row * WRS4 + pc + pc / PP] = pc < q4 ? src[row * q4 + pc] : make_int4(-1, -1, -1, -1);
-        }
-      }
-    }
-    if (t <= WROWS) hist[t] = 0;
-    __syncthreads();
+    if (!(PERS && prestaged && wk0 == own)) stage(wk0, wrows, r, own);  // (PERS: else staged during the barrier)
+    prestaged = false;
     if (dgt && !rt1) rt1 = __builtin_amdgcn_s_memrealtime();
     if (p8 && d.round_ilp2) {
       // byte rows, two candidates per lane group at once (passes pass and
@@ -1003,9 +1028,19 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // ---- grid barrier (PERS) ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
   __syncthreads();
+  const bool lead = t == 0 && pbar_arrive(d, it, xcc, gx);
+  {
+    // the next round's first window, staged while the other workgroups
+    // arrive: its rows start at this round's result, its shared base is
+    // B[r] (stored before the previous barrier)
+    const int wrows_n = min(WROWS, len - result);
+    if (wrows_n > 0 && d.prestage) {
+      stage(result, wrows_n, r + 1, result);
+      prestaged = true;
+    }
+  }
   if (t == 0) {
-    pbar_arrive(d, it, xcc, gx);
-    sh_res = pbar_wait(d, it, gridDim.x, nx) ? 0 : -1;
+    sh_res = pbar_wait(d, it, gridDim.x, nx, xcc, lead) ? 0 : -1;
     if (it == 0) pbar_counts(d, xcc, gx, nx);
   }
   __syncthreads();
@@ -1545,23 +1580,9 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   };
   own_loads();
   if (t == 0) sh_fail = 0;
-  // BH_PBAR=xcd (pbar_mode 1): from the second iteration on, an XCD-
-  // hierarchical barrier -- each workgroup adds to its XCD's counter, the
-  // XCD's last arriver adds to the top counter, every workgroup polls the
-  // top one (16 arrivals per counter instead of 128 on one).  The workgroups
-  // count themselves per XCD first (an add whose return is waited for, so it
-  // is performed before this workgroup's first arrival below).  pbar layout
-  // (ints): [0] flat / top counter, [32 (1 + x)] XCD x's counter, [288 + x]
-  // XCD x's workgroups; each on 128-B lines of its own
-  int xcc = 0;
-  if (d.pbar_mode == 1) {
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-    xcc &= 7;
-    if (t == 0) {
-      const int32_t o = __hip_atomic_fetch_add(d.pbar + 288 + xcc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (o < 0) sh_fail = 1;  // (never: consumes the returned value)
-    }
-  }
+  // the grid barrier (pbar_register / _arrive / _wait / _counts: one counter,
+  // or XCD-hierarchical from 64 workgroups up)
+  const int xcc = t == 0 ? pbar_register(d) : 0;
   int32_t gx = 0, nx = 0;  // workgroups on this XCD, XCDs with workgroups (read after the first barrier)
   if (npad > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
     for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
@@ -1715,35 +1736,15 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // ---- grid barrier ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
     __syncthreads();
-    const bool hier = d.pbar_mode == 1 && it > 0;
-    if (t == 0) {
-      if (hier) {
-        const int32_t o = __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (o == it * gx - 1) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    const bool lead = t == 0 && pbar_arrive(d, it, xcc, gx);
     ++r;
     p ^= 1;
     k0 = result;
     hin.j0 = result < len ? fdv : FD_NONE;
     own_loads();  // lands during the wait
     if (t == 0) {
-      // flat: (it + 1) G arrivals; hierarchical: G after the first barrier, then nx per iteration
-      const int32_t target = hier ? G + it * nx : (it + 1) * G;
-      int spins = 0;
-      while (__hip_atomic_load(d.pbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > d.pbar_spin) {
-          sh_fail = 1;
-          break;
-        }
-      }
-    }
-    if (d.pbar_mode == 1 && it == 0 && t == 0) {  // every workgroup has counted itself by now
-      gx = __hip_atomic_load(d.pbar + 288 + xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int x = 0; x < 8; ++x) nx += __hip_atomic_load(d.pbar + 288 + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0;
+      if (!pbar_wait(d, it, G, nx, xcc, lead)) sh_fail = 1;
+      if (it == 0) pbar_counts(d, xcc, gx, nx);
     }
     __syncthreads();
     if (sh_fail) {
@@ -1793,7 +1794,7 @@ bool round_wide_persist_eligible(const Dev &d) {
 void launch_round_wide_persist(const Dev &d, hipStream_t s) {
   const int lpc = lanes_per_candidate(d.npad);
   const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
-  (void)hipMemsetAsync(d.pbar, 0, 2048, s);
+  (void)hipMemsetAsync(d.pbar, 0, 4096, s);
   if (lpc == 8) k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
   else k_round_wide<4, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
 }
@@ -1801,7 +1802,7 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
 void launch_round_persist(const Dev &d, hipStream_t s) {
   const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
-  (void)hipMemsetAsync(d.pbar, 0, 2048, s);  // (the counters' lines; 16-B multiple from the allocation's start)
+  (void)hipMemsetAsync(d.pbar, 0, 4096, s);  // (the barrier's lines; 16-B multiple from the allocation's start)
   if (d.npad <= 32) k_round2p<1><<<d.n, nt, lds, s>>>(d);
   else if (d.npad <= 64) k_round2p<2><<<d.n, nt, lds, s>>>(d);
   else k_round2p<4><<<d.n, nt, lds, s>>>(d);
