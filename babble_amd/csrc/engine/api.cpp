@@ -1749,7 +1749,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   A(&d.lt, C + 64); A(&d.depth, C); A(&d.chunk_maxd, C / 64 + 1); A(&d.desc, (size_t)C + 64);
   A(&d.B, R1 * n); A(&d.wofs, R1); A(&d.wcnt, R1); A(&d.wids, (size_t)d.W_cap);
   A(&d.wrow, (size_t)d.W_cap);
-  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 1024);
+  A(&d.Bp, (size_t)2 * n); A(&d.state, bh::ST_COUNT); A(&d.pbar, 1024 + 32 * 512);  // (kernels_rounds.hip PBAR_INTS)
   // the persistent loops' input snapshot (run_round_loop): Bp, candfd, the
   // state block, cand8 and its tags, each rounded to 16 B
   A(&d.psnap, (size_t)n + 4 + (size_t)n * d.npad + bh::ST_COUNT + (size_t)n * ((d.npad + 15) / 16 * 4) + n + 4);

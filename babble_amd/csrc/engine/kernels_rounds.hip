@@ -153,17 +153,23 @@ __device__ __forceinline__ int4 ld128(__amdgpu_buffer_rsrc_t rs, const int4 *bas
   else return base[idx];
 }
 
-// The persistent loops' grid barrier (thread 0 of each workgroup calls these).
-// pbar layout (ints): [0] the counter (flat) / top counter (hierarchical),
-// [32 (1 + x)] XCD x's arrivals, [288 + x] XCD x's workgroups, [320 + 32 x]
-// XCD x's release generation, each group on 128-B lines of its own.
-// pbar_mode 1 (XCD-hierarchical) from the second barrier on: a workgroup
-// adds to its XCD's counter; the XCD's last arriver (told by the value its
-// add returns) adds to the top counter, polls it until every XCD's leader
-// has added, and releases its XCD by storing the generation its other
-// workgroups poll -- 16 or 64 arrivals per counter and 8 pollers of the top
-// one, instead of every workgroup's adds and polls on one line.
-__device__ __forceinline__ int pbar_register(const Dev &d) {  // at the start: this workgroup's XCD, counted
+// The persistent loops' grid barrier.  pbar layout (ints): [0] the counter
+// (flat) / top counter (hierarchical), [32 (1 + x)] XCD x's arrivals,
+// [288 + x] XCD x's workgroups, [PBAR_REL + 32 w] workgroup w's release word,
+// each on 128-B lines of its own.  pbar_mode 1 (XCD-hierarchical) from the
+// second barrier on: a workgroup adds to its XCD's counter; the XCD's last
+// arriver (told by the value its add returns) adds to the top counter; the
+// workgroup whose top add completes it (told the same way) releases every
+// workgroup by storing the round into its release word, which each polls
+// alone.  The chain from the last arrival to a release is two returned
+// atomics and one store, and no line is polled by more than one workgroup
+// (a shared release line polled by 64 workgroups spread the releases over
+// 5 us).  Flat (pbar_mode 0, and the first barrier): every workgroup adds to
+// and polls [0].
+constexpr int PBAR_REL = 1024;
+constexpr int PBAR_INTS = PBAR_REL + 32 * 512;  // (n <= 512 workgroups)
+
+__device__ __forceinline__ int pbar_register(const Dev &d) {  // thread 0, at the start: this workgroup's XCD, counted
   int xcc = 0;
   if (d.pbar_mode == 1) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
@@ -173,16 +179,20 @@ __device__ __forceinline__ int pbar_register(const Dev &d) {  // at the start: t
   }
   return xcc;
 }
-// returns whether this workgroup is its XCD's leader for this barrier
-__device__ __forceinline__ bool pbar_arrive(const Dev &d, int it, int xcc, int32_t gx) {
-  if (d.pbar_mode == 1 && it > 0) {
-    const int32_t o = __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (o != it * gx - 1) return false;
-    __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
+// wave 0 of each workgroup (lane 0 holds xcc, gx, nx), after every wave's
+// stores have drained and a workgroup barrier
+__device__ __forceinline__ void pbar_arrive(const Dev &d, int it, int xcc, int32_t gx, int G, int32_t nx) {
+  const int lane = threadIdx.x & 63;
+  if (!(d.pbar_mode == 1 && it > 0)) {
+    if (lane == 0) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
-  __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return false;
+  int last = 0;
+  if (lane == 0 &&
+      __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it * gx - 1)
+    last = __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G + it * nx - 1;
+  if (__shfl(last, 0))
+    for (int w = lane; w < G; w += 64) __hip_atomic_store(d.pbar + PBAR_REL + 32 * w, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool pbar_poll(const Dev &d, const int32_t *w, int32_t target) {
   int spins = 0;
@@ -192,14 +202,10 @@ __device__ __forceinline__ bool pbar_poll(const Dev &d, const int32_t *w, int32_
   }
   return true;
 }
-// false: the barrier gave up (d.pbar_spin polls)
-__device__ __forceinline__ bool pbar_wait(const Dev &d, int it, int G, int32_t nx, int xcc, bool lead) {
-  if (!(d.pbar_mode == 1 && it > 0)) return pbar_poll(d, d.pbar, (it + 1) * G);
-  if (!lead) return pbar_poll(d, d.pbar + 320 + 32 * xcc, it);
-  const bool ok = pbar_poll(d, d.pbar, G + it * nx);
-  // released (or given up: the waiters then give up too, at their own limit)
-  if (ok) __hip_atomic_store(d.pbar + 320 + 32 * xcc, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return ok;
+// thread 0; false: the barrier gave up (d.pbar_spin polls)
+__device__ __forceinline__ bool pbar_wait(const Dev &d, int it, int G) {
+  if (d.pbar_mode == 1 && it > 0) return pbar_poll(d, d.pbar + PBAR_REL + 32 * blockIdx.x, it);
+  return pbar_poll(d, d.pbar, (it + 1) * G);
 }
 // after the first barrier every workgroup has counted itself
 __device__ __forceinline__ void pbar_counts(const Dev &d, int xcc, int32_t &gx, int32_t &nx) {
@@ -1028,7 +1034,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // ---- grid barrier (PERS) ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
   __syncthreads();
-  const bool lead = t == 0 && pbar_arrive(d, it, xcc, gx);
+  if (t < 64) pbar_arrive(d, it, xcc, gx, gridDim.x, nx);
   {
     // the next round's first window, staged while the other workgroups
     // arrive: its rows start at this round's result, its shared base is
@@ -1040,7 +1046,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     }
   }
   if (t == 0) {
-    sh_res = pbar_wait(d, it, gridDim.x, nx, xcc, lead) ? 0 : -1;
+    sh_res = pbar_wait(d, it, gridDim.x) ? 0 : -1;
     if (it == 0) pbar_counts(d, xcc, gx, nx);
   }
   __syncthreads();
@@ -1736,14 +1742,14 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // ---- grid barrier ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
     __syncthreads();
-    const bool lead = t == 0 && pbar_arrive(d, it, xcc, gx);
+    if (t < 64) pbar_arrive(d, it, xcc, gx, G, nx);
     ++r;
     p ^= 1;
     k0 = result;
     hin.j0 = result < len ? fdv : FD_NONE;
     own_loads();  // lands during the wait
     if (t == 0) {
-      if (!pbar_wait(d, it, G, nx, xcc, lead)) sh_fail = 1;
+      if (!pbar_wait(d, it, G)) sh_fail = 1;
       if (it == 0) pbar_counts(d, xcc, gx, nx);
     }
     __syncthreads();
@@ -1794,7 +1800,7 @@ bool round_wide_persist_eligible(const Dev &d) {
 void launch_round_wide_persist(const Dev &d, hipStream_t s) {
   const int lpc = lanes_per_candidate(d.npad);
   const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
-  (void)hipMemsetAsync(d.pbar, 0, 4096, s);
+  (void)hipMemsetAsync(d.pbar, 0, (size_t)PBAR_INTS * 4, s);
   if (lpc == 8) k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
   else k_round_wide<4, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
 }
@@ -1802,7 +1808,7 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
 void launch_round_persist(const Dev &d, hipStream_t s) {
   const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
-  (void)hipMemsetAsync(d.pbar, 0, 4096, s);  // (the barrier's lines; 16-B multiple from the allocation's start)
+  (void)hipMemsetAsync(d.pbar, 0, (size_t)PBAR_INTS * 4, s);  // (the barrier's lines; 16-B multiple from the allocation's start)
   if (d.npad <= 32) k_round2p<1><<<d.n, nt, lds, s>>>(d);
   else if (d.npad <= 64) k_round2p<2><<<d.n, nt, lds, s>>>(d);
   else k_round2p<4><<<d.n, nt, lds, s>>>(d);
