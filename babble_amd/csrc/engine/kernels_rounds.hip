@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_round(Dev d, int p) {
 // workgroups hand each other -- boundaries (Bp, B), candidates' rows (cand16,
 // cand8) and tags -- goes through sc1 stores and loads.  512 workgroups, two
 // per compute unit, all resident.
-template <int LPC, bool P16, int COLS = 0, int NT = 256, bool PERS = false>
+template <int LPC, bool P16, int COLS = 0, int NT = 256, bool PERS = false, int ILPK = 2>
 __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  // 2 workgroups per CU (NT / 128 waves per SIMD)
   extern __shared__ __attribute__((aligned(16))) int4 win4[];  // [WROWS][WRS4]
   constexpr int PP = P16 ? 8 : PIECES;  // 16-B pieces per lane
@@ -741,9 +741,9 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     prestaged = false;
     if (dgt && !rt1) rt1 = __builtin_amdgcn_s_memrealtime();
     if (p8 && d.round_ilp2) {
-      // byte rows, two candidates per lane group at once (passes pass and
-      // pass + 1): their binary searches interleave, so each probe's LDS
-      // reads and compares overlap the other's (two waves per SIMD hide
+      // byte rows, ILPK candidates per lane group at once (passes pass ..
+      // pass + ILPK - 1): their binary searches interleave, so each probe's
+      // LDS reads and compares overlap the others' (two waves per SIMD hide
       // little of a lone search's LDS latency)
       // a candidate's byte row, its tag and its chain's B / length are loaded
       // together, none waiting on another (the tag decides only afterwards
@@ -781,67 +781,83 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
         }
       };
       const int4 *xb8 = win4 + part * (PP8 + 1);
-      for (int pass = 0; pass < npass; pass += 2) {
-        const int qa = pass * CPP + t / LPC, qb = qa + CPP;
-        const int qa1 = min(qa, n - 1), qb1 = min(qb, n - 1);
-        const int32_t ba = ldx<PERS>(Bp + qa1), la_ = d.chain_len[qa1], bb_ = ldx<PERS>(Bp + qb1), lb = d.chain_len[qb1];
-        const int32_t taga = ldx<PERS>(d.c8tag + (int64_t)p * n + qa1), tagb = ldx<PERS>(d.c8tag + (int64_t)p * n + qb1);
-        uint32_t fa[4 * PP8], fb[4 * PP8];
-        raw_f8(qa, fa);
-        raw_f8(qb, fb);
-        const bool acta = qa < n && ba < la_, actb = qb < n && bb_ < lb;
-        load_f8(qa, acta, taga, fa);
-        load_f8(qb, actb, tagb, fb);
-        auto ss2 = [&](int ra, int rb, bool &sa, bool &sb) {
-          const int4 *xa4 = xb8 + ra * WRS8, *xb4 = xb8 + rb * WRS8;
-          int4 xa[PP8], xb[PP8];
+      for (int pass = 0; pass < npass; pass += ILPK) {
+        int qv[ILPK];
+        bool act[ILPK];
+        int32_t tag[ILPK];
+        uint32_t f[ILPK][4 * PP8];
 #pragma unroll
-          for (int u = 0; u < PP8; ++u) { xa[u] = xa4[u]; xb[u] = xb4[u]; }
-          int ga = 0, gb = 0;
+        for (int k = 0; k < ILPK; ++k) {
+          qv[k] = (pass + k) * CPP + t / LPC;
+          const int q1 = min(qv[k], n - 1);
+          const int32_t bq = ldx<PERS>(Bp + q1), lq = d.chain_len[q1];
+          tag[k] = ldx<PERS>(d.c8tag + (int64_t)p * n + q1);
+          raw_f8(qv[k], f[k]);
+          act[k] = qv[k] < n && bq < lq;
+        }
 #pragma unroll
-          for (int u = 0; u < PP8; ++u) {
-            ga += __builtin_popcount(((uint32_t)xa[u].x - fa[4 * u]) & 0x80808080u);
-            gb += __builtin_popcount(((uint32_t)xb[u].x - fb[4 * u]) & 0x80808080u);
-            ga += __builtin_popcount(((uint32_t)xa[u].y - fa[4 * u + 1]) & 0x80808080u);
-            gb += __builtin_popcount(((uint32_t)xb[u].y - fb[4 * u + 1]) & 0x80808080u);
-            ga += __builtin_popcount(((uint32_t)xa[u].z - fa[4 * u + 2]) & 0x80808080u);
-            gb += __builtin_popcount(((uint32_t)xb[u].z - fb[4 * u + 2]) & 0x80808080u);
-            ga += __builtin_popcount(((uint32_t)xa[u].w - fa[4 * u + 3]) & 0x80808080u);
-            gb += __builtin_popcount(((uint32_t)xb[u].w - fb[4 * u + 3]) & 0x80808080u);
-          }
-          sa = group_total<LPC>(ga) >= sm;
-          sb = group_total<LPC>(gb) >= sm;
+        for (int k = 0; k < ILPK; ++k) load_f8(qv[k], act[k], tag[k], f[k]);
+        // the ILPK candidates' probes of rows rw[k], all reads issued first
+        auto ssk = [&](const int (&rw)[ILPK], bool (&sv)[ILPK]) {
+          int4 x[ILPK][PP8];
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k)
+#pragma unroll
+            for (int u = 0; u < PP8; ++u) x[k][u] = xb8[rw[k] * WRS8 + u];
+          int g[ILPK];
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k) g[k] = 0;
+#pragma unroll
+          for (int u = 0; u < PP8; ++u)
+#pragma unroll
+            for (int k = 0; k < ILPK; ++k) {
+              g[k] += __builtin_popcount(((uint32_t)x[k][u].x - f[k][4 * u]) & 0x80808080u);
+              g[k] += __builtin_popcount(((uint32_t)x[k][u].y - f[k][4 * u + 1]) & 0x80808080u);
+              g[k] += __builtin_popcount(((uint32_t)x[k][u].z - f[k][4 * u + 2]) & 0x80808080u);
+              g[k] += __builtin_popcount(((uint32_t)x[k][u].w - f[k][4 * u + 3]) & 0x80808080u);
+            }
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k) sv[k] = group_total<LPC>(g[k]) >= sm;
         };
         // binary search over [0, wrows - 1] without probing the last row
         // first: that row is probed afterwards only where no probe came out
         // true (the candidate is seen at the last row, or not at all -- few);
         // a short window's spare iterations probe lo == hi itself
-        int loa = 0, hia = wrows - 1, lob = 0, hib = wrows - 1;
-        bool va = false, vb = false;
+        int lo[ILPK], hi[ILPK];
+        bool vf[ILPK];
 #pragma unroll
-        for (int it = 0; it < 5; ++it) {
-          const int mida = (loa + hia) >> 1, midb = (lob + hib) >> 1;  // (<= hi, also once lo = hi + 1)
-          bool ta, tb;
-          ss2(mida, midb, ta, tb);
-          if (loa <= hia) {
-            if (ta) { hia = mida; va = true; } else { loa = mida + 1; }
-          }
-          if (lob <= hib) {
-            if (tb) { hib = midb; vb = true; } else { lob = midb + 1; }
-          }
+        for (int k = 0; k < ILPK; ++k) { lo[k] = 0; hi[k] = wrows - 1; vf[k] = false; }
+#pragma unroll
+        for (int pr = 0; pr < 5; ++pr) {
+          int mid[ILPK];
+          bool tv[ILPK];
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k) mid[k] = (lo[k] + hi[k]) >> 1;  // (<= hi, also once lo = hi + 1)
+          ssk(mid, tv);
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k)
+            if (lo[k] <= hi[k]) {
+              if (tv[k]) { hi[k] = mid[k]; vf[k] = true; } else { lo[k] = mid[k] + 1; }
+            }
         }
-        const bool ua = !va && loa < wrows, ub = !vb && lob < wrows;  // lo = hi = wrows - 1, unverified
-        if (__any(ua || ub)) {
-          bool ta, tb;
-          ss2(wrows - 1, wrows - 1, ta, tb);
-          va = va || (ua && ta);
-          vb = vb || (ub && tb);
+        bool un[ILPK], anyu = false;  // lo = hi = wrows - 1, unverified
+#pragma unroll
+        for (int k = 0; k < ILPK; ++k) { un[k] = !vf[k] && lo[k] < wrows; anyu |= un[k]; }
+        if (__any(anyu)) {
+          int last[ILPK];
+          bool tv[ILPK];
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k) last[k] = wrows - 1;
+          ssk(last, tv);
+#pragma unroll
+          for (int k = 0; k < ILPK; ++k) vf[k] = vf[k] || (un[k] && tv[k]);
         }
-        const int twa = va ? loa : WROWS, twb = vb ? lob : WROWS;
-        if (acta && part == 0 && twa < WROWS) atomicAdd(&hist[twa], 1);
-        if (actb && part == 0 && twb < WROWS) atomicAdd(&hist[twb], 1);
-        if (d.ssw && part == 0 && qa < n) tq_s[qa] = (int8_t)(acta ? twa : WROWS);
-        if (d.ssw && part == 0 && qb < n) tq_s[qb] = (int8_t)(actb ? twb : WROWS);
+#pragma unroll
+        for (int k = 0; k < ILPK; ++k) {
+          const int tw = vf[k] ? lo[k] : WROWS;
+          if (act[k] && part == 0 && tw < WROWS) atomicAdd(&hist[tw], 1);
+          if (d.ssw && part == 0 && qv[k] < n) tq_s[qv[k]] = (int8_t)(act[k] ? tw : WROWS);
+        }
       }
     } else
     for (int pass = 0; pass < npass; ++pass) {
@@ -1801,7 +1817,10 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
   const int lpc = lanes_per_candidate(d.npad);
   const size_t wb16 = (size_t)WROWS * lpc * 9 * 16;
   (void)hipMemsetAsync(d.pbar, 0, (size_t)PBAR_INTS * 4, s);
-  if (lpc == 8) k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  const bool ilp4 = getenv("BH_WIDE_ILP") && atoi(getenv("BH_WIDE_ILP")) == 4;  // (A/B: four searches interleaved)
+  if (lpc == 8 && ilp4) k_round_wide<8, true, 0, 256, true, 4><<<d.n, 256, wb16, s>>>(d, 0);
+  else if (lpc == 8) k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  else if (ilp4) k_round_wide<4, true, 0, 256, true, 4><<<d.n, 256, wb16, s>>>(d, 0);
   else k_round_wide<4, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
 }
 
@@ -2355,6 +2374,7 @@ void configure_round_kernels() {
   CFG((k_round_wide<4, true, 1>)); CFG((k_round_wide<8, true, 1>));
   CFG((k_round_wide<4, true, 2>)); CFG((k_round_wide<8, true, 2>));
   CFG((k_round_wide<4, true, 0, 256, true>)); CFG((k_round_wide<8, true, 0, 256, true>));
+  CFG((k_round_wide<4, true, 0, 256, true, 4>)); CFG((k_round_wide<8, true, 0, 256, true, 4>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
