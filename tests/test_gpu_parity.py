@@ -370,8 +370,7 @@ def test_chunk_sweep_wild(monkeypatch):
 @pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p8_single", "p8g_tight_single",
                                   "p16", "p32", "fdt_p8", "fdt_p16", "cols_p8", "cols_p8g_tight", "cols_p16",
                                   "cols2_p8", "cols2_p16", "iter_p8", "iter_p8_mixed", "iter_p8g_tight",
-                                  "fallback_p8", "noprestage_p8", "flat_p8_mixed", "ilp4_p8", "ilp4_p8_mixed",
-                                  "ilp4_p8g_tight"])
+                                  "fallback_p8", "noprestage_p8", "flat_p8_mixed"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -399,9 +398,6 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     if rows.startswith("iter_"):
         monkeypatch.setenv("BH_ROUND_PERSIST", "0")
         rows = rows[len("iter_"):]
-    if rows.startswith("ilp4_"):  # four candidates' searches interleaved per lane group
-        monkeypatch.setenv("BH_WIDE_ILP", "4")
-        rows = rows[len("ilp4_"):]
     if rows.startswith("noprestage_"):  # the next window staged after the barrier, not during it
         monkeypatch.setenv("BH_PRESTAGE", "0")
         rows = rows[len("noprestage_"):]
