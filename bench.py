@@ -222,11 +222,15 @@ def main():
     achieved = value * B / 1e9
     traffic_step = sum(v["hbm_bytes_per_step"] for v in pmc.values()) if pmc else None
     # the dominant kernel: the round loop, timed live by HIP events around it
-    # (stage 7).  n <= 128: the persistent k_round2p, one launch per pipeline
-    # segment running all of that segment's rounds (N / launches events per
-    # launch); else k_round_wide, one launch per round
+    # (stage 7).  Persistent (the default): n <= 128 k_round2p, one launch per
+    # pipeline segment running all of that segment's rounds; n <= 512
+    # k_round_wide<..., true>, one launch per call (N / launches events per
+    # launch).  Otherwise one k_round2 / k_round_wide launch per round
     persistent = persist_per_step > 0
-    round_kernel = "k_round2p" if persistent else ("k_round2" if npad <= 128 else "k_round_wide")
+    if npad <= 128:
+        round_kernel = "k_round2p" if persistent else "k_round2"
+    else:
+        round_kernel = "k_round_wide"
     # the loop's own device time (stage 7): with the segment pipeline the
     # rounds stage [1] only counts what runs after the coordinates
     loop_ms = float(stage_tot[7] / args.steps) if len(stage_tot) > 7 else 0.0
@@ -277,8 +281,8 @@ def main():
                          "events_per_launch": ev_per_launch, "alg_bytes_per_launch": dom_alg,
                          "achieved": dom_achieved, "frac": dom_achieved / HBM_PEAK_GBS,
                          "traffic": dom["hbm_bytes_per_launch"] if dom else None,
-                         "note": "latency-bound: rounds are a serial chain (k_round2p: a grid barrier "
-                                 "per round inside one launch per segment; k_round_wide: one launch per round)"},
+                         "note": "latency-bound: rounds are a serial chain, a grid barrier per round inside "
+                                 "one persistent launch per segment (k_round2p) or per call (k_round_wide)"},
                      "l2_level": {"kernel": round_kernel, "bytes_per_iteration": l2_bytes,
                                   "GBps": l2_bytes / (iter_us * 1e-6) / 1e9,
                                   "note": "candidate FD rows + LA/FD windows re-read by every workgroup "
