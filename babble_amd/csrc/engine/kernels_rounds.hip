@@ -1009,12 +1009,16 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // fame's input for the new candidate y = (c, result): the candidates of
   // round r it strongly sees are those whose T_q in the final window is at
   // most y's row (stronglySee is monotone along the chain)
-  if (d.ssw && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
+  constexpr int NSW = 512 / NT;  // ssw words per wave
+  unsigned long long swm[NSW];
+  const bool has_ssw = d.ssw && sh_nc > 0 && result < len && r + 1 < d.R_cap;
+  if (has_ssw) {
     const int res = sh_res;
-    for (int q0 = 0; q0 < 512; q0 += NT) {
-      const int q = q0 + t;
-      const unsigned long long m = __ballot(q < n && tq_s[q] <= res);
-      if (lane == 0) d.ssw[ballot_row(d, c, r + 1) * 8 + (q0 >> 6) + wave] = m;
+#pragma unroll
+    for (int k = 0; k < NSW; ++k) {
+      const int q = k * NT + t;
+      swm[k] = __ballot(q < n && tq_s[q] <= res);
+      if (!PERS && lane == 0) d.ssw[ballot_row(d, c, r + 1) * 8 + ((k * NT) >> 6) + wave] = swm[k];
     }
   }
   // the hand-off: the new candidate's FD row for the next iteration
@@ -1039,7 +1043,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       if (c == 0) { d.state[ST_ERR] = 1; d.state[ST_ROUNDS] = r; d.state[ST_DONE] = 1; signal_done(d); }
     } else {
       stx<PERS>(d.Bp + (int64_t)(p ^ 1) * n + c, result);
-      stx<PERS>(d.B + (int64_t)(r + 1) * n + c, result);
+      if (!PERS) d.B[(int64_t)(r + 1) * n + c] = result;  // (PERS: after the arrival below)
       if (c == 0) {
         d.state[ST_CUR0 + (p ^ 1)] = r + 1;
         d.state[ST_ITERS] = r + 1;
@@ -1051,6 +1055,13 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
   __syncthreads();
   if (t < 64) pbar_arrive(d, it, xcc, gx, gridDim.x, nx);
+  // fame's ballots and the round table: read after the loop, or B[r + 1]
+  // two barriers from now (the shared base) -- stored after the arrival, so
+  // the drain above waits only for the hand-over
+  if (has_ssw && lane == 0)
+#pragma unroll
+    for (int k = 0; k < NSW; ++k) d.ssw[ballot_row(d, c, r + 1) * 8 + ((k * NT) >> 6) + wave] = swm[k];
+  if (t == 0) stx<PERS>(d.B + (int64_t)(r + 1) * n + c, result);
   {
     // the next round's first window, staged while the other workgroups
     // arrive: its rows start at this round's result, its shared base is
@@ -1610,6 +1621,11 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
   int p = 0;
   for (int it = 0;; ++it) {
+    // BH_DIAG timeline (tools/timeline.py): iteration start (released),
+    // window staged, search done, hand-off issued -- rounds TL_R0 .. + TL_NR
+    const bool dgt = d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
+    const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long rt1 = 0, rt2 = 0;
     // round r's candidates: boundaries and FD rows, stored by other workgroups
     const int32_t bq = q < n ? __hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     int4 f[PPL];
@@ -1634,6 +1650,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     if (t < 16) cntk[t] = 0;
     if (t <= HW) hist[t] = 0;
     __syncthreads();
+    if (dgt) rt1 = __builtin_amdgcn_s_memrealtime();
     auto ss_row = [&](const int4 *x4) {
       int4 x[PPL];
 #pragma unroll
@@ -1685,6 +1702,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       __syncthreads();
     }
     const int nc = cntk[0];
+    if (dgt) rt2 = __builtin_amdgcn_s_memrealtime();
     int32_t result = len;
     int lrow = 0;
     if (res >= 0) {
@@ -1748,17 +1766,27 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       if ((t & 7) == 0 && (t >> 3) < npad)
         __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + (t >> 3), fdv, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
-      if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
     }
-    if (t == 0) {
-      __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, result, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      d.B[(int64_t)(r + 1) * n + c] = result;
+    if (t == 0) __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, result, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dgt && c < 128) {
+      unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
+      tl[0] = rt0;
+      tl[1] = rt2;
+      tl[2] = rt1;
+      tl[3] = __builtin_amdgcn_s_memrealtime();
     }
     // ---- grid barrier ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
     __syncthreads();
     if (t < 64) pbar_arrive(d, it, xcc, gx, G, nx);
+    // what no workgroup reads inside the loop -- fame's inputs (the new
+    // candidate's LA row and its ballots) and the round table -- is stored
+    // after the arrival, so the drain above waits only for the hand-over
+    if (result < len) {
+      if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
+      if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
+    }
+    if (t == 0) d.B[(int64_t)(r + 1) * n + c] = result;
     ++r;
     p ^= 1;
     k0 = result;
