@@ -160,12 +160,12 @@ __device__ __forceinline__ int4 ld128(__amdgpu_buffer_rsrc_t rs, const int4 *bas
 // second barrier on: a workgroup adds to its XCD's counter; the XCD's last
 // arriver (told by the value its add returns) adds to the top counter; the
 // workgroup whose top add completes it (told the same way) releases every
-// workgroup by storing the round into its release word, which each polls
+// workgroup by storing it + 1 into its release word, which each polls
 // alone.  The chain from the last arrival to a release is two returned
 // atomics and one store, and no line is polled by more than one workgroup
 // (a shared release line polled by 64 workgroups spread the releases over
 // 5 us).  Flat (pbar_mode 0, and the first barrier): every workgroup adds to
-// and polls [0].
+// [0], and the add that completes it releases everyone the same way.
 constexpr int PBAR_REL = 1024;
 constexpr int PBAR_INTS = PBAR_REL + 32 * 512;  // (n <= 512 workgroups)
 
@@ -180,19 +180,24 @@ __device__ __forceinline__ int pbar_register(const Dev &d) {  // thread 0, at th
   return xcc;
 }
 // wave 0 of each workgroup (lane 0 holds xcc, gx, nx), after every wave's
-// stores have drained and a workgroup barrier
+// stores have drained and a workgroup barrier.  The arrival that completes
+// the barrier -- of the top counter (hierarchical) or of the one counter
+// (flat, and the first barrier) -- is told so by its add's returned value
+// and releases every workgroup: release word w = it + 1.
 __device__ __forceinline__ void pbar_arrive(const Dev &d, int it, int xcc, int32_t gx, int G, int32_t nx) {
   const int lane = threadIdx.x & 63;
-  if (!(d.pbar_mode == 1 && it > 0)) {
-    if (lane == 0) __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
   int last = 0;
-  if (lane == 0 &&
-      __hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it * gx - 1)
-    last = __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G + it * nx - 1;
+  if (lane == 0) {
+    if (d.pbar_mode == 1 && it > 0) {
+      if (__hip_atomic_fetch_add(d.pbar + 32 * (1 + xcc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == it * gx - 1)
+        last = __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G + it * nx - 1;
+    } else {  // flat: (it + 1) G arrivals in all; the hierarchical top counter starts from the first barrier's G
+      last = __hip_atomic_fetch_add(d.pbar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (it + 1) * G - 1;
+    }
+  }
   if (__shfl(last, 0))
-    for (int w = lane; w < G; w += 64) __hip_atomic_store(d.pbar + PBAR_REL + 32 * w, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int w = lane; w < G; w += 64)
+      __hip_atomic_store(d.pbar + PBAR_REL + 32 * w, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool pbar_poll(const Dev &d, const int32_t *w, int32_t target) {
   int spins = 0;
@@ -204,8 +209,8 @@ __device__ __forceinline__ bool pbar_poll(const Dev &d, const int32_t *w, int32_
 }
 // thread 0; false: the barrier gave up (d.pbar_spin polls)
 __device__ __forceinline__ bool pbar_wait(const Dev &d, int it, int G) {
-  if (d.pbar_mode == 1 && it > 0) return pbar_poll(d, d.pbar + PBAR_REL + 32 * blockIdx.x, it);
-  return pbar_poll(d, d.pbar, (it + 1) * G);
+  (void)G;
+  return pbar_poll(d, d.pbar + PBAR_REL + 32 * blockIdx.x, it + 1);
 }
 // after the first barrier every workgroup has counted itself
 __device__ __forceinline__ void pbar_counts(const Dev &d, int xcc, int32_t &gx, int32_t &nx) {
