@@ -1674,10 +1674,11 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
-  // the XCD-hierarchical barrier from 64 workgroups up (C3: 8.4 -> 7.2 us per
-  // iteration, C5: 6.9 -> 6.7; C2's 32 workgroups: 4.3 -> 4.6, one counter
-  // stays); BH_PBAR=xcd|flat overrides
-  d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n >= 64 ? 1 : 0);
+  // the XCD-hierarchical barrier above 64 workgroups (with per-workgroup
+  // release words in both forms: C3 7.6 -> 7.05 us per iteration; C5's 64
+  // workgroups 6.9 -> 6.6 and C2's 32 4.2 -> 3.9 keep the one counter,
+  // profiles/r4_ab_xcd_barrier.txt); BH_PBAR=xcd|flat overrides
+  d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n > 64 ? 1 : 0);
   d.prestage = getenv("BH_PRESTAGE") ? atoi(getenv("BH_PRESTAGE")) != 0 : 1;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;

@@ -131,7 +131,7 @@ struct Dev {
   int32_t round_persist;  // k_round2p: the whole n <= 128 loop in one launch (default; BH_ROUND_PERSIST=0: one launch per iteration)
   int32_t *pbar;          // k_round2p's grid-barrier counter
   int32_t pbar_spin;      // k_round2p's barrier polls before it gives up (BH_PBAR_SPIN lowers it to test the fallback)
-  int32_t pbar_mode;      // the persistent loops' barrier: 0 one counter, 1 XCD-hierarchical (n >= 64; BH_PBAR=xcd|flat)
+  int32_t pbar_mode;      // the persistent loops' barrier: 0 one counter, 1 XCD-hierarchical (n > 64; BH_PBAR=xcd|flat)
   int32_t prestage;       // the wide persistent loop stages its next window while the barrier completes (BH_PRESTAGE=0: off)
   int32_t *psnap;         // the loop's inputs (Bp and candfd of parity 0, the state block) kept for that fallback
   int32_t round_src_rows;  // k_round2r: windows from the row-major LA, hand-off from FDT (BH_ROUND_SRC=rows, A/B)
