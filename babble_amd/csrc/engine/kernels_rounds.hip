@@ -1590,6 +1590,15 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   __shared__ int32_t sh_fail;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x, G = gridDim.x;
+  // BH_ROUND_PRIO (A/B): a loop workgroup that shares its compute unit with
+  // a coordinate workgroup takes the issue arbitration back from the older
+  // waves beside it
+  switch (d.round_prio) {
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: break;
+  }
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int rs4 = q4 + 1, rs = 4 * rs4;
   const int64_t stride = la_col_stride(d);
