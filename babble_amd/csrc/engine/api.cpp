@@ -1038,8 +1038,12 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     }
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
     if (eager) {
-      bh::launch_flow_transpose(v, sc);  // (its LT copy is redone by k_lt_rows below)
-      bh::launch_fd_idle(v, sc);
+      // (wide_cols 2: the loop's windows need the row-major LA, its hand-off
+      // no FDT -- the transpose writes LA rows only)
+      Dev vt = v;
+      vt.xpose_fd = d.wide_cols == 2 ? 0 : 1;
+      bh::launch_flow_transpose(vt, sc);  // (its LT copy is redone by k_lt_rows below)
+      if (vt.xpose_fd) bh::launch_fd_idle(v, sc);
     }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));  // the segment's LA is ready for the loop
@@ -1175,7 +1179,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // order reads LT) wait for the coordinate stream's end
   HIPCHK(h, hipStreamWaitEvent(sr, h->ev[1], 0));
   h->coords_for = (int)N;
-  h->rows_stale = !eager;
+  h->rows_stale = !eager || d.wide_cols == 2;  // (wide_cols 2 built no FDT)
   float ms = 0;
   h->sweep_ms = 0;
   for (int k = 0; k < K; ++k)
@@ -1680,6 +1684,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   // profiles/r4_ab_xcd_barrier.txt); BH_PBAR=xcd|flat overrides
   d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n > 64 ? 1 : 0);
   d.prestage = getenv("BH_PRESTAGE") ? atoi(getenv("BH_PRESTAGE")) != 0 : 1;
+  d.xpose_fd = 1;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;

@@ -640,6 +640,7 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
     }
   }
   __syncthreads();
+  if (!d.xpose_fd) return;  // (the wide loop that counts its hand-off in la_col reads no FDT)
   const uint64_t segs = segmask;
   const int lane = t & 63, wave = t >> 6;
   for (uint64_t m = segs; m; m &= m - 1) {

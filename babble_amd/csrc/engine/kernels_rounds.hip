@@ -280,11 +280,15 @@ __device__ __forceinline__ int32_t first_ge_wave(const int32_t *col, int32_t lo,
 // (an advance of more than ~45 rows) is searched by the wave
 // (first_ge_wave).  Writes cand16 (16-bit FD + 1), cand8 against the shared
 // base (as handoff_wide) and the candidate's LA row into cla (fame).
-template <int NT>
+template <int GL>
+__device__ __forceinline__ int32_t first_ge_group(const int32_t *col, int32_t lo, int32_t hi, int32_t k, bool on,
+                                                  bool near);
+
+template <int NT, bool SC1 = false>
 __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, int32_t row, const int32_t *Bcur,
                                                   int32_t rnext) {
   constexpr int K = 2048 / NT, HR = 48, KL = 512 / NT;  // chains per thread (n <= 512), rows per chain, LA values per thread
-  const int t = threadIdx.x, lane = t & 63, l4 = t & 3;
+  const int t = threadIdx.x, l4 = t & 3;
   const int n = d.n, npad = d.npad, w16 = (npad + 7) / 8 * 4, w8 = (npad + 15) / 16 * 16;
   const int64_t stride = la_col_stride(d);
   const int32_t *colc = d.la_col + (int64_t)c * stride;
@@ -303,7 +307,11 @@ __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, in
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int i = (t >> 2) + (NT / 4) * k;
-    const uint32_t h = i < n ? prev[i] : 0xFFFFu;
+    uint32_t h = 0xFFFFu;
+    if (i < n) {  // (SC1: the row this workgroup stored sc1 last round, read the same way)
+      if constexpr (SC1) h = (uint32_t)ldx<true>(reinterpret_cast<const int32_t *>(prev) + i / 2) >> (16 * (i & 1)) & 0xFFFFu;
+      else h = prev[i];
+    }
     cs[k] = i < n ? d.chain_start[i] : 0;
     end[k] = i < n ? cs[k] + d.chain_len[i] : 0;
     a[k] = h == 0xFFFFu ? -1 : cs[k] + (int32_t)h - 1;  // the previous entry (absolute row), -1: none
@@ -344,25 +352,37 @@ __device__ __forceinline__ void handoff_wide_cols(const Dev &d, int p, int c, in
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    unsigned long long mm = __ballot(miss[k] && l4 == 0);
-    while (mm) {  // (rare) beyond the 48 rows: the wave searches each such chain
-      const int src = __builtin_ctzll(mm);
-      mm &= mm - 1;
-      const int32_t lo = __shfl(min((a[k] & ~3) + HR, end[k]), src), hi = __shfl(end[k], src), b = __shfl(cs[k], src);
-      const int32_t j = first_ge_wave(colc, lo, hi, row);
-      if (lane == src) fd[k] = j < hi ? j - b : FD_NONE;
-    }
-    const int i = (t >> 2) + (NT / 4) * k;
-    if (l4 == 0 && i < 2 * w16) {
-      const uint32_t h = i < n ? min((uint32_t)fd[k] + 1u, 0xFFFFu) : 0xFFFFu;  // FD_NONE + 1 wraps to 2^31
-      dst16[i] = (uint16_t)h;
-      if (g && i < w8) {
-        const int32_t base = i < n ? max(Bcur[i] - d.round_p8g, 0) : 0;
-        dst8[i] = (uint8_t)(i < n ? min((uint32_t)max((int32_t)h - base, 0), 127u) : 127u);
-      }
+    // beyond the 48 rows (a candidate that jumped far): each such chain's 4
+    // lanes search on at once, the first pass over the next 256 rows
+    if (__any(miss[k])) {
+      const int32_t lo = min((a[k] & ~3) + HR, end[k]);
+      const int32_t j = first_ge_group<4>(colc, lo, end[k], row, miss[k], true);
+      if (miss[k]) fd[k] = j < end[k] ? j - cs[k] : FD_NONE;
     }
   }
-  if (g && t == 0) d.c8tag[(int64_t)(p ^ 1) * n + c] = rnext;
+  // the 16-bit and byte rows, 4 entries per lane into one dword each
+  // (SC1: stored sc1, read by the other workgroups after the grid barrier)
+  uint32_t *d16 = reinterpret_cast<uint32_t *>(dst16);
+  uint32_t *d8 = reinterpret_cast<uint32_t *>(dst8);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int i = (t >> 2) + (NT / 4) * k;
+    const uint32_t h = i < n ? min((uint32_t)fd[k] + 1u, 0xFFFFu) : 0xFFFFu;  // FD_NONE + 1 wraps to 2^31
+    uint32_t b = 127u;
+    if (g && i < n) {
+      const int32_t base = max(ldx<SC1>(Bcur + i) - d.round_p8g, 0);
+      b = min((uint32_t)max((int32_t)h - base, 0), 127u);
+    }
+    // chains i .. i + 3 sit in lanes l4 = 0 of four consecutive lane quads: gather them to the first
+    const uint32_t h1 = __shfl_down(h, 4), h2 = __shfl_down(h, 8), h3 = __shfl_down(h, 12);
+    const uint32_t b1 = __shfl_down(b, 4), b2 = __shfl_down(b, 8), b3 = __shfl_down(b, 12);
+    if (l4 == 0 && (i & 3) == 0 && i < 2 * w16) {
+      stx<SC1>(d16 + i / 2, h | (h1 << 16));
+      if (i + 2 < 2 * w16) stx<SC1>(d16 + i / 2 + 1, h2 | (h3 << 16));
+      if (g && i < w8) stx<SC1>(d8 + i / 4, b | (b1 << 8) | (b2 << 16) | (b3 << 24));
+    }
+  }
+  if (g && t == 0) stx<SC1>(d.c8tag + (int64_t)(p ^ 1) * n + c, rnext);
 }
 
 template <int LPC>
@@ -1028,7 +1048,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   }
   // the hand-off: the new candidate's FD row for the next iteration
   if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
-    if constexpr (COLS != 0) handoff_wide_cols<NT>(d, p, c, result, Bp, r + 1);
+    if constexpr (COLS != 0) handoff_wide_cols<NT, PERS>(d, p, c, result, Bp, r + 1);
     else handoff_wide<PERS>(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
   }
   if (dgt) {
@@ -1848,7 +1868,8 @@ static int wide_resident(int lpc) {
 }
 
 bool round_wide_persist_eligible(const Dev &d) {
-  if (!d.round_persist || d.fd_cols || !d.cand16 || d.fd_rows || d.wide_cols || !d.round_ilp2 || !d.pbar ||
+  // (wide_cols 1, the window from la_col, stays one launch per round)
+  if (!d.round_persist || d.fd_cols || !d.cand16 || d.fd_rows || d.wide_cols == 1 || !d.round_ilp2 || !d.pbar ||
       !round_p16(d))
     return false;
   const int lpc = lanes_per_candidate(d.npad);
@@ -1861,8 +1882,14 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
   (void)hipMemsetAsync(d.pbar, 0, (size_t)PBAR_INTS * 4, s);
   // (ILPK = 4, four searches interleaved per lane group: 256 VGPRs, search
   // 20.1 -> 22.3 us per round -- the probes' LDS reads, not their latency, bound it)
-  if (lpc == 8) k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
-  else k_round_wide<4, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  if (d.wide_cols == 2) {  // the hand-off counted in la_col (no FDT)
+    if (lpc == 8) k_round_wide<8, true, 2, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+    else k_round_wide<4, true, 2, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  } else if (lpc == 8) {
+    k_round_wide<8, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  } else {
+    k_round_wide<4, true, 0, 256, true><<<d.n, 256, wb16, s>>>(d, 0);
+  }
 }
 
 void launch_round_persist(const Dev &d, hipStream_t s) {
@@ -2415,6 +2442,7 @@ void configure_round_kernels() {
   CFG((k_round_wide<4, true, 1>)); CFG((k_round_wide<8, true, 1>));
   CFG((k_round_wide<4, true, 2>)); CFG((k_round_wide<8, true, 2>));
   CFG((k_round_wide<4, true, 0, 256, true>)); CFG((k_round_wide<8, true, 0, 256, true>));
+  CFG((k_round_wide<4, true, 2, 256, true>)); CFG((k_round_wide<8, true, 2, 256, true>));
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
