@@ -666,7 +666,9 @@ bool segments_eligible(const bh_handle *h) {
 int segments_for(const Dev &d, int64_t events) {
   // (round 3: C5, 2M events, 79.0M events/s at 4 segments, 87.0M at 8,
   // 88.1M at 12; C2, 1M events, 48.6M at 4, 48.3M at 8; C3 equal at 8 and 12)
-  int K = !d.fd_cols ? 1 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
+  // (round 4, persistent loop, C3: 8 segments 181.5M events/s, 12 182.6M,
+  // 16 184.2M -- shorter segments start the loop sooner)
+  int K = !d.fd_cols ? 1 : events >= 6000000 ? 16 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
 }
@@ -992,6 +994,14 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
                       : (2 * n + 1 <= h->ncu ? 1 : 0);
   const bool lt_combined = lt_mode == 1;
   hipStream_t sl = h->stream3;
+  auto lt_after = [&](int kk) {  // (lt_mode 0) segment kk's LT workgroup and per-event LT, on the coordinate stream
+    const Dev vk = view(kk);
+    Dev vl = vk;
+    vl.ncol = 0;
+    vl.flow_lt = 1;
+    bh::launch_flow(vl, sc);
+    bh::launch_lt_rows(vk, sc);
+  };
   auto coords = [&](int k) -> int {
     if (sp) return receive(k);
     Dev v = view(k);
@@ -1049,6 +1059,12 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));  // the segment's LA is ready for the loop
     if (!wide && lt_combined) {
       bh::launch_lt_rows(v, sc);
+    } else if (!wide && lt_mode == 0) {
+      // the Lamport timestamps of the segment before this one, after this
+      // segment's columns: the loop's next segment waits only for columns
+      // (the last segment's follow its own columns)
+      if (k > 0) lt_after(k - 1);
+      if (k == K - 1) lt_after(k);
     } else if (!wide) {  // the segment's Lamport timestamps: one workgroup, beside the loop
       hipStream_t st = lt_mode == 2 ? sl : sc;
       if (lt_mode == 2) HIPCHK(h, hipStreamWaitEvent(sl, h->seg_ev[(size_t)3 * k], 0));  // (after the segment's columns)
