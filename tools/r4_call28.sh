@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_schedule.py tests/test_gpu_fullsize.py tests/test_gpu_whole.py tests/test_gpu_shard.py -m gpu -v --timeout 400 --timeout-method thread -rf \
-  -k "segment or lt_fallback or random_dag or wild or trap or c3 or small_n or la_col or persistent or lazy or split" > gpurun_out/r4_tests28.log 2>&1
+  -k "c3_whole or c3_multi or segment_pipeline" > gpurun_out/r4_tests28.log 2>&1
 rc=$?
 echo "tests rc=$rc"; grep -E "passed|failed" gpurun_out/r4_tests28.log | tail -2; grep FAILED gpurun_out/r4_tests28.log | head
 if [ $rc -ne 0 ]; then exit $rc; fi
