@@ -666,9 +666,9 @@ bool segments_eligible(const bh_handle *h) {
 int segments_for(const Dev &d, int64_t events) {
   // (round 3: C5, 2M events, 79.0M events/s at 4 segments, 87.0M at 8,
   // 88.1M at 12; C2, 1M events, 48.6M at 4, 48.3M at 8; C3 equal at 8 and 12)
-  // (round 4, persistent loop, C3: 8 segments 181.5M events/s, 12 182.6M,
-  // 16 184.2M -- shorter segments start the loop sooner)
-  int K = !d.fd_cols ? 1 : events >= 6000000 ? 16 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
+  // (round 4, persistent loop, C3: with each segment's LT after the next
+  // one's columns, 8 segments 188.8M events/s, 16 187.6M, 24 184.1M)
+  int K = !d.fd_cols ? 1 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
 }

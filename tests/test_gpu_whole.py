@@ -58,11 +58,11 @@ def _whole_digest(name, monkeypatch=None, segments=None):
 @pytest.mark.timeout(900)
 def test_c3_whole_dag():
     """The bench's headline DAG, all 10M events, through the default pipeline
-    (16 segments from 6M events, each segment's LT after the next one's
-    columns, the persistent loop)."""
+    (8 segments, each segment's LT after the next one's columns, the
+    persistent loop)."""
     d, hg = _whole_digest("c3")
-    assert hg.pipeline()[0] == 16 and hg.profile_kernel() == "k_flow32"
-    assert hg.loop_stats() == (16, 0)
+    assert hg.pipeline()[0] == 8 and hg.profile_kernel() == "k_flow32"
+    assert hg.loop_stats() == (8, 0)
     invariants(d, hg)
 
 
