@@ -582,7 +582,14 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   int32_t gx = 0, nx = 0;
   if (PERS && t == 0) xcc = pbar_register(d);
   bool prestaged = false;  // (PERS) the first window of this round is in LDS already
-  constexpr int PP8 = PP / 2, WRS8 = LPC * (PP8 + 1);  // P8: 16-B pieces of 16 columns per lane
+  // P8 window rows: 16-B pieces of 16 columns, PP8 per lane; piece u of lane
+  // part sits at u LPC + part (a row is 512 B at LPC 8), so the four lane
+  // groups of a ds_read_b128 lane set -- two candidates' parts 0-3, two
+  // candidates' parts 4-7 -- cover the 64 banks once whatever rows they
+  // probe, when odd candidate groups read their pieces rotated by one (rot8)
+  constexpr int PP8 = PP / 2, WRS8 = LPC * PP8;
+  auto p8idx = [](int pc) { return (pc % PP8) * LPC + pc / PP8; };  // (pc = part PP8 + u)
+  const int rot8 = ((t & 63) / LPC) & 1;
   // the first window of chain c from row wk0 for round rr (own_: its
   // boundary): the fit check against the window's own and the shared base,
   // then the rows staged in LDS (sets p8, p8g, wb2).  PERS: the next round's
@@ -668,7 +675,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           bs[0] = b01 & 0xFFFFu; bs[1] = b01 >> 16; bs[2] = b23 & 0xFFFFu; bs[3] = b23 >> 16;
         }
         const int pc8 = cg >> 2, pc16 = cg >> 1;
-        const int o8 = (pc8 + pc8 / PP8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
+        const int o8 = p8idx(pc8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
   #pragma unroll
         for (int u = 0; u < CNP; ++u) {
           const int pc = ch + u * CT;
@@ -712,7 +719,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             }
             w[h] = v;
           }
-          win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+          win4[row * WRS8 + p8idx(pc)] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
         }
       } else {
         constexpr int RP = LPC * PP;  // pieces per padded row
@@ -805,7 +812,18 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       };
-      const int4 *xb8 = win4 + part * (PP8 + 1);
+      // a candidate's bytes in the lane's piece order: piece u holds (u + rot8) % PP8
+      auto rot_f8 = [&](uint32_t (&f8)[4 * PP8]) {
+        uint32_t g8[4 * PP8];
+#pragma unroll
+        for (int i = 0; i < 4 * PP8; ++i) g8[i] = f8[i];
+#pragma unroll
+        for (int i = 0; i < 4 * PP8; ++i) f8[i] = rot8 ? g8[(i + 4) % (4 * PP8)] : g8[i];
+      };
+      const int4 *xb8 = win4 + part;
+      int roff[PP8];  // the lane's piece u read order (rot8)
+#pragma unroll
+      for (int u = 0; u < PP8; ++u) roff[u] = ((u + rot8) % PP8) * LPC;
       for (int pass = 0; pass < npass; pass += ILPK) {
         int qv[ILPK];
         bool act[ILPK];
@@ -821,14 +839,17 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           act[k] = qv[k] < n && bq < lq;
         }
 #pragma unroll
-        for (int k = 0; k < ILPK; ++k) load_f8(qv[k], act[k], tag[k], f[k]);
+        for (int k = 0; k < ILPK; ++k) {
+          load_f8(qv[k], act[k], tag[k], f[k]);
+          rot_f8(f[k]);
+        }
         // the ILPK candidates' probes of rows rw[k], all reads issued first
         auto ssk = [&](const int (&rw)[ILPK], bool (&sv)[ILPK]) {
           int4 x[ILPK][PP8];
 #pragma unroll
           for (int k = 0; k < ILPK; ++k)
 #pragma unroll
-            for (int u = 0; u < PP8; ++u) x[k][u] = xb8[rw[k] * WRS8 + u];
+            for (int u = 0; u < PP8; ++u) x[k][u] = xb8[rw[k] * WRS8 + roff[u]];
           int g[ILPK];
 #pragma unroll
           for (int k = 0; k < ILPK; ++k) g[k] = 0;
@@ -924,12 +945,19 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             f8[2 * u + 1] = pack8(e2, e3);
           }
         }
-        const int4 *xb8 = win4 + part * (PP8 + 1);
+        {  // the bytes in the lane's piece order (rot8, as the paired search)
+          uint32_t g8[4 * PP8];
+#pragma unroll
+          for (int i = 0; i < 4 * PP8; ++i) g8[i] = f8[i];
+#pragma unroll
+          for (int i = 0; i < 4 * PP8; ++i) f8[i] = rot8 ? g8[(i + 4) % (4 * PP8)] : g8[i];
+        }
+        const int4 *xb8 = win4 + part;
         auto ss8 = [&](int row) -> bool {
           const int4 *x4 = xb8 + row * WRS8;
           int4 x[PP8];
 #pragma unroll
-          for (int u = 0; u < PP8; ++u) x[u] = x4[u];
+          for (int u = 0; u < PP8; ++u) x[u] = x4[((u + rot8) % PP8) * LPC];
           int ge = 0;
 #pragma unroll
           for (int u = 0; u < PP8; ++u) {
