@@ -582,14 +582,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   int32_t gx = 0, nx = 0;
   if (PERS && t == 0) xcc = pbar_register(d);
   bool prestaged = false;  // (PERS) the first window of this round is in LDS already
-  // P8 window rows: 16-B pieces of 16 columns, PP8 per lane; piece u of lane
-  // part sits at u LPC + part (a row is 512 B at LPC 8), so the four lane
-  // groups of a ds_read_b128 lane set -- two candidates' parts 0-3, two
-  // candidates' parts 4-7 -- cover the 64 banks once whatever rows they
-  // probe, when odd candidate groups read their pieces rotated by one (rot8)
-  constexpr int PP8 = PP / 2, WRS8 = LPC * PP8;
-  auto p8idx = [](int pc) { return (pc % PP8) * LPC + pc / PP8; };  // (pc = part PP8 + u)
-  const int rot8 = ((t & 63) / LPC) & 1;
+  constexpr int PP8 = PP / 2, WRS8 = LPC * (PP8 + 1);  // P8: 16-B pieces of 16 columns per lane
   // the first window of chain c from row wk0 for round rr (own_: its
   // boundary): the fit check against the window's own and the shared base,
   // then the rows staged in LDS (sets p8, p8g, wb2).  PERS: the next round's
@@ -675,7 +668,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           bs[0] = b01 & 0xFFFFu; bs[1] = b01 >> 16; bs[2] = b23 & 0xFFFFu; bs[3] = b23 >> 16;
         }
         const int pc8 = cg >> 2, pc16 = cg >> 1;
-        const int o8 = p8idx(pc8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
+        const int o8 = (pc8 + pc8 / PP8) * 4 + (cg & 3), o16 = (pc16 + pc16 / PP) * 4 + 2 * (cg & 1);
   #pragma unroll
         for (int u = 0; u < CNP; ++u) {
           const int pc = ch + u * CT;
@@ -719,7 +712,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             }
             w[h] = v;
           }
-          win4[row * WRS8 + p8idx(pc)] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+          win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
         }
       } else {
         constexpr int RP = LPC * PP;  // pieces per padded row
@@ -812,18 +805,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       };
-      // a candidate's bytes in the lane's piece order: piece u holds (u + rot8) % PP8
-      auto rot_f8 = [&](uint32_t (&f8)[4 * PP8]) {
-        uint32_t g8[4 * PP8];
-#pragma unroll
-        for (int i = 0; i < 4 * PP8; ++i) g8[i] = f8[i];
-#pragma unroll
-        for (int i = 0; i < 4 * PP8; ++i) f8[i] = rot8 ? g8[(i + 4) % (4 * PP8)] : g8[i];
-      };
-      const int4 *xb8 = win4 + part;
-      int roff[PP8];  // the lane's piece u read order (rot8)
-#pragma unroll
-      for (int u = 0; u < PP8; ++u) roff[u] = ((u + rot8) % PP8) * LPC;
+      const int4 *xb8 = win4 + part * (PP8 + 1);
       for (int pass = 0; pass < npass; pass += ILPK) {
         int qv[ILPK];
         bool act[ILPK];
@@ -839,17 +821,14 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           act[k] = qv[k] < n && bq < lq;
         }
 #pragma unroll
-        for (int k = 0; k < ILPK; ++k) {
-          load_f8(qv[k], act[k], tag[k], f[k]);
-          rot_f8(f[k]);
-        }
+        for (int k = 0; k < ILPK; ++k) load_f8(qv[k], act[k], tag[k], f[k]);
         // the ILPK candidates' probes of rows rw[k], all reads issued first
         auto ssk = [&](const int (&rw)[ILPK], bool (&sv)[ILPK]) {
           int4 x[ILPK][PP8];
 #pragma unroll
           for (int k = 0; k < ILPK; ++k)
 #pragma unroll
-            for (int u = 0; u < PP8; ++u) x[k][u] = xb8[rw[k] * WRS8 + roff[u]];
+            for (int u = 0; u < PP8; ++u) x[k][u] = xb8[rw[k] * WRS8 + u];
           int g[ILPK];
 #pragma unroll
           for (int k = 0; k < ILPK; ++k) g[k] = 0;
@@ -945,19 +924,12 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             f8[2 * u + 1] = pack8(e2, e3);
           }
         }
-        {  // the bytes in the lane's piece order (rot8, as the paired search)
-          uint32_t g8[4 * PP8];
-#pragma unroll
-          for (int i = 0; i < 4 * PP8; ++i) g8[i] = f8[i];
-#pragma unroll
-          for (int i = 0; i < 4 * PP8; ++i) f8[i] = rot8 ? g8[(i + 4) % (4 * PP8)] : g8[i];
-        }
-        const int4 *xb8 = win4 + part;
+        const int4 *xb8 = win4 + part * (PP8 + 1);
         auto ss8 = [&](int row) -> bool {
           const int4 *x4 = xb8 + row * WRS8;
           int4 x[PP8];
 #pragma unroll
-          for (int u = 0; u < PP8; ++u) x[u] = x4[((u + rot8) % PP8) * LPC];
+          for (int u = 0; u < PP8; ++u) x[u] = x4[u];
           int ge = 0;
 #pragma unroll
           for (int u = 0; u < PP8; ++u) {
@@ -1105,9 +1077,14 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   }
   if (!PERS || stop) return;
   // ---- grid barrier (PERS) ----
+  // BH_DIAG barrier phases (every chain): end, arrived, staged, released
+  const bool dgb = d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
+  unsigned long long *tlb = dgb ? d.diag + DG_TLB + ((int64_t)(r - TL_R0) * 512 + c) * 4 : nullptr;
+  if (dgb) tlb[0] = __builtin_amdgcn_s_memrealtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
   __syncthreads();
   if (t < 64) pbar_arrive(d, it, xcc, gx, gridDim.x, nx);
+  if (dgb) tlb[1] = __builtin_amdgcn_s_memrealtime();
   // fame's ballots and the round table: read after the loop, or B[r + 1]
   // two barriers from now (the shared base) -- stored after the arrival, so
   // the drain above waits only for the hand-over
@@ -1125,10 +1102,12 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       prestaged = true;
     }
   }
+  if (dgb) tlb[2] = __builtin_amdgcn_s_memrealtime();
   if (t == 0) {
     sh_res = pbar_wait(d, it, gridDim.x) ? 0 : -1;
     if (it == 0) pbar_counts(d, xcc, gx, nx);
   }
+  if (dgb) tlb[3] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   if (sh_res < 0) {  // the barrier gave up: the host restores the inputs and relaunches per iteration
     if (t == 0) {
@@ -1837,10 +1816,13 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       tl[2] = rt1;
       tl[3] = __builtin_amdgcn_s_memrealtime();
     }
-    // ---- grid barrier ----
+    // ---- grid barrier ----  (BH_DIAG phases: end, arrived, loads issued, released)
+    unsigned long long *tlb = dgt ? d.diag + DG_TLB + ((int64_t)(r - TL_R0) * 512 + c) * 4 : nullptr;
+    if (dgt) tlb[0] = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
     __syncthreads();
     if (t < 64) pbar_arrive(d, it, xcc, gx, G, nx);
+    if (dgt) tlb[1] = __builtin_amdgcn_s_memrealtime();
     // what no workgroup reads inside the loop -- fame's inputs (the new
     // candidate's LA row and its ballots) and the round table -- is stored
     // after the arrival, so the drain above waits only for the hand-over
@@ -1854,10 +1836,12 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     k0 = result;
     hin.j0 = result < len ? fdv : FD_NONE;
     own_loads();  // lands during the wait
+    if (dgt) tlb[2] = __builtin_amdgcn_s_memrealtime();
     if (t == 0) {
       if (!pbar_wait(d, it, G)) sh_fail = 1;
       if (it == 0) pbar_counts(d, xcc, gx, nx);
     }
+    if (dgt) tlb[3] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     if (sh_fail) {
       if (t == 0) {

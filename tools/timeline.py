@@ -44,6 +44,37 @@ def main(path):
         print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
     per_round = np.diff(np.array([start[r, live[r]].min() for r in range(TL_NR) if live[r].sum() > 1]))
     print(f"{'round period':14s} median {np.median(per_round) * ns / 1000:6.2f} us")
+    barrier(path)
+
+
+def barrier(path):
+    """The persistent loops' barrier phases (second block, every chain): per
+    round, drain (arrived - end), stage (staged - arrived; k_round2p: its
+    loads issued), end spread, last arrival -> first release (the barrier's
+    own latency), release spread, and last staged - first release (> 0: the
+    next round waits on staging, not on the barrier)."""
+    b = np.fromfile(path, dtype=np.uint64)
+    off = TL_NR * NC * 4
+    if b.size < off + TL_NR * 512 * 4:
+        return
+    b = b[off: off + TL_NR * 512 * 4].reshape(TL_NR, 512, 4).astype(np.int64)
+    live = (b > 0).all(axis=2)
+    rows = []
+    for r in range(TL_NR):
+        m = live[r]
+        if m.sum() < 2:
+            continue
+        e, a, s, rl = (b[r, m, k] for k in range(4))
+        rows.append((np.median(a - e), np.median(s - a), e.max() - e.min(), rl.min() - a.max(), rl.max() - rl.min(),
+                     s.max() - rl.min(), int(m.sum())))
+    if not rows:
+        return
+    ns = 10.0
+    names = ["drain", "stage", "end spread", "last arr->rel", "release spread", "last staged-rel"]
+    for i, name in enumerate(names):
+        v = [x[i] for x in rows]
+        print(f"{name:15s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
+    print(f"{'workgroups':15s} {rows[0][6]}")
 
 
 if __name__ == "__main__":
