@@ -610,6 +610,26 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       }
+      // P8 (COLS 0, 2): the window's int32 rows are loaded into registers here,
+      // before the fit check's loads, so both are in flight together -- one
+      // round trip for the whole stage instead of one per row group after it
+      constexpr int RP8 = LPC * (PP / 2), NPI = (WROWS * RP8 + NT - 1) / NT;
+      constexpr bool PRE = COLS != 1 && P16;
+      int4 pre[PRE ? NPI : 1][4];
+      if constexpr (PRE) {
+        if (d.round_p8) {
+          const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+#pragma unroll
+          for (int u = 0; u < NPI; ++u) {
+            const int i = t + u * NT, row = i / RP8, pc = i - row * RP8;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
+              pre[u][h] = i < wrows * RP8 && col < npad ? src[row * q4 + col / 4] : make_int4(0, 0, 0, 0);
+            }
+          }
+        }
+      }
       p8 = false;
       p8g = false;
       if constexpr (P16) {
@@ -693,10 +713,11 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       } else if (p8) {
-        // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
-        constexpr int RP8 = LPC * PP8;
-        const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-        for (int i = t; i < wrows * RP8; i += NT) {
+        // columns 16 pc .. 16 pc + 15 as bytes x | 0x80 (rows loaded above)
+#pragma unroll
+        for (int u = 0; u < (PRE ? NPI : 1); ++u) {
+          const int i = t + u * NT;
+          if (i >= wrows * RP8) continue;
           const int row = i / RP8, pc = i - row * RP8;
           uint32_t w[4];
   #pragma unroll
@@ -704,7 +725,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
             uint32_t v = 0x80808080u;
             if (col < npad) {
-              const int4 a = src[row * q4 + col / 4];
+              const int4 a = pre[u][h];
               const uint32_t b01 = wb2[col / 2], b23 = wb2[col / 2 + 1];
               const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
               const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
