@@ -1701,7 +1701,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n > 64 ? 1 : 0);
   d.prestage = getenv("BH_PRESTAGE") ? atoi(getenv("BH_PRESTAGE")) != 0 : 1;
   d.xpose_fd = 1;
-  d.xpose_walk = getenv("BH_XPOSE_WALK") ? atoi(getenv("BH_XPOSE_WALK")) : 1;
+  d.wide_prio = getenv("BH_WIDE_PRIO") ? atoi(getenv("BH_WIDE_PRIO")) : 0;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;

@@ -659,41 +659,6 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
         const int32_t hi = tile[c * (TR + 1) + rb - 1];
         for (int32_t j = hi + 1 + lane; j < clen[c]; j += 64) xstore(d.fdt + fdt_pos(cstart[c] + j, i, npad), FD_NONE);
       }
-    if (d.xpose_walk) {
-      // the scatter: lane (column c, row k) owns the entries j in
-      // (LA[k - 1][c], LA[k][c]] -- the events of chain c that row k is the
-      // first of the segment to see -- and writes k's chain index to each.
-      // TR lanes per column, 64 / TR columns per wave pass; a lane's first
-      // SHORT entries are its own stores (one or two on average: the rows of
-      // a column advance together), longer runs are written by the whole
-      // wave, 64 consecutive entries per store.  Same entries and values as
-      // the binary search below, in about a third of its instructions.
-      constexpr int CPW = 64 / TR, SHORT = 4;
-      const int sub = lane / TR, kr = lane % TR, k = ra1 + kr;
-      const bool rowok = k < rb;
-      const int32_t v = ka + kr;
-      for (int cb = wave * CPW; cb < n; cb += (BT / 64) * CPW) {
-        const int c = cb + sub;
-        const bool ok = rowok && c < n;
-        int32_t lo = 0, cnt = 0;
-        int64_t cbase = 0;
-        if (ok) {
-          const int32_t *col = tile + c * (TR + 1);
-          lo = kr > 0 ? col[k - 1] : (ka == 0 ? -1 : (ra1 == 0 ? prev[c] : col[ra1 - 1]));
-          cnt = col[k] - lo;
-          cbase = (int64_t)cstart[c] + lo + 1;
-        }
-        for (int mm = 0; __any(mm < min(cnt, SHORT)); ++mm)
-          if (mm < min(cnt, SHORT)) xstore(d.fdt + fdt_pos(cbase + mm, i, npad), v);
-        for (uint64_t lm = __ballot(cnt > SHORT); lm; lm &= lm - 1) {
-          const int src = __builtin_ctzll(lm);
-          const int64_t b = __shfl(cbase, src);
-          const int32_t ce = __shfl(cnt, src), vv = __shfl(v, src);
-          for (int32_t j = SHORT + lane; j < ce; j += 64) xstore(d.fdt + fdt_pos(b + j, i, npad), vv);
-        }
-      }
-      continue;
-    }
     // four columns per pass: their binary searches (at most 6 halvings of
     // a <= 64-row segment) interleave, so LDS latency is paid once per
     // four columns; the first 64 entries of each run here, longer runs'

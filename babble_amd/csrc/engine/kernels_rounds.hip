@@ -610,26 +610,6 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       }
-      // P8 (COLS 0, 2): the window's int32 rows are loaded into registers here,
-      // before the fit check's loads, so both are in flight together -- one
-      // round trip for the whole stage instead of one per row group after it
-      constexpr int RP8 = LPC * (PP / 2), NPI = (WROWS * RP8 + NT - 1) / NT;
-      constexpr bool PRE = COLS != 1 && P16;
-      int4 pre[PRE ? NPI : 1][4];
-      if constexpr (PRE) {
-        if (d.round_p8) {
-          const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-#pragma unroll
-          for (int u = 0; u < NPI; ++u) {
-            const int i = t + u * NT, row = i / RP8, pc = i - row * RP8;
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
-              pre[u][h] = i < wrows * RP8 && col < npad ? src[row * q4 + col / 4] : make_int4(0, 0, 0, 0);
-            }
-          }
-        }
-      }
       p8 = false;
       p8g = false;
       if constexpr (P16) {
@@ -713,11 +693,10 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       } else if (p8) {
-        // columns 16 pc .. 16 pc + 15 as bytes x | 0x80 (rows loaded above)
-#pragma unroll
-        for (int u = 0; u < (PRE ? NPI : 1); ++u) {
-          const int i = t + u * NT;
-          if (i >= wrows * RP8) continue;
+        // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
+        constexpr int RP8 = LPC * PP8;
+        const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
+        for (int i = t; i < wrows * RP8; i += NT) {
           const int row = i / RP8, pc = i - row * RP8;
           uint32_t w[4];
   #pragma unroll
@@ -725,7 +704,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
             uint32_t v = 0x80808080u;
             if (col < npad) {
-              const int4 a = pre[u][h];
+              const int4 a = src[row * q4 + col / 4];
               const uint32_t b01 = wb2[col / 2], b23 = wb2[col / 2 + 1];
               const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
               const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
@@ -785,6 +764,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     if (wrows <= 0) break;
     if (!(PERS && prestaged && wk0 == own)) stage(wk0, wrows, r, own);  // (PERS: else staged during the barrier)
     prestaged = false;
+    if (PERS && d.wide_prio) __builtin_amdgcn_s_setprio(0);
     if (dgt && !rt1) rt1 = __builtin_amdgcn_s_memrealtime();
     if (p8 && d.round_ilp2) {
       // byte rows, ILPK candidates per lane group at once (passes pass ..
@@ -828,6 +808,13 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       };
       const int4 *xb8 = win4 + part * (PP8 + 1);
       for (int pass = 0; pass < npass; pass += ILPK) {
+        // (BH_WIDE_PRIO=2: the two workgroups of a compute unit -- c and c +
+        // G/2 in dispatch order -- take turns at the higher priority, pass by
+        // pass, instead of the older one issuing first throughout)
+        if (PERS && d.wide_prio == 2) {
+          if (((pass / ILPK) ^ (2 * c >= (int)gridDim.x)) & 1) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
         int qv[ILPK];
         bool act[ILPK];
         int32_t tag[ILPK];
@@ -1052,6 +1039,12 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     if (sh_res >= 0) { result = wk0 + sh_res; break; }
     wk0 += wrows;
   }
+  // BH_WIDE_PRIO: the hand-off, the arrival and the next window's staging at
+  // a higher priority -- the workgroup that ends a round last stages its next
+  // window after everyone else has been released, beside its compute unit's
+  // other workgroup's search, and that staging is the next round's critical
+  // path (profiles/r4_ab_wide.txt, barrier phases)
+  if (PERS && d.wide_prio) __builtin_amdgcn_s_setprio(2);
   // fame's input for the new candidate y = (c, result): the candidates of
   // round r it strongly sees are those whose T_q in the final window is at
   // most y's row (stronglySee is monotone along the chain)

@@ -370,7 +370,8 @@ def test_chunk_sweep_wild(monkeypatch):
 @pytest.mark.parametrize("rows", ["p8", "p8_window", "p8g_tight", "p8_mixed", "p8_single", "p8g_tight_single",
                                   "p16", "p32", "fdt_p8", "fdt_p16", "cols_p8", "cols_p8g_tight", "cols_p16",
                                   "cols2_p8", "cols2_p16", "iter_p8", "iter_p8_mixed", "iter_p8g_tight",
-                                  "fallback_p8", "noprestage_p8", "flat_p8_mixed", "bsearch_p8"])
+                                  "fallback_p8", "noprestage_p8", "flat_p8_mixed",
+                                  "prio_p8", "prio2_p8_mixed"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -395,9 +396,9 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     round); iter_*: one launch per round (BH_ROUND_PERSIST=0); fallback_*: the
     persistent loop's barrier gives up at once (BH_PBAR_SPIN=0), the host
     restores the loop's inputs and runs the per-round launches."""
-    if rows.startswith("bsearch_"):  # the transpose's FD walk as a binary search per entry
-        monkeypatch.setenv("BH_XPOSE_WALK", "0")
-        rows = rows[len("bsearch_"):]
+    if rows.startswith("prio"):  # the persistent loop's priority schemes (BH_WIDE_PRIO)
+        monkeypatch.setenv("BH_WIDE_PRIO", "2" if rows.startswith("prio2_") else "1")
+        rows = rows[rows.index("_") + 1:]
     if rows.startswith("iter_"):
         monkeypatch.setenv("BH_ROUND_PERSIST", "0")
         rows = rows[len("iter_"):]
@@ -464,18 +465,14 @@ def test_coordinates_random(monkeypatch, sweep, n, N, seed, lag):
     assert nmax > 0  # the unseen tails were exercised
 
 
-@pytest.mark.parametrize("walk", ["scatter", "bsearch"])
 @pytest.mark.parametrize("n,N,seed,lag", [(16, 4_000, 64, 2), (128, 20_000, 65, 0), (300, 30_000, 66, 0),
                                           (512, 40_000, 67, 0)])
-def test_transpose_fd_walk(monkeypatch, walk, n, N, seed, lag):
+def test_transpose_fd_walk(monkeypatch, n, N, seed, lag):
     """k_flow_transpose's firstDescendants walk (hashgraph.go:520-544 as the
-    oracle restates it): the scatter -- one lane per (row, column), each
-    writing the entries its row is the first to see, long runs by the whole
-    wave -- and the binary search per entry (BH_XPOSE_WALK=0), through 64-row
-    tiles (n <= 128) and 32-row ones (wide), every chain's first and last
-    events included."""
+    oracle restates it) through 64-row tiles (n <= 128) and 32-row ones
+    (wide), every chain's first and last events included, then consensus
+    over the FDT it wrote."""
     from babble_amd.dag import Dag
-    monkeypatch.setenv("BH_XPOSE_WALK", "1" if walk == "scatter" else "0")
     if n <= 128:
         monkeypatch.setenv("BH_ROUND_SRC", "rows")  # (the transpose runs, not the la_col loop alone)
     d = Dag(n, N, seed, lagging=lag, sig_mode=0)
@@ -494,7 +491,7 @@ def test_transpose_fd_walk(monkeypatch, walk, n, N, seed, lag):
         assert np.array_equal(fd_r, fd_g), (e, fd_r, fd_g)
     o.run_consensus()
     hg.run_consensus()
-    _compare(o, hg, f"fd walk {walk} n={n}")
+    _compare(o, hg, f"fd walk n={n}")
 
 
 def test_flow32_lt_fallback(monkeypatch):
