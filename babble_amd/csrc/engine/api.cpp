@@ -1701,7 +1701,11 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.pbar_mode = getenv("BH_PBAR") ? (!strcmp(getenv("BH_PBAR"), "xcd") ? 1 : 0) : (n > 64 ? 1 : 0);
   d.prestage = getenv("BH_PRESTAGE") ? atoi(getenv("BH_PRESTAGE")) != 0 : 1;
   d.xpose_fd = 1;
-  d.wide_prio = getenv("BH_WIDE_PRIO") ? atoi(getenv("BH_WIDE_PRIO")) : 0;
+  // the persistent wide loop's priorities: hand-off / barrier / staging at 2,
+  // the CU's two workgroups alternating through the search (C4 42.3 -> 40.6 us
+  // per round, profiles/r4_ab_wide.txt); BH_WIDE_PRIO=0|1 for A/B
+  d.wide_prio = getenv("BH_WIDE_PRIO") ? atoi(getenv("BH_WIDE_PRIO")) : 2;
+  d.stage_b2 = getenv("BH_STAGE_B2") ? atoi(getenv("BH_STAGE_B2")) : 1;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;

@@ -696,23 +696,48 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
         // columns 16 pc .. 16 pc + 15 as bytes x | 0x80
         constexpr int RP8 = LPC * PP8;
         const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-        for (int i = t; i < wrows * RP8; i += NT) {
+        const int lim = wrows * RP8;
+        auto ld8 = [&](int i, int4 (&a)[4]) {
+  #pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const int row = i / RP8, col = 16 * (i - row * RP8) + 4 * h;  // npad is a multiple of 4
+            a[h] = i < lim && col < npad ? src[row * q4 + col / 4] : make_int4(0, 0, 0, 0);
+          }
+        };
+        auto put8 = [&](int i, const int4 (&a)[4]) {
           const int row = i / RP8, pc = i - row * RP8;
           uint32_t w[4];
   #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            const int col = 16 * pc + 4 * h;  // npad is a multiple of 4
+            const int col = 16 * pc + 4 * h;
             uint32_t v = 0x80808080u;
             if (col < npad) {
-              const int4 a = src[row * q4 + col / 4];
               const uint32_t b01 = wb2[col / 2], b23 = wb2[col / 2 + 1];
-              const uint32_t x0 = (uint32_t)(a.x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a.y + 1 - (int32_t)(b01 >> 16));
-              const uint32_t x2 = (uint32_t)(a.z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a.w + 1 - (int32_t)(b23 >> 16));
+              const uint32_t x0 = (uint32_t)(a[h].x + 1 - (int32_t)(b01 & 0xFFFFu)), x1 = (uint32_t)(a[h].y + 1 - (int32_t)(b01 >> 16));
+              const uint32_t x2 = (uint32_t)(a[h].z + 1 - (int32_t)(b23 & 0xFFFFu)), x3 = (uint32_t)(a[h].w + 1 - (int32_t)(b23 >> 16));
               v = (x0 | (x1 << 8) | (x2 << 16) | (x3 << 24)) | 0x80808080u;
             }
             w[h] = v;
           }
           win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+        };
+        if (d.stage_b2) {
+          // two row groups' loads in flight per trip (BH_STAGE_B2): half the
+          // round trips of the staging, which the round's last workgroup pays
+          // on the next round's critical path
+          for (int i = t; i < lim; i += 2 * NT) {
+            int4 a[4], b[4];
+            ld8(i, a);
+            ld8(i + NT, b);
+            put8(i, a);
+            if (i + NT < lim) put8(i + NT, b);
+          }
+        } else {
+          for (int i = t; i < lim; i += NT) {
+            int4 a[4];
+            ld8(i, a);
+            put8(i, a);
+          }
         }
       } else {
         constexpr int RP = LPC * PP;  // pieces per padded row
