@@ -659,12 +659,12 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
         const int32_t hi = tile[c * (TR + 1) + rb - 1];
         for (int32_t j = hi + 1 + lane; j < clen[c]; j += 64) xstore(d.fdt + fdt_pos(cstart[c] + j, i, npad), FD_NONE);
       }
-    // four columns per pass: their binary searches (at most 6 halvings of
-    // a <= 64-row segment) interleave, so LDS latency is paid once per
+    // four columns per pass: their binary searches (log2 TR halvings of a
+    // <= TR-row segment) interleave, so LDS latency is paid once per
     // four columns; the first 64 entries of each run here, longer runs'
     // remainders after
     for (int c0 = wave * 4; c0 < n; c0 += BT / 16) {
-      int32_t lo[4], hi[4], a[4], z[4];
+      int32_t lo[4], hi[4], a[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int c = min(c0 + u, n - 1);
@@ -672,17 +672,16 @@ __device__ __forceinline__ void xpose_tile(const Dev &d, const int64_t tix, int3
         lo[u] = ka == 0 ? -1 : (ra1 == 0 ? prev[c] : col[ra1 - 1]);
         hi[u] = c0 + u < n ? col[rb - 1] : lo[u];
         a[u] = ra1;
-        z[u] = rb - 1;
       }
+      // the first row a in [ra1, rb) with LA >= j, as a fixed-length
+      // lower bound over TR rows (log2 TR halvings, TR a power of two): rows
+      // past rb - 1 read as row rb - 1, whose LA hi >= j
 #pragma unroll
-      for (int st = 0; st < 6; ++st) {
+      for (int half = TR / 2; half >= 1; half >>= 1) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int mm = (a[u] + z[u]) >> 1;
-          const bool ge = tile[(c0 + u) * (TR + 1) + mm] >= lo[u] + 1 + lane;
-          const bool go = a[u] < z[u];
-          z[u] = go && ge ? mm : z[u];
-          a[u] = go && !ge ? mm + 1 : a[u];
+          const int idx = min(a[u] + half - 1, rb - 1);
+          a[u] += tile[(c0 + u) * (TR + 1) + idx] < lo[u] + 1 + lane ? half : 0;
         }
       }
 #pragma unroll

@@ -590,7 +590,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // B[r] are known before the barrier)
   bool p8 = false, p8g = false;
   const uint32_t *wb2 = wbase2;
-  auto stage = [&](const int32_t wk0, const int wrows, const int rr, const int32_t own_) {
+  auto stage = [&](const int32_t wk0, const int wrows, const int rr, const int32_t own_, unsigned long long *sst = nullptr) {
       // COLS: the window's 36 aligned rows of every column from la_col, issued
       // before the fit check below reads its two rows
       constexpr int CQ = LPC * 16, CT = NT / CQ, CNP = (9 + CT - 1) / CT;  // column quads, threads per quad, pieces per thread
@@ -622,6 +622,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           const bool tryg = d.cand8 != nullptr && d.round_p8g > 0 && rr > d.r0 && wk0 == own_;
           if (t == 0) { sh_wide = 0; sh_gbad = !tryg; }
           __syncthreads();
+          if (sst) sst[0] = __builtin_amdgcn_s_memrealtime();
           const int32_t *r0p = d.la + (int64_t)(cs + wk0) * npad, *r1p = r0p + (int64_t)(wrows - 1) * npad;
           const int32_t *Bprev = d.B + (int64_t)(rr - 1) * n;
           // LA of column i at the window's first / last row (-1 past n, 0 past npad)
@@ -651,6 +652,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           if (__any(bad) && lane == 0) sh_wide = 1;
           if (__any(gbad) && lane == 0) sh_gbad = 1;
           __syncthreads();
+          if (sst) sst[1] = __builtin_amdgcn_s_memrealtime();
           p8g = !sh_gbad;
           p8 = p8g || !sh_wide;
         }
@@ -758,6 +760,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       }
       if (t <= WROWS) hist[t] = 0;
       __syncthreads();
+      if (sst) sst[2] = __builtin_amdgcn_s_memrealtime();
   };
   for (int it = 0;; ++it) {
   const int32_t *Bp = d.Bp + (int64_t)p * n;
@@ -1137,7 +1140,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     // B[r] (stored before the previous barrier)
     const int wrows_n = min(WROWS, len - result);
     if (wrows_n > 0 && d.prestage) {
-      stage(result, wrows_n, r + 1, result);
+      stage(result, wrows_n, r + 1, result, dgb ? d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4 : nullptr);
       prestaged = true;
     }
   }

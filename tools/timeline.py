@@ -75,6 +75,26 @@ def barrier(path):
         v = [x[i] for x in rows]
         print(f"{name:15s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
     print(f"{'workgroups':15s} {rows[0][6]}")
+    # k_round_wide's staging phases (third block): arrived -> fit check start -> fit decided -> window staged
+    off3 = off + TL_NR * 512 * 4
+    full = np.fromfile(path, dtype=np.uint64)
+    if full.size < off3 + TL_NR * 512 * 4:
+        return
+    g = full[off3: off3 + TL_NR * 512 * 4].reshape(TL_NR, 512, 4).astype(np.int64)
+    ok = live & (g[:, :, :3] > 0).all(axis=2)
+    if ok.sum() < 2:
+        return
+    a1 = b[:, :, 1][ok]
+    f0, f1, f2 = g[:, :, 0][ok], g[:, :, 1][ok], g[:, :, 2][ok]
+    for name, v in (("stage entry", f0 - a1), ("fit check", f1 - f0), ("window", f2 - f1)):
+        print(f"{name:15s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
+    # the workgroup that arrived last, per round
+    lastw = [int(np.argmax(np.where(live[r], b[r, :, 1], 0))) for r in range(TL_NR) if live[r].sum() > 1]
+    rr = [r for r in range(TL_NR) if live[r].sum() > 1]
+    v = np.array([[g[r, w, 0] - b[r, w, 1], g[r, w, 1] - g[r, w, 0], g[r, w, 2] - g[r, w, 1]] for r, w in zip(rr, lastw)
+                  if (g[r, w, :3] > 0).all()])
+    if len(v):
+        print("last arriver: stage entry / fit check / window: " + " / ".join(f"{np.median(v[:, k]) * ns / 1000:.2f}" for k in range(3)) + " us")
 
 
 if __name__ == "__main__":
