@@ -590,6 +590,13 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // B[r] are known before the barrier)
   bool p8 = false, p8g = false;
   const uint32_t *wb2 = wbase2;
+  // (PERS, P8) the window last staged: its first row, rows, base; the next
+  // window reuses the rows both share -- re-based in LDS by each column's
+  // base difference, split into a non-negative add and subtract (dpos, dneg)
+  // so no byte carries -- and loads only the rows past them (BH_WIN_REUSE)
+  int32_t ws_old = -1, wr_old = 0;
+  bool p8_old = false, g_old = false;
+  __shared__ uint16_t dpos16[256], dneg16[256];
   auto stage = [&](const int32_t wk0, const int wrows, const int rr, const int32_t own_, unsigned long long *sst = nullptr) {
       // COLS: the window's 36 aligned rows of every column from la_col, issued
       // before the fit check below reads its two rows
@@ -634,6 +641,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
               return (last ? r1p : r0p)[i];
           };
           bool bad = false, gbad = false;
+          const uint32_t ob2 = (g_old ? gbase2 : wbase2)[t & 255];  // (the last window's base, columns 2t, 2t + 1)
           for (int j = t; j < 256; j += 256) {
             const int i0 = 2 * j, i1 = 2 * j + 1;
             const int32_t a0 = la_w(i0, 0), a1 = la_w(i1, 0);
@@ -655,6 +663,12 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           if (sst) sst[1] = __builtin_amdgcn_s_memrealtime();
           p8g = !sh_gbad;
           p8 = p8g || !sh_wide;
+          if (PERS && COLS != 1 && d.win_reuse && p8 && p8_old && t < 256) {
+            const uint32_t nb2 = (p8g ? gbase2 : wbase2)[t];
+            const int32_t e0 = (int32_t)(ob2 & 0xFFFFu) - (int32_t)(nb2 & 0xFFFFu), e1 = (int32_t)(ob2 >> 16) - (int32_t)(nb2 >> 16);
+            dpos16[t] = (uint16_t)(max(e0, 0) | (max(e1, 0) << 8));
+            dneg16[t] = (uint16_t)(max(-e0, 0) | (max(-e1, 0) << 8));
+          }
         }
       }
       wb2 = p8g ? gbase2 : wbase2;
@@ -723,23 +737,35 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
           win4[row * WRS8 + pc + pc / PP8] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
         };
-        if (d.stage_b2) {
-          // two row groups' loads in flight per trip (BH_STAGE_B2): half the
-          // round trips of the staging, which the round's last workgroup pays
-          // on the next round's critical path
-          for (int i = t; i < lim; i += 2 * NT) {
-            int4 a[4], b[4];
-            ld8(i, a);
-            ld8(i + NT, b);
-            put8(i, a);
-            if (i + NT < lim) put8(i + NT, b);
+        // rows shared with the last window: new row k = old row k + dl
+        const int dl = wk0 - ws_old;
+        const int nr = PERS && COLS != 1 && d.win_reuse && p8 && p8_old && ws_old >= 0 && dl >= 0 && dl < wr_old
+                           ? min(wr_old - dl, wrows) : 0;
+        if (nr > 0) {
+          constexpr int NRI = (WROWS * RP8 + NT - 1) / NT;
+          int4 o[NRI];
+          const uint32_t *dp = reinterpret_cast<const uint32_t *>(dpos16), *dn = reinterpret_cast<const uint32_t *>(dneg16);
+#pragma unroll
+          for (int u = 0; u < NRI; ++u) {
+            const int i = t + u * NT, row = i / RP8, pc = i - row * RP8;
+            if (i < nr * RP8) o[u] = win4[(row + dl) * WRS8 + pc + pc / PP8];
           }
-        } else {
-          for (int i = t; i < lim; i += NT) {
-            int4 a[4];
-            ld8(i, a);
-            put8(i, a);
+          __syncthreads();
+#pragma unroll
+          for (int u = 0; u < NRI; ++u) {
+            const int i = t + u * NT, row = i / RP8, pc = i - row * RP8;
+            if (i < nr * RP8) {
+              const int m = 4 * pc;  // dwords of columns 16 pc ..
+              win4[row * WRS8 + pc + pc / PP8] =
+                  make_int4((int)(((uint32_t)o[u].x + dp[m]) - dn[m]), (int)(((uint32_t)o[u].y + dp[m + 1]) - dn[m + 1]),
+                            (int)(((uint32_t)o[u].z + dp[m + 2]) - dn[m + 2]), (int)(((uint32_t)o[u].w + dp[m + 3]) - dn[m + 3]));
+            }
           }
+        }
+        for (int i = nr * RP8 + t; i < lim; i += NT) {
+          int4 a[4];
+          ld8(i, a);
+          put8(i, a);
         }
       } else {
         constexpr int RP = LPC * PP;  // pieces per padded row
@@ -759,6 +785,10 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
         }
       }
       if (t <= WROWS) hist[t] = 0;
+      ws_old = wk0;
+      wr_old = wrows;
+      p8_old = p8;
+      g_old = p8g;
       __syncthreads();
       if (sst) sst[2] = __builtin_amdgcn_s_memrealtime();
   };
