@@ -255,54 +255,6 @@ __device__ __forceinline__ void handoff_wide(const Dev &d, int64_t row, int p1, 
   if (g && threadIdx.x == 0) stx<SC1>(d.c8tag + (int64_t)p1 * n + c, rnext);
 }
 
-// handoff_wide in two halves, so that the persistent loop can stage its next
-// window between them (the hand-off's loads in flight meanwhile): thread j <
-// w8 / 4 loads columns 4j .. 4j + 3 (every such thread has one: blockDim >=
-// 128 >= w8 / 4 at n <= 512), then converts and stores them
-struct WideHand {
-  int32_t v[4], bq[4];
-};
-template <bool SC1>
-__device__ __forceinline__ WideHand handoff_wide_load(const Dev &d, int64_t row, const int32_t *Bcur) {
-  const int npad = d.npad, n = d.n, w8 = (npad + 15) / 16 * 16;
-  const bool g = d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;
-  const int j = threadIdx.x;
-  WideHand x;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = 4 * j + k;
-    const bool ok = j < w8 / 4 && i < n;
-    x.v[k] = ok ? d.fdt[fdt_pos(row, i, npad)] : FD_NONE;
-    x.bq[k] = ok && g ? ldx<SC1>(Bcur + i) : 0;
-  }
-  return x;
-}
-template <bool SC1>
-__device__ __forceinline__ void handoff_wide_store(const Dev &d, const WideHand &x, int p1, int c, int32_t rnext) {
-  const int npad = d.npad, n = d.n, w16 = (npad + 7) / 8 * 4, w8 = (npad + 15) / 16 * 16;
-  uint32_t *dst16 = d.cand16 + ((int64_t)p1 * n + c) * w16;
-  const bool g = d.cand8 != nullptr && d.round_p8g > 0 && d.round_p8 > 0;
-  uint32_t *dst8 = g ? reinterpret_cast<uint32_t *>(d.cand8 + ((int64_t)p1 * n + c) * w8) : nullptr;
-  const int j = threadIdx.x;
-  if (j < w8 / 4) {
-    uint32_t h[4], b8 = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = 4 * j + k;
-      h[k] = min((uint32_t)x.v[k] + 1u, 0xFFFFu);
-      if (g) {
-        const int32_t base = i < n ? max(x.bq[k] - d.round_p8g, 0) : 0;
-        const uint32_t f = i < n ? min((uint32_t)max((int32_t)h[k] - base, 0), 127u) : 127u;
-        b8 |= f << (8 * k);
-      }
-    }
-    if (2 * j < w16) stx<SC1>(dst16 + 2 * j, h[0] | (h[1] << 16));
-    if (2 * j + 1 < w16) stx<SC1>(dst16 + 2 * j + 1, h[2] | (h[3] << 16));
-    if (g) stx<SC1>(dst8 + j, b8);
-  }
-  if (g && threadIdx.x == 0) stx<SC1>(d.c8tag + (int64_t)p1 * n + c, rnext);
-}
-
 // The first j in [lo, hi) with col[j] >= k (col non-decreasing), or hi:
 // the whole wave searches (lo, hi, k uniform), 64 probes per pass.
 __device__ __forceinline__ int32_t first_ge_wave(const int32_t *col, int32_t lo, int32_t hi, int32_t k) {
@@ -1166,23 +1118,8 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
       if (!PERS && lane == 0) d.ssw[ballot_row(d, c, r + 1) * 8 + ((k * NT) >> 6) + wave] = swm[k];
     }
   }
-  // the hand-off: the new candidate's FD row for the next iteration.
-  // PERS (BH_STAGE_EARLY): the next round's first window is staged between
-  // the hand-off's loads and its stores, so the round's last workgroup pays
-  // for the two at once rather than one after the other (its staging was
-  // the next round's critical path, behind its hand-off and the barrier)
-  const bool hand = P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap;
-  bool staged_early = false;
-  if (PERS && COLS == 0 && hand && d.prestage && d.stage_early && NT >= 128) {
-    const WideHand hx = handoff_wide_load<PERS>(d, (int64_t)cs + result, Bp);
-    const int wrows_n = min(WROWS, len - result);
-    if (wrows_n > 0) {
-      const bool dgs = d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
-      stage(result, wrows_n, r + 1, result, dgs ? d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4 : nullptr);
-      staged_early = true;
-    }
-    handoff_wide_store<PERS>(d, hx, p ^ 1, c, r + 1);
-  } else if (hand) {
+  // the hand-off: the new candidate's FD row for the next iteration
+  if (P16 && sh_nc > 0 && result < len && r + 1 < d.R_cap) {
     if constexpr (COLS != 0) handoff_wide_cols<NT, PERS>(d, p, c, result, Bp, r + 1);
     else handoff_wide<PERS>(d, (int64_t)cs + result, p ^ 1, c, Bp, r + 1);
   }
@@ -1232,9 +1169,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
     // arrive: its rows start at this round's result, its shared base is
     // B[r] (stored before the previous barrier)
     const int wrows_n = min(WROWS, len - result);
-    if (staged_early) {
-      prestaged = true;
-    } else if (wrows_n > 0 && d.prestage) {
+    if (wrows_n > 0 && d.prestage) {
       stage(result, wrows_n, r + 1, result, dgb ? d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4 : nullptr);
       prestaged = true;
     }

@@ -371,8 +371,7 @@ def test_chunk_sweep_wild(monkeypatch):
                                   "p16", "p32", "fdt_p8", "fdt_p16", "cols_p8", "cols_p8g_tight", "cols_p16",
                                   "cols2_p8", "cols2_p16", "iter_p8", "iter_p8_mixed", "iter_p8g_tight",
                                   "fallback_p8", "noprestage_p8", "flat_p8_mixed",
-                                  "prio_p8", "prio2_p8_mixed", "noreuse_p8", "noreuse_p8g_tight",
-                                  "noearly_p8", "noearly_p8_mixed"])
+                                  "prio_p8", "prio2_p8_mixed", "noreuse_p8", "noreuse_p8g_tight"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -397,9 +396,6 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     round); iter_*: one launch per round (BH_ROUND_PERSIST=0); fallback_*: the
     persistent loop's barrier gives up at once (BH_PBAR_SPIN=0), the host
     restores the loop's inputs and runs the per-round launches."""
-    if rows.startswith("noearly_"):  # the next window staged after the arrival, not inside the hand-off
-        monkeypatch.setenv("BH_STAGE_EARLY", "0")
-        rows = rows[len("noearly_"):]
     if rows.startswith("noreuse_"):  # every window staged whole (no rows kept from the last one)
         monkeypatch.setenv("BH_WIN_REUSE", "0")
         rows = rows[len("noreuse_"):]
