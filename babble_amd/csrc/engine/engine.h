@@ -303,7 +303,8 @@ enum DiagSlot {
   DG_TL = 32,  // k_round2 timeline: rounds TL_R0 .. TL_R0+TL_NR, [r][c][4] realtime stamps
   DG_TLB = 32 + 64 * 128 * 4,  // persistent loops' barrier phases: [r][c < 512][4] (end, arrived, staged, released)
   DG_TLS = DG_TLB + 64 * 512 * 4,  // k_round_wide's staging of the next window: [r][c][4] (fit loads, fit decided, staged)
-  DG_COUNT = DG_TLS + 64 * 512 * 4
+  DG_TQ = DG_TLS + 64 * 512 * 4,  // k_round_wide chains < 8: [r][c][66] (T_q bytes of 512 candidates, offsets)
+  DG_COUNT = DG_TQ + 64 * 8 * 66
 };
 constexpr int TL_R0 = 1000, TL_NR = 64;
 #ifdef __HIPCC__  // (kernel-side helper; the host files also build with g++ for the host-ASan library)

@@ -1108,6 +1108,18 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
   // most y's row (stronglySee is monotone along the chain)
   constexpr int NSW = 512 / NT;  // ssw words per wave
   unsigned long long swm[NSW];
+  if (d.diag != nullptr && d.ssw && r >= TL_R0 && r < TL_R0 + TL_NR && c < 8) {
+    // BH_DIAG: the candidates' T_q in the final window, its offset and the
+    // result's (tools/tq_stats.py: how spread the searches' answers are)
+    uint32_t *tq = reinterpret_cast<uint32_t *>(d.diag + DG_TQ + ((int64_t)(r - TL_R0) * 8 + c) * 66);
+    for (int q = t; q < 128; q += NT) tq[q] = reinterpret_cast<const uint32_t *>(tq_s)[q];
+    if (t == 0) {
+      tq[128] = (uint32_t)(wk0 - own);
+      tq[129] = (uint32_t)(result - own);
+      tq[130] = (uint32_t)sh_nc;
+      tq[131] = (uint32_t)n;
+    }
+  }
   const bool has_ssw = d.ssw && sh_nc > 0 && result < len && r + 1 < d.R_cap;
   if (has_ssw) {
     const int res = sh_res;
