@@ -386,16 +386,19 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     path for chains beyond P16_MAXLEN).  *_single: one candidate's search per
     lane group instead of two interleaved (BH_ROUND_ILP2=0, its own tag check
     and cand8 read).  n = 160 / 300 leave the last lanes of a candidate's
-    group past the end of its byte row.  The default loop reads its windows,
-    its candidates' FD rows (searched from the previous candidate's) and
-    fame's LA rows from the dataflow's column-major LA; fdt_*: the loop over
-    the transposed row-major LA and the complete FDT (BH_WIDE_ROWS=1).
-    cols_*: the loop over the column-major LA (BH_WIDE_COLS=1); cols2_*: the
-    window from the row-major LA, the hand-off from la_col (BH_WIDE_COLS=2).
-    The default 8-bit loop runs as one persistent launch (a grid barrier per
-    round); iter_*: one launch per round (BH_ROUND_PERSIST=0); fallback_*: the
+    group past the end of its byte row.  The default loop reads its windows
+    from the transposed row-major LA and its candidates' FD rows from FDT;
+    fdt_*: the same, pinned (BH_WIDE_ROWS=1).  cols_*: the loop over the
+    column-major LA (BH_WIDE_COLS=1); cols2_*: the window from the row-major
+    LA, the hand-off from la_col (BH_WIDE_COLS=2).  The default 8-bit loop
+    runs as one persistent launch (a grid barrier per round), stages its next
+    window during the barrier and keeps the rows it shares with the last
+    window; iter_*: one launch per round (BH_ROUND_PERSIST=0); fallback_*: the
     persistent loop's barrier gives up at once (BH_PBAR_SPIN=0), the host
-    restores the loop's inputs and runs the per-round launches."""
+    restores the loop's inputs and runs the per-round launches;
+    noprestage_*: staging after the barrier; flat_*: the one-counter
+    barrier; prio_* / prio2_*: BH_WIDE_PRIO=1 / 2 (the default is 2);
+    noreuse_*: every window staged whole (BH_WIN_REUSE=0)."""
     if rows.startswith("noreuse_"):  # every window staged whole (no rows kept from the last one)
         monkeypatch.setenv("BH_WIN_REUSE", "0")
         rows = rows[len("noreuse_"):]
