@@ -1706,7 +1706,6 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   // per round, profiles/r4_ab_wide.txt); BH_WIDE_PRIO=0|1 for A/B
   d.wide_prio = getenv("BH_WIDE_PRIO") ? atoi(getenv("BH_WIDE_PRIO")) : 2;
   d.win_reuse = getenv("BH_WIN_REUSE") ? atoi(getenv("BH_WIN_REUSE")) : 1;
-  d.stage_pf = getenv("BH_STAGE_PF") ? atoi(getenv("BH_STAGE_PF")) : 1;
   d.round_src_rows = getenv("BH_ROUND_SRC") && !strcmp(getenv("BH_ROUND_SRC"), "rows");
   d.N = 0;
   d.col0 = 0;

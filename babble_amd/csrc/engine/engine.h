@@ -134,7 +134,6 @@ struct Dev {
   int32_t pbar_mode;      // the persistent loops' barrier: 0 one counter, 1 XCD-hierarchical (n > 64; BH_PBAR=xcd|flat)
   int32_t prestage;       // the wide persistent loop stages its next window while the barrier completes (BH_PRESTAGE=0: off)
   int32_t xpose_fd;       // k_flow_transpose also walks firstDescendants into FDT (0: LA rows only)
-  int32_t stage_pf;       // persistent k_round_wide: the window's new rows loaded ahead of its fit check
   int32_t win_reuse;      // persistent k_round_wide: the next window reuses the rows it shares with the last
   int32_t wide_prio;      // persistent k_round_wide: 1 hand-off / barrier / staging at priority 2, 2 also alternate the search
   int32_t *psnap;         // the loop's inputs (Bp and candfd of parity 0, the state block) kept for that fallback

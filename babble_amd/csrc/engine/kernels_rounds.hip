@@ -617,31 +617,6 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
           }
         }
       }
-      // (PERS, P8; BH_STAGE_PF) the first two row groups past the rows the
-      // last window shares -- the reuse condition, P8 assumed -- are loaded
-      // ahead of the fit check's loads, so the two round trips overlap
-      // (discarded if the fit check picks 16-bit rows)
-      constexpr int NPF = 2;
-      constexpr bool PFC = PERS && COLS != 1 && P16;
-      const int dl0 = wk0 - ws_old;
-      const int nr0 = PFC && d.win_reuse && p8_old && ws_old >= 0 && dl0 >= 0 && dl0 < wr_old ? min(wr_old - dl0, wrows) : 0;
-      const bool pf = PFC && d.stage_pf && d.round_p8;
-      int4 pfv[PFC ? NPF : 1][4];
-      if constexpr (PFC) {
-        if (pf) {
-          constexpr int RPF = LPC * (PP / 2);
-          const int4 *src = reinterpret_cast<const int4 *>(d.la + (int64_t)(cs + wk0) * npad);
-#pragma unroll
-          for (int u = 0; u < NPF; ++u) {
-            const int i = nr0 * RPF + t + u * NT, row = i / RPF;
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              const int col = 16 * (i - row * RPF) + 4 * h;
-              pfv[u][h] = i < wrows * RPF && col < npad ? src[row * q4 + col / 4] : make_int4(0, 0, 0, 0);
-            }
-          }
-        }
-      }
       p8 = false;
       p8g = false;
       if constexpr (P16) {
@@ -787,15 +762,7 @@ __global__ __launch_bounds__(NT, NT / 128) void k_round_wide(Dev d, int p) {  //
             }
           }
         }
-        const int i0 = nr * RP8 + t;  // (pf: nr = nr0, the rows prefetched)
-        if constexpr (PFC) {
-          if (pf) {
-#pragma unroll
-            for (int u = 0; u < NPF; ++u)
-              if (i0 + u * NT < lim) put8(i0 + u * NT, pfv[u]);
-          }
-        }
-        for (int i = i0 + (pf ? NPF * NT : 0); i < lim; i += NT) {
+        for (int i = nr * RP8 + t; i < lim; i += NT) {
           int4 a[4];
           ld8(i, a);
           put8(i, a);

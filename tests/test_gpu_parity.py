@@ -371,8 +371,7 @@ def test_chunk_sweep_wild(monkeypatch):
                                   "p16", "p32", "fdt_p8", "fdt_p16", "cols_p8", "cols_p8g_tight", "cols_p16",
                                   "cols2_p8", "cols2_p16", "iter_p8", "iter_p8_mixed", "iter_p8g_tight",
                                   "fallback_p8", "noprestage_p8", "flat_p8_mixed",
-                                  "prio_p8", "prio2_p8_mixed", "noreuse_p8", "noreuse_p8g_tight",
-                                  "nopf_p8", "nopf_p8_mixed"])
+                                  "prio_p8", "prio2_p8_mixed", "noreuse_p8", "noreuse_p8g_tight"])
 @pytest.mark.parametrize("n,N,seed", [(160, 30_000, 51), (300, 30_000, 52)])
 def test_wide_parity(monkeypatch, n, N, seed, rows):
     """More participants than k_round2 / LDS fame support: k_round_wide
@@ -399,11 +398,7 @@ def test_wide_parity(monkeypatch, n, N, seed, rows):
     restores the loop's inputs and runs the per-round launches;
     noprestage_*: staging after the barrier; flat_*: the one-counter
     barrier; prio_* / prio2_*: BH_WIDE_PRIO=1 / 2 (the default is 2);
-    noreuse_*: every window staged whole (BH_WIN_REUSE=0); nopf_*: its new
-    rows loaded after the fit check (BH_STAGE_PF=0)."""
-    if rows.startswith("nopf_"):  # the window's new rows loaded after its fit check, not ahead of it
-        monkeypatch.setenv("BH_STAGE_PF", "0")
-        rows = rows[len("nopf_"):]
+    noreuse_*: every window staged whole (BH_WIN_REUSE=0)."""
     if rows.startswith("noreuse_"):  # every window staged whole (no rows kept from the last one)
         monkeypatch.setenv("BH_WIN_REUSE", "0")
         rows = rows[len("noreuse_"):]
