@@ -105,3 +105,14 @@ def test_c2_block_projection():
         if b % 97 == 0:
             assert hg.frame_json(rr) == o.frame_json(rr), f"frame {rr} JSON"
             assert hg.block_json(b) == bj, f"block {b} JSON"
+    # the bench's timed state: bh_reset_consensus + RunConsensus over the
+    # resident DAG and event bytes, twice; every hash and per-event output again
+    for run in (1, 2):
+        hg.reset_consensus()
+        hg.run_consensus()
+        _compare(o, hg, f"cfg2 frames, rerun {run}")
+        fh2, bh2, ok2 = hg.block_hashes()
+        assert ok2.all() and (fh2 == fh).all() and (bh2 == bh).all(), f"rerun {run}: block hashes"
+        for b in range(0, len(ob["round_received"]), 389):
+            rr = int(ob["round_received"][b])
+            assert hg.frame_roots(rr) == o.frame_roots(rr), f"rerun {run}: roots of frame {rr}"

@@ -157,6 +157,31 @@ def test_split_pipeline_incremental(monkeypatch, devs, K, n, N, seed, lag, step)
     assert grp.pipeline()[1] >= N // step - 2
 
 
+@pytest.mark.parametrize("coords,devs", [("split", [0, 0]), ("split", [0, 0, 0, 0]), ("replicate", [0, 0])])
+def test_group_rerun_after_reset(monkeypatch, coords, devs):
+    """The state bench.py times, on a shard group: bh_reset_consensus +
+    RunConsensus over the resident DAG, twice, after a first run -- every
+    device table but `blocked` carries over between runs -- each equal to the
+    oracle's batch run (n = 128, 8 segments: the split's per-segment blocks)."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_SHARD_COORDS", coords)
+    monkeypatch.setenv("BH_SEGMENTS", "8")
+    n, N = 128, 120_000
+    d = Dag(n, N, 97, sig_mode=0)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    grp = Hashgraph(d.participant_ids, N, devices=devs)
+    assert not grp.insert_dag(d).any()
+    for run in range(3):
+        if run:
+            grp.reset_consensus()
+        grp.run_consensus()
+        _compare(o, grp, f"{coords} {len(devs)} shards, run {run}")
+        assert grp.pipeline()[0] == 8
+
+
 @pytest.mark.parametrize("rng", [2, 60, 120, 250])
 def test_split_overflow_chunks(monkeypatch, rng):
     """Chunks whose 64 rows span more than the 16-bit range travel raw in the

@@ -33,7 +33,7 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _whole_digest(name, monkeypatch=None, segments=None):
+def _whole_digest(name, monkeypatch=None, segments=None, reruns=2):
     from babble_amd import Hashgraph
     from babble_amd.dag import Dag
     with open(os.path.join(GOLDEN, f"whole_{name}.json")) as f:
@@ -48,27 +48,36 @@ def _whole_digest(name, monkeypatch=None, segments=None):
     assert int(np.bincount(d.creator, minlength=d.n).max()) == sp["max_chain"], "generator drift"
     hg = Hashgraph(d.participant_ids, d.N)
     assert not hg.insert_dag(d).any()
-    hg.run_consensus()
-    got = engine_digest(hg)
-    bad = diff({k: v for k, v in ref.items() if k not in ("spec", "oracle")}, got)
-    assert not bad, f"{name}: engine differs from the oracle's whole-DAG run at {bad[:12]}"
+    want = {k: v for k, v in ref.items() if k not in ("spec", "oracle")}
+    # the first run on a fresh handle, then the state bench.py times: each of
+    # its steps is bh_reset_consensus + RunConsensus over the resident DAG
+    # (BenchmarkConsensus, hashgraph_test.go:1522-1534, reruns the passes on
+    # one inserted DAG), where every device table but `blocked` carries over
+    # from the previous run
+    for run in range(1 + reruns):
+        if run:
+            hg.reset_consensus()
+        hg.run_consensus()
+        bad = diff(want, engine_digest(hg))
+        assert not bad, f"{name} run {run}: engine differs from the oracle's whole-DAG run at {bad[:12]}"
     return d, hg
 
 
 @pytest.mark.timeout(900)
 def test_c3_whole_dag():
     """The bench's headline DAG, all 10M events, through the default pipeline
-    (8 segments, each segment's LT after the next one's columns, the
-    persistent loop)."""
+    (8 segments, the persistent loop), on a fresh handle and on two reruns
+    after bh_reset_consensus (the bench's timed step)."""
     d, hg = _whole_digest("c3")
     assert hg.pipeline()[0] == 8 and hg.profile_kernel() == "k_flow32"
-    assert hg.loop_stats() == (8, 0)
+    assert hg.loop_stats() == (8 * 3, 0)  # one persistent loop per segment and run, no fallback
     invariants(d, hg)
 
 
 @pytest.mark.timeout(900)
 def test_c4_whole_dag():
-    """C4, all 20M events (512 peers: k_floww2 and the 16-bit k_round_wide)."""
+    """C4, all 20M events (512 peers: k_floww2 and the 16-bit k_round_wide),
+    fresh and on two reruns after bh_reset_consensus."""
     if not os.path.exists(os.path.join(GOLDEN, "whole_c4.json")):
         pytest.fail("tests/golden/whole_c4.json missing: run tests/golden/make_whole_digests.py --cfg 4 --coord16")
     d, hg = _whole_digest("c4")
