@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <thread>
 #include <cstdarg>
 #include <cstdio>
@@ -449,7 +450,7 @@ int reset_coords(bh_handle *h, hipStream_t s) {
     if (bh::flow32_eligible(d) && use_flow(d)) {
       bh::launch_flow_desc(vb, s);
       bh::launch_flow(vb, s);
-      h->sweep_kernel = "k_flow32";
+      h->sweep_kernel = bh::flow_kernel(d);
     } else {
       bh::launch_floww(vb, s);
       h->sweep_kernel = bh::floww_kernel(d);
@@ -487,7 +488,7 @@ int rounds_coords(bh_handle *h) {
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
     bh::launch_flow(d, s);
     HIPCHK(h, hipEventRecord(h->ev_sweep[1], s));
-    h->sweep_kernel = bh::flow32_eligible(d) ? "k_flow32" : "k_flow";
+    h->sweep_kernel = bh::flow_kernel(d);
   } else if (bh::floww_eligible(d)) {
     HIPCHK(h, hipEventRecord(h->ev_sweep[0], s));
     bh::launch_floww(d, s);
@@ -670,7 +671,7 @@ int segments_for(const Dev &d, int64_t events) {
   // one's columns, 8 segments 188.8M events/s, 16 187.6M, 24 184.1M)
   int K = !d.fd_cols ? 1 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(K, events / 4096 + 1));
+  return (int)std::max<int64_t>(1, std::min<int64_t>({K, events / 4096 + 1, 64}));
 }
 
 // ---------------------------------------------------------------------------
@@ -681,19 +682,30 @@ int segments_for(const Dev &d, int64_t events) {
 // them to shard 0, packed as 16-bit offsets, over xGMI (peer copies in
 // process, ncclSend / ncclRecv across processes)
 
-// segment boundaries of a K-segment pipeline over events [base, N): the
-// first segment is short (1/(4K) of the events; BH_SEG_FIRST=<permille>
-// sets it), the rest equal.  The loop waits for the first segment's
-// coordinates only: the dataflow then stays ahead of it (C3: 57 ms of
-// coordinates against 62 ms of loop), so a short first segment starts the
-// loop ~5 ms earlier than K equal ones would
+// segment boundaries of a K-segment pipeline over events [base, N):
+// sizes grow geometrically, s_k proportional to 1.5^k.  The loop waits for
+// the first segment's coordinates only if every later segment's
+// coordinates finish before the loop's previous segment does: segment k + 1's
+// dataflow starts when the loop starts segment k (the segment views are
+// double-buffered), so s_(k+1) <= (loop time / dataflow time per event) s_k
+// suffices -- 1.8 at C3 with k_flow32x2 (5.65 against 3.1 ms per 1.25M
+// events), and 1.5 leaves margin.  The pipeline's fill is then the first
+// segment's dataflow, 1/49 of the events at K = 8 (round 4: a first segment
+// of 1/(4K) and K - 1 equal ones after it, which at C3 left the loop waiting
+// ~2 ms for the second segment)
 static void segment_bounds(int64_t base, int64_t N, int K, int64_t *Ns) {
   Ns[0] = base;
   if (K <= 1) { Ns[1] = N; return; }
-  static const int pm = getenv("BH_SEG_FIRST") ? std::clamp(atoi(getenv("BH_SEG_FIRST")), 1, 1000) : 0;
-  const int64_t first = pm ? (N - base) * pm / 1000 : (N - base) / (4 * K);
-  Ns[1] = base + std::max<int64_t>(first, 1);
-  for (int k = 2; k <= K; ++k) Ns[k] = Ns[1] + (N - Ns[1]) * (k - 1) / (K - 1);
+  double w[64], tot = 0;
+  K = std::min(K, 64);
+  for (int k = 0; k < K; ++k) tot += (w[k] = std::pow(1.5, k));
+  double acc = 0;
+  for (int k = 1; k < K; ++k) {
+    acc += w[k - 1];
+    // at least one event per segment (segments_for keeps >= 4096 per segment on average)
+    Ns[k] = std::max(Ns[k - 1] + 1, base + (int64_t)((double)(N - base) * acc / tot));
+  }
+  Ns[K] = N;
 }
 
 // the LA columns of coordinate shard `rank` (>= 1) of a split group
@@ -851,7 +863,7 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
   x->lens_coord = x->lens_h;
   x->inc_valid = true;
   x->rows_stale = true;
-  x->sweep_kernel = "k_flow32";
+  x->sweep_kernel = bh::flow_kernel(dv);
   return BH_OK;
 }
 
@@ -980,21 +992,16 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));
     return BH_OK;
   };
-  // where a segment's Lamport timestamps (one more dataflow workgroup, the LT
-  // lane) run: 1 = inside the column launch (n + 1 workgroups) while 2n + 1
-  // fit the compute units, so the loop's n workgroups still find units of
-  // their own (C5: 82 -> 101M events/s against 0); 0 = after the segment's
-  // columns on the coordinate stream (n = 128: 129 column workgroups would
-  // share a unit with a loop workgroup, which every barrier then waits for;
-  // C3: 161M with 1); 2 = on a stream of their own after the columns, beside
-  // the next segment's (C3: 176M against 0's 180M: the loop shares more).
-  // BH_LT_MODE=<0|1|2> overrides (profiles/r4_ab_lt.txt)
-  const int lt_mode = getenv("BH_LT_MODE") ? std::clamp(atoi(getenv("BH_LT_MODE")), 0, 2)
-                      : (getenv("BH_LT_COMBINED") && atoi(getenv("BH_LT_COMBINED"))) ? 1
-                      : (2 * n + 1 <= h->ncu ? 1 : 0);
-  const bool lt_combined = lt_mode == 1;
-  hipStream_t sl = h->stream3;
-  auto lt_after = [&](int kk) {  // (lt_mode 0) segment kk's LT workgroup and per-event LT, on the coordinate stream
+  // where a segment's Lamport timestamps run: k_flow32x2 (the default)
+  // carries them in its first workgroup, (n + 1) / 2 workgroups in all.  The
+  // one-value k_flow32 (chains past X2_MAXLEN; BH_FLOW1) needs a workgroup of
+  // its own for them: inside the column launch while 2n + 1 workgroups fit
+  // the compute units beside the loop's n (C5: 82 -> 101M events/s in round
+  // 4), else after the next segment's columns on the coordinate stream (at
+  // n = 128 a 129th column workgroup would share a unit with a loop
+  // workgroup, which every barrier then waits for; profiles/r4_ab_lt.txt)
+  const bool lt_combined = wide || bh::flow32x2_eligible(d) || 2 * n + 1 <= h->ncu;
+  auto lt_after = [&](int kk) {  // (!lt_combined) segment kk's LT workgroup and per-event LT, on the coordinate stream
     const Dev vk = view(kk);
     Dev vl = vk;
     vl.ncol = 0;
@@ -1059,30 +1066,12 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));  // the segment's LA is ready for the loop
     if (!wide && lt_combined) {
       bh::launch_lt_rows(v, sc);
-    } else if (!wide && lt_mode == 0) {
+    } else if (!wide) {
       // the Lamport timestamps of the segment before this one, after this
       // segment's columns: the loop's next segment waits only for columns
       // (the last segment's follow its own columns)
       if (k > 0) lt_after(k - 1);
       if (k == K - 1) lt_after(k);
-    } else if (!wide) {  // the segment's Lamport timestamps: one workgroup, beside the loop
-      hipStream_t st = lt_mode == 2 ? sl : sc;
-      if (lt_mode == 2) HIPCHK(h, hipStreamWaitEvent(sl, h->seg_ev[(size_t)3 * k], 0));  // (after the segment's columns)
-      Dev vl = v;
-      vl.ncol = 0;
-      vl.flow_lt = 1;
-      bh::launch_flow(vl, st);
-      bh::launch_lt_rows(v, st);
-      HIPCHK(h, hipGetLastError());
-      if (lt_mode == 2) {
-        // segment k + 2 reuses this view's segbuf half: the coordinate
-        // stream waits for this LT first (below, before coords(k + 2))
-        HIPCHK(h, hipEventRecord(h->lt_ev[k & 1], sl));
-        h->lt_ev_live[k & 1] = true;
-        if (k == K - 1) {  // the pipeline's end includes the last LT
-          HIPCHK(h, hipStreamWaitEvent(sc, h->lt_ev[k & 1], 0));
-        }
-      }
     } else if (!eager) {  // wide: k_floww2 wrote lt_row; per-event LT (the transpose copies it otherwise)
       bh::launch_lt_rows(v, sc);
       HIPCHK(h, hipGetLastError());
@@ -1173,7 +1162,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       int32_t r0 = 0;
       (void)copy_sync(sr, &r0, rv.state + bh::ST_RESUME, 4, hipMemcpyDeviceToHost);
       fprintf(stderr, "[seg %d] coords %.2f ms (%s %.2f) | loop %.2f ms, rounds %d, iters %d, next resume at %d\n", k,
-              cms, wide ? "k_floww2" : "k_flow32", fms, lms, st[bh::ST_ROUNDS], st[bh::ST_ITERS], r0);
+              cms, wide ? "k_floww2" : bh::flow_kernel(d), fms, lms, st[bh::ST_ROUNDS], st[bh::ST_ITERS], r0);
     }
   }
   if (lt0) (void)hipEventDestroy(lt0);
@@ -1200,7 +1189,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   h->sweep_ms = 0;
   for (int k = 0; k < K; ++k)
     if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
-  h->sweep_kernel = wide ? bh::floww_kernel(d) : "k_flow32";
+  h->sweep_kernel = wide ? bh::floww_kernel(d) : bh::flow_kernel(d);
   if (sp) {  // the coordinate time is the coordinate shards'; the receive windows are the exchange
     h->xchg_ms = h->sweep_ms;
     h->sweep_ms = 0;

@@ -322,6 +322,8 @@ void launch_flow_coordinates(const Dev &d, hipStream_t s);  // LA + LT, chain da
 void launch_flow_desc(const Dev &d, hipStream_t s);
 void launch_flow(const Dev &d, hipStream_t s);
 bool flow32_eligible(const Dev &d);
+bool flow32x2_eligible(const Dev &d);  // k_flow32x2: two values per workgroup
+const char *flow_kernel(const Dev &d);  // k_flow32x2, k_flow32 or k_flow
 void launch_flow_lt_fallback(const Dev &d, hipStream_t s);
 void launch_sha256(const uint8_t *data, const int64_t *off, const int32_t *len, int64_t count, uint8_t *out,
                    hipStream_t s);  // kernels_sha.hip

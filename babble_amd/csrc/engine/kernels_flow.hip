@@ -568,6 +568,285 @@ __global__ __launch_bounds__(256) void k_flow32(Dev d) {
   else flow32_body<false>(d, L);
 }
 
+// ---------------------------------------------------------------------------
+// k_flow32x2: k_flow32's dataflow carrying TWO values per workgroup (round
+// 5).  Every LA column and LT follow the same schedule -- a lane advances
+// when its other-parent's slot holds the event, whatever the value -- so a
+// lane can carry two of them per step at three more VALU ops (a max, an add,
+// a select), and n columns + LT need (n + 1) / 2 workgroups: at n = 128, 65
+// workgroups run the columns AND the Lamport timestamps in one launch (the
+// one-value kernel needs 129, so LT ran as a second phase after the columns:
+// 129 + the round loop's 128 workgroups exceed 256 compute units).
+//   slot (8 B) = {generation (k / 64, 11 bits) << 21 | A + 1 (21 bits),
+//                 B + 1 (32 bits)}
+// in 64-slot rings (67 KiB, the LDS k_flow32's 128 one-dword slots took); a
+// ds_read_b64 / ds_write_b64 of an aligned slot is one LDS access, so the
+// generation in the low dword vouches for both (as in k_floww2).  The
+// descriptor entries are k_flow32's ({other-parent's slot, own slot of the
+// row before}, prepared by k_flow_desc32x2) with 64-slot addresses.  B is
+// LT in workgroup 0 (32 bits: no clamp, no fallback) and an LA column
+// elsewhere.  Chains up to 0x7FE * 64 = 131,008 events; longer ones (up to
+// F2_MAXLEN) take k_flow32.
+constexpr int X2_R = 64, X2_RS = X2_R + 1;     // value-ring slots (8 B) per chain, + 1 pad
+constexpr int X2_DR = 64, X2_DRS = X2_DR + 1;  // descriptor-ring entries (int2) per chain
+constexpr uint32_t X2_VMASK = 0x1FFFFFu, X2_GMASK = 0xFFE00000u;
+constexpr uint32_t X2_GNOOP = 0x7FF, X2_GWAIT = 0x7FE, X2_GINIT = 0x7FF;
+constexpr int32_t X2_MAXLEN = 0x7FE * X2_R;
+
+__host__ __device__ constexpr uint32_t x2_desc(int32_t dch, int32_t j) {
+  return ((uint32_t)(j >> 6) << 21) | (uint32_t)((dch * X2_RS + (j & (X2_R - 1))) * 8);
+}
+__host__ __device__ constexpr uint32_t x2_noop(int n) { return (X2_GNOOP << 21) | (uint32_t)((n * X2_RS + X2_R - 1) * 8); }
+__host__ __device__ constexpr uint32_t x2_wait(int n) { return (X2_GWAIT << 21) | (uint32_t)((n * X2_RS + X2_R - 2) * 8); }
+
+__global__ void k_flow_desc32x2(Dev d) {
+  const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.N) return;
+  int2 *opw = reinterpret_cast<int2 *>(d.opdesc);
+  const int32_t o = d.op[e], p = d.epos[e];
+  opw[p].x = (int32_t)(o < 0 ? x2_noop(d.n) : x2_desc(d.creator[o], d.index[o]));
+  opw[p + 1].y = (int32_t)x2_desc(d.creator[e], d.index[e]);
+}
+
+struct FlowLdsX2 {
+  uint2 vring[FL_MAXN + 1][X2_RS];  // 67 KiB, LDS offset 0
+  int2 dring[FL_MAXN][X2_DRS];      // 66.5 KiB
+  int32_t filled[FL_MAXN], consumed[FL_MAXN], pub[FL_MAXN], cs[FL_MAXN], stored[FL_MAXN];
+};
+
+// colA / colB: the LA columns this workgroup carries (-1: none); ltB: B is LT
+__device__ __forceinline__ void flow32x2_body(const Dev &d, FlowLdsX2 &L, int colA, int colB, bool ltB) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int n = d.n;
+  const int nw = (n + 63) >> 6;
+  const int64_t stride = d.la_rows + 64;
+  const bool hasA = colA >= 0, hasB = ltB || colB >= 0;
+  int32_t *const pA = hasA ? d.la_col + (int64_t)colA * stride : nullptr;
+  int32_t *const pB = ltB ? d.lt_row : colB >= 0 ? d.la_col + (int64_t)colB * stride : nullptr;
+  // (an absent value reads the other one's array, and is never stored)
+  int32_t *const outA = hasA ? pA : pB;
+  int32_t *const outB = hasB ? pB : pA;
+  for (int c = t; c < n; c += blockDim.x) {
+    const int32_t lo = d.seg_lo[c];
+    L.filled[c] = lo;
+    L.consumed[c] = lo;
+    L.pub[c] = lo;
+    L.stored[c] = lo;
+    L.cs[c] = d.chain_start[c];
+    for (int s = 0; s < X2_R; ++s) L.vring[c][s] = make_uint2(X2_GINIT << 21, 0u);  // matches no real event
+  }
+  for (int s = t; s < X2_R; s += blockDim.x) L.vring[n][s] = make_uint2(s == X2_R - 1 ? (X2_GNOOP << 21) : 0u, 0u);
+  __syncthreads();
+  lds_vint *filled = (lds_vint *)L.filled, *consumed = (lds_vint *)L.consumed, *pub = (lds_vint *)L.pub,
+           *stored = (lds_vint *)L.stored;
+  const int2 *opw = reinterpret_cast<const int2 *>(d.opdesc);
+
+  if (wave == nw) {
+    // ---------------- prefetch wave: descriptor rings, 32 entries per DMA (as k_flow32) ----------------
+    int32_t f[2], tot[2], cs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane + 64 * h;
+      const int32_t len = c < n ? d.chain_len[c] : 0;
+      const int32_t lo = c < n ? d.seg_lo[c] : 0;
+      f[h] = lo & ~31;
+      tot[h] = len > lo ? len + 1 : 0;  // entry len carries the last event's own slot
+      cs[h] = c < n ? d.chain_start[c] : 0;
+    }
+    for (;;) {
+      bool left = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        const int32_t cons = c < n ? consumed[c] : 0;
+        const bool need = f[h] < tot[h] && f[h] - cons <= X2_DR - 32;
+        left |= f[h] < tot[h];
+        unsigned long long m = __ballot(need);
+        while (m) {
+          const int b = __builtin_ctzll(m);
+          m &= m - 1;
+          const int cc = b + 64 * h;
+          const int32_t fc = __builtin_amdgcn_readlane(f[h], b);
+          const int32_t csc = __builtin_amdgcn_readlane(cs[h], b);
+          __builtin_amdgcn_global_load_lds((const void *)(reinterpret_cast<const int32_t *>(opw + csc + fc) + lane),
+                                           (lds_void_t *)&L.dring[cc][fc & (X2_DR - 1)], 4, 0, 0);
+        }
+        if (need) f[h] += 32;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = lane + 64 * h;
+        if (c < n) filled[c] = min(f[h], tot[h]);
+      }
+      if (!__any(left)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    return;
+  }
+  if (wave == nw + 1) {
+    // ---------------- store wave: rings -> HBM, both values ----------------
+    int32_t sp[2], len[2], cs[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = lane + 64 * h;
+      len[h] = c < n ? d.chain_len[c] : 0;
+      cs[h] = c < n ? d.chain_start[c] : 0;
+      sp[h] = c < n ? d.seg_lo[c] : 0;
+    }
+    const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(outA, (short)0, (int)(stride * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(outB, (short)0, (int)(stride * 4), 0x00020000);
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    auto gen_ok = [](uint32_t v, int32_t j) { return (v ^ ((uint32_t)(j >> 6) << 21)) < (1u << 21); };
+    for (int pass = 1;; ++pass) {
+      bool left = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = min(lane + 64 * h, n);  // row n: sentinel, never matches below
+        const uint2 *ring = &L.vring[c][0];
+        for (int it = 0; it < 8; ++it) {
+          const int32_t j = sp[h];
+          // rows cs + j = 0 mod 4: one 16-B store of four events per value
+          const bool grp = ((cs[h] + j) & 3) == 0 && j + 4 <= len[h];
+          const uint2 v3 = ring[(j + (grp ? 3 : 0)) & (X2_R - 1)];
+          const bool ok = j < len[h] && gen_ok(v3.x, j + (grp ? 3 : 0));
+          if (!__any(ok)) break;
+          if (ok) {
+            const int o = (int)((cs[h] + j) * 4);
+            if (grp) {
+              const uint2 v0 = ring[j & (X2_R - 1)], v1 = ring[(j + 1) & (X2_R - 1)], v2 = ring[(j + 2) & (X2_R - 1)];
+              if (hasA)
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{(v0.x & X2_VMASK) - 1u, (v1.x & X2_VMASK) - 1u,
+                                                             (v2.x & X2_VMASK) - 1u, (v3.x & X2_VMASK) - 1u},
+                                                       rA, o, 0, 0);
+              if (hasB) __builtin_amdgcn_raw_buffer_store_b128(u32x4{v0.y - 1u, v1.y - 1u, v2.y - 1u, v3.y - 1u}, rB, o, 0, 0);
+              sp[h] = j + 4;
+            } else {
+              if (hasA) __builtin_amdgcn_raw_buffer_store_b32((v3.x & X2_VMASK) - 1u, rA, o, 0, 0);
+              if (hasB) __builtin_amdgcn_raw_buffer_store_b32(v3.y - 1u, rB, o, 0, 0);
+              sp[h] = j + 1;
+            }
+          }
+        }
+        left |= sp[h] < len[h];
+        if (lane + 64 * h < n) stored[lane + 64 * h] = sp[h];
+      }
+      if ((pass & 7) == 0 || !__any(left)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (lane + 64 * h < n) pub[lane + 64 * h] = sp[h];
+      }
+      if (!__any(left)) break;
+    }
+    return;
+  }
+  if (wave > nw + 1) return;
+
+  // ---------------- compute waves: one chain per lane, two values ----------------
+  const int c = wave * 64 + lane;
+  const bool valid = c < n;
+  const int32_t len = valid ? d.chain_len[c] : 0;
+  const int cc = valid ? c : 0;
+  const int32_t incA = c == colA ? 1 : 0;               // LA[e][creator] = index
+  const int32_t incB = ltB ? 1 : (c == colB ? 1 : 0);  // LT + 1
+  // lanes that do not advance write slots 0..31 of the sentinel row (62 and
+  // 63 are the WAIT and no-other-parent slots)
+  const uint32_t wscratch = (uint32_t)((n * X2_RS + (lane & 31)) * 8);
+  const uint32_t WAIT = x2_wait(n);
+  char *const lds = reinterpret_cast<char *>(&L.vring[0][0]);  // vring is at LDS offset 0
+  const int2 *dring_c = &L.dring[cc][0];
+  // cur*: value of event k-1 + 1 (0: no self-parent); a resumed segment
+  // starts from the values its chain's previous event left in HBM
+  int32_t k = valid ? d.seg_lo[c] : 0, curA = 0, curB = 0, lim = 0;
+  if (k > 0) {
+    const int64_t r = (int64_t)d.chain_start[c] + k - 1;
+    curA = outA[r] + 1;
+    curB = outB[r] + 1;
+  } else if (ltB && valid && d.lt_seed) {
+    curB = d.lt_seed[c] + 1;  // a Reset root's SelfParent LamportTimestamp
+  }
+  uint32_t dsc = WAIT;
+  const bool dg = d.diag != nullptr && blockIdx.x == 0 && wave == 0;
+  const unsigned long long t_start = dg ? stamp() : 0;
+  int32_t step = 0;
+#define X2_STEP()                                                                        \
+  do {                                                                                   \
+    const uint2 slot_ = *reinterpret_cast<const uint2 *>(lds + (dsc & 0x1FFFFu));        \
+    const int32_t kn_ = k + 1;                                                           \
+    const int2 e_ = dring_c[kn_ & (X2_DR - 1)];                                          \
+    const bool ready_ = (slot_.x ^ dsc) < (1u << 21);                                    \
+    const int32_t a_ = max(curA, (int32_t)(slot_.x & X2_VMASK)) + incA;                  \
+    const int32_t b_ = max(curB, (int32_t)slot_.y) + incB;                               \
+    const uint32_t wa_ = ready_ ? ((uint32_t)e_.y & 0x1FFFFu) : wscratch;                \
+    *reinterpret_cast<uint2 *>(lds + wa_) = make_uint2(((uint32_t)e_.y & X2_GMASK) | (uint32_t)a_, (uint32_t)b_); \
+    curA = ready_ ? a_ : curA;                                                           \
+    curB = ready_ ? b_ : curB;                                                           \
+    dsc = ready_ ? (kn_ < lim ? (uint32_t)e_.x : WAIT) : dsc;                            \
+    k = ready_ ? kn_ : k;                                                                \
+  } while (0)
+  for (;; step += 32) {
+    // header: limits (entry k + 1 must be loaded: it holds k's own slot),
+    // stalled descriptors, read-backs, exit
+    lim = valid ? min(filled[cc] - 1, stored[cc] + X2_R - 16) : 0;
+    if (dsc == WAIT && k < lim) dsc = (uint32_t)dring_c[k & (X2_DR - 1)].x;
+    if (valid) consumed[c] = k;
+    if (!__any(k < len)) break;
+    {
+      // a parent the ring has moved past: read both values back once its
+      // chain has published them
+      const uint32_t sa = dsc & 0x1FFFFu;
+      const uint32_t slot = *reinterpret_cast<const uint32_t *>(lds + sa);
+      const int32_t si = (int32_t)(sa >> 3), dd = si / X2_RS;
+      const int32_t jj = (int32_t)((dsc >> 21) << 6) | (si - dd * X2_RS);
+      const bool far = (slot & X2_GMASK) > (dsc & X2_GMASK) && pub[dd] > jj;
+      if (__builtin_expect(__any(far), 0)) {
+        if (far) {
+          const int64_t pr = (int64_t)L.cs[dd] + jj;
+          int32_t va, vb;
+          asm volatile("global_load_dword %0, %2, off nt\n\tglobal_load_dword %1, %3, off nt\n\ts_waitcnt vmcnt(0)"
+                       : "=&v"(va), "=&v"(vb)
+                       : "v"(outA + pr), "v"(outB + pr)
+                       : "memory");
+          const int32_t a = max(curA, va + 1) + incA, b = max(curB, vb + 1) + incB;
+          const uint32_t wd = (uint32_t)dring_c[(k + 1) & (X2_DR - 1)].y;
+          *reinterpret_cast<uint2 *>(lds + (wd & 0x1FFFFu)) = make_uint2((wd & X2_GMASK) | (uint32_t)a, (uint32_t)b);
+          curA = a;
+          curB = b;
+          ++k;
+          dsc = k < lim ? (uint32_t)dring_c[k & (X2_DR - 1)].x : WAIT;
+        }
+      }
+    }
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+    X2_STEP(); X2_STEP(); X2_STEP(); X2_STEP();
+  }
+#undef X2_STEP
+  if (valid) consumed[c] = len;
+  if (dg && lane == 0) {
+    d.diag[DG_FL_STEPS] = step;
+    d.diag[DG_FL_CYC] = stamp() - t_start;
+  }
+}
+
+// values: the LA columns col0 .. col0 + ncol - 1 and, with flow_lt, LT.
+// With LT, workgroup 0 carries {col0, LT} and workgroup w >= 1 {col0 + 2w -
+// 1, col0 + 2w}; without, workgroup w carries {col0 + 2w, col0 + 2w + 1}.
+// The last workgroup of an odd count carries one column.
+__global__ __launch_bounds__(256) void k_flow32x2(Dev d) {
+  __shared__ FlowLdsX2 L;  // static: the ring's LDS base is the constant 0
+  const int w = (int)blockIdx.x, c0 = d.col0, c1 = d.col0 + d.ncol;
+  const bool lt = d.flow_lt && w == 0;
+  const int a = d.flow_lt ? c0 + 2 * w - 1 : c0 + 2 * w;  // (one call site: one copy of the unrolled loop)
+  flow32x2_body(d, L, lt ? (d.ncol > 0 ? c0 : -1) : a, !lt && a + 1 < c1 ? a + 1 : -1, lt);
+}
+
 // column-major LA (chain-major rows) -> row-major LA; LT rows -> event
 // ids; and the firstDescendants walk (kernels_fd.hip) on the same tile:
 // the TR rows staged column-major are exactly what the walk searches, so
@@ -751,17 +1030,35 @@ bool flow32_eligible(const Dev &d) {
   return flow_eligible(d) && d.max_chain_len <= F2_MAXLEN && !(e && !strcmp(e, "flow64"));
 }
 
+// two values per workgroup (k_flow32x2) for chains up to X2_MAXLEN;
+// BH_FLOW1=1 keeps the one-value k_flow32 (the fallback for chains up to
+// F2_MAXLEN, parity-tested through this switch)
+bool flow32x2_eligible(const Dev &d) {
+  return flow32_eligible(d) && d.max_chain_len <= X2_MAXLEN && !(getenv("BH_FLOW1") && atoi(getenv("BH_FLOW1")));
+}
+
+const char *flow_kernel(const Dev &d) {
+  return flow32x2_eligible(d) ? "k_flow32x2" : flow32_eligible(d) ? "k_flow32" : "k_flow";
+}
+
 void launch_flow_desc(const Dev &d, hipStream_t s) {
   if (d.N <= d.e0) return;
-  if (flow32_eligible(d)) k_flow_desc32<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+  if (flow32x2_eligible(d)) k_flow_desc32x2<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+  else if (flow32_eligible(d)) k_flow_desc32<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
   else k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
 }
 
 void launch_flow(const Dev &d, hipStream_t s) {
   if (d.N == 0) return;
   const int nw = (d.n + 63) / 64;
-  if (flow32_eligible(d)) k_flow32<<<d.ncol + (d.flow_lt ? 1 : 0), (nw + 2) * 64, 0, s>>>(d);
-  else k_flow<<<d.ncol + 1, (nw + 2) * 64, 0, s>>>(d, 0);
+  if (flow32x2_eligible(d)) {
+    const int nv = d.ncol + (d.flow_lt ? 1 : 0);
+    if (nv > 0) k_flow32x2<<<(nv + 1) / 2, (nw + 2) * 64, 0, s>>>(d);
+  } else if (flow32_eligible(d)) {
+    k_flow32<<<d.ncol + (d.flow_lt ? 1 : 0), (nw + 2) * 64, 0, s>>>(d);
+  } else {
+    k_flow<<<d.ncol + 1, (nw + 2) * 64, 0, s>>>(d, 0);
+  }
 }
 
 // LT overflowed k_flow32's 21-bit values (ST_FLOWOVF): recompute LT with

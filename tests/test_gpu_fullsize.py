@@ -61,7 +61,7 @@ def test_c5_whole_dag():
 def test_c3_multisegment(monkeypatch):
     hg = _whole(3, N=2_500_000, segments=5, monkeypatch=monkeypatch)
     assert hg.pipeline()[0] == 5
-    assert hg.profile_kernel() == "k_flow32"
+    assert hg.profile_kernel() == "k_flow32x2"
 
 
 @pytest.mark.timeout(600)

@@ -501,10 +501,12 @@ def test_transpose_fd_walk(monkeypatch, n, N, seed, lag):
 
 
 def test_flow32_lt_fallback(monkeypatch):
-    """k_flow32 carries values in 21 bits; Lamport timestamps beyond its
+    """The one-value k_flow32 (BH_FLOW1=1; the default k_flow32x2 carries LT
+    in 32 bits) carries values in 21 bits; Lamport timestamps beyond its
     limit are flagged and recomputed by the two-dword kernel.  A lowered
     limit (BH_FLOW_LTCLAMP, read at handle creation) forces that path on a
     DAG whose timestamps exceed it."""
+    monkeypatch.setenv("BH_FLOW1", "1")
     monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
     hg = _random_parity(16, 20_000, 71, 2)
     assert hg.results()["lamport"].max() > 300
@@ -559,6 +561,61 @@ def test_floww_watchdog_fallback(monkeypatch, segments):
         hg.run_consensus()
         _compare(o, hg, f"watchdog fallback, events [0, {hi})")
         assert hg.profile_kernel() == "k_la_sweep"
+
+
+@pytest.mark.parametrize("segments", [None, 8])
+@pytest.mark.parametrize("kernel", ["k_flow32x2", "k_flow32"])
+def test_flow32_variants(monkeypatch, kernel, segments):
+    """The two-value dataflow (k_flow32x2, the default at n <= 128: a
+    workgroup carries two LA columns, or a column and LT) and the one-value
+    k_flow32 it falls back to for chains past 131,008 events (BH_FLOW1=1
+    forces it), whole and through 8 segments: n = 128 (65 workgroups with
+    LT inside; k_flow32: LT after the next segment's columns), n = 127 (an
+    even value count: no single-column workgroup), n = 64 lagging, and wild
+    DAGs whose parents fall far behind the 64-slot rings."""
+    if kernel == "k_flow32":
+        monkeypatch.setenv("BH_FLOW1", "1")
+    if segments:
+        monkeypatch.setenv("BH_SEGMENTS", str(segments))
+    for n, N, seed, lag in ((128, 80_000, 171, 0), (127, 60_000, 172, 0), (64, 60_000, 173, 21), (5, 20_000, 174, 1)):
+        hg = _random_parity(n, N, seed, lag)
+        assert hg.profile_kernel() == kernel
+        if segments:
+            assert hg.pipeline()[0] == min(segments, N // 4096 + 1)  # (segments_for)
+    _wild_parity(128, 40_000, 175, 30_000)
+    _wild_parity(33, 40_000, 176, 20_000)
+
+
+def test_flow32_long_chains():
+    """Chains past k_flow32x2's 131,008 events (11-bit generations of
+    64-slot rings) take the one-value k_flow32 (128-slot rings): a batch,
+    then per-sync calls whose chains cross the limit between calls (the
+    descriptor format changes with the kernel; each call writes its new
+    rows' entries)."""
+    from babble_amd.dag import Dag
+    from babble_amd import Hashgraph
+    n, N = 3, 420_000
+    assert int(np.bincount(Dag(n, N, 177, sig_mode=0).creator).max()) > 131_008
+    hg = _random_parity(n, N, 177, 0)
+    assert hg.profile_kernel() == "k_flow32"
+    d = Dag(2, 300_000, 178, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(2, d.participant_ids, capacity=d.N)
+    hg = Hashgraph(d.participant_ids, d.N)
+    spi, opc, opi = d.wire()
+    pid = d.participant_ids
+    opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
+    kernels = set()
+    for lo in range(0, d.N, 25_000):
+        hi = min(d.N, lo + 25_000)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi], opi[lo:hi],
+                                    d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi]).any()
+        hg.run_consensus()
+        kernels.add(hg.profile_kernel())
+        _compare(o, hg, f"n=2 per-sync, after [0, {hi})")
+    assert kernels == {"k_flow32x2", "k_flow32"}
 
 
 def test_flow64_parity(monkeypatch):
@@ -658,6 +715,7 @@ def test_segment_pipeline_wild(monkeypatch, K):
 
 
 def test_segment_pipeline_lt_fallback(monkeypatch):
+    monkeypatch.setenv("BH_FLOW1", "1")
     monkeypatch.setenv("BH_SEGMENTS", "4")
     monkeypatch.setenv("BH_FLOW_LTCLAMP", "300")
     hg = _random_parity(16, 20_000, 97, 2)

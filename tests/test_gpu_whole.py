@@ -69,7 +69,7 @@ def test_c3_whole_dag():
     (8 segments, the persistent loop), on a fresh handle and on two reruns
     after bh_reset_consensus (the bench's timed step)."""
     d, hg = _whole_digest("c3")
-    assert hg.pipeline()[0] == 8 and hg.profile_kernel() == "k_flow32"
+    assert hg.pipeline()[0] == 8 and hg.profile_kernel() == "k_flow32x2"
     assert hg.loop_stats() == (8 * 3, 0)  # one persistent loop per segment and run, no fallback
     invariants(d, hg)
 
