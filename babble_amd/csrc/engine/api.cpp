@@ -59,8 +59,7 @@ void free_all(bh_handle *h) {
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
-  if (h->stream3) (void)hipStreamDestroy(h->stream3);
-  for (auto &e : h->lt_ev)
+  for (auto &e : h->loop_evs)
     if (e) (void)hipEventDestroy(e);
   for (auto &g : h->seg_graph)
     if (g) (void)hipGraphExecDestroy(g);
@@ -1012,28 +1011,33 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   auto coords = [&](int k) -> int {
     if (sp) return receive(k);
     Dev v = view(k);
-    if (h->lt_ev_live[k & 1]) {  // the LT of segment k - 2 still reads this segbuf half
-      HIPCHK(h, hipStreamWaitEvent(sc, h->lt_ev[k & 1], 0));
-      h->lt_ev_live[k & 1] = false;
-    }
-    int32_t *stg = h->seg_stage + (size_t)(k & 1) * 2 * n;
+    // pinned staging of its own per segment: with the loops enqueued without
+    // host waits (async below) the host runs ahead of these copies
+    int32_t *stg = h->seg_stage + (size_t)k * 2 * n;
     lens_at(Ns[(size_t)k], stg);
     lens_at(Ns[(size_t)k + 1], stg + n);
     HIPCHK(h, hipMemcpyAsync(v.seg_lo, stg, (size_t)2 * n * 4, hipMemcpyHostToDevice, sc));
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sc));  // the segment's lengths are on the device
-    // the 64-row tiles holding the segment's rows: each chain's run
-    // [start + lo, start + hi), in layout order, shared boundary tiles once
-    int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
-    int64_t nt = 0;
-    for (int c = 0; c < n; ++c) {
-      if (stg[n + c] <= stg[c]) continue;
-      const int64_t a = ((int64_t)h->cstart_h[(size_t)c] + stg[c]) >> 6, b = ((int64_t)h->cstart_h[(size_t)c] + stg[n + c] - 1) >> 6;
-      for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
+    if (eager) {
+      // the 64-row tiles holding the segment's rows (the transpose's work
+      // list): each chain's run [start + lo, start + hi), in layout order,
+      // shared boundary tiles once (eager runs wait for each loop: the
+      // staging's two halves cannot be overtaken)
+      int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
+      int64_t nt = 0;
+      for (int c = 0; c < n; ++c) {
+        if (stg[n + c] <= stg[c]) continue;
+        const int64_t a = ((int64_t)h->cstart_h[(size_t)c] + stg[c]) >> 6, b = ((int64_t)h->cstart_h[(size_t)c] + stg[n + c] - 1) >> 6;
+        for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
+      }
+      int32_t *dtl = h->tlist + (size_t)(k & 1) * h->tlist_cap;
+      if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
+      v.tile_list = dtl;
+      v.ntiles = nt;
+    } else {
+      v.tile_list = nullptr;
+      v.ntiles = 0;
     }
-    int32_t *dtl = h->tlist + (size_t)(k & 1) * h->tlist_cap;
-    if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
-    v.tile_list = dtl;
-    v.ntiles = nt;
     // a whole-DAG wide run takes the whole-layout transpose (32-row tiles,
     // several workgroups per compute unit) instead of 64-row tile lists
     if (wide && K == 1 && base == 0) v.tile_list = nullptr;
@@ -1079,13 +1083,27 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));  // the coordinate pipeline's end
     return BH_OK;
   };
+  // n <= 128 with the persistent loop: every segment's loop is enqueued
+  // without a host round trip (each used to wait for its loop's state: ~0.2
+  // ms of idle device per segment at C3, profiles/r5_gaps_c3.txt).  The
+  // resume point reads the round count on the device, a failed loop makes
+  // the later ones leave at once (ST_PFAIL), and the host reads the state
+  // once, after the last loop.  Other loops (wide, one launch per round,
+  // BH_SEG_DEBUG) wait for each segment as before
+  static const bool dbg = getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG"));  // per-segment timings to stderr
+  const bool async = !wide && !eager && !dbg && bh::round_persist_eligible(d);
+  HIPCHK(h, hipMemsetAsync(d.state + bh::ST_PFAIL, 0, 4, sr));
+  if (async && (int)h->loop_evs.size() < 2 * K) {
+    for (int i = (int)h->loop_evs.size(); i < 2 * K; ++i) {
+      hipEvent_t e;
+      HIPCHK(h, hipEventCreate(&e));
+      h->loop_evs.push_back(e);
+    }
+  }
   if ((rc = coords(0))) return rc;
   int32_t st[bh::ST_COUNT];
   hipEvent_t sr_mark;  // the loop stream's progress, for segbuf reuse by stream2
   HIPCHK(h, hipEventCreateWithFlags(&sr_mark, hipEventDisableTiming));
-  // BH_SEG_DEBUG=1: per-segment timings to stderr; BH_SEG_SERIAL=1: no overlap (A/B)
-  static const bool dbg = getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG"));
-  static const bool serial = getenv("BH_SEG_SERIAL") && atoi(getenv("BH_SEG_SERIAL"));
   hipEvent_t lt0 = nullptr, lt1 = nullptr;
   if (dbg) {
     HIPCHK(h, hipEventCreate(&lt0));
@@ -1094,20 +1112,19 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   bool wd_fired = false;
   for (int k = 0; k < K; ++k) {
     HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * k], 0));
-    if (serial) HIPCHK(h, hipStreamSynchronize(sr));
-    if (wide || sp) {
+    if ((wide || sp) && !async) {
       // k_floww2's watchdog (ST_FLOWOVF = 2; the split: a block that ran out
-      // of overflow slots) is read before a loop runs on
-      // the segment: a loop over unfinished coordinates could fail ("did not
-      // terminate", capacity) before the fallback below is reached.  One
-      // host synchronisation per segment; a wide batch runs one segment
+      // of overflow slots) is read before a loop runs on the segment: a loop
+      // over unfinished coordinates could fail ("did not terminate",
+      // capacity) before the fallback below is reached.  One host
+      // synchronisation per segment; a wide batch runs one segment.  (The
+      // persistent n <= 128 loop leaves at once on the flag itself.)  Every
+      // segment's receive is still posted, so no coordinate rank's send is
+      // left unmatched
       int32_t *ovf = h->pinned_state + bh::ST_COUNT + 4;
       HIPCHK(h, hipMemcpyAsync(ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, sr));
       HIPCHK(h, hipStreamSynchronize(sr));
-      if (*ovf == 2) {
-        wd_fired = true;
-        break;
-      }
+      if (*ovf == 2) wd_fired = true;
     }
     if (k + 1 < K) {
       // segment k + 1 reuses the segbuf parity of k - 1, last read by its
@@ -1116,9 +1133,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       HIPCHK(h, hipStreamWaitEvent(sc, sr_mark, 0));
       if ((rc = coords(k + 1))) { (void)hipEventDestroy(sr_mark); return rc; }
     }
+    if (wd_fired) continue;  // (the remaining segments' receives are posted above)
     Dev rv = d;  // the loop's view: only the prefix lengths differ from d
     rv.chain_len = view(k).chain_len;
-    if (serial) HIPCHK(h, hipStreamSynchronize(sc));
     if (dbg) HIPCHK(h, hipEventRecord(lt0, sr));
     if (k == 0 && base == 0) {
       bh::launch_round_init(rv, sr);
@@ -1140,8 +1157,14 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       }
       bh::launch_round_resume(rv, sr);
     }
-    if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], &h->seg_graph_s[k & 1],
-                             &h->seg_graph_dev_s[k & 1], st))) {
+    if (async) {
+      HIPCHK(h, hipEventRecord(h->loop_evs[(size_t)2 * k], sr));
+      ++h->persist_loops;
+      bh::launch_round_persist(rv, sr);
+      HIPCHK(h, hipGetLastError());
+      HIPCHK(h, hipEventRecord(h->loop_evs[(size_t)2 * k + 1], sr));
+    } else if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], &h->seg_graph_s[k & 1],
+                                    &h->seg_graph_dev_s[k & 1], st))) {
       (void)hipEventDestroy(sr_mark);
       return rc;
     }
@@ -1151,7 +1174,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * K + k + 1], 0));
       next_len = view(k + 1).chain_len;
     }
-    bh::launch_resume_point(rv, st[bh::ST_ROUNDS], next_len, sr);
+    bh::launch_resume_point(rv, async ? -1 : st[bh::ST_ROUNDS], next_len, sr);
     if (dbg) {
       HIPCHK(h, hipEventRecord(lt1, sr));
       HIPCHK(h, hipStreamSynchronize(sr));
@@ -1168,6 +1191,32 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   if (lt0) (void)hipEventDestroy(lt0);
   if (lt1) (void)hipEventDestroy(lt1);
   (void)hipEventDestroy(sr_mark);
+  if (async) {  // every loop's end: one host synchronisation for the call
+    HIPCHK(h, copy_sync(sr, st, d.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
+    static const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
+    float lms = 0;
+    for (int k = 0; loop_timing && k < K; ++k)
+      if (hipEventElapsedTime(&lms, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]) == hipSuccess)
+        h->loop_ms_acc += lms;
+    const int32_t fail = std::max(st[bh::ST_PFAIL], st[bh::ST_ERR]);
+    if (fail == 1 || (fail == 0 && st[bh::ST_FLOWOVF] != 2 && !st[bh::ST_DONE]))
+      return h->fail(fail == 1 ? BH_ERR_CAPACITY : BH_ERR_STATE,
+                     fail == 1 ? "round table capacity exceeded" : "round loop did not terminate");
+    if (fail == 3) {
+      // a grid barrier gave up (some workgroup was never placed): the whole
+      // call again through the unpipelined passes, one loop launch per
+      // iteration (counted in persist_fallbacks)
+      ++h->persist_fallbacks;
+      h->inc_valid = false;
+      h->segments_used = 1;
+      HIPCHK(h, hipStreamSynchronize(sc));
+      const int32_t keep = d.round_persist;
+      d.round_persist = 0;
+      if (!(rc = rounds_coords(h))) rc = rounds_loop(h);
+      d.round_persist = keep;
+      return rc;
+    }
+  }
   if ((wide || sp) && (wd_fired || st[bh::ST_FLOWOVF] == 2)) {
     // k_floww2's watchdog left a segment's coordinates unfinished (or a
     // split block could not carry its columns): the whole DAG again through
@@ -1800,18 +1849,13 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
       if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
         rc = BH_ERR_DEVICE;
     }
-    // the segments' Lamport timestamps (rounds_pipelined, lt_mode 2)
-    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking, lo_pri) != hipSuccess)
-      rc = BH_ERR_DEVICE;
-    for (auto &e : h->lt_ev)
-      if (rc == BH_OK && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = BH_ERR_DEVICE;
     hipDeviceProp_t prop;
     if (rc == BH_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) h->ncu = prop.multiProcessorCount;
   }
   if (rc == BH_OK) rc = dalloc(h, &h->seg_zero, (size_t)n);
   if (rc == BH_OK) rc = dalloc(h, &h->segbuf, (size_t)4 * n);
   if (rc == BH_OK && hipMemset(h->seg_zero, 0, (size_t)n * 4) != hipSuccess) rc = BH_ERR_DEVICE;
-  if (rc == BH_OK && hipHostMalloc((void **)&h->seg_stage, (size_t)4 * n * 4, hipHostMallocDefault) != hipSuccess)
+  if (rc == BH_OK && hipHostMalloc((void **)&h->seg_stage, (size_t)2 * 64 * n * 4, hipHostMallocDefault) != hipSuccess)
     rc = BH_ERR_DEVICE;
   d.seg_lo = h->seg_zero;
   d.e0 = 0;

@@ -40,7 +40,7 @@ enum StateSlot {
   ST_P = 5,        // processed prefix: rounds [0, P) are decided and ordered
   ST_NCONS = 6,    // consensus events (int32 ok: < 2^31)
   ST_ITERS = 7,    // round-loop iterations executed
-  ST_FLAGGED = 8,  // candidates that needed the exact witness resolution
+  ST_PFAIL = 8,    // sticky within a DivideRounds call: a segment's loop failed (1 capacity, 3 barrier gave up)
   ST_NBLOCKS = 9,
   ST_FLOWOVF = 10,  // k_flow32: a Lamport timestamp reached 2^21 (LT recomputed by k_flow)
   ST_RESUME = 11,   // k_resume_point: the last round whose boundaries B[r][*] a prefix run fixed

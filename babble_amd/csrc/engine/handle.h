@@ -98,13 +98,11 @@ struct bh_handle {
   // segment pipeline: coordinates of prefix s + 1 on
   // stream2 while the round loop runs prefix s on `stream`
   hipStream_t stream2 = nullptr;
-  hipStream_t stream3 = nullptr;              // the segments' Lamport timestamps (lt_mode 2)
-  hipEvent_t lt_ev[2] = {nullptr, nullptr};    // a segment's LT done, by segbuf half
-  bool lt_ev_live[2] = {false, false};         // ... and not yet waited for
+  std::vector<hipEvent_t> loop_evs;            // around each segment's loop launch (rounds_pipelined, async)
   int ncu = 256;                               // compute units of the device
   int32_t *seg_zero = nullptr;   // [n] zeros: seg_lo of a one-segment view
   int32_t *segbuf = nullptr;     // [2 parities][lo, len][n]
-  int32_t *seg_stage = nullptr;  // pinned staging of segbuf, same layout
+  int32_t *seg_stage = nullptr;  // pinned staging of the segments' [lo, len] rows, one per segment (<= 64)
   hipGraphExec_t seg_graph[2] = {nullptr, nullptr}, seg_graph_s[2] = {nullptr, nullptr};
   Dev seg_graph_dev[2]{}, seg_graph_dev_s[2]{};
   std::vector<hipEvent_t> seg_ev;  // per segment: coordinates done, k_flow32 start / end

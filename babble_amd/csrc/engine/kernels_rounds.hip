@@ -1701,6 +1701,18 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   __shared__ int32_t sh_fail;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x, G = gridDim.x;
+  // the segment pipeline enqueues every segment's loop without a host round
+  // trip: after a failed one (ST_PFAIL: capacity, or a barrier that gave up)
+  // or unfinished coordinates (ST_FLOWOVF = 2: a split block without room),
+  // the later ones leave at once -- every workgroup reads the same words,
+  // written before the launch -- and the host falls back after the last
+  if (d.state[ST_PFAIL] || d.state[ST_FLOWOVF] == 2) {
+    if (c == 0 && t == 0) {
+      d.state[ST_DONE] = 1;
+      signal_done(d);
+    }
+    return;
+  }
   // BH_ROUND_PRIO (A/B): a loop workgroup that shares its compute unit with
   // a coordinate workgroup takes the issue arbitration back from the older
   // waves beside it
@@ -2436,6 +2448,7 @@ void launch_round_solo(const Dev &d, hipStream_t s) {
 // closed form's first round (a Reset hashgraph's r0, else 0).
 __global__ __launch_bounds__(1024) void k_resume_point(Dev d, int32_t R, const int32_t *next_len) {
   __shared__ int32_t m;
+  if (R < 0) R = d.state[ST_ROUNDS];  // (a loop the host did not wait for)
   if (threadIdx.x == 0) m = R;
   __syncthreads();
   for (int q = threadIdx.x; q < d.n; q += blockDim.x) {
@@ -2471,6 +2484,8 @@ __global__ __launch_bounds__(256) void k_round_resume(Dev d) {
   if (b < len && !d.fd_cols && !d.wide_cols && d.cand16 && !d.fd_rows)
     gather_cand16(d, (int64_t)cs + b, d.cand16 + (int64_t)c * ((d.npad + 7) / 8 * 4));
   if (c == 0 && threadIdx.x == 0) {
+    // the previous segment's failure stays visible to the host (ST_PFAIL)
+    d.state[ST_PFAIL] = max(d.state[ST_PFAIL], d.state[ST_ERR]);
     d.state[ST_CUR0] = r0;
     d.state[ST_CUR0 + 1] = 0;
     d.state[ST_DONE] = 0;

@@ -843,11 +843,20 @@ def test_round2_persistent_fallback(monkeypatch, n, N, seed, lag, K):
     assert loops >= 1 and fallbacks >= 1
 
 
-def test_round2_persistent_incremental(monkeypatch):
+@pytest.mark.parametrize("fallback", [False, True])
+def test_round2_persistent_incremental(monkeypatch, fallback):
+    """Per-sync calls through the persistent loop; with fallback, every
+    segment's barrier gives up (BH_PBAR_SPIN=0): the loops after the first
+    failed one leave at once (ST_PFAIL), and each call is recomputed whole
+    with one launch per iteration -- state equal to the oracle's after every
+    call either way."""
     from babble_amd import Hashgraph
     from babble_amd.dag import Dag
     from test_gpu_schedule import _wire_batches
     monkeypatch.setenv("BH_ROUND_PERSIST", "1")
+    if fallback:
+        monkeypatch.setenv("BH_PBAR_SPIN", "0")
+        monkeypatch.setenv("BH_SEGMENTS", "3")
     n, N, step = 96, 40_000, 5_000
     d = Dag(n, N, 0xC6, lagging=3, sig_mode=0)
     args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
@@ -861,6 +870,7 @@ def test_round2_persistent_incremental(monkeypatch):
         assert not np.asarray(hg.insert_events(*batch(lo, hi))).any()
         hg.run_consensus()
         _compare(o, hg, f"persistent after [0, {hi})")
+    assert (hg.loop_stats()[1] > 0) == fallback
 
 
 @pytest.mark.parametrize("n,N,seed,lag,K", [(64, 40_000, 0xBD, 21, 4), (128, 60_000, 0xBE, 40, 3)])
