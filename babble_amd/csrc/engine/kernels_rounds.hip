@@ -1295,6 +1295,10 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
   const int32_t r = from_resume ? d.state[ST_RESUME] : 0;
   const int32_t b = from_resume ? d.B[(int64_t)r * d.n + c] : 0;
   if (t == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
+  if (d.fd_cols) {  // k_round2p's parity-1 hand-off slots: tag 0, which its iteration 1 does not accept
+    for (int i = t; i < d.npad; i += blockDim.x) d.candfd[((int64_t)d.n + c) * d.npad + i] = 0;
+    if (t == 0) d.Bp[d.n + c] = 0;
+  }
   if (b >= d.chain_len[c]) return;  // no candidate on chain c
   if (d.cla && t < d.npad)  // the candidate's LA row (fame)
     d.cla[cla_row(d, c, r) * d.npad + t] =
@@ -1700,7 +1704,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   __shared__ int32_t hist[HW + 1];
   __shared__ int32_t sh_fail;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
-  const int c = blockIdx.x, G = gridDim.x;
+  const int c = blockIdx.x;
   // the segment pipeline enqueues every segment's loop without a host round
   // trip: after a failed one (ST_PFAIL: capacity, or a barrier that gave up)
   // or unfinished coordinates (ST_FLOWOVF = 2: a split block without room),
@@ -1750,31 +1754,70 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   };
   own_loads();
   if (t == 0) sh_fail = 0;
-  // the grid barrier (pbar_register / _arrive / _wait / _counts: one counter,
-  // or XCD-hierarchical from 64 workgroups up)
-  const int xcc = t == 0 ? pbar_register(d) : 0;
-  int32_t gx = 0, nx = 0;  // workgroups on this XCD, XCDs with workgroups (read after the first barrier)
   if (npad > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
     for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
   int p = 0;
+  // a candidate piece's dwords all carry tag `want` in their top byte
+  auto tagged = [](int4 v, uint32_t want) {
+    const uint32_t an = (uint32_t)(v.x & v.y & v.z & v.w) >> 24, o = (uint32_t)(v.x | v.y | v.z | v.w) >> 24;
+    return an == want && o == want;
+  };
+  constexpr uint32_t VMASK24 = 0xFFFFFFu;  // value bits of a handed-over dword (0xFFFFFF: FD_NONE)
   for (int it = 0;; ++it) {
-    // BH_DIAG timeline (tools/timeline.py): iteration start (released),
-    // window staged, search done, hand-off issued -- rounds TL_R0 .. + TL_NR
+    // BH_DIAG timeline (tools/timeline.py): iteration start (inputs current),
+    // window staged, search done, hand-off stored -- rounds TL_R0 .. + TL_NR
     const bool dgt = d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
-    const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
-    unsigned long long rt1 = 0, rt2 = 0;
-    // round r's candidates: boundaries and FD rows, stored by other workgroups
-    const int32_t bq = q < n ? __hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    // round r's candidates: boundaries (Bp) and FD rows (candfd), stored by
+    // the other workgroups at the end of round r - 1 as self-validating
+    // dwords -- tag `it` & 255 (the launch's iteration) in the top byte, the
+    // value below it -- with no barrier: a lane reloads until every dword it
+    // needs carries the tag (MI355X_MICROARCH.md, data-tagged granules: one
+    // hop instead of a flag or a grid barrier and the loads behind it).  An
+    // iteration's buffer (parity p) last held iteration it - 2's rows, whose
+    // tag differs, and no workgroup writes it again before every workgroup
+    // has published iteration it + 1's -- i.e. has finished reading this
+    // one's.  Iteration 0's inputs were written before the launch (untagged
+    // values, top byte 0 or 0x7F: the same decode), and k_cand_rows zeroed
+    // parity 1 (tag 0), which iteration 1 must not take for its own
+    const uint32_t want = (uint32_t)it & 0xFFu;
+    uint32_t bqr = 0;
     int4 f[PPL];
-    {
-      const int32_t row0 = (int32_t)(((int64_t)p * n + min(q, n - 1)) * npad * 4);
+    const int32_t row0 = (int32_t)(((int64_t)p * n + min(q, n - 1)) * npad * 4);
+    auto load_in = [&]() {
+      bqr = q < n ? (uint32_t)__hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 #pragma unroll
       for (int u = 0; u < PPL; ++u) {
         const int pc = part + LPC * ((u + rot) & (PPL - 1));
-        f[u] = pc < q4 ? __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * pc, 0, 16))
+        // (sc1, and volatile -- bit 31 -- so the poll below reloads)
+        f[u] = pc < q4 ? __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * pc, 0,
+                                                                                         (int)0x80000010u))
                        : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
       }
+    };
+    load_in();
+    if (it > 0) {
+      for (int32_t spin = 0;; ++spin) {
+        bool ok = q >= n || (bqr >> 24) == want;
+        if (ok && q < n && (int32_t)(bqr & VMASK24) < lq) {  // a live candidate: its row as well
+#pragma unroll
+          for (int u = 0; u < PPL; ++u)
+            ok &= part + LPC * ((u + rot) & (PPL - 1)) >= q4 || tagged(f[u], want);
+        }
+        if (__all(ok)) break;
+        if (spin >= d.pbar_spin) {  // a workgroup never published: the host falls back
+          sh_fail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (!ok) load_in();
+      }
     }
+    const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long rt1 = 0, rt2 = 0;
+    const int32_t bq = (int32_t)(bqr & VMASK24);
+#pragma unroll
+    for (int u = 0; u < PPL; ++u)
+      f[u] = make_int4(f[u].x & VMASK24, f[u].y & VMASK24, f[u].z & VMASK24, f[u].w & VMASK24);
     const bool act = q < n && bq < lq;
     const int off = (cs + k0) & 3;
     const int rows = min(HWL - off, max(0, len - k0));
@@ -1787,6 +1830,15 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     if (t < 16) cntk[t] = 0;
     if (t <= HW) hist[t] = 0;
     __syncthreads();
+    if (sh_fail) {
+      if (t == 0) {
+        d.state[ST_ERR] = 3;
+        d.state[ST_ROUNDS] = r;
+        d.state[ST_DONE] = 1;
+        if (c == 0) signal_done(d);
+      }
+      break;
+    }
     if (dgt) rt1 = __builtin_amdgcn_s_memrealtime();
     auto ss_row = [&](const int4 *x4) {
       int4 x[PPL];
@@ -1896,15 +1948,18 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       }
       break;
     }
-    // ---- hand-off: FD[(c, result)][i] ----
+    // ---- hand-off: FD[(c, result)][i] and B[r + 1][c], tagged it + 1 ----
+    const uint32_t tagw = (uint32_t)((it + 1) & 0xFF) << 24;
     int32_t fdv = FD_NONE;
     if (result < len) {
       fdv = hand_entry(colc, hin, t >> 3, c, result);
       if ((t & 7) == 0 && (t >> 3) < npad)
-        __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + (t >> 3), fdv, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + (t >> 3),
+                           (int32_t)(tagw | ((uint32_t)fdv & VMASK24)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (t == 0) __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, result, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0)
+      __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     if (dgt && c < 128) {
       unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
       tl[0] = rt0;
@@ -1912,16 +1967,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       tl[2] = rt1;
       tl[3] = __builtin_amdgcn_s_memrealtime();
     }
-    // ---- grid barrier ----  (BH_DIAG phases: end, arrived, loads issued, released)
-    unsigned long long *tlb = dgt ? d.diag + DG_TLB + ((int64_t)(r - TL_R0) * 512 + c) * 4 : nullptr;
-    if (dgt) tlb[0] = __builtin_amdgcn_s_memrealtime();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
-    __syncthreads();
-    if (t < 64) pbar_arrive(d, it, xcc, gx, G, nx);
-    if (dgt) tlb[1] = __builtin_amdgcn_s_memrealtime();
     // what no workgroup reads inside the loop -- fame's inputs (the new
-    // candidate's LA row and its ballots) and the round table -- is stored
-    // after the arrival, so the drain above waits only for the hand-over
+    // candidate's LA row and its ballots) and the round table
     if (result < len) {
       if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
       if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
@@ -1931,23 +1978,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     p ^= 1;
     k0 = result;
     hin.j0 = result < len ? fdv : FD_NONE;
-    own_loads();  // lands during the wait
-    if (dgt) tlb[2] = __builtin_amdgcn_s_memrealtime();
-    if (t == 0) {
-      if (!pbar_wait(d, it, G)) sh_fail = 1;
-      if (it == 0) pbar_counts(d, xcc, gx, nx);
-    }
-    if (dgt) tlb[3] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
-    if (sh_fail) {
-      if (t == 0) {
-        d.state[ST_ERR] = 3;
-        d.state[ST_ROUNDS] = r;
-        d.state[ST_DONE] = 1;
-        if (c == 0) signal_done(d);
-      }
-      break;
-    }
+    own_loads();  // the next window and hand-off rows: they land while the candidates are awaited
+    __syncthreads();  // (the window, cntk and hist are rewritten next)
   }
 }
 
@@ -2003,7 +2035,6 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
 void launch_round_persist(const Dev &d, hipStream_t s) {
   const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
-  (void)hipMemsetAsync(d.pbar, 0, (size_t)PBAR_INTS * 4, s);  // (the barrier's lines; 16-B multiple from the allocation's start)
   if (d.npad <= 32) k_round2p<1><<<d.n, nt, lds, s>>>(d);
   else if (d.npad <= 64) k_round2p<2><<<d.n, nt, lds, s>>>(d);
   else k_round2p<4><<<d.n, nt, lds, s>>>(d);

@@ -54,14 +54,19 @@ def sum_over_ranks(x, dist=None):
 
 def _pmc_table(n, N):
     """Per-kernel PMC HBM bytes of this config (tools/pmc.sh ->
-    tools/pmc_summary.py -> profiles/pmc_traffic.json), or {}."""
+    tools/pmc_summary.py -> profiles/pmc_traffic.json) and the commit they
+    were measured at, or ({}, None).  bench.py cannot read PMC counters
+    itself (rocprofv3 --pmc runs the program under the profiler), so the
+    line names the table it quotes."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             tab = json.load(f)
     except (OSError, ValueError):
-        return {}
+        return {}, None
     cfg = tab.get(f"n{n}_N{N}", {})
-    return cfg if all("hbm_bytes_per_step" in v for v in cfg.values()) else {}
+    meta = (tab.get("_meta") or {}).get(f"n{n}_N{N}")
+    ok = all(isinstance(v, dict) and "hbm_bytes_per_step" in v for v in cfg.values())
+    return (cfg if ok else {}), meta
 
 
 def _parallelism(world, n):
@@ -213,7 +218,11 @@ def main():
     npad = (n + 3) & ~3
     stages = dict(zip(["coordinates", "rounds", "fame", "round_received", "order", "exchange"],
                       (stage_tot / args.steps).round(3).tolist()))
-    pmc = _pmc_table(n, N)
+    pmc, pmc_meta = _pmc_table(n, N)
+    # the table holds THIS build's kernels only if it names the coordinate
+    # kernel this run timed (a table of an older build reads as no table)
+    if pmc and hg.profile_kernel() not in pmc:
+        pmc, pmc_meta = {}, None
     # roofline: the path is integer and
     # HBM-bound; algorithmic bytes per ordered event B(n) = 12n + 96 (two
     # parent LA rows read, own row written, per-event scalars, sort key and
@@ -221,34 +230,52 @@ def main():
     B = 12 * n + 96
     achieved = value * B / 1e9
     traffic_step = sum(v["hbm_bytes_per_step"] for v in pmc.values()) if pmc else None
-    # the dominant kernel: the round loop, timed live by HIP events around it
-    # (stage 7).  Persistent (the default): n <= 128 k_round2p, one launch per
-    # pipeline segment running all of that segment's rounds; n <= 512
-    # k_round_wide<..., true>, one launch per call (N / launches events per
-    # launch).  Otherwise one k_round2 / k_round_wide launch per round
+    traffic_source = ("profiles/pmc_traffic.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (FETCH_SIZE x 2 + "
+                      f"WRITE_SIZE) of this config, measured at commit {pmc_meta.get('commit') if pmc_meta else '?'}"
+                      if pmc else "none: profiles/pmc_traffic.json holds no table of this build's kernels for "
+                                  "this config")
+    # the round loop, timed live by HIP events around each launch on the
+    # loop's stream (stage 7).  Persistent (the default): n <= 128 k_round2p,
+    # one launch per pipeline segment running all of that segment's rounds;
+    # n <= 512 k_round_wide<..., true>, one launch per call.  Otherwise one
+    # k_round2 / k_round_wide launch per round
     persistent = persist_per_step > 0
     if npad <= 128:
         round_kernel = "k_round2p" if persistent else "k_round2"
     else:
         round_kernel = "k_round_wide"
-    # the loop's own device time (stage 7): with the segment pipeline the
-    # rounds stage [1] only counts what runs after the coordinates
+    segments = hg.pipeline()[0]
     loop_ms = float(stage_tot[7] / args.steps) if len(stage_tot) > 7 else 0.0
     if loop_ms <= 0:  # (BH_LOOP_TIMING=0: the rounds stage instead)
         loop_ms = float(stage_tot[1] / args.steps)
     iter_us = 1000.0 * loop_ms / max(iters, 1)
-    launches = persist_per_step if persistent else iters
-    round_avg_ms = loop_ms / max(launches, 1e-9)
-    ev_per_launch = N / max(launches, 1e-9)
-    dom_alg = ev_per_launch * B
-    dom_achieved = dom_alg / (round_avg_ms * 1e-3) / 1e9
-    dom = pmc.get(round_kernel) if pmc else None
-    # the L2-level view of the same kernel (round 1's figure): each of the n
-    # workgroups streams every candidate's FD row and its 32-row LA / FD
-    # windows from L2 / MALL -- not HBM bytes, reported under its own key
-    l2_bytes = n * (n * npad * 4 + 2 * 32 * npad * 4)
-    sweep_avg_ms = float(np.mean(sweep_ms))
+    loop_launches = persist_per_step if persistent else iters
+    loop_alg = ordered * B  # the loop orders every event once: B(n) per event over its launches
+    loop_obj = {"kernel": round_kernel, "launches_per_step": loop_launches, "device_ms_per_step": loop_ms,
+                "avg_launch_ms": loop_ms / max(loop_launches, 1e-9),
+                "alg_bytes_per_launch": loop_alg / max(loop_launches, 1e-9),
+                "achieved": loop_alg / (loop_ms * 1e-3) / 1e9, "frac": loop_alg / (loop_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "round_iterations": iters, "us_per_iteration": iter_us,
+                "traffic_per_launch": (pmc.get(round_kernel) or {}).get("hbm_bytes_per_launch"),
+                "note": "latency-bound: the rounds are a serial chain; one persistent launch per pipeline "
+                        "segment (k_round2p: workgroups hand each other the candidates' rows as data-tagged "
+                        "dwords) or per call (k_round_wide: a grid barrier per round)"}
+    # the coordinate kernel: the sum of its launches per step (one per
+    # segment; k_flow32x2 carries LT inside them), HIP events on the
+    # coordinate stream around each launch
+    coord_ms = float(np.mean(sweep_ms))
+    coord_launches = segments if hg.profile_kernel() in ("k_flow32x2", "k_flow32", "k_floww2", "k_floww") else 1
     coord_alg = N * (12 * n + 12)
+    coord_obj = {"kernel": hg.profile_kernel(), "launches_per_step": coord_launches, "device_ms_per_step": coord_ms,
+                 "avg_launch_ms": coord_ms / max(coord_launches, 1),
+                 "alg_bytes_per_launch": coord_alg / max(coord_launches, 1),
+                 "achieved": coord_alg / (coord_ms * 1e-3) / 1e9,
+                 "frac": coord_alg / (coord_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 "traffic_per_launch": (pmc.get(hg.profile_kernel()) or {}).get("hbm_bytes_per_launch"),
+                 "note": "LA columns and Lamport timestamps (12n + 12 B per event); bound by the DAG's critical "
+                         "path x per-step issue, not bandwidth"}
+    # the dominant kernel: the larger device-time share of the step
+    dom = loop_obj if loop_ms >= coord_ms else coord_obj
     out = {
         "metric": METRIC,
         "value": value,
@@ -269,32 +296,20 @@ def main():
                    "rounds": stats.last_round + 1, "blocks": stats.blocks,
                    "parallelism": _parallelism(world, n) if sharded else
                                   (f"replicas x{world}" if world > 1 else "1 GPU")},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_step,
-                     "scope": "whole step: events ordered/s x B(n), SURVEY 8(d)",
-                     "alg_bytes_per_event": B, "alg_bytes_per_step": ordered * B,
-                     "traffic_total_note": "PMC HBM bytes of every kernel of one step "
-                                           "(profiles/pmc_traffic.json; FETCH_SIZE x 2 + WRITE_SIZE)",
-                     "dominant_kernel": {
-                         "kernel": round_kernel, "launches": launches, "avg_launch_ms": round_avg_ms,
-                         "round_iterations": iters, "us_per_iteration": iter_us,
-                         "events_per_launch": ev_per_launch, "alg_bytes_per_launch": dom_alg,
-                         "achieved": dom_achieved, "frac": dom_achieved / HBM_PEAK_GBS,
-                         "traffic": dom["hbm_bytes_per_launch"] if dom else None,
-                         "note": "latency-bound: rounds are a serial chain, a grid barrier per round inside "
-                                 "one persistent launch per segment (k_round2p) or per call (k_round_wide)"},
-                     "l2_level": {"kernel": round_kernel, "bytes_per_iteration": l2_bytes,
-                                  "GBps": l2_bytes / (iter_us * 1e-6) / 1e9,
-                                  "note": "candidate FD rows + LA/FD windows re-read by every workgroup "
-                                          "from L2/MALL; not HBM traffic"}},
-        "roofline_coordinates": {"kernel": hg.profile_kernel(), "avg_launch_ms": sweep_avg_ms,
-                                 "alg_bytes_per_launch": coord_alg,
-                                 "achieved": coord_alg / (sweep_avg_ms * 1e-3) / 1e9,
-                                 "traffic": (pmc.get(hg.profile_kernel()) or {}).get("hbm_bytes_per_launch"),
-                                 "note": "bound by the DAG's critical path x per-step issue, not bandwidth"},
+        # the dominant kernel's roofline (per launch), then the whole step's
+        "roofline": {"bound": "hbm", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic_per_launch"],
+                     "alg_bytes_per_launch": dom["alg_bytes_per_launch"], "avg_launch_ms": dom["avg_launch_ms"],
+                     "chosen_by": f"device time per step: loop {loop_ms:.2f} ms, coordinates {coord_ms:.2f} ms",
+                     "traffic_source": traffic_source,
+                     "whole_step": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+                                    "alg_bytes_per_event": B, "alg_bytes_per_step": ordered * B,
+                                    "traffic": traffic_step,
+                                    "scope": "events ordered/s x B(n), SURVEY 8(d)"},
+                     "loop": loop_obj, "coordinates": coord_obj},
         "stages_ms": stages,
         "round_loop_iterations": iters,
-        "pipeline": {"segments": hg.pipeline()[0], "incremental_calls": hg.pipeline()[1]},
+        "pipeline": {"segments": segments, "incremental_calls": hg.pipeline()[1]},
     }
     cpu_sample = args.cpu_sample
     if cpu_sample < 0:
