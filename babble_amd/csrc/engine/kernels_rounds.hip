@@ -1794,31 +1794,12 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
                        : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
       }
     };
+    const unsigned long long rtp = dgt ? __builtin_amdgcn_s_memrealtime() : 0;  // waiting starts
+    int32_t polls = 0;
     load_in();
-    if (it > 0) {
-      for (int32_t spin = 0;; ++spin) {
-        bool ok = q >= n || (bqr >> 24) == want;
-        if (ok && q < n && (int32_t)(bqr & VMASK24) < lq) {  // a live candidate: its row as well
-#pragma unroll
-          for (int u = 0; u < PPL; ++u)
-            ok &= part + LPC * ((u + rot) & (PPL - 1)) >= q4 || tagged(f[u], want);
-        }
-        if (__all(ok)) break;
-        if (spin >= d.pbar_spin) {  // a workgroup never published: the host falls back
-          sh_fail = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        if (!ok) load_in();
-      }
-    }
-    const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
-    unsigned long long rt1 = 0, rt2 = 0;
-    const int32_t bq = (int32_t)(bqr & VMASK24);
-#pragma unroll
-    for (int u = 0; u < PPL; ++u)
-      f[u] = make_int4(f[u].x & VMASK24, f[u].y & VMASK24, f[u].z & VMASK24, f[u].w & VMASK24);
-    const bool act = q < n && bq < lq;
+    // the window first (its rows were loaded at the end of the last
+    // iteration): staged while the candidates' rows are in flight, so each
+    // wave starts its search as soon as ITS candidates' rows are current
     const int off = (cs + k0) & 3;
     const int rows = min(HWL - off, max(0, len - k0));
     if (wi < n) {
@@ -1830,16 +1811,31 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     if (t < 16) cntk[t] = 0;
     if (t <= HW) hist[t] = 0;
     __syncthreads();
-    if (sh_fail) {
-      if (t == 0) {
-        d.state[ST_ERR] = 3;
-        d.state[ST_ROUNDS] = r;
-        d.state[ST_DONE] = 1;
-        if (c == 0) signal_done(d);
+    const unsigned long long rt1 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (it > 0) {
+      for (int32_t spin = 0;; ++spin, ++polls) {
+        bool ok = q >= n || (bqr >> 24) == want;
+        if (ok && q < n && (int32_t)(bqr & VMASK24) < lq) {  // a live candidate: its row as well
+#pragma unroll
+          for (int u = 0; u < PPL; ++u)
+            ok &= part + LPC * ((u + rot) & (PPL - 1)) >= q4 || tagged(f[u], want);
+        }
+        if (__all(ok)) break;
+        if (spin >= d.pbar_spin) {  // a workgroup never published: the host falls back
+          sh_fail = 1;  // (read after the search's first workgroup barrier)
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (!ok) load_in();
       }
-      break;
     }
-    if (dgt) rt1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long rt2 = 0;
+    const int32_t bq = (int32_t)(bqr & VMASK24);
+#pragma unroll
+    for (int u = 0; u < PPL; ++u)
+      f[u] = make_int4(f[u].x & VMASK24, f[u].y & VMASK24, f[u].z & VMASK24, f[u].w & VMASK24);
+    const bool act = q < n && bq < lq;
     auto ss_row = [&](const int4 *x4) {
       int4 x[PPL];
 #pragma unroll
@@ -1874,6 +1870,15 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       }
       if (act && part == 0 && lo < rows) atomicAdd(&hist[lo], 1);
       __syncthreads();
+      if (sh_fail) {  // a workgroup never published: ST_ERR = 3, the host falls back
+        if (t == 0) {
+          d.state[ST_ERR] = 3;
+          d.state[ST_ROUNDS] = r;
+          d.state[ST_DONE] = 1;
+          if (c == 0) signal_done(d);
+        }
+        break;
+      }
       if (wave == 0) {
         int h = lane < rows ? hist[lane] : 0;
 #pragma unroll
@@ -1889,6 +1894,15 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       ssb = __ballot(act && part == 0 && res >= 0 && lo <= res);
     } else {
       __syncthreads();
+      if (sh_fail) {  // a workgroup never published: ST_ERR = 3, the host falls back
+        if (t == 0) {
+          d.state[ST_ERR] = 3;
+          d.state[ST_ROUNDS] = r;
+          d.state[ST_DONE] = 1;
+          if (c == 0) signal_done(d);
+        }
+        break;
+      }
     }
     const int nc = cntk[0];
     if (dgt) rt2 = __builtin_amdgcn_s_memrealtime();
@@ -1966,6 +1980,13 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       tl[1] = rt2;
       tl[2] = rt1;
       tl[3] = __builtin_amdgcn_s_memrealtime();
+      // the hand-over's phases (tools/timeline.py --tagged): waiting starts,
+      // inputs current, polls, this round's rows stored
+      unsigned long long *tb = d.diag + DG_TLB + ((int64_t)(r - TL_R0) * 512 + c) * 4;
+      tb[0] = rtp;
+      tb[1] = rt0;
+      tb[2] = (unsigned long long)polls;
+      tb[3] = tl[3];
     }
     // what no workgroup reads inside the loop -- fame's inputs (the new
     // candidate's LA row and its ballots) and the round table

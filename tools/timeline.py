@@ -47,6 +47,40 @@ def main(path):
     barrier(path)
 
 
+def tagged(path):
+    """k_round2p's data-tagged hand-over (round 5; BH_DIAG=1 BH_TIMELINE=file):
+    per round r and chain c, the second block holds (waiting starts, inputs
+    current, polls, rows stored).  Prints medians over rounds of: the hop
+    (the last producer's store of round r - 1 -> each consumer's inputs
+    current: first, median, last), the wait per workgroup, the work
+    (current -> stored), the store spread, polls per workgroup and the round
+    period (first current to first current)."""
+    b = np.fromfile(path, dtype=np.uint64)
+    off = TL_NR * NC * 4
+    b = b[off: off + TL_NR * 512 * 4].reshape(TL_NR, 512, 4).astype(np.int64)[:, :NC]
+    live = (b[:, :, 1] > 0) & (b[:, :, 3] > 0)
+    rows = []
+    for r in range(1, TL_NR):
+        m, mp = live[r], live[r - 1]
+        if m.sum() < 2 or mp.sum() < 2:
+            continue
+        last_store = b[r - 1, mp, 3].max()
+        cur = b[r, m, 1]
+        rows.append((cur.min() - last_store, np.median(cur - last_store), cur.max() - last_store,
+                     np.median(b[r, m, 1] - b[r, m, 0]), np.median(b[r, m, 3] - b[r, m, 1]),
+                     b[r, m, 3].max() - b[r, m, 3].min(), np.median(b[r, m, 2]), cur.min() - b[r - 1, mp, 1].min()))
+    if not rows:
+        print("no tagged stamps")
+        return
+    ns = 10.0
+    names = ["hop first", "hop median", "hop last", "wait", "work", "store spread", "polls", "round period"]
+    for i, name in enumerate(names):
+        v = [x[i] for x in rows]
+        scale = 1.0 if name == "polls" else ns / 1000
+        unit = "" if name == "polls" else " us"
+        print(f"{name:14s} median {np.median(v) * scale:6.2f}{unit}  p90 {np.percentile(v, 90) * scale:6.2f}{unit}")
+
+
 def barrier(path):
     """The persistent loops' barrier phases (second block, every chain): per
     round, drain (arrived - end), stage (staged - arrived; k_round2p: its
@@ -97,5 +131,8 @@ def barrier(path):
         print("last arriver: stage entry / fit check / window: " + " / ".join(f"{np.median(v[:, k]) * ns / 1000:.2f}" for k in range(3)) + " us")
 
 
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[1] == "--tagged":
+    tagged(sys.argv[2])
+    sys.exit(0)
 if __name__ == "__main__":
     main(sys.argv[1])
