@@ -25,7 +25,8 @@ SYMBOLS = (
     "bh_get_consensus_order", "bh_get_blocks", "bh_get_pending_rounds", "bh_get_undetermined",
     "bh_get_round_info", "bh_get_coordinates", "bh_query_events", "bh_get_stage_ms", "bh_get_profile", "bh_get_profile_kernel",
     "bh_get_pipeline", "bh_get_loop_stats", "bh_hash_bodies", "bh_verify_signatures", "bh_set_event_bytes", "bh_get_frame_roots",
-    "bh_get_frame_json", "bh_get_block_hashes", "bh_get_block_json", "bh_comm_unique_id", "bh_comm_init", "bh_shard_range",
+    "bh_get_frame_json", "bh_get_block_hashes", "bh_get_block_json", "bh_comm_unique_id", "bh_comm_init", "bh_comm_init_transport",
+    "bh_shard_range",
 )
 
 
@@ -34,6 +35,16 @@ class Config(C.Structure):
                 ("max_events", C.c_int64), ("device", C.c_int32),
                 ("n_devices", C.c_int32), ("device_ids", C.POINTER(C.c_int32)),
                 ("frames", C.c_int32)]
+
+
+# bh_transport: the caller's blocking host-memory send / recv / broadcast
+SEND_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32)
+RECV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32)
+BCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_int32)
+
+
+class Transport(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("send", SEND_FN), ("recv", RECV_FN), ("broadcast", BCAST_FN)]
 
 
 class Events(C.Structure):
@@ -130,6 +141,8 @@ def load():
     L.bh_comm_unique_id.restype = C.c_int
     L.bh_comm_init.argtypes = [P, I32, I32, VP]
     L.bh_comm_init.restype = C.c_int
+    L.bh_comm_init_transport.argtypes = [P, I32, I32, C.POINTER(Transport)]
+    L.bh_comm_init_transport.restype = C.c_int
     L.bh_shard_range.argtypes = [I64, I32, I32, C.POINTER(I64), C.POINTER(I64)]
     L.bh_shard_range.restype = None
     _LIB = L

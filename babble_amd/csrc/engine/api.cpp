@@ -72,7 +72,8 @@ void free_all(bh_handle *h) {
   if (h->seg_stage) (void)hipHostFree(h->seg_stage);
   if (h->tlist) (void)hipFree(h->tlist);
   if (h->tlist_stage) (void)hipHostFree(h->tlist_stage);
-  if (h->comm) (void)ncclCommDestroy(h->comm);
+  delete h->xport;
+  h->xport = nullptr;
   if (h->xbuf) (void)hipFree(h->xbuf);
   if (h->xseg) (void)hipFree(h->xseg);
   if (h->xbase) (void)hipFree(h->xbase);
@@ -347,15 +348,16 @@ template <class Sel>
 int exchange(bh_handle *h, Sel sel, const std::vector<size_t> &off, const std::vector<size_t> &len) {
   if (h->world <= 1) return BH_OK;
   const auto t0 = std::chrono::steady_clock::now();
-  if (h->comm) {
+  if (h->xport) {
     uint8_t *base = reinterpret_cast<uint8_t *>(sel(h));
-    if (ncclGroupStart() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupStart");
+    int rc;
+    if ((rc = h->xport->group_start(h))) return rc;
     for (int r = 0; r < h->world; ++r)
-      if (len[r] && ncclBroadcast(base + off[r], base + off[r], len[r], ncclChar, r, h->comm, h->stream) != ncclSuccess) {
-        (void)ncclGroupEnd();
-        return h->fail(BH_ERR_DEVICE, "ncclBroadcast");
+      if (len[r] && (rc = h->xport->bcast(h, base + off[r], len[r], r, h->stream))) {
+        (void)h->xport->group_end(h);
+        return rc;
       }
-    if (ncclGroupEnd() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupEnd");
+    if ((rc = h->xport->group_end(h))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
   } else {
     const size_t G = h->group.size();
@@ -847,9 +849,8 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
     const bh::SplitBlock b = p.block(x, k, x->rank, x->xbuf + off);
     bh::launch_split_pack(v, p.dpq(x, k), b, sc);
     const size_t bb = p.block_bytes(x, k, x->rank);
-    if (x->comm) {
-      if (ncclSend(x->xbuf + off, bb, ncclChar, 0, x->comm, sc) != ncclSuccess)
-        return x->fail(BH_ERR_DEVICE, "ncclSend (segment %d)", k);
+    if (x->xport) {
+      if ((rc = x->xport->send(x, x->xbuf + off, bb, 0, sc))) return rc;
     } else {
       HIPCHK(x, hipEventRecord(x->seg_ev[(size_t)k], sc));
     }
@@ -869,7 +870,7 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
 // base > 0: an incremental call -- events [0, base) hold coordinates and
 // the round loop left its resume point (ST_RESUME) for that prefix.  sp: the
 // coordinate split -- shard 0's segments arrive from the coordinate shards
-// (grp: the in-process group, else over h->comm) instead of being computed
+// (grp: the in-process group, else over h->xport) instead of being computed
 int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nullptr,
                      const std::vector<bh_handle *> *grp = nullptr) {
   int rc;
@@ -971,17 +972,18 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
         xoff += bb;
       }
     } else {
-      if (ncclGroupStart() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupStart");
+      int rc2;
+      if ((rc2 = h->xport->group_start(h))) return rc2;
       for (int r = 1; r < h->world; ++r) {
         const size_t bb = sp->block_bytes(h, k, r);
         blk[(size_t)r] = sp->block(h, k, r, h->xbuf + xoff);
-        if (ncclRecv(h->xbuf + xoff, bb, ncclChar, r, h->comm, sc) != ncclSuccess) {
-          (void)ncclGroupEnd();
-          return h->fail(BH_ERR_DEVICE, "ncclRecv (segment %d, rank %d)", k, r);
+        if ((rc2 = h->xport->recv(h, h->xbuf + xoff, bb, r, sc))) {
+          (void)h->xport->group_end(h);
+          return rc2;
         }
         xoff += bb;
       }
-      if (ncclGroupEnd() != ncclSuccess) return h->fail(BH_ERR_DEVICE, "ncclGroupEnd");
+      if ((rc2 = h->xport->group_end(h))) return rc2;
     }
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
     for (int r = 1; r < h->world; ++r) bh::launch_split_unpack(v, sp->dpq(h, k), blk[(size_t)r], sc);
@@ -1306,13 +1308,12 @@ int rounds_split_stage(bh_handle *h) {
   const int64_t N = sh[0]->d.N;
   int64_t base = 0;
   if (h0) base = (!h0->layout_changed && h0->inc_valid && N >= h0->n_coord) ? h0->n_coord : 0;
-  if (h->comm) {  // across processes: rank 0's base
+  if (h->xport) {  // across processes: rank 0's base
     if (!h->xbase) HIPCHK(h, hipMalloc((void **)&h->xbase, 8));
     int64_t *pin = reinterpret_cast<int64_t *>(h->pinned_state + bh::ST_COUNT + 6);  // (8-B aligned pinned words)
     *pin = base;
     HIPCHK(h, hipMemcpyAsync(h->xbase, pin, 8, hipMemcpyHostToDevice, h->stream));
-    if (ncclBroadcast(h->xbase, h->xbase, 1, ncclInt64, 0, h->comm, h->stream) != ncclSuccess)
-      return h->fail(BH_ERR_DEVICE, "ncclBroadcast (base)");
+    if ((rc = h->xport->bcast(h, h->xbase, 8, 0, h->stream))) return rc;
     HIPCHK(h, copy_sync(h->stream, pin, h->xbase, 8, hipMemcpyDeviceToHost));
     base = *pin;
   }
@@ -1350,7 +1351,7 @@ int rounds_split_stage(bh_handle *h) {
     h0->d.e0 = 0;
     h0->d.seg_lo = h0->seg_zero;
     h0->inc_calls += base > 0;
-    rc = rounds_pipelined(h0, plan.K, base, &plan, h->comm ? nullptr : &sh);
+    rc = rounds_pipelined(h0, plan.K, base, &plan, h->xport ? nullptr : &sh);
   }
   for (bh_handle *x : sh) {  // the sends / copies of this call are done
     if (x->rank == 0) continue;
@@ -2360,20 +2361,9 @@ int bh_comm_unique_id(uint8_t *id) {
   return BH_OK;
 }
 
-int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id) {
-  if (!h || !id || world < 1 || rank < 0 || rank >= world || !h->group.empty() || h->comm)
-    return BH_ERR_INVALID;
-  if (h->n_div || !h->h_creator.empty()) return h->fail(BH_ERR_STATE, "bh_comm_init after events were inserted");
-  (void)hipSetDevice(h->device);
-  if (world > 1) {
-    ncclUniqueId u;
-    memcpy(u.internal, id, sizeof u.internal);
-    const ncclResult_t nr = ncclCommInitRank(&h->comm, world, u, rank);
-    if (nr != ncclSuccess) {
-      h->comm = nullptr;
-      return h->fail(BH_ERR_DEVICE, "ncclCommInitRank(%d of %d): %s", rank, world, ncclGetErrorString(nr));
-    }
-  }
+// a process's shard of a multi-process group: its transport, rank and role
+static int comm_join(bh_handle *h, int32_t rank, int32_t world, bh::Comm *x) {
+  h->xport = x;
   h->rank = rank;
   h->world = world;
   const int mode = world > 1 ? shard_mode(h->d.n) : 0;  // see bh_create
@@ -2386,6 +2376,25 @@ int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id) {
   return BH_OK;
 }
 
+int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id) {
+  if (!h || !id || world < 1 || rank < 0 || rank >= world || !h->group.empty() || h->xport)
+    return BH_ERR_INVALID;
+  if (h->n_div || !h->h_creator.empty()) return h->fail(BH_ERR_STATE, "bh_comm_init after events were inserted");
+  (void)hipSetDevice(h->device);
+  bh::Comm *x = nullptr;
+  if (world > 1 && !(x = bh::make_rccl_comm(h, rank, world, id))) return BH_ERR_DEVICE;
+  return comm_join(h, rank, world, x);
+}
+
+int bh_comm_init_transport(bh_handle *h, int32_t rank, int32_t world, const bh_transport *t) {
+  if (!h || !t || !t->send || !t->recv || !t->broadcast || world < 1 || rank < 0 || rank >= world ||
+      !h->group.empty() || h->xport)
+    return BH_ERR_INVALID;
+  if (h->n_div || !h->h_creator.empty())
+    return h->fail(BH_ERR_STATE, "bh_comm_init_transport after events were inserted");
+  return comm_join(h, rank, world, world > 1 ? bh::make_host_comm(*t, rank) : nullptr);
+}
+
 void bh_shard_range(int64_t items, int32_t world, int32_t rank, int64_t *lo, int64_t *hi) {
   int64_t a = 0, b = 0;
   if (world >= 1 && rank >= 0 && rank < world && items >= 0) shard_range(items, world, rank, &a, &b);
@@ -2395,6 +2404,7 @@ void bh_shard_range(int64_t items, int32_t world, int32_t rank, int64_t *lo, int
 
 int bh_get_stats(bh_handle *h, bh_stats *o) {
   if (!h || !o) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   memset(o, 0, sizeof *o);
   o->n_events = (int64_t)h->h_creator.size();
   o->last_round = h->R - 1;
@@ -2413,6 +2423,7 @@ int bh_get_stats(bh_handle *h, bh_stats *o) {
 int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round, int8_t *witness,
                       int32_t *lamport, int32_t *round_received, int8_t *fame, int64_t *consensus_pos) {
   if (!h || first < 0 || count < 0 || first + count > (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (count == 0) return BH_OK;
   (void)hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2443,6 +2454,7 @@ int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round
 
 int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *ids) {
   if (!h || !ids || first < 0 || count < 0) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (first + count > h->ncons) return h->fail(BH_ERR_INVALID, "range beyond consensus");
   (void)hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2453,6 +2465,7 @@ int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *
 int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_received,
                   int64_t *first_event, int64_t *n_events, int64_t *n_transactions) {
   if (!h || first < 0 || count < 0 || first + count > (int64_t)h->blocks.size()) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   for (int64_t i = 0; i < count; ++i) {
     const Block &b = h->blocks[(size_t)(first + i)];
     if (round_received) round_received[i] = b.rr;
@@ -2465,6 +2478,7 @@ int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_rec
 
 int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap) {
   if (!h) return 0;
+  if (h->no_results()) return -h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   const int32_t head = stale_head(h), cnt = std::max(0, h->R - h->P) + head;
   for (int32_t i = 0; i < cnt && i < cap; ++i) {
     if (index) index[i] = h->P - head + i;
@@ -2475,6 +2489,7 @@ int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int
 
 int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap) {
   if (!h) return 0;
+  if (h->no_results()) return -h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   const int64_t N = (int64_t)h->h_creator.size();
   const int64_t total = h->nundet + (N - h->n_rr);
   if (!ids || cap <= 0) return total;
@@ -2492,6 +2507,7 @@ int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap) {
 int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *witness_ids, int8_t *fame,
                       int32_t cap) {
   if (!h || !info) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (r < 0 || r >= h->R) return h->fail(BH_ERR_KEY_NOT_FOUND, "GetRound %d: Not Found", r);
   (void)hipSetDevice(h->device);
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2656,6 +2672,7 @@ static int ensure_coords(bh_handle *h) {
 
 int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_t *first_descendants) {
   if (!h || id < 0 || id >= (int64_t)h->h_creator.size()) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   (void)hipSetDevice(h->device);
   Dev &d = h->d;
   if (int rc = ensure_coords(h)) return rc;
@@ -2680,6 +2697,7 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
 
 int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x, const int64_t *y, int32_t *out) {
   if (!h) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (kind < BH_Q_ANCESTOR || kind > BH_Q_ROUND_DIFF || count < 0 || (count > 0 && (!x || !y || !out)))
     return h->fail(BH_ERR_INVALID, "bh_query_events: bad kind or buffers");
   const int64_t N = (int64_t)h->h_creator.size();

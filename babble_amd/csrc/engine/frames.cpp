@@ -335,6 +335,7 @@ int bh_set_event_bytes(bh_handle *h, int64_t first, int64_t count, const uint8_t
 int32_t bh_get_frame_roots(bh_handle *h, int32_t rr, int32_t *next_round, int32_t *self_parent, int32_t *n_others,
                            int32_t *other_key, int32_t *other_value, int32_t cap) {
   if (!h) return -BH_ERR_INVALID;
+  if (h->no_results()) return -h->fail(BH_ERR_STATE, "results live on rank 0 of a split group");
   if (!h->frames_on) return -h->fail(BH_ERR_STATE, "bh_get_frame_roots: the handle was created without frames");
   if (rr < 0 || rr >= h->P) return -h->fail(BH_ERR_KEY_NOT_FOUND, "GetFrame(%d): not a processed round", rr);
   const int n = h->d.n;
@@ -363,6 +364,7 @@ int32_t bh_get_frame_roots(bh_handle *h, int32_t rr, int32_t *next_round, int32_
 
 int64_t bh_get_frame_json(bh_handle *h, int32_t rr, uint8_t *buf, int64_t cap) {
   if (!h) return -BH_ERR_INVALID;
+  if (h->no_results()) return -h->fail(BH_ERR_STATE, "results live on rank 0 of a split group");
   if (!h->frames_on) return -h->fail(BH_ERR_STATE, "bh_get_frame_json: the handle was created without frames");
   if (rr < 0 || rr >= h->P) return -h->fail(BH_ERR_KEY_NOT_FOUND, "GetFrame(%d): not a processed round", rr);
   (void)hipSetDevice(h->device);
@@ -384,6 +386,7 @@ int64_t bh_get_frame_json(bh_handle *h, int32_t rr, uint8_t *buf, int64_t cap) {
 int bh_get_block_hashes(bh_handle *h, int64_t first, int64_t count, uint8_t *frame_hash, uint8_t *block_hash,
                         int8_t *valid) {
   if (!h) return BH_ERR_INVALID;
+  if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group");
   if (!h->frames_on) return h->fail(BH_ERR_STATE, "bh_get_block_hashes: the handle was created without frames");
   if (first < 0 || count < 0 || first + count > (int64_t)h->blocks.size())
     return h->fail(BH_ERR_INVALID, "bh_get_block_hashes: blocks [%lld, %lld) out of range", (long long)first,
@@ -415,6 +418,7 @@ int bh_get_block_hashes(bh_handle *h, int64_t first, int64_t count, uint8_t *fra
 
 int64_t bh_get_block_json(bh_handle *h, int64_t b, int32_t body_only, uint8_t *buf, int64_t cap) {
   if (!h) return -BH_ERR_INVALID;
+  if (h->no_results()) return -h->fail(BH_ERR_STATE, "results live on rank 0 of a split group");
   if (!h->frames_on) return -h->fail(BH_ERR_STATE, "bh_get_block_json: the handle was created without frames");
   if (b < 0 || b >= (int64_t)h->blocks.size())
     return -h->fail(BH_ERR_KEY_NOT_FOUND, "GetBlock(%lld): no such block", (long long)b);

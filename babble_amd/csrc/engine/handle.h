@@ -27,6 +27,19 @@ struct Block {
   int64_t first, count, ntx;
 };
 
+// a multi-process group's exchange (comm.cpp): RCCL or the caller's host
+// transport; device buffers, ordered on stream s
+struct Comm {
+  virtual ~Comm() = default;
+  virtual int bcast(bh_handle *h, void *buf, size_t bytes, int32_t root, hipStream_t s) = 0;
+  virtual int send(bh_handle *h, const void *buf, size_t bytes, int32_t peer, hipStream_t s) = 0;
+  virtual int recv(bh_handle *h, void *buf, size_t bytes, int32_t peer, hipStream_t s) = 0;
+  virtual int group_start(bh_handle *) { return 0; }  // (RCCL: receives from several peers at once)
+  virtual int group_end(bh_handle *) { return 0; }
+};
+Comm *make_rccl_comm(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id);  // nullptr on failure (h->err)
+Comm *make_host_comm(const bh_transport &t, int32_t rank);
+
 }  // namespace bh
 
 using bh::Block;
@@ -127,7 +140,7 @@ struct bh_handle {
   // sharding
   int32_t rank = 0, world = 1;
   std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
-  ncclComm_t comm = nullptr;       // multi-process group (bh_comm_init)
+  bh::Comm *xport = nullptr;       // multi-process group (bh_comm_init / bh_comm_init_transport)
   bool shard_cols = false;         // split the coordinate dataflow's LA columns (else every shard computes all)
   // the coordinate split (kernels_split.hip): shard 0
   // runs the round loop, fame and order; shards 1 .. G-1 the dataflow for a
@@ -182,6 +195,9 @@ struct bh_handle {
   // it was); -1 otherwise
   int fail_alloc_in = -1;
 
+  // a coordinate rank of a multi-process split group: it ran no consensus
+  // pass, so it holds no results (rank 0 does)
+  bool no_results() const { return split && rank > 0 && xport != nullptr; }
   int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;

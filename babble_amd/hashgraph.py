@@ -88,6 +88,27 @@ class Hashgraph:
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
         self._check(self._L.bh_comm_init(self._h, int(rank), int(world), buf))
 
+    def comm_init_transport(self, rank, world, send, recv, broadcast):
+        """Make this handle shard `rank` of `world` processes over a host
+        transport of the caller's (bh_comm_init_transport): send(buf, peer),
+        recv(buf, peer) and broadcast(buf, root) get a writable memoryview of
+        the staged bytes and block until done.  Call before inserting
+        events; every pass is then collective."""
+        def wrap(fn):
+            def cb(_ctx, buf, nbytes, peer):
+                try:
+                    fn(memoryview((C.c_uint8 * nbytes).from_address(buf)).cast("B"), int(peer))
+                    return 0
+                except Exception:  # the engine reports the failure (BH_ERR_DEVICE)
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+            return cb
+        t = _native.Transport(None, _native.SEND_FN(wrap(send)), _native.RECV_FN(wrap(recv)),
+                              _native.BCAST_FN(wrap(broadcast)))
+        self._transport = t  # the callbacks must outlive the handle's calls
+        self._check(self._L.bh_comm_init_transport(self._h, int(rank), int(world), C.byref(t)))
+
     def close(self):
         if getattr(self, "_h", None):
             self._L.bh_destroy(self._h)

@@ -69,9 +69,14 @@ def _pmc_table(n, N):
     return (cfg if ok else {}), meta
 
 
-def _parallelism(world, n):
+def _shard_mode(n):
     """the engine's shard mode (BH_SHARD_COORDS; api.cpp shard_mode)"""
-    mode = os.environ.get("BH_SHARD_COORDS") or ("split" if n <= 128 else "replicate")
+    e = os.environ.get("BH_SHARD_COORDS")
+    return e if e in ("columns", "replicate") else ("split" if n <= 128 else "replicate")
+
+
+def _parallelism(world, n):
+    mode = _shard_mode(n)
     if mode == "split":
         return (f"{world} shards (RCCL send/recv over xGMI): rank 0 runs the round loop, fame and order; "
                 f"ranks 1..{world - 1} run the coordinate dataflow over LA column ranges and ship every "
@@ -206,6 +211,12 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist)
     persist_per_step = (hg.loop_stats()[0] - persist0) / args.steps  # persistent loop launches (one per segment)
+    if sharded and rank > 0 and _shard_mode(c["n"]) == "split":
+        # a coordinate rank of the split holds no consensus results (the
+        # engine refuses the query); rank 0 reports the step
+        hg.close()
+        dist.destroy_process_group()
+        return
     stats = hg.stats()
     ordered = stats.consensus_events
     # whole-job events ordered: one DAG per step when sharded, one per rank per step as replicas

@@ -13,6 +13,7 @@
  */
 #ifndef BABBLE_HIP_H
 #define BABBLE_HIP_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -291,9 +292,26 @@ int64_t bh_get_block_json(bh_handle *h, int64_t b, int32_t body_only, uint8_t *b
  * each holding the whole DAG, joined by an RCCL communicator.  Rank 0 makes
  * the id, every rank passes the same bytes (NCCL_UNIQUE_ID_BYTES = 128)
  * before inserting any event.  Every pass is then collective: all ranks must
- * call the same passes in the same order. */
+ * call the same passes in the same order.  With the coordinate split (the
+ * default at n <= 128) only rank 0 holds consensus results: the result
+ * getters of ranks > 0 return BH_ERR_STATE. */
 int bh_comm_unique_id(uint8_t *id);
 int bh_comm_init(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id);
+/* The same group over a transport of the caller's (a Go node's own links
+ * between its processes; the tests' gloo group): host-memory, blocking
+ * point-to-point messages and broadcasts, each returning 0 on success.  The
+ * engine stages every exchange through pinned host memory and calls these
+ * at exactly the places the RCCL group calls ncclSend / ncclRecv /
+ * ncclBroadcast, in the same order on every rank: the call sequence is
+ * identical, so a transport that delivers messages between each pair in
+ * order suffices.  The struct is copied; ctx is passed back untouched. */
+typedef struct bh_transport {
+  void *ctx;
+  int (*send)(void *ctx, const void *buf, size_t bytes, int32_t peer);
+  int (*recv)(void *ctx, void *buf, size_t bytes, int32_t peer);
+  int (*broadcast)(void *ctx, void *buf, size_t bytes, int32_t root);
+} bh_transport;
+int bh_comm_init_transport(bh_handle *h, int32_t rank, int32_t world, const bh_transport *t);
 /* The split rule every shard uses for LA columns, fame rounds and frames:
  * shard `rank` of `world` owns [items*rank/world, items*(rank+1)/world). */
 void bh_shard_range(int64_t items, int32_t world, int32_t rank, int64_t *lo, int64_t *hi);
