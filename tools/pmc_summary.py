@@ -49,6 +49,15 @@ def main():
                   "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, {os.path.basename(d.rstrip('/'))}"}
         print(k, tab[k])
     out[key] = tab
+    # the build the counters were collected on (bench.py quotes it)
+    import subprocess
+    try:
+        rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                             cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip()
+    except OSError:
+        rev = "?"
+    out.setdefault("_meta", {})[key] = {"commit": rev, "dir": os.path.basename(d.rstrip("/")),
+                                        "kernels": sorted(tab)}
     json.dump(out, open(out_path, "w"), indent=1)
 
 
