@@ -1730,7 +1730,6 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.flow_ltclamp = getenv("BH_FLOW_LTCLAMP") ? atoi(getenv("BH_FLOW_LTCLAMP")) : INT32_MAX;
   d.flow_wd = getenv("BH_FLOWW_WATCHDOG") ? atoi(getenv("BH_FLOWW_WATCHDOG")) : (1 << 20);
   d.flow_lt = 1;
-  d.round_prio = getenv("BH_ROUND_PRIO") ? std::clamp(atoi(getenv("BH_ROUND_PRIO")), 0, 3) : 0;
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
   // the XCD-hierarchical barrier above 64 workgroups (with per-workgroup
@@ -1836,20 +1835,10 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
      // the critical path while the coordinate pipeline streams beside it
     int lo_pri = 0, hi_pri = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
-    // BH_CU_SPLIT=k (A/B): the loop's stream on CUs [0, k) and the
-    // coordinate stream on the others (hipExtStreamCreateWithCUMask)
-    const int cus = getenv("BH_CU_SPLIT") ? atoi(getenv("BH_CU_SPLIT")) : 0;
-    if (cus > 0) {
-      uint32_t m0[8] = {0}, m1[8] = {0};
-      for (int i = 0; i < 256; ++i) (i < cus ? m0 : m1)[i / 32] |= 1u << (i % 32);
-      if (rc == BH_OK && hipExtStreamCreateWithCUMask(&h->stream, 8, m0) != hipSuccess) rc = BH_ERR_DEVICE;
-      if (rc == BH_OK && hipExtStreamCreateWithCUMask(&h->stream2, 8, m1) != hipSuccess) rc = BH_ERR_DEVICE;
-    } else {
-      if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi_pri) != hipSuccess)
-        rc = BH_ERR_DEVICE;
-      if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
-        rc = BH_ERR_DEVICE;
-    }
+    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, hi_pri) != hipSuccess)
+      rc = BH_ERR_DEVICE;
+    if (rc == BH_OK && hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, lo_pri) != hipSuccess)
+      rc = BH_ERR_DEVICE;
     hipDeviceProp_t prop;
     if (rc == BH_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) h->ncu = prop.multiProcessorCount;
   }

@@ -138,7 +138,6 @@ struct Dev {
   int32_t wide_prio;      // persistent k_round_wide: 1 hand-off / barrier / staging at priority 2, 2 also alternate the search
   int32_t *psnap;         // the loop's inputs (Bp and candfd of parity 0, the state block) kept for that fallback
   int32_t round_src_rows;  // k_round2r: windows from the row-major LA, hand-off from FDT (BH_ROUND_SRC=rows, A/B)
-  int32_t round_prio;  // k_round2's wave priority (s_setprio) against co-resident coordinate waves (BH_ROUND_PRIO)
   int32_t rbase, rspan;
   int32_t round_lpc;  // lanes per candidate of k_round2 (8), the layout of its ssm ballots
   int32_t round_p8;   // k_round_wide<*, true>: 8-bit window-relative rows where the window's LA spread is at most this

@@ -184,14 +184,10 @@ void launch_first_descendants(const Dev &d, hipStream_t s, bool walked) {
   // tile rows: LDS is npad x (TR + 1) words, so wide groups take short
   // tiles and several workgroups per compute unit (the kernel is bound by
   // its loads' latency: n = 512 with 64-row tiles left one 4-wave workgroup
-  // per CU, 1.2 TB/s); BH_FDT_TR overrides (A/B)
-  static const int tr_env = getenv("BH_FDT_TR") ? atoi(getenv("BH_FDT_TR")) : 0;
-  const int tr = tr_env ? tr_env : d.npad <= 128 ? 64 : 16;
+  // per CU, 1.2 TB/s)
   const int64_t rows = d.rows > 0 ? d.rows : d.N;  // the layout's rows, gaps included
-  if (tr >= 64)
+  if (d.npad <= 128)
     k_fd_transpose<64><<<(unsigned)((rows + 63) / 64), 256, (size_t)d.npad * 65 * 4, s>>>(d);
-  else if (tr >= 32)
-    k_fd_transpose<32><<<(unsigned)((rows + 31) / 32), 256, (size_t)d.npad * 33 * 4, s>>>(d);
   else
     k_fd_transpose<16><<<(unsigned)((rows + 15) / 16), 256, (size_t)d.npad * 17 * 4, s>>>(d);
 }
@@ -200,8 +196,6 @@ void configure_fd_kernels() {
   (void)hipFuncSetAttribute((const void *)k_fd_walk, hipFuncAttributeMaxDynamicSharedMemorySize,
                             150 * 1024);
   (void)hipFuncSetAttribute((const void *)k_fd_transpose<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            150 * 1024);
-  (void)hipFuncSetAttribute((const void *)k_fd_transpose<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             150 * 1024);
 }
 

@@ -1075,26 +1075,16 @@ void launch_flow_transpose(const Dev &d, hipStream_t s) {
   if (d.rows == 0) return;
   if (d.tile_list) {
     if (d.ntiles == 0) return;
-    const char *e = getenv("BH_XPOSE_WG");
-    const int64_t wg = std::min<int64_t>(d.ntiles, e ? std::max(1, atoi(e)) : 512);
+    const int64_t wg = std::min<int64_t>(d.ntiles, 512);
     k_flow_transpose<64, 512><<<(unsigned)wg, 512, (size_t)d.npad * 66 * 4, s>>>(d);
     return;
   }
   if (d.npad > 128) {
-    // wide rows: short tiles so several workgroups share a compute unit --
-    // the walk's LDS round trips are latency, not bandwidth (BH_XPOSE_TR:
-    // 16, 32 or 64 rows, A/B)
-    static const int tr = getenv("BH_XPOSE_TR") ? atoi(getenv("BH_XPOSE_TR")) : 32;
-    if (tr <= 16) {
-      const unsigned tiles = (unsigned)((d.rows + 15) / 16);
-      k_flow_transpose<16, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 18 * 4, s>>>(d);
-    } else if (tr >= 64) {  // (one workgroup per compute unit at n = 512: 135 KB)
-      const unsigned tiles = (unsigned)((d.rows + 63) / 64);
-      k_flow_transpose<64, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 66 * 4, s>>>(d);
-    } else {
-      const unsigned tiles = (unsigned)((d.rows + 31) / 32);
-      k_flow_transpose<32, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 34 * 4, s>>>(d);
-    }
+    // wide rows: 32-row tiles so several workgroups share a compute unit --
+    // the walk's LDS round trips are latency, not bandwidth (16- and 64-row
+    // tiles measured slower, round 3)
+    const unsigned tiles = (unsigned)((d.rows + 31) / 32);
+    k_flow_transpose<32, 512><<<(tiles + 7) / 8 * 8, 512, (size_t)d.npad * 34 * 4, s>>>(d);
     return;
   }
   const unsigned tiles = (unsigned)((d.rows + 63) / 64);

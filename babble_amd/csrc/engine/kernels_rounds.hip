@@ -1427,15 +1427,6 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   __shared__ int32_t hist[HW + 1];  // TQ: T_q histogram; [HW] = the answer row
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x;
-  // a loop workgroup placed on a compute unit beside a k_flow32 workgroup
-  // (the segment pipeline: 129 + 128 workgroups on 256 CUs) loses VALU
-  // arbitration to those older waves; a higher priority takes it back
-  switch (d.round_prio) {
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    case 3: __builtin_amdgcn_s_setprio(3); break;
-    default: break;
-  }
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int rs4 = q4 + 1, rs = 4 * rs4;  // window row stride (one spare piece: staging stores spread over banks)
   const int64_t stride = la_col_stride(d);
@@ -1716,15 +1707,6 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       signal_done(d);
     }
     return;
-  }
-  // BH_ROUND_PRIO (A/B): a loop workgroup that shares its compute unit with
-  // a coordinate workgroup takes the issue arbitration back from the older
-  // waves beside it
-  switch (d.round_prio) {
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    case 3: __builtin_amdgcn_s_setprio(3); break;
-    default: break;
   }
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
   const int rs4 = q4 + 1, rs = 4 * rs4;
