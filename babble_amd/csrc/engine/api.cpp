@@ -137,7 +137,8 @@ int set_chain_tables(bh_handle *h) {
   for (int c = 0; fits && c < n; ++c) fits = len[(size_t)c] <= h->cap_h[(size_t)c];
   h->layout_changed = !fits;
   if (!fits) {
-    static const int64_t min_slack = getenv("BH_LAYOUT_SLACK") ? atoll(getenv("BH_LAYOUT_SLACK")) : 1024;
+    h->rows_built = false;  // (rows built for the old layout)
+    const int64_t min_slack = getenv("BH_LAYOUT_SLACK") ? atoll(getenv("BH_LAYOUT_SLACK")) : 1024;
     const bool slack = h->d.la_rows > h->cap;  // the allocation reserved room for it
     int64_t need = 0;
     for (int c = 0; c < n; ++c) need += len[(size_t)c] + std::max<int64_t>(min_slack, len[(size_t)c] / 8);
@@ -191,8 +192,8 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
   hipStream_t s = h->stream;
   // BH_NO_GRAPH=1: launch the iterations directly instead of replaying a
   // captured graph (profiling / A-B; results are identical)
-  static const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
-  static const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
+  const bool no_graph = getenv("BH_NO_GRAPH") && atoi(getenv("BH_NO_GRAPH"));
+  const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
   if (bh::round_solo_eligible(v)) {  // one launch runs every round (k_round_solo)
     if (loop_timing) HIPCHK(h, hipEventRecord(h->ev_loop[0], s));
     bh::launch_round_solo(v, s);
@@ -463,6 +464,55 @@ int reset_coords(bh_handle *h, hipStream_t s) {
   return BH_OK;
 }
 
+// The segments left only the column-major LA (rounds_pipelined, n <= 128):
+// the row-major LA and the complete FDT of the layout's rows up to the
+// chain lengths `upto` -- a query's, or an eager call resuming a prefix --
+// as the segment pipeline's eager transpose builds them: only the tiles of
+// rows past the ones an earlier build covered (their FD entries of older
+// rows are completed by the new rows' walk and k_fd_idle), or every row the
+// first time and after a relayout.  Synchronous (its staging is reused).
+int build_rows(bh_handle *h, const std::vector<int32_t> &upto, hipStream_t s) {
+  const int n = h->d.n;
+  Dev v = h->d;
+  v.e0 = 0;
+  v.rows = h->layout_rows;
+  v.col0 = 0;
+  v.ncol = n;
+  v.xpose_fd = 1;
+  const bool inc = h->rows_built && (int)h->rows_lens.size() == n;
+  int32_t *stg = h->seg_stage;  // [lo | len] per chain
+  for (int c = 0; c < n; ++c) {
+    stg[c] = inc ? std::min(h->rows_lens[(size_t)c], upto[(size_t)c]) : 0;
+    stg[n + c] = upto[(size_t)c];
+  }
+  HIPCHK(h, hipMemcpyAsync(h->segbuf, stg, (size_t)2 * n * 4, hipMemcpyHostToDevice, s));
+  v.seg_lo = h->segbuf;
+  v.chain_len = h->segbuf + n;
+  v.tile_list = nullptr;
+  v.ntiles = 0;
+  if (inc) {  // the 64-row tiles holding the new rows, shared boundary tiles once
+    int32_t *tl = h->tlist_stage;
+    int64_t nt = 0;
+    for (int c = 0; c < n; ++c) {
+      if (stg[n + c] <= stg[c]) continue;
+      const int64_t a = ((int64_t)h->cstart_h[(size_t)c] + stg[c]) >> 6,
+                    b = ((int64_t)h->cstart_h[(size_t)c] + stg[n + c] - 1) >> 6;
+      for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
+    }
+    if (nt) HIPCHK(h, hipMemcpyAsync(h->tlist, tl, (size_t)nt * 4, hipMemcpyHostToDevice, s));
+    v.tile_list = h->tlist;
+    v.ntiles = nt;
+  }
+  if (!inc || v.ntiles > 0) bh::launch_flow_transpose(v, s);
+  bh::launch_fd_idle(v, s);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(s));
+  h->rows_lens = upto;
+  h->rows_built = true;
+  h->rows_stale = false;
+  return BH_OK;
+}
+
 // coordinates up to the dataflow kernel (this shard's LA columns when split)
 int rounds_coords(bh_handle *h) {
   int rc;
@@ -476,6 +526,7 @@ int rounds_coords(bh_handle *h) {
   h->inc_valid = false;
   h->fdt_lost = false;
   h->rows_stale = false;  // (rounds_loop transposes)
+  h->rows_built = false;
   if ((rc = set_chain_tables(h))) return rc;
   d.rows = h->layout_rows;
   hipStream_t s = h->stream;
@@ -625,6 +676,7 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
       // coordinates, the next pass starts from scratch
       h->coords_for = -1;
       h->fdt_lost = true;
+      h->rows_built = false;
     } else {
       bh::launch_flow_lt_fallback(d, s);
     }
@@ -886,7 +938,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // 128 < n <= 512: the 16-bit wide loop reads la_col as well (window,
   // candidates' FD rows, fame's LA rows; k_round_wide<*, true, true>) --
   // BH_WIDE_ROWS=1 keeps the FDT / row-major LA loop (A/B)
-  static const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
+  const bool eager_env = getenv("BH_EAGER_ROWS") && atoi(getenv("BH_EAGER_ROWS"));
   const bool wide_rows_env = !getenv("BH_WIDE_COLS") || !atoi(getenv("BH_WIDE_COLS")) ||
                              (getenv("BH_WIDE_ROWS") && atoi(getenv("BH_WIDE_ROWS")));  // (off until verified; read per call: the tests switch it)
   d.wide_cols = wide && !sp && !h->reset_on && !wide_rows_env && !eager_env && bh::round_p16(d) && d.cla && d.n <= 512;
@@ -896,6 +948,11 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
                              d.round_src_rows);
   d.use_cla = (d.fd_cols || d.wide_cols) && !bh::round_solo_eligible(d);
   if (sp) d.round_src_rows = 0;  // the split ships the column-major LA only
+  if (base > 0 && eager && h->rows_stale) {
+    // the previous call left the prefix's rows unbuilt (a lazy-rows path)
+    // and this one resumes on a path that reads them: build them first
+    if ((rc = build_rows(h, h->lens_coord, h->stream))) return rc;
+  }
   hipStream_t sr = h->stream, sc = h->stream2;
   h->segments_used = K;
   h->fdt_lost = false;
@@ -1092,7 +1149,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // the later ones leave at once (ST_PFAIL), and the host reads the state
   // once, after the last loop.  Other loops (wide, one launch per round,
   // BH_SEG_DEBUG) wait for each segment as before
-  static const bool dbg = getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG"));  // per-segment timings to stderr
+  const bool dbg = getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG"));  // per-segment timings to stderr
   const bool async = !wide && !eager && !dbg && bh::round_persist_eligible(d);
   HIPCHK(h, hipMemsetAsync(d.state + bh::ST_PFAIL, 0, 4, sr));
   if (async && (int)h->loop_evs.size() < 2 * K) {
@@ -1195,7 +1252,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   (void)hipEventDestroy(sr_mark);
   if (async) {  // every loop's end: one host synchronisation for the call
     HIPCHK(h, copy_sync(sr, st, d.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
-    static const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
+    const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
     float lms = 0;
     for (int k = 0; loop_timing && k < K; ++k)
       if (hipEventElapsedTime(&lms, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]) == hipSuccess)
@@ -1236,6 +1293,10 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   HIPCHK(h, hipStreamWaitEvent(sr, h->ev[1], 0));
   h->coords_for = (int)N;
   h->rows_stale = !eager || d.wide_cols == 2;  // (wide_cols 2 built no FDT)
+  if (!h->rows_stale) {  // (the segments' eager transposes built every row so far)
+    h->rows_lens = h->lens_h;
+    h->rows_built = true;
+  }
   float ms = 0;
   h->sweep_ms = 0;
   for (int k = 0; k < K; ++k)
@@ -2564,20 +2625,8 @@ static int ensure_coords(bh_handle *h) {
   Dev &d = h->d;
   const int64_t N = (int64_t)h->h_creator.size();
   if (h->coords_for == N && h->rows_stale) {
-    // the segments left only the column-major LA (rounds_pipelined): the
-    // row-major LA and the complete FDT of every row, as a whole-layout
-    // transpose builds them
-    Dev full = d;
-    full.e0 = 0;
-    full.seg_lo = h->seg_zero;
-    full.tile_list = nullptr;
-    full.rows = h->layout_rows;
-    full.col0 = 0;
-    full.ncol = d.n;
-    bh::launch_flow_transpose(full, h->stream);
-    bh::launch_fd_idle(full, h->stream);
-    HIPCHK(h, hipGetLastError());
-    h->rows_stale = false;
+    int rc;
+    if ((rc = build_rows(h, h->lens_coord, h->stream))) return rc;
   }
   if (h->coords_for != N) {
     int rc;

@@ -133,6 +133,10 @@ struct bh_handle {
   bool inc_valid = false;
   bool fdt_lost = false;  // the wide LT fallback's sweep overwrote FDT (no resume from it)
   bool rows_stale = false;  // n <= 128 segments built la_col only: row-major LA / FDT wait for a query
+  // the row-major LA / FDT built (build_rows) for these chain lengths of the
+  // current layout: a later build transposes only the rows past them
+  bool rows_built = false;
+  std::vector<int32_t> rows_lens;
   int64_t n_coord = 0;
   int64_t inc_calls = 0;  // DivideRounds calls that resumed (statistics)
   int64_t persist_loops = 0, persist_fallbacks = 0;  // k_round2p loops run / given up (bh_get_loop_stats)

@@ -891,18 +891,24 @@ def test_lazy_rows_queries(monkeypatch, n, N, seed, lag, K):
     pid = d.participant_ids
     opc_id = np.where(opc >= 0, pid[np.maximum(opc, 0)], -1)
     rng = np.random.default_rng(seed)
-    for lo, hi in ((0, half), (half, N)):
+    prev = 0
+    # quarters: the queries after the second call on build only the rows
+    # past the ones the previous query built (build_rows), and the older
+    # rows' FD entries into the new rows; sampled among the events just
+    # before the previous boundary as well
+    for lo, hi in ((0, N // 4), (N // 4, half), (half, 3 * N // 4), (3 * N // 4, N)):
         o.insert_dag(*(a[lo:hi] for a in args))
         o.run_consensus()
         assert not hg.insert_events(pid[d.creator[lo:hi]], d.index[lo:hi], spi[lo:hi], opc_id[lo:hi], opi[lo:hi],
                                     d.hash[lo:hi], d.sig_r[lo:hi], d.ntx[lo:hi]).any()
         hg.run_consensus()
         _compare(o, hg, f"lazy rows, events [0, {hi})")
-        for e in rng.integers(0, hi, 40).tolist():
+        for e in rng.integers(0, hi, 40).tolist() + list(range(max(0, prev - 20), prev)):
             la, fd = hg.coordinates(e)
             ola, ofd = o.coordinates(e)
             assert la.tolist() == ola.tolist() and fd.tolist() == ofd.tolist(), e
         x, y = rng.integers(0, hi, 300), rng.integers(0, hi, 300)
         got = hg.query("strongly_see", x, y)
         assert [bool(v) for v in got] == [o.strongly_see(int(a), int(b)) for a, b in zip(x, y)]
+        prev = hi
     assert hg.pipeline()[1] >= 1
