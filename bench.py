@@ -5,16 +5,24 @@ A step = one pass of the hot path over the resident DAG: coordinates
 ProcessDecidedRounds (frame sort + blocks), all in libbabble_hip on one GPU.
 The DAG (generation, hashing, signing, H2D copy) is prepared before the timed
 region.  Workload: BASELINE.json's headline config C3 (128 participants,
-10M-event random-gossip DAG).  Multi-GPU: one process per GPU, the ranks
-order one DAG together (strong scaling).  By default (n <= 128) rank 0
-runs the round loop -- the serial chain of the path -- with fame and the
-order, and ranks 1..N-1 run the coordinate dataflow for ranges of LA
-columns, shipping every pipeline segment's columns to rank 0 (ncclSend /
-ncclRecv over xGMI, 16-bit packed); BH_SHARD_COORDS=replicate / columns
-select the round-3 splits.  --mode replicas runs independent DAGs per rank
-(weak scaling).
+10M-event random-gossip DAG).
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--events N]
+Multi-GPU (one process per GPU):
+  --mode replicas (the default): every rank orders a DAG of its own (a
+      node's independent hashgraphs; weak scaling) -- value = events ordered
+      by all ranks / the slowest rank's time.  One hashgraph's rounds are a
+      serial chain (the round loop is 90 % of the step), so this is how the
+      path scales;
+  --mode shards: the ranks order ONE DAG together (strong scaling): rank 0
+      runs the round loop, fame and the order, ranks 1..N-1 the coordinate
+      dataflow over LA column ranges, shipping every pipeline segment's
+      columns to rank 0 (ncclSend / ncclRecv over xGMI, 16-bit packed);
+      BH_SHARD_COORDS=replicate / columns select the round-3 splits.  Rank
+      0's step is bounded by the loop alone: 5.81 against 5.94 us per round
+      beside the coordinates on one GPU (profiles/r5_bench_seg1.json), so
+      at most ~2 % faster than one GPU.
+
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--events N] [--mode replicas|shards]
        torchrun ... bench.py --gpus N ...
 """
 import argparse
@@ -133,16 +141,17 @@ def main():
     ap.add_argument("--sig", type=int, default=0, help="1 = deterministic ECDSA signatures")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="events for the CPU baseline (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
-    ap.add_argument("--mode", choices=("shards", "replicas"), default="shards",
-                    help="N>1: shard one DAG over the ranks (strong) or order one DAG per rank (weak)")
+    ap.add_argument("--mode", choices=("shards", "replicas"), default="replicas",
+                    help="N>1: order one DAG per rank (weak, the default) or shard one DAG over the ranks (strong)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # BH_BENCH_ONE_DEVICE=1: every rank on device 0, the barrier over gloo
-    # (rehearses the multi-process RCCL path on a one-GPU box)
+    # BH_BENCH_ONE_DEVICE=1: every rank on device 0, the barrier (and the
+    # shards' exchange) over gloo -- rehearses the multi-process paths on a
+    # one-GPU box
     one_dev = os.environ.get("BH_BENCH_ONE_DEVICE") == "1"
     if one_dev:
         local = 0
@@ -166,7 +175,16 @@ def main():
     log(f"generated cfg{args.cfg} n={c['n']} N={N} in {time.perf_counter() - t0:.1f}s")
     t0 = time.perf_counter()
     hg = Hashgraph(dag.participant_ids, N, device=local)
-    if sharded:  # one RCCL communicator of the engine's own, id from rank 0
+    if sharded and one_dev:
+        # RCCL refuses two ranks on one device: the engine's host transport
+        # over the gloo group carries the same exchanges (bh_comm_init_transport)
+        import torch
+
+        def tb(b):
+            return torch.frombuffer(b, dtype=torch.uint8)
+        hg.comm_init_transport(rank, world, lambda b, p: dist.send(tb(b), dst=p),
+                               lambda b, p: dist.recv(tb(b), src=p), lambda b, r: dist.broadcast(tb(b), src=r))
+    elif sharded:  # one RCCL communicator of the engine's own, id from rank 0
         obj = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         hg.comm_init(rank, world, obj[0])
@@ -280,8 +298,9 @@ def main():
     coord_obj = {"kernel": hg.profile_kernel(), "launches_per_step": coord_launches, "device_ms_per_step": coord_ms,
                  "avg_launch_ms": coord_ms / max(coord_launches, 1),
                  "alg_bytes_per_launch": coord_alg / max(coord_launches, 1),
-                 "achieved": coord_alg / (coord_ms * 1e-3) / 1e9,
-                 "frac": coord_alg / (coord_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 # (shards: rank 0 runs no dataflow -- its coordinate time is the exchange)
+                 "achieved": coord_alg / (coord_ms * 1e-3) / 1e9 if coord_ms > 0 else None,
+                 "frac": coord_alg / (coord_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if coord_ms > 0 else None,
                  "traffic_per_launch": (pmc.get(hg.profile_kernel()) or {}).get("hbm_bytes_per_launch"),
                  "note": "LA columns and Lamport timestamps (12n + 12 B per event); bound by the DAG's critical "
                          "path x per-step issue, not bandwidth"}
