@@ -129,9 +129,9 @@ struct Dev {
   int32_t use_cla;  // the loop that ran wrote cla (k_round2; not the resident k_round_solo)
   int32_t wide_cols;  // the 16-bit wide loop reads la_col (k_round_wide<*, true, true>; no FDT)
   int32_t round_persist;  // k_round2p: the whole n <= 128 loop in one launch (default; BH_ROUND_PERSIST=0: one launch per iteration)
-  int32_t *pbar;          // k_round2p's grid-barrier counter
-  int32_t pbar_spin;      // k_round2p's barrier polls before it gives up (BH_PBAR_SPIN lowers it to test the fallback)
-  int32_t pbar_mode;      // the persistent loops' barrier: 0 one counter, 1 XCD-hierarchical (n > 64; BH_PBAR=xcd|flat)
+  int32_t *pbar;          // the persistent wide loop's grid barrier (k_round2p hands off through tagged Bp / candfd dwords instead)
+  int32_t pbar_spin;      // polls before a persistent loop gives up waiting (barrier or tagged hand-off; BH_PBAR_SPIN lowers it to test the fallback)
+  int32_t pbar_mode;      // the wide persistent loop's barrier: 0 one counter, 1 XCD-hierarchical (n > 64; BH_PBAR=xcd|flat)
   int32_t prestage;       // the wide persistent loop stages its next window while the barrier completes (BH_PRESTAGE=0: off)
   int32_t xpose_fd;       // k_flow_transpose also walks firstDescendants into FDT (0: LA rows only)
   int32_t win_reuse;      // persistent k_round_wide: the next window reuses the rows it shares with the last

@@ -1664,28 +1664,26 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
   }
 }
 
-// k_round2r (BH_ROUND_SRC=rows, A/B): the round-3 iteration, reading its
-// window from the row-major LA and its hand-off from the FDT tiles that the
-// segments' transpose builds (eager rows); k_round2 reads only la_col
-// ---------------------------------------------------------------------------
 // k_round2p: the n <= 128 round loop as ONE launch of n workgroups, one per
-// chain (BH_ROUND_PERSIST=1, the A/B against one k_round2 launch per
-// iteration).  Each iteration is k_round2's (TQ search, hand-off counted
-// from 64 LA rows per chain); a grid barrier replaces the kernel boundary.
-// What crosses it -- each candidate's FD row (candfd) and boundary (Bp) --
-// is stored sc1; every workgroup then adds to one agent-scope counter after
-// its stores have drained, polls the counter with sc1 loads and reads the
-// rows back with sc1 loads (MI355X_MICROARCH.md, the hand-off table's first
-// row: no L2 write-back or invalidate).  What a workgroup needs of its own
-// chain -- the next window (rows from its new boundary) and the LA rows its
-// next hand-off counts from (its new FD row is in registers) -- is issued
-// before the barrier wait and lands during it.  Every workgroup sees the
-// same candidate count, so each decides the loop's end itself.  The spin is
-// bounded (d.pbar_spin polls, ~0.5 s by default; ST_ERR = 3: the barrier
-// gave up -- the host then restores the loop's inputs and runs one launch per
-// iteration instead).  Co-residency: n <= 128 workgroups of 16 waves fit the
-// 256 compute units beside the segment pipeline's n coordinate workgroups,
-// and those never wait for the loop, so every loop workgroup is placed.
+// chain (default; BH_ROUND_PERSIST=0: one k_round2 launch per iteration).
+// Each iteration is k_round2's (TQ search, hand-off counted from 64 LA rows
+// per chain); no kernel boundary and no grid barrier between iterations
+// (round 5): what crosses from one iteration to the next -- each
+// candidate's boundary (Bp) and FD row (candfd) -- is stored sc1 as
+// self-validating dwords, the iteration's low 8 bits in the top byte, and a
+// consumer reloads (sc1, volatile) until every dword it needs carries the
+// tag (MI355X_MICROARCH.md, data-tagged granules: one hop, where a barrier
+// costs an arrival, a release and the loads behind it).  Values fit 24 bits
+// (chain rows < 2^24 - 1; 0xFFFFFF is FD_NONE).  What a workgroup needs of
+// its own chain -- the next window (rows from its new boundary) and the LA
+// rows its next hand-off counts from -- is loaded before the wait and staged
+// while the candidates' rows are in flight.  Every workgroup sees the same
+// candidate count, so each decides the loop's end itself.  The wait is
+// bounded (d.pbar_spin polls; ST_ERR = 3: a word never arrived -- the host
+// then restores the loop's inputs and runs one launch per iteration).
+// Co-residency: n <= 128 workgroups of 16 waves fit the 256 compute units
+// beside the segment pipeline's coordinate workgroups, and those never wait
+// for the loop, so every loop workgroup is placed.
 
 template <int PPL>
 __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
@@ -1987,7 +1985,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
 }
 
 bool round_persist_eligible(const Dev &d) {
-  return d.round_persist && round2_eligible(d) && !d.round_src_rows && d.pbar != nullptr && d.n <= 256;
+  // (the tagged hand-off carries chain rows in 24 bits: 0xFFFFFF is FD_NONE)
+  return d.round_persist && round2_eligible(d) && !d.round_src_rows && d.n <= 256 && d.max_chain_len < 0xFFFFFF;
 }
 
 static int lanes_per_candidate(int npad);
@@ -2043,6 +2042,9 @@ void launch_round_persist(const Dev &d, hipStream_t s) {
   else k_round2p<4><<<d.n, nt, lds, s>>>(d);
 }
 
+// k_round2r (BH_ROUND_SRC=rows, A/B): the round-3 iteration, reading its
+// window from the row-major LA and its hand-off from the FDT tiles that the
+// segments' transpose builds (eager rows); k_round2 reads only la_col
 template <int PPL, bool TQ>
 __global__ __launch_bounds__(1024) void k_round2r(Dev d, int p) {
   constexpr int LPC = 8;

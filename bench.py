@@ -77,21 +77,32 @@ def _pmc_table(n, N):
     return (cfg if ok else {}), meta
 
 
+def _per_launch(pmc, kernel, launches):
+    """a kernel's PMC HBM bytes per launch of THIS run: the table's bytes per
+    step over this run's launches per step (BH_SEGMENTS changes the launch
+    count, not the step's bytes)"""
+    v = pmc.get(kernel)
+    return v["hbm_bytes_per_step"] / launches if v and launches else None
+
+
 def _shard_mode(n):
     """the engine's shard mode (BH_SHARD_COORDS; api.cpp shard_mode)"""
     e = os.environ.get("BH_SHARD_COORDS")
     return e if e in ("columns", "replicate") else ("split" if n <= 128 else "replicate")
 
 
-def _parallelism(world, n):
+def _parallelism(world, n, one_dev=False):
     mode = _shard_mode(n)
+    xp = "host transport over gloo, all ranks on device 0" if one_dev else None
     if mode == "split":
-        return (f"{world} shards (RCCL send/recv over xGMI): rank 0 runs the round loop, fame and order; "
-                f"ranks 1..{world - 1} run the coordinate dataflow over LA column ranges and ship every "
+        return (f"{world} shards ({xp or 'RCCL send/recv over xGMI'}): rank 0 runs the round loop, fame and "
+                f"order; ranks 1..{world - 1} run the coordinate dataflow over LA column ranges and ship every "
                 f"segment's columns to rank 0 (16-bit packed)")
     if mode == "columns":
-        return f"{world} shards (RCCL broadcast): LA columns, fame rounds and frame sorts split, round loop replicated"
-    return f"{world} shards (RCCL broadcast): fame rounds + frame sorts split, coordinates and round loop replicated"
+        return (f"{world} shards ({xp or 'RCCL broadcast'}): LA columns, fame rounds and frame sorts split, "
+                f"round loop replicated")
+    return (f"{world} shards ({xp or 'RCCL broadcast'}): fame rounds + frame sorts split, coordinates and "
+            f"round loop replicated")
 
 
 def _cpu_model():
@@ -285,7 +296,7 @@ def main():
                 "alg_bytes_per_launch": loop_alg / max(loop_launches, 1e-9),
                 "achieved": loop_alg / (loop_ms * 1e-3) / 1e9, "frac": loop_alg / (loop_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "round_iterations": iters, "us_per_iteration": iter_us,
-                "traffic_per_launch": (pmc.get(round_kernel) or {}).get("hbm_bytes_per_launch"),
+                "traffic_per_launch": _per_launch(pmc, round_kernel, loop_launches),
                 "note": "latency-bound: the rounds are a serial chain; one persistent launch per pipeline "
                         "segment (k_round2p: workgroups hand each other the candidates' rows as data-tagged "
                         "dwords) or per call (k_round_wide: a grid barrier per round)"}
@@ -301,7 +312,7 @@ def main():
                  # (shards: rank 0 runs no dataflow -- its coordinate time is the exchange)
                  "achieved": coord_alg / (coord_ms * 1e-3) / 1e9 if coord_ms > 0 else None,
                  "frac": coord_alg / (coord_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if coord_ms > 0 else None,
-                 "traffic_per_launch": (pmc.get(hg.profile_kernel()) or {}).get("hbm_bytes_per_launch"),
+                 "traffic_per_launch": _per_launch(pmc, hg.profile_kernel(), coord_launches),
                  "note": "LA columns and Lamport timestamps (12n + 12 B per event); bound by the DAG's critical "
                          "path x per-step issue, not bandwidth"}
     # the dominant kernel: the larger device-time share of the step
@@ -324,8 +335,9 @@ def main():
                                f"DivideRounds + DecideFame + DecideRoundReceived + ProcessDecidedRounds",
                    "participants": n, "events": N, "events_ordered_per_step": ordered,
                    "rounds": stats.last_round + 1, "blocks": stats.blocks,
-                   "parallelism": _parallelism(world, n) if sharded else
-                                  (f"replicas x{world}" if world > 1 else "1 GPU")},
+                   "parallelism": _parallelism(world, n, one_dev) if sharded else
+                                  (f"replicas x{world}" + (" on device 0" if one_dev else "") if world > 1
+                                   else "1 GPU")},
         # the dominant kernel's roofline (per launch), then the whole step's
         "roofline": {"bound": "hbm", "kernel": dom["kernel"], "achieved": dom["achieved"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": dom["frac"], "traffic": dom["traffic_per_launch"],

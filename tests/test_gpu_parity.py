@@ -819,21 +819,25 @@ def test_round2_persistent(monkeypatch, n, N, seed, lag, K):
         _wild_parity(128, 40_000, 0xC5, 35_000)
 
 
-@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xC9, 0, 1), (100, 50_000, 0xCA, 4, 3), (7, 5_000, 0xCB, 2, 2)])
-def test_round2_persistent_xcd_barrier(monkeypatch, n, N, seed, lag, K):
-    """The persistent loop with its XCD-hierarchical grid barrier (BH_PBAR=xcd:
-    per-XCD arrival counters, the XCD's last arriver adds to the top one)."""
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 500_000, 0xC9, 0, 1), (16, 60_000, 0xCA, 2, 1), (5, 20_000, 0xCB, 1, 2)])
+def test_round2_persistent_tag_wrap(monkeypatch, n, N, seed, lag, K):
+    """The persistent loop's hand-off words carry the iteration's low 8 bits
+    as a tag (k_round2p: a consumer waits for tag == it & 0xFF): loops of
+    more than 256 iterations in one launch reuse every tag, so a stale word
+    from 256 iterations back must never pass for a fresh one (oracle: 317,
+    523 and 897 rounds)."""
     monkeypatch.setenv("BH_ROUND_PERSIST", "1")
-    monkeypatch.setenv("BH_PBAR", "xcd")
     monkeypatch.setenv("BH_SEGMENTS", str(K))
-    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
+    hg = _random_parity(n, N, seed, lag)
+    loops, fallbacks = hg.loop_stats()
     assert loops >= 1 and fallbacks == 0
+    assert hg.stats().last_round > 256 * K
 
 
 @pytest.mark.parametrize("n,N,seed,lag,K", [(128, 30_000, 0xC7, 0, 1), (64, 30_000, 0xC8, 21, 3)])
 def test_round2_persistent_fallback(monkeypatch, n, N, seed, lag, K):
-    """A grid barrier that gives up (BH_PBAR_SPIN=0: at its first poll that
-    finds a workgroup missing) ends the persistent loop with ST_ERR = 3; the
+    """A hand-off wait that gives up (BH_PBAR_SPIN=0: at its first poll that
+    finds a word not yet published) ends the persistent loop with ST_ERR = 3; the
     host restores the loop's inputs and runs one launch per iteration, and
     the results are the oracle's."""
     monkeypatch.setenv("BH_ROUND_PERSIST", "1")
@@ -846,7 +850,7 @@ def test_round2_persistent_fallback(monkeypatch, n, N, seed, lag, K):
 @pytest.mark.parametrize("fallback", [False, True])
 def test_round2_persistent_incremental(monkeypatch, fallback):
     """Per-sync calls through the persistent loop; with fallback, every
-    segment's barrier gives up (BH_PBAR_SPIN=0): the loops after the first
+    segment's hand-off wait gives up (BH_PBAR_SPIN=0): the loops after the first
     failed one leave at once (ST_PFAIL), and each call is recomputed whole
     with one launch per iteration -- state equal to the oracle's after every
     call either way."""
