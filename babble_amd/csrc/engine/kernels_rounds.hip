@@ -1685,7 +1685,26 @@ __global__ __launch_bounds__(1024) void k_round2(Dev d, int p) {
 // beside the segment pipeline's coordinate workgroups, and those never wait
 // for the loop, so every loop workgroup is placed.
 
-template <int PPL>
+// F32 search (round 5): LA and FD entries are integers below 2^24, exact in
+// f32, so #{LA < FD} over two columns is one packed subtract whose clamp
+// output modifier turns each difference FD - LA (an integer) into the
+// indicator [LA < FD] -- v_pk_add_f32 with the clamp bit, which the compiler
+// does not form from fmin/fmax -- and a packed add accumulates the pairs:
+// one instruction per column instead of 2.5 (subtract, shift, 3-way add)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 lt_ind2(f32x2 fd, f32x2 la) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1] clamp" : "=v"(r) : "v"(fd), "v"(la));
+  return r;
+}
+__device__ __forceinline__ f32x2 lo2(int4 v) { return f32x2{__int_as_float(v.x), __int_as_float(v.y)}; }
+__device__ __forceinline__ f32x2 hi2(int4 v) { return f32x2{__int_as_float(v.z), __int_as_float(v.w)}; }
+__device__ __forceinline__ int4 f32_bits4(int4 v) {
+  return make_int4(__float_as_int((float)v.x), __float_as_int((float)v.y), __float_as_int((float)v.z),
+                   __float_as_int((float)v.w));
+}
+
+template <int PPL, bool F32>
 __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   constexpr int LPC = 8;
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
@@ -1735,7 +1754,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   own_loads();
   if (t == 0) sh_fail = 0;
   if (npad > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
-    for (int j = t; j < (npad - n) * HWL; j += nt) win32[(j / (npad - n)) * rs + n + j % (npad - n)] = -1;
+    for (int j = t; j < (npad - n) * HWL; j += nt)
+      win32[(j / (npad - n)) * rs + n + j % (npad - n)] = F32 ? __float_as_int(-1.f) : -1;
   int p = 0;
   // a candidate piece's dwords all carry tag `want` in their top byte
   auto tagged = [](int4 v, uint32_t want) {
@@ -1783,10 +1803,11 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     const int off = (cs + k0) & 3;
     const int rows = min(HWL - off, max(0, len - k0));
     if (wi < n) {
-      win32[(wr4 + 0) * rs + wi] = wv.x;
-      win32[(wr4 + 1) * rs + wi] = wv.y;
-      win32[(wr4 + 2) * rs + wi] = wv.z;
-      win32[(wr4 + 3) * rs + wi] = wv.w;
+      const int4 sv = F32 ? f32_bits4(wv) : wv;
+      win32[(wr4 + 0) * rs + wi] = sv.x;
+      win32[(wr4 + 1) * rs + wi] = sv.y;
+      win32[(wr4 + 2) * rs + wi] = sv.z;
+      win32[(wr4 + 3) * rs + wi] = sv.w;
     }
     if (t < 16) cntk[t] = 0;
     if (t <= HW) hist[t] = 0;
@@ -1813,16 +1834,34 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     unsigned long long rt2 = 0;
     const int32_t bq = (int32_t)(bqr & VMASK24);
 #pragma unroll
-    for (int u = 0; u < PPL; ++u)
+    for (int u = 0; u < PPL; ++u) {
       f[u] = make_int4(f[u].x & VMASK24, f[u].y & VMASK24, f[u].z & VMASK24, f[u].w & VMASK24);
+      if (F32) f[u] = f32_bits4(f[u]);
+    }
     const bool act = q < n && bq < lq;
     auto ss_row = [&](const int4 *x4) {
       int4 x[PPL];
 #pragma unroll
       for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * ((u + rot) & (PPL - 1)), q4 - 1)];
       int lt = 0;
+      if constexpr (F32) {
+        // every indicator pair first, then a tree of packed adds (no
+        // dependent VOP3P back to back)
+        f32x2 a[2 * PPL];
 #pragma unroll
-      for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
+        for (int u = 0; u < PPL; ++u) {
+          a[2 * u] = lt_ind2(lo2(f[u]), lo2(x[u]));
+          a[2 * u + 1] = lt_ind2(hi2(f[u]), hi2(x[u]));
+        }
+#pragma unroll
+        for (int w = 1; w < 2 * PPL; w *= 2)
+#pragma unroll
+          for (int u = 0; u + w < 2 * PPL; u += 2 * w) a[u] += a[u + w];
+        lt = (int)(a[0].x + a[0].y);
+      } else {
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
+      }
       return LPC * PPL * 4 - group_sum<LPC>(lt) >= sm;
     };
     auto probe = [&](const int4 *x4, int slot) {
@@ -1842,7 +1881,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       int lo = 0, hi = rows;
       while (__any(lo < hi)) {
         const int mid = (lo + hi) >> 1;
-        const bool sv = ss_row(w0 + min(mid, rows - 1) * rs4);
+        const bool sv = ss_row(w0 + __mul24(min(mid, rows - 1), rs4));  // (24-bit multiply: full rate)
         if (lo < hi) {
           hi = sv ? mid : hi;
           lo = sv ? lo : mid + 1;
@@ -1899,7 +1938,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
         wr = min(HWL - off2, len - wk);
         __syncthreads();
         if (wi < n) {
-          const int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb2 + wr4));
+          int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb2 + wr4));
+          if (F32) v = f32_bits4(v);
           win32[(wr4 + 0) * rs + wi] = v.x;
           win32[(wr4 + 1) * rs + wi] = v.y;
           win32[(wr4 + 2) * rs + wi] = v.z;
@@ -1971,7 +2011,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // what no workgroup reads inside the loop -- fame's inputs (the new
     // candidate's LA row and its ballots) and the round table
     if (result < len) {
-      if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = win32[lrow * rs + t];
+      if (t < npad)
+        d.cla[cla_row(d, c, r + 1) * npad + t] = F32 ? (int32_t)__int_as_float(win32[lrow * rs + t]) : win32[lrow * rs + t];
       if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
     }
     if (t == 0) d.B[(int64_t)(r + 1) * n + c] = result;
@@ -2037,9 +2078,15 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
 void launch_round_persist(const Dev &d, hipStream_t s) {
   const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
-  if (d.npad <= 32) k_round2p<1><<<d.n, nt, lds, s>>>(d);
-  else if (d.npad <= 64) k_round2p<2><<<d.n, nt, lds, s>>>(d);
-  else k_round2p<4><<<d.n, nt, lds, s>>>(d);
+  if (d.round_f32) {
+    if (d.npad <= 32) k_round2p<1, true><<<d.n, nt, lds, s>>>(d);
+    else if (d.npad <= 64) k_round2p<2, true><<<d.n, nt, lds, s>>>(d);
+    else k_round2p<4, true><<<d.n, nt, lds, s>>>(d);
+  } else {
+    if (d.npad <= 32) k_round2p<1, false><<<d.n, nt, lds, s>>>(d);
+    else if (d.npad <= 64) k_round2p<2, false><<<d.n, nt, lds, s>>>(d);
+    else k_round2p<4, false><<<d.n, nt, lds, s>>>(d);
+  }
 }
 
 // k_round2r (BH_ROUND_SRC=rows, A/B): the round-3 iteration, reading its
@@ -2593,7 +2640,8 @@ void configure_round_kernels() {
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
-  CFG(k_round2p<1>); CFG(k_round2p<2>); CFG(k_round2p<4>);
+  CFG((k_round2p<1, true>)); CFG((k_round2p<2, true>)); CFG((k_round2p<4, true>));
+  CFG((k_round2p<1, false>)); CFG((k_round2p<2, false>)); CFG((k_round2p<4, false>));
   CFG(k_round_solo);
 #undef CFG
 }

@@ -11,7 +11,9 @@ test_gpu_shard.py, test_gpu_comm.py).
 * BH_DIAG=1 with BH_SEG_DEBUG=1 and BH_TIMELINE -- the diagnostic build of
   the kernels (realtime stamps, counters) and the segment pipeline waiting
   for every segment's loop;
-* BH_LOOP_TIMING=0 -- no HIP events around the loop (stage 7 reads 0).
+* BH_LOOP_TIMING=0 -- no HIP events around the loop (stage 7 reads 0);
+* BH_ROUND_F32=0 -- k_round2p's search counting in int32 (sign bits of
+  LA - FD) instead of packed f32 with the clamp modifier (the default).
 """
 import os
 
@@ -74,3 +76,11 @@ def test_loop_timing_off(monkeypatch):
     monkeypatch.setenv("BH_SEGMENTS", "3")
     hg = _random_parity(96, 40_000, 0xD8, 3)
     assert hg.stage_ms()[7] == 0
+
+
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xD9, 0, 3), (100, 40_000, 0xDA, 4, 1), (7, 6_000, 0xDB, 2, 2)])
+def test_round_int32_search(monkeypatch, n, N, seed, lag, K):
+    monkeypatch.setenv("BH_ROUND_F32", "0")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
+    assert loops >= 1 and fallbacks == 0

@@ -79,6 +79,13 @@ def tagged(path):
         scale = 1.0 if name == "polls" else ns / 1000
         unit = "" if name == "polls" else " us"
         print(f"{name:14s} median {np.median(v) * scale:6.2f}{unit}  p90 {np.percentile(v, 90) * scale:6.2f}{unit}")
+    # the work's two phases from the first block (k_round2p: inputs current,
+    # search done, window staged, rows stored): search, then the hand-off
+    # (the new candidate's FD entries counted, its rows stored)
+    a = np.fromfile(path, dtype=np.uint64)[: TL_NR * NC * 4].reshape(TL_NR, NC, 4).astype(np.int64)
+    ok = (a > 0).all(axis=2)
+    for name, v in (("search", (a[:, :, 1] - a[:, :, 0])[ok]), ("hand-off", (a[:, :, 3] - a[:, :, 1])[ok])):
+        print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
 
 
 def barrier(path):
