@@ -1877,9 +1877,12 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     const int4 *w0 = win + off * rs4;
     int32_t res = -1;
     unsigned long long ssb = 0;
+    unsigned long long rs1 = 0, rs2 = 0;  // (BH_DIAG: probes done, histogram complete)
+    int nprobe = 0;
     if (rows > 0) {  // T_q per lane group, then the histogram (k_round2's TQ search)
       int lo = 0, hi = rows;
       while (__any(lo < hi)) {
+        ++nprobe;
         const int mid = (lo + hi) >> 1;
         const bool sv = ss_row(w0 + __mul24(min(mid, rows - 1), rs4));  // (24-bit multiply: full rate)
         if (lo < hi) {
@@ -1887,8 +1890,10 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
           lo = sv ? lo : mid + 1;
         }
       }
+      if (dgt) rs1 = __builtin_amdgcn_s_memrealtime();
       if (act && part == 0 && lo < rows) atomicAdd(&hist[lo], 1);
       __syncthreads();
+      if (dgt) rs2 = __builtin_amdgcn_s_memrealtime();
       if (sh_fail) {  // a workgroup never published: ST_ERR = 3, the host falls back
         if (t == 0) {
           d.state[ST_ERR] = 3;
@@ -2007,6 +2012,13 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       tb[1] = rt0;
       tb[2] = (unsigned long long)polls;
       tb[3] = tl[3];
+      // the search's phases (tools/timeline.py --tagged): wave 0's probes
+      // done, the histogram complete (every wave's probes), probes of wave 0
+      unsigned long long *ts = d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4;
+      ts[0] = rs1;
+      ts[1] = rs2;
+      ts[2] = (unsigned long long)nprobe;
+      ts[3] = rt2;
     }
     // what no workgroup reads inside the loop -- fame's inputs (the new
     // candidate's LA row and its ballots) and the round table

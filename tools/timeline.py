@@ -86,6 +86,18 @@ def tagged(path):
     ok = (a > 0).all(axis=2)
     for name, v in (("search", (a[:, :, 1] - a[:, :, 0])[ok]), ("hand-off", (a[:, :, 3] - a[:, :, 1])[ok])):
         print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
+    # the search's phases (third block): wave 0's probes, the other waves'
+    # (to the histogram barrier), the scan (to the search's end), probe count
+    raw = np.fromfile(path, dtype=np.uint64)
+    off3 = TL_NR * NC * 4 + TL_NR * 512 * 4
+    if raw.size >= off3 + TL_NR * 512 * 4:
+        g = raw[off3: off3 + TL_NR * 512 * 4].reshape(TL_NR, 512, 4).astype(np.int64)[:, :NC]
+        m = ok & (g[:, :, 0] > 0) & (g[:, :, 1] > 0)
+        if m.any():
+            for name, v in (("probes (w0)", (g[:, :, 0] - a[:, :, 0])[m]), ("other waves", (g[:, :, 1] - g[:, :, 0])[m]),
+                            ("scan", (g[:, :, 3] - g[:, :, 1])[m])):
+                print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
+            print(f"{'probe count':14s} median {np.median(g[:, :, 2][m]):6.1f}     p90 {np.percentile(g[:, :, 2][m], 90):6.1f}")
 
 
 def barrier(path):
