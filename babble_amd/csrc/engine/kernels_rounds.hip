@@ -1744,11 +1744,12 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     if (k0 < len) hin.j0 = d.candfd[(int64_t)c * npad + (t >> 3)];
   }
   const int wi = t >> 3, wr4 = 4 * (t & 7);
+  const bool wst = wi < n;
   int4 wv;
   auto own_loads = [&]() {  // chain c's window from k0 and its hand-off rows from j0
     const int32_t rb = (cs + k0) & ~3;
-    wv = wi < n && k0 < len ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
-                            : make_int4(-1, -1, -1, -1);
+    wv = wst && k0 < len ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
+                         : make_int4(-1, -1, -1, -1);
     hand_load(colc, hin);
   };
   own_loads();
@@ -1802,7 +1803,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // wave starts its search as soon as ITS candidates' rows are current
     const int off = (cs + k0) & 3;
     const int rows = min(HWL - off, max(0, len - k0));
-    if (wi < n) {
+    if (wst) {
       const int4 sv = F32 ? f32_bits4(wv) : wv;
       win32[(wr4 + 0) * rs + wi] = sv.x;
       win32[(wr4 + 1) * rs + wi] = sv.y;
@@ -1903,18 +1904,20 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
         }
         break;
       }
-      if (wave == 0) {
+      // every wave: the first row whose prefix count reaches SM -- an
+      // inclusive DPP scan of the bins (row_shr 1, 2, 4, 8 within 16 lanes,
+      // then row_bcast 15 / 31 across them), no second barrier
+      {
         int h = lane < rows ? hist[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int x = __shfl_up(h, o);
-          h += lane >= o ? x : 0;
-        }
+        h += __builtin_amdgcn_update_dpp(0, h, 0x111, 0xF, 0xF, true);  // row_shr:1
+        h += __builtin_amdgcn_update_dpp(0, h, 0x112, 0xF, 0xF, true);  // row_shr:2
+        h += __builtin_amdgcn_update_dpp(0, h, 0x114, 0xF, 0xF, true);  // row_shr:4
+        h += __builtin_amdgcn_update_dpp(0, h, 0x118, 0xF, 0xF, true);  // row_shr:8
+        h += __builtin_amdgcn_update_dpp(0, h, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+        h += __builtin_amdgcn_update_dpp(0, h, 0x143, 0xC, 0xF, false);  // row_bcast:31 into rows 2, 3
         const unsigned long long hit = __ballot(lane < rows && h >= sm);
-        if (lane == 0) hist[HW] = hit ? (int)__builtin_ctzll(hit) : -1;
+        res = hit ? (int)__builtin_ctzll(hit) : -1;
       }
-      __syncthreads();
-      res = hist[HW];
       ssb = __ballot(act && part == 0 && res >= 0 && lo <= res);
     } else {
       __syncthreads();
@@ -1942,7 +1945,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
         const int off2 = cs + wk - rb2;
         wr = min(HWL - off2, len - wk);
         __syncthreads();
-        if (wi < n) {
+        if (wst) {
           int4 v = *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb2 + wr4));
           if (F32) v = f32_bits4(v);
           win32[(wr4 + 0) * rs + wi] = v.x;

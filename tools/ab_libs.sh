@@ -19,7 +19,7 @@ for k in $(seq 1 "$rounds"); do
     fi
     rc=$?
     if [ $rc -ne 0 ]; then echo "$lib failed rc=$rc"; tail -5 "${out%.json}.err"; exit $rc; fi
-    python -c "import json,sys; d=json.load(open('$out')); print('$lib', 'run $k', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],2), 'ms', 'loop', round(d['roofline']['dominant_kernel']['avg_launch_ms']*1e3,2), 'us', d.get('stages_ms'))"
+    python -c "import json,sys; d=json.load(open('$out')); print('$lib', 'run $k', round(d['value']/1e6,2), 'M/s', round(d['ms_per_step'],2), 'ms', 'loop us/round', round(d['roofline']['loop']['us_per_iteration'],3))"
     i=$((i+1))
   done
 done
