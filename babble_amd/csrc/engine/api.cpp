@@ -722,7 +722,9 @@ int segments_for(const Dev &d, int64_t events) {
   // 88.1M at 12; C2, 1M events, 48.6M at 4, 48.3M at 8; C3 equal at 8 and 12)
   // (round 4, persistent loop, C3: with each segment's LT after the next
   // one's columns, 8 segments 188.8M events/s, 16 187.6M, 24 184.1M)
-  int K = !d.fd_cols ? 1 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
+  // (round 5, C3 10M events, segment k holding a 1.38^k share: 38.1-38.4 ms
+  // per step at 10-14 segments against 40.1 at 8 segments of 1.5^k)
+  int K = !d.fd_cols ? 1 : events >= 4000000 ? 12 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>({K, events / 4096 + 1, 64}));
 }
@@ -751,7 +753,11 @@ static void segment_bounds(int64_t base, int64_t N, int K, int64_t *Ns) {
   if (K <= 1) { Ns[1] = N; return; }
   double w[64], tot = 0;
   K = std::min(K, 64);
-  for (int k = 0; k < K; ++k) tot += (w[k] = std::pow(1.5, k));
+  // segment k holds a ratio^k share: a short first segment (the loop waits
+  // for its coordinates) and segments growing about as fast as the loop
+  // outruns the dataflow (BH_SEG_RATIO: A/B)
+  const double ratio = getenv("BH_SEG_RATIO") ? std::max(1.0, atof(getenv("BH_SEG_RATIO"))) : 1.38;
+  for (int k = 0; k < K; ++k) tot += (w[k] = std::pow(ratio, k));
   double acc = 0;
   for (int k = 1; k < K; ++k) {
     acc += w[k - 1];
