@@ -232,9 +232,10 @@ __device__ void bitonic_lds(uint64_t *key, int32_t *id, int32_t p2) {
   for (int32_t k = 2; k <= p2; k <<= 1) {
     for (int32_t j = k >> 1; j > 0; j >>= 1) {
       // comparator c: pair (i, partner) with i = the lower slot
+      const int lj = __builtin_ctz(j);  // (j is a power of 2: shifts, not an integer division per comparator)
       for (int32_t c = t; c < p2 / 2; c += nt) {
-        const int32_t blk = c / j, off = c - blk * j;
-        const int32_t i = blk * 2 * j + off;
+        const int32_t blk = c >> lj, off = c & (j - 1);
+        const int32_t i = (blk << (lj + 1)) + off;
         const int32_t partner = (j == (k >> 1)) ? (i ^ (k - 1)) : (i + j);
         const int32_t lo = min(i, partner), hi = max(i, partner);
         const uint64_t klo = key[lo], khi = key[hi];
