@@ -256,9 +256,19 @@ __device__ void bitonic_lds(uint64_t *key, int32_t *id, int32_t p2) {
   __syncthreads();
 }
 
+// A frame's events span few Lamport timestamps (C3: a median of 72, at most
+// 88 over ~1,575 events), so the frame sorts by counting: a histogram of the
+// timestamps, their prefix, every event scattered into its timestamp's
+// bucket, then its rank inside the bucket by (signature r, id) -- a few
+// dozen LDS compares per event and six workgroup barriers, where the bitonic
+// network took 66 stages over 2,048 slots.  Frames whose timestamps span
+// FS_BUCKETS or more take the bitonic network.
+constexpr int FS_BUCKETS = 1024;
+
 __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char osm[];
   __shared__ unsigned long long sh_ntx, sh_loaded;
+  __shared__ int32_t bend[FS_BUCKETS + 1], sh_lt[2], wsum[16];
   const int32_t f = f0 + (int32_t)blockIdx.x;
   const int32_t cnt = d.frame_cnt[f];
   if (cnt == 0) {
@@ -268,8 +278,79 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
   const int t = threadIdx.x, nt = blockDim.x;
   const int32_t off = d.frame_ofs[f];
   int32_t *ids = d.order + off;
-  if (t == 0) { sh_ntx = 0; sh_loaded = 0; }
+  if (t == 0) { sh_ntx = 0; sh_loaded = 0; sh_lt[0] = INT32_MAX; sh_lt[1] = INT32_MIN; }
+  // the timestamps' range
+  int32_t lmin = INT32_MAX, lmax = INT32_MIN;
   if (cnt <= FRAME_LDS_MAX) {
+    for (int32_t i = t; i < cnt; i += nt) {
+      const int32_t v = d.lt[ids[i]];
+      lmin = min(lmin, v);
+      lmax = max(lmax, v);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lmin = min(lmin, __shfl_xor(lmin, o));
+      lmax = max(lmax, __shfl_xor(lmax, o));
+    }
+    __syncthreads();  // (sh_lt initialised)
+    if ((t & 63) == 0) {
+      atomicMin(&sh_lt[0], lmin);
+      atomicMax(&sh_lt[1], lmax);
+    }
+    __syncthreads();
+    lmin = sh_lt[0];
+    lmax = sh_lt[1];
+  }
+  if (cnt <= FRAME_LDS_MAX && (int64_t)lmax - lmin < FS_BUCKETS) {
+    const int32_t span = lmax - lmin + 1;
+    uint32_t *sk = reinterpret_cast<uint32_t *>(osm);  // bucketed: signature word 0, id, bucket
+    int32_t *sid = reinterpret_cast<int32_t *>(sk + cnt), *sb = sid + cnt;
+    for (int32_t b = t; b <= FS_BUCKETS; b += nt) bend[b] = 0;
+    __syncthreads();
+    for (int32_t i = t; i < cnt; i += nt) atomicAdd(&bend[d.lt[ids[i]] - lmin], 1);
+    __syncthreads();
+    // exclusive prefix of the counts (span <= 1024 = one per thread): DPP
+    // scan per wave, then the waves' totals
+    {
+      const int32_t v = t < span ? bend[t] : 0;
+      int32_t h = v;
+      h += __builtin_amdgcn_update_dpp(0, h, 0x111, 0xF, 0xF, true);  // row_shr:1
+      h += __builtin_amdgcn_update_dpp(0, h, 0x112, 0xF, 0xF, true);  // row_shr:2
+      h += __builtin_amdgcn_update_dpp(0, h, 0x114, 0xF, 0xF, true);  // row_shr:4
+      h += __builtin_amdgcn_update_dpp(0, h, 0x118, 0xF, 0xF, true);  // row_shr:8
+      h += __builtin_amdgcn_update_dpp(0, h, 0x142, 0xA, 0xF, false);  // row_bcast:15
+      h += __builtin_amdgcn_update_dpp(0, h, 0x143, 0xC, 0xF, false);  // row_bcast:31
+      if ((t & 63) == 63) wsum[t >> 6] = h;
+      __syncthreads();
+      int32_t base = 0;
+      for (int w = 0; w < (t >> 6); ++w) base += wsum[w];
+      __syncthreads();  // (every count read before the cursors overwrite them)
+      if (t < span) bend[t] = base + h - v;  // the bucket's cursor: its first position
+    }
+    __syncthreads();
+    for (int32_t i = t; i < cnt; i += nt) {
+      const int32_t e = ids[i], b = d.lt[e] - lmin;
+      const int32_t pos = atomicAdd(&bend[b], 1);  // (order inside the bucket: any)
+      sk[pos] = d.sigw[(int64_t)e * 8];
+      sid[pos] = e;
+      sb[pos] = b;
+    }
+    __syncthreads();
+    // bend[b] now ends bucket b (and starts b + 1): each event's rank among
+    // its bucket by (r, id) -- ByLamportTimestamp.Less within equal timestamps
+    for (int32_t p = t; p < cnt; p += nt) {
+      const int32_t b = sb[p], hi = bend[b], lo = b > 0 ? bend[b - 1] : 0;
+      const uint32_t kp = sk[p];
+      const int32_t ep = sid[p];
+      int32_t rank = 0;
+      for (int32_t q = lo; q < hi; ++q) {
+        const uint32_t kq = sk[q];
+        rank += kq < kp || (kq == kp && q != p && full_less(d, sid[q], ep));
+      }
+      ids[lo + rank] = ep;
+    }
+    __syncthreads();
+  } else if (cnt <= FRAME_LDS_MAX) {
     int32_t p2 = 64;
     while (p2 < cnt) p2 <<= 1;
     uint64_t *key = reinterpret_cast<uint64_t *>(osm);
