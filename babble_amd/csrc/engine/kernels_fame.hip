@@ -206,6 +206,25 @@ __device__ __forceinline__ uint32_t fame_wmask_word(const Dev &d, int j, int w) 
   return m;
 }
 
+// the W(j) chain mask, every thread one chain's bit (a ballot per wave):
+// words [0, NW) of dst, written by the waves' first lanes (2 words a wave;
+// 64 NW threads cover 32 NW chains twice over)
+template <int NW>
+__device__ __forceinline__ void fame_wmask_coop(const Dev &d, int j, uint32_t *dst) {
+  const int q = threadIdx.x;
+  bool bit = false;
+  if (q < d.n) {
+    const int32_t b0 = d.B[(int64_t)j * d.n + q], b1 = d.B[(int64_t)(j + 1) * d.n + q];
+    bit = b0 < d.chain_len[q] && b1 > b0;
+  }
+  const unsigned long long m = __ballot(bit);
+  const int w = 2 * (q >> 6);
+  if ((q & 63) == 0 && w < NW) {
+    dst[w] = (uint32_t)m;
+    if (w + 1 < NW) dst[w + 1] = (uint32_t)(m >> 32);
+  }
+}
+
 // the k_round2 ballots of (chain c, round j) packed into a 128-bit chain mask
 __device__ __forceinline__ uint32_t fame_ballot_word(const unsigned long long *b, int lpc, int w) {
   uint32_t word = 0;
@@ -267,7 +286,7 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   // no loop wrote and the ring does not hold): then la_at
   const bool cy = d.use_cla && r + 1 >= d.r0 && r + 1 > R - d.cla_span;
   const bool cx = d.use_cla && r >= d.r0 && r > R - d.cla_span;
-  if (t < NW) L.wx[t] = fame_wmask_word(d, r, t);
+  fame_wmask_coop<NW>(d, r, L.wx);
   for (int q = t; q < MAXN; q += nt) {
     L.dec[q] = 0;
     L.nd[q] = 0;
@@ -295,17 +314,31 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
   int cur = 0;
   if (r + 1 < R) {
     // ---- j = r+1: vote(y, x) = see(y, x) ----
-    if (t < NW) L.wc[t] = fame_wmask_word(d, r + 1, t);
+    fame_wmask_coop<NW>(d, r + 1, L.wc);
     __syncthreads();
     {
       const int xc = min(x, n - 1);
       for (int k = 0; k < HW_; ++k) {
+        // the word's 32 voters' LA entries loaded together (independent
+        // gathers in flight), then compared
+        const uint32_t wk = (h * HY + k * 32) < n ? L.wc[(h * HY + k * 32) >> 5] : 0u;
         uint32_t v = 0;
-        for (int b = 0; b < 32; ++b) {
-          const int y = h * HY + k * 32 + b;
-          if (y >= n || !((L.wc[y >> 5] >> (y & 31)) & 1u)) continue;
-          const int32_t a = cy ? d.cla[(int64_t)L.yev[y] * npad + xc] : la_at(d, L.yev[y], xc);
-          if (a >= L.xk[xc]) v |= 1u << b;
+        if (cy) {
+          int32_t a[32];
+#pragma unroll
+          for (int b = 0; b < 32; ++b) {
+            const int y = min(h * HY + k * 32 + b, n - 1);
+            a[b] = (wk >> b & 1u) ? d.cla[(int64_t)L.yev[y] * npad + xc] : INT32_MIN;
+          }
+#pragma unroll
+          for (int b = 0; b < 32; ++b)
+            if (a[b] >= L.xk[xc] && (wk >> b & 1u)) v |= 1u << b;
+        } else {
+          for (int b = 0; b < 32; ++b) {
+            const int y = h * HY + k * 32 + b;
+            if (y >= n || !(wk >> b & 1u)) continue;
+            if (la_at(d, L.yev[y], xc) >= L.xk[xc]) v |= 1u << b;
+          }
         }
         L.V[0][h * HW_ + k][x] = v;
       }
@@ -314,10 +347,9 @@ __global__ __launch_bounds__(64 * NW) void k_fame_masks(Dev d, int32_t R, int32_
     // ---- j >= r+2 ----
     for (int j = r + 2; j < R; ++j) {
       if (L.misc[0] == 0) break;
-      if (t < NW) {
-        L.wp[t] = L.wc[t];
-        L.wc[t] = fame_wmask_word(d, j, t);
-      }
+      if (t < NW) L.wp[t] = L.wc[t];
+      __syncthreads();  // (wc read into wp before it is rewritten)
+      fame_wmask_coop<NW>(d, j, L.wc);
       __syncthreads();
       for (int y = t; y < n; y += nt) {
         const bool isy = (L.wc[y >> 5] >> (y & 31)) & 1u;
