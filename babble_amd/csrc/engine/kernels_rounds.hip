@@ -1711,6 +1711,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   __shared__ int32_t cntk[16];
   __shared__ int32_t hist[HW + 1];
   __shared__ int32_t sh_fail;
+  __shared__ uint32_t sh_cur;  // (BH_DIAG: the last wave's inputs-current time this round, low 32 bits)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x;
   // the segment pipeline enqueues every segment's loop without a host round
@@ -1812,6 +1813,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     }
     if (t < 16) cntk[t] = 0;
     if (t <= HW) hist[t] = 0;
+    if (t == 0) sh_cur = 0;
     __syncthreads();
     const unsigned long long rt1 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
     if (it > 0) {
@@ -1832,6 +1834,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       }
     }
     const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (d.diag != nullptr && lane == 0) atomicMax(&sh_cur, (uint32_t)__builtin_amdgcn_s_memrealtime());
     unsigned long long rt2 = 0;
     const int32_t bq = (int32_t)(bqr & VMASK24);
 #pragma unroll
@@ -2020,7 +2023,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       unsigned long long *ts = d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4;
       ts[0] = rs1;
       ts[1] = rs2;
-      ts[2] = (unsigned long long)nprobe;
+      ts[2] = (unsigned long long)nprobe | (unsigned long long)(sh_cur - (uint32_t)rt0) << 32;
       ts[3] = rt2;
     }
     // what no workgroup reads inside the loop -- fame's inputs (the new

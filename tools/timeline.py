@@ -97,7 +97,11 @@ def tagged(path):
             for name, v in (("probes (w0)", (g[:, :, 0] - a[:, :, 0])[m]), ("other waves", (g[:, :, 1] - g[:, :, 0])[m]),
                             ("scan", (g[:, :, 3] - g[:, :, 1])[m])):
                 print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
-            print(f"{'probe count':14s} median {np.median(g[:, :, 2][m]):6.1f}     p90 {np.percentile(g[:, :, 2][m], 90):6.1f}")
+            pc = g[:, :, 2][m] & 0xFFFFFFFF
+            spread = (g[:, :, 2][m] >> 32).astype(np.int64)
+            print(f"{'probe count':14s} median {np.median(pc):6.1f}     p90 {np.percentile(pc, 90):6.1f}")
+            if spread.any():
+                print(f"{'waves current':14s} median {np.median(spread) * ns / 1000:6.2f} us  p90 {np.percentile(spread, 90) * ns / 1000:6.2f} us  (last wave's inputs current - wave 0's)")
 
 
 def barrier(path):
