@@ -772,10 +772,15 @@ inline void split_cols(const bh_handle *h, int32_t rank, int64_t *c0, int64_t *c
   shard_range(h->d.n, h->world - 1, rank - 1, c0, c1);
 }
 
-// the split runs on the n <= 128 chain dataflow (k_flow32 + k_round2);
-// every shard decides it alike from its (identical) host tables
+// the split runs on the chain dataflows: n <= 128 (k_flow32 + k_round2p)
+// and 128 < n <= 512 (k_floww2 on the coordinate shards; shard 0 transposes
+// each segment for the 16-bit k_round_wide); every shard decides it alike
+// from its (identical) host tables
 bool split_active(const bh_handle *h) {
-  return h->split && !h->reset_on && h->d.N > 0 && bh::flow_eligible(h->d) && bh::flow32_eligible(h->d) &&
+  const Dev &d = h->d;
+  const bool narrow = bh::flow_eligible(d) && bh::flow32_eligible(d);
+  const bool wide = !d.fd_cols && bh::floww_eligible(d) && bh::round_p16(d);
+  return h->split && !h->reset_on && d.N > 0 && (narrow || wide) &&
          !(getenv("BH_SWEEP") && !strcmp(getenv("BH_SWEEP"), "chunk"));
 }
 
@@ -884,6 +889,7 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
   dv.col0 = (int32_t)c0;
   dv.ncol = (int32_t)(c1 - c0);
   dv.flow_lt = x->rank == 1;
+  const bool wide = !dv.fd_cols;  // 128 < n <= 512: k_floww2
   size_t bytes = 0;
   for (int k = 0; k < p.K; ++k) bytes += p.block_bytes(x, k, x->rank);
   int rc;
@@ -902,8 +908,14 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
     v.e0 = p.Ns[(size_t)k];
     v.rows = x->layout_rows;
     v.tile_list = nullptr;
-    bh::launch_flow_desc(v, sc);
-    if (dv.ncol > 0 || dv.flow_lt) bh::launch_flow(v, sc);
+    if (wide) {
+      // k_floww2 over the shard's columns (its LT value as well: every
+      // workgroup set carries one; only rank 1's travels)
+      if (dv.ncol > 0) bh::launch_floww(v, sc);
+    } else {
+      bh::launch_flow_desc(v, sc);
+      if (dv.ncol > 0 || dv.flow_lt) bh::launch_flow(v, sc);
+    }
     const bh::SplitBlock b = p.block(x, k, x->rank, x->xbuf + off);
     bh::launch_split_pack(v, p.dpq(x, k), b, sc);
     const size_t bb = p.block_bytes(x, k, x->rank);
@@ -921,7 +933,7 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
   x->lens_coord = x->lens_h;
   x->inc_valid = true;
   x->rows_stale = true;
-  x->sweep_kernel = bh::flow_kernel(dv);
+  x->sweep_kernel = wide ? bh::floww_kernel(dv) : bh::flow_kernel(dv);
   return BH_OK;
 }
 
@@ -950,8 +962,11 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   d.wide_cols = wide && !sp && !h->reset_on && !wide_rows_env && !eager_env && bh::round_p16(d) && d.cla && d.n <= 512;
   // BH_WIDE_COLS=2 (A/B): the window from the transposed row-major LA, the hand-off from la_col
   if (d.wide_cols && atoi(getenv("BH_WIDE_COLS")) == 2) d.wide_cols = 2;
-  const bool eager = !sp && ((wide && d.wide_cols != 1) || h->reset_on || eager_env || bh::round_solo_eligible(d) ||
-                             d.round_src_rows);
+  // (the wide split: shard 0 transposes each received segment for the
+  // row-major loop)
+  const bool eager = sp ? wide
+                        : ((wide && d.wide_cols != 1) || h->reset_on || eager_env || bh::round_solo_eligible(d) ||
+                           d.round_src_rows);
   d.use_cla = (d.fd_cols || d.wide_cols) && !bh::round_solo_eligible(d);
   if (sp) d.round_src_rows = 0;  // the split ships the column-major LA only
   if (base > 0 && eager && h->rows_stale) {
@@ -1015,6 +1030,24 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     v.rows = h->layout_rows;
     return v;
   };
+  // the 64-row tiles holding segment k's rows (the transpose's work list):
+  // each chain's run [start + lo, start + hi), in layout order, shared
+  // boundary tiles once (eager runs wait for each loop: the staging's two
+  // halves cannot be overtaken)
+  auto tiles = [&](int k, const int32_t *lo, const int32_t *hi, Dev &v) -> int {
+    int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
+    int64_t nt = 0;
+    for (int c = 0; c < n; ++c) {
+      if (hi[c] <= lo[c]) continue;
+      const int64_t a = ((int64_t)h->cstart_h[(size_t)c] + lo[c]) >> 6, b = ((int64_t)h->cstart_h[(size_t)c] + hi[c] - 1) >> 6;
+      for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
+    }
+    int32_t *dtl = h->tlist + (size_t)(k & 1) * h->tlist_cap;
+    if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
+    v.tile_list = dtl;
+    v.ntiles = nt;
+    return BH_OK;
+  };
   size_t xoff = 0;  // the receive buffer's next block
   auto receive = [&](int k) -> int {  // the split: segment k's columns from the coordinate shards
     Dev v = view(k);
@@ -1051,6 +1084,14 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
     for (int r = 1; r < h->world; ++r) bh::launch_split_unpack(v, sp->dpq(h, k), blk[(size_t)r], sc);
     bh::launch_lt_rows(v, sc);
+    if (eager) {
+      // the wide loop reads the row-major LA and FDT: the segment's rows
+      // transposed here, from the columns just unpacked
+      const int32_t *lo = sp->tab.data() + (size_t)k * 2 * n;
+      if ((rc = tiles(k, lo, lo + n, v))) return rc;
+      bh::launch_flow_transpose(v, sc);
+      bh::launch_fd_idle(v, sc);
+    }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));
     if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));
@@ -1084,21 +1125,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     HIPCHK(h, hipMemcpyAsync(v.seg_lo, stg, (size_t)2 * n * 4, hipMemcpyHostToDevice, sc));
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sc));  // the segment's lengths are on the device
     if (eager) {
-      // the 64-row tiles holding the segment's rows (the transpose's work
-      // list): each chain's run [start + lo, start + hi), in layout order,
-      // shared boundary tiles once (eager runs wait for each loop: the
-      // staging's two halves cannot be overtaken)
-      int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
-      int64_t nt = 0;
-      for (int c = 0; c < n; ++c) {
-        if (stg[n + c] <= stg[c]) continue;
-        const int64_t a = ((int64_t)h->cstart_h[(size_t)c] + stg[c]) >> 6, b = ((int64_t)h->cstart_h[(size_t)c] + stg[n + c] - 1) >> 6;
-        for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
-      }
-      int32_t *dtl = h->tlist + (size_t)(k & 1) * h->tlist_cap;
-      if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
-      v.tile_list = dtl;
-      v.ntiles = nt;
+      if ((rc = tiles(k, stg, stg + n, v))) return rc;
     } else {
       v.tile_list = nullptr;
       v.ntiles = 0;
@@ -1401,7 +1428,13 @@ int rounds_split_stage(bh_handle *h) {
     if (h0) h0->stage = std::max(h0->stage, 1);
     return BH_OK;
   }
-  const SplitPlan plan = split_plan(sh[0], segments_for(sh[0]->d, N - base), base);
+  // the wide split pipelines as well: k_floww2 runs on the coordinate
+  // shards, so shard 0's loop over segment k no longer shares its compute
+  // units with the dataflow of segment k + 1 (segments_for keeps the
+  // unsplit wide path at one segment for that reason)
+  int K = segments_for(sh[0]->d, N - base);
+  if (!sh[0]->d.fd_cols && !getenv("BH_SEGMENTS")) K = N - base >= 1000000 ? 4 : 1;
+  const SplitPlan plan = split_plan(sh[0], K, base);
   // the coordinate shards' work first: shard 0's receive waits on it
   for (bh_handle *x : sh) {
     if (x->rank == 0) continue;
@@ -1701,9 +1734,9 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out);
 void bh_destroy(bh_handle *h);
 
 // How a group shares the coordinates (BH_SHARD_COORDS):
-//   split (2, the default where it applies: n <= 128) -- shard 0 runs the
-//     round loop, fame and order; the other shards compute LA columns and
-//     ship them to it per segment (kernels_split.hip);
+//   split (2, the default at n <= 128; BH_SHARD_COORDS=split above it) --
+//     shard 0 runs the round loop, fame and order; the other shards compute
+//     LA columns and ship them to it per segment (kernels_split.hip);
 //   columns (1) -- every shard computes a range of LA columns, all-gathered;
 //   replicate (0, the default above n = 128) -- every shard computes all of
 //     it; fame rounds and frame sorts are split.
@@ -1711,6 +1744,7 @@ static int shard_mode(int n) {
   const char *e = getenv("BH_SHARD_COORDS");
   if (e && !strcmp(e, "columns")) return 1;
   if (e && !strcmp(e, "replicate")) return 0;
+  if (e && !strcmp(e, "split")) return 2;  // (n > 128 as well: the wide split)
   return n <= bh::FL_MAXN ? 2 : 0;
 }
 

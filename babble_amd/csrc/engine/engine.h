@@ -31,6 +31,7 @@ constexpr int P8_XMAX = 126;  // largest window-relative LA of k_round_wide's 8-
 constexpr int SCAN_WIN = 32;            // rows per round-boundary scan window
 constexpr int FRAME_LDS_MAX = 8192;     // frames sorted in LDS up to this size (96 KiB)
 constexpr int FL_MAXN = 128;            // participants the dataflow sweep (k_flow) handles
+constexpr int FW_MAXN = 512;            // participants the wide dataflow (k_floww2) handles
 
 enum StateSlot {
   ST_CUR0 = 0,     // round r of the iteration with parity 0 (ST_CUR0 + 1: parity 1)

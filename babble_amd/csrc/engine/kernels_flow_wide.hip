@@ -28,7 +28,6 @@
 
 namespace bh {
 
-constexpr int FW_MAXN = 512;
 constexpr int FW_R = 32, FW_RS = FW_R + 1;    // value-ring slots per chain (+1 pad)
 constexpr int FW_DR = 32, FW_DRS = FW_DR + 1;  // descriptor-ring entries per chain
 constexpr int FW_REFILL = 16;                  // entries per descriptor refill

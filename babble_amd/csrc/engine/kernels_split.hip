@@ -1,7 +1,7 @@
 // kernels_split.hip -- the coordinate split across shards.
 //
-// Shards 1 .. G-1 ("coordinate shards") run the chain dataflow (k_flow32) for
-// a range of LA columns each; shard 0 runs the round loop, fame and order,
+// Shards 1 .. G-1 ("coordinate shards") run the chain dataflow (k_flow32 at
+// n <= 128, k_floww2 up to 512) for a range of LA columns each; shard 0 runs the round loop, fame and order,
 // and computes no coordinates.  Per pipeline segment a coordinate shard packs
 // the segment's rows of its columns of la_col and ships them to shard 0,
 // which unpacks them into its own la_col before the segment's round loop.
@@ -54,7 +54,7 @@ __device__ __forceinline__ void split_tables(const int32_t *pq, int n, int32_t *
 
 // chunk headers: one thread per (column, chunk); grid (chunks / 256, ncol)
 __global__ __launch_bounds__(256) void k_split_hdr(Dev v, const int32_t *pq, SplitBlock b) {
-  __shared__ int32_t P[FL_MAXN + 1], Q[FL_MAXN + 1];
+  __shared__ int32_t P[FW_MAXN + 1], Q[FW_MAXN + 1];
   const int n = v.n;
   split_tables(pq, n, P, Q);
   const int32_t q = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_split_hdr(Dev v, const int32_t *pq, Spl
 // payload: one thread per (column, packed index); grid (S / 256, ncol); the
 // LT owner's block also carries the segment's LT rows (blockIdx.y == ncol)
 __global__ __launch_bounds__(256) void k_split_pack(Dev v, const int32_t *pq, SplitBlock b) {
-  __shared__ int32_t P[FL_MAXN + 1], Q[FL_MAXN + 1];
+  __shared__ int32_t P[FW_MAXN + 1], Q[FW_MAXN + 1];
   const int n = v.n;
   split_tables(pq, n, P, Q);
   const int32_t x = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -108,17 +108,18 @@ __global__ __launch_bounds__(256) void k_split_pack(Dev v, const int32_t *pq, Sp
 // shard 0: a block into la_col columns [c0, c0 + ncol) (and lt_row);
 // grid (S / 256, ncol [+ 1])
 __global__ __launch_bounds__(256) void k_split_unpack(Dev v, const int32_t *pq, SplitBlock b) {
-  __shared__ int32_t P[FL_MAXN + 1], Q[FL_MAXN + 1];
+  __shared__ int32_t P[FW_MAXN + 1], Q[FW_MAXN + 1];
   const int n = v.n;
   split_tables(pq, n, P, Q);
   const int32_t x = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
   const int col = (int)blockIdx.y;
   if (x == 0 && col == 0) {
     // the sender's flags: overflow slots exhausted (the call is recomputed
-    // unsplit, ST_FLOWOVF = 2 as a dataflow watchdog), LT beyond k_flow32's
-    // range (the LT fallback, 1)
+    // unsplit, ST_FLOWOVF = 2 as a dataflow watchdog), and the sender's own
+    // ST_FLOWOVF -- 1: LT beyond the dataflow's range (the LT fallback), 2:
+    // its dataflow's watchdog (unfinished columns: recomputed unsplit)
     if (b.err[0]) atomicMax(&v.state[ST_FLOWOVF], 2);
-    if (b.err[1]) atomicMax(&v.state[ST_FLOWOVF], 1);
+    if (b.err[1]) atomicMax(&v.state[ST_FLOWOVF], min(b.err[1], 2));
   }
   if (x >= b.S) return;
   const int c = split_chain(P, n, x);
@@ -164,7 +165,9 @@ void launch_split_pack(const Dev &v, const int32_t *pq, const SplitBlock &b, hip
   if (b.S > 0 && b.ncol > 0) k_split_hdr<<<dim3((unsigned)((b.NQ + 255) / 256), (unsigned)b.ncol), 256, 0, s>>>(v, pq, b);
   const unsigned ny = (unsigned)(b.ncol + (b.lt_on ? 1 : 0));
   if (b.S > 0 && ny) k_split_pack<<<dim3((unsigned)((b.S + 255) / 256), ny), 256, 0, s>>>(v, pq, b);
-  if (b.lt_on) (void)hipMemcpyAsync(b.err + 1, v.state + ST_FLOWOVF, 4, hipMemcpyDeviceToDevice, s);
+  // every sender's dataflow flags travel (a watchdog on any shard leaves its
+  // columns unfinished)
+  (void)hipMemcpyAsync(b.err + 1, v.state + ST_FLOWOVF, 4, hipMemcpyDeviceToDevice, s);
 }
 
 void launch_split_unpack(const Dev &v, const int32_t *pq, const SplitBlock &b, hipStream_t s) {

@@ -40,6 +40,7 @@ def _free_port():
     ("split", 3, 64, 50_000, 21, 4, 10_000, {}),
     ("split", 3, 32, 30_000, 4, 3, 10_000, {"BH_SPLIT_RANGE": "2"}),  # overflow: rank 0 unsplit, sends matched
     ("split", 2, 96, 40_000, 3, 3, 8_000, {"BH_ROUND_PERSIST": "0"}),  # loops that wait per segment
+    ("split", 3, 160, 30_000, 2, 3, 10_000, {}),  # the wide split: k_floww2 on ranks 1-2, transposes on rank 0
     ("replicate", 2, 64, 40_000, 3, 3, 10_000, {}),
     ("columns", 2, 32, 30_000, 0, 1, 15_000, {}),
 ])

@@ -6,7 +6,9 @@ bit for bit: the coordinate split (the default at n <= 128: shard 0 runs the
 round loop, fame and order; the other shards compute LA columns and ship
 them per segment), LA columns all-gathered (BH_SHARD_COORDS=columns) or
 replicated coordinates with fame by round ranges and frames sorted by
-range (BH_SHARD_COORDS=replicate)."""
+range (BH_SHARD_COORDS=replicate).  The split at 128 < n <= 512 (k_floww2 on
+the coordinate shards, shard 0 transposing each received segment) is opt-in
+(BH_SHARD_COORDS=split)."""
 import numpy as np
 import pytest
 
@@ -202,3 +204,84 @@ def test_split_overflow_chunks(monkeypatch, rng):
     assert not grp.insert_dag(d).any()
     grp.run_consensus()
     _compare(o, grp, f"split, range {rng}")
+
+
+@pytest.mark.parametrize("devs,K", [([0, 0], 3), ([0, 0, 0, 0], 4)])
+@pytest.mark.parametrize("n,N,seed,lag,step", [(160, 30_000, 101, 2, 10_000), (512, 40_000, 102, 0, 20_000)])
+def test_wide_split_pipeline_incremental(monkeypatch, devs, K, n, N, seed, lag, step):
+    """The coordinate split at 128 < n <= 512 (BH_SHARD_COORDS=split): the
+    coordinate shards run k_floww2 over their LA column ranges and ship each
+    segment's packed columns (rank 1 also LT); shard 0 unpacks them,
+    transposes the segment into the row-major LA and FDT and runs the 16-bit
+    k_round_wide on it -- through the segment pipeline and incremental calls,
+    equal to the oracle after every call."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    from test_gpu_schedule import _wire_batches
+    monkeypatch.setenv("BH_SHARD_COORDS", "split")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    d = Dag(n, N, seed, lagging=lag, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    grp = Hashgraph(d.participant_ids, N, devices=devs)
+    batch = _wire_batches(d)
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        o.run_consensus()
+        assert not np.asarray(grp.insert_events(*batch(lo, hi))).any()
+        grp.run_consensus()
+        _compare(o, grp, f"wide split {len(devs)} shards n={n} after [0, {hi})")
+        assert 1 <= grp.pipeline()[0] <= K
+        assert grp.stage_ms()[5] > 0  # the receive windows
+    assert grp.pipeline()[1] >= N // step - 2
+
+
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0, 0]])
+def test_wide_split_matches_single(monkeypatch, devs):
+    """A whole DAG at n = 512 through the wide split (default segment count:
+    one below 1M events) and then bh_reset_consensus + RunConsensus again
+    (the state bench.py times): equal to the single-shard engine and to the
+    oracle."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    n, N = 512, 60_000
+    d = Dag(n, N, 103, sig_mode=0)
+    one = Hashgraph(d.participant_ids, N)
+    assert not one.insert_dag(d).any()
+    one.run_consensus()
+    monkeypatch.setenv("BH_SHARD_COORDS", "split")
+    grp = Hashgraph(d.participant_ids, N, devices=devs)
+    assert not grp.insert_dag(d).any()
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    for run in range(2):
+        if run:
+            grp.reset_consensus()
+        grp.run_consensus()
+        _same_engine(one, grp, f"wide split {len(devs)} shards, run {run}")
+        _compare(o, grp, f"wide split vs oracle, run {run}")
+        assert grp.stage_ms()[5] > 0
+
+
+@pytest.mark.parametrize("knob,val", [("BH_FLOWW_WATCHDOG", "-1"), ("BH_FLOW_LTCLAMP", "300")])
+def test_wide_split_flags(monkeypatch, knob, val):
+    """A coordinate shard's dataflow flags reach shard 0 in its block: the
+    k_floww2 watchdog (unfinished columns: the call is recomputed unsplit on
+    shard 0) and LT past the dataflow's clamp (the chunked sweep recomputes
+    LT) -- either way the oracle's result."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_SHARD_COORDS", "split")
+    monkeypatch.setenv("BH_SEGMENTS", "3")
+    monkeypatch.setenv(knob, val)  # (read at handle creation)
+    n, N = 160, 20_000
+    d = Dag(n, N, 104, lagging=2, sig_mode=0)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o.run_consensus()
+    grp = Hashgraph(d.participant_ids, N, devices=[0, 0, 0])
+    assert not grp.insert_dag(d).any()
+    grp.run_consensus()
+    _compare(o, grp, f"wide split, {knob}={val}")
