@@ -47,6 +47,7 @@ void free_all(bh_handle *h) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (h->pinned_state) (void)hipHostFree(h->pinned_state);
+  if (h->pin_rd) (void)hipHostFree(h->pin_rd);
   if (h->sha_buf) (void)hipFree(h->sha_buf);
   if (h->q_buf) (void)hipFree(h->q_buf);
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
@@ -80,6 +81,8 @@ void free_all(bh_handle *h) {
 }
 
 // upload events inserted since the last upload
+hipError_t wait_stream(hipStream_t s);
+
 int upload(bh_handle *h) {
   const int64_t a = h->uploaded, b = (int64_t)h->h_creator.size();
   if (b == a) return BH_OK;
@@ -101,11 +104,17 @@ int upload(bh_handle *h) {
     if (h->fr.oth_of)
       HIPCHK(h, hipMemcpyAsync(h->fr.oth_of + a, h->h_oth.data() + a, k * 4, hipMemcpyHostToDevice, s));
   }
-  HIPCHK(h, hipStreamSynchronize(s));
+  HIPCHK(h, wait_stream(s));
   h->h_hash.clear();
   h->uploaded = b;
   return BH_OK;
 }
+
+// A host wait for stream s.  (Spinning on hipStreamQuery instead woke the
+// host ~50 us sooner after the round loop, but measured no faster per C3
+// step on one box, same-box A/B: profiles/r5_ab_spin.txt -- so the host
+// sleeps in hipStreamSynchronize)
+hipError_t wait_stream(hipStream_t s) { return hipStreamSynchronize(s); }
 
 // A blocking copy ordered on stream s.  The passes never touch the legacy
 // stream: the shards of an in-process group run on threads of their own, and
@@ -113,7 +122,39 @@ int upload(bh_handle *h) {
 // device fails ("would make the legacy stream depend on a capturing stream")
 hipError_t copy_sync(hipStream_t s, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
   hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
-  return e == hipSuccess ? hipStreamSynchronize(s) : e;
+  return e == hipSuccess ? wait_stream(s) : e;
+}
+
+// A pass's device-to-host reads behind one synchronisation: rd_async
+// enqueues each into pinned staging on s, rd_wait synchronises s once and
+// copies them out (~20 us per pageable read otherwise: each is a blocking
+// staged copy of its own)
+int rd_wait(bh_handle *h, hipStream_t s) {
+  HIPCHK(h, wait_stream(s));
+  for (const auto &r : h->pin_rd_list) memcpy(r.dst, h->pin_rd + r.off, r.bytes);
+  h->pin_rd_list.clear();
+  h->pin_rd_used = 0;
+  return BH_OK;
+}
+
+int rd_async(bh_handle *h, hipStream_t s, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return BH_OK;
+  const size_t need = ((h->pin_rd_used + 63) & ~(size_t)63) + bytes;
+  if (need > h->pin_rd_cap) {
+    int rc;
+    if (!h->pin_rd_list.empty() && (rc = rd_wait(h, s))) return rc;  // (drain before the buffer moves)
+    const size_t cap = std::max<size_t>(need + need / 2, 1 << 16);
+    if (h->pin_rd) (void)hipHostFree(h->pin_rd);
+    h->pin_rd = nullptr;
+    h->pin_rd_cap = 0;
+    HIPCHK(h, hipHostMalloc((void **)&h->pin_rd, cap, hipHostMallocDefault));
+    h->pin_rd_cap = cap;
+  }
+  const size_t off = (h->pin_rd_used + 63) & ~(size_t)63;
+  HIPCHK(h, hipMemcpyAsync(h->pin_rd + off, src, bytes, hipMemcpyDeviceToHost, s));
+  h->pin_rd_list.push_back({dst, off, bytes});
+  h->pin_rd_used = off + bytes;
+  return BH_OK;
 }
 
 // Chain-major layout: chain c's events occupy rows [chain_start[c],
@@ -158,7 +199,7 @@ int set_chain_tables(bh_handle *h) {
   h->d.max_chain_len = mx;
   h->lens_h = len;
   HIPCHK(h, hipMemcpyAsync(h->d.chain_len, h->lens_h.data(), n * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   return BH_OK;
 }
 
@@ -359,7 +400,7 @@ int exchange(bh_handle *h, Sel sel, const std::vector<size_t> &off, const std::v
         return rc;
       }
     if ((rc = h->xport->group_end(h))) return rc;
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, wait_stream(h->stream));
   } else {
     const size_t G = h->group.size();
     std::vector<hipEvent_t> ready(G);
@@ -383,7 +424,7 @@ int exchange(bh_handle *h, Sel sel, const std::vector<size_t> &off, const std::v
     }
     for (size_t t = 0; t < G; ++t) {
       HIPCHK(h, hipSetDevice(h->group[t]->device));
-      HIPCHK(h, hipStreamSynchronize(h->group[t]->stream));
+      HIPCHK(h, wait_stream(h->group[t]->stream));
       (void)hipEventDestroy(ready[t]);
     }
     HIPCHK(h, hipSetDevice(h->device));
@@ -506,7 +547,7 @@ int build_rows(bh_handle *h, const std::vector<int32_t> &upto, hipStream_t s) {
   if (!inc || v.ntiles > 0) bh::launch_flow_transpose(v, s);
   bh::launch_fd_idle(v, s);
   HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipStreamSynchronize(s));
+  HIPCHK(h, wait_stream(s));
   h->rows_lens = upto;
   h->rows_built = true;
   h->rows_stale = false;
@@ -570,7 +611,7 @@ int rounds_loop(bh_handle *h) {
   if (wide_flow) {  // k_floww's watchdog (ST_FLOWOVF = 2): the chunked sweep instead
     int32_t ovf = 0;
     HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipStreamSynchronize(s));
+    HIPCHK(h, wait_stream(s));
     if (ovf == 2 && h->reset_on) {
       // the watchdog counts stalled headers, not a proven deadlock (other
       // work sharing the compute units can starve a wave): the Reset
@@ -580,7 +621,7 @@ int rounds_loop(bh_handle *h) {
       int rc2 = reset_coords(h, s);
       if (rc2) return rc2;
       HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(h, hipStreamSynchronize(s));
+      HIPCHK(h, wait_stream(s));
     }
     if (ovf && h->reset_on)
       return h->fail(BH_ERR_CAPACITY, ovf == 2 ? "the wide dataflow gave up twice on a Reset hashgraph"
@@ -626,7 +667,7 @@ int rounds_loop(bh_handle *h) {
     if (getenv("BH_FIAT_DEBUG")) {
       int32_t fs[4] = {0, 0, 0, 0};
       HIPCHK(h, hipMemcpyAsync(fs, d.state + bh::ST_FIATMAX, 16, hipMemcpyDeviceToHost, s));
-      HIPCHK(h, hipStreamSynchronize(s));
+      HIPCHK(h, wait_stream(s));
       fprintf(stderr, "[k_fiat] max round %d, chains done %d of %d, events visited %d, chunks %d (r0 %d)\n", fs[0], fs[1],
               d.n, fs[2], fs[3], d.r0);
       if (d.diag) {
@@ -686,8 +727,8 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[2], s));
   h->wofs_h.resize((size_t)h->R + 1);
-  HIPCHK(h, hipMemcpyAsync(h->wofs_h.data(), d.wofs, ((size_t)h->R + 1) * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(h, hipStreamSynchronize(s));
+  int rc;
+  if ((rc = rd_async(h, s, h->wofs_h.data(), d.wofs, ((size_t)h->R + 1) * 4)) || (rc = rd_wait(h, s))) return rc;
   h->n_div = d.N;
   // rounds new to this call join PendingRounds undecided (hashgraph.go:809-815;
   // every round >= LastConsensusRound is queued when it first appears)
@@ -785,11 +826,25 @@ bool split_active(const bh_handle *h) {
 }
 
 // per-chain prefix lengths at an insertion-order boundary (ids of a chain
-// ascend with its index)
+// ascend with its index); bounds at or below the events inserted so far
+// are kept (lens_memo)
 void chain_lens_at(const bh_handle *h, int64_t bound, int32_t *out) {
-  for (int c = 0; c < h->d.n; ++c) {
+  const int n = h->d.n;
+  const bool keep = bound <= (int64_t)h->h_creator.size();
+  if (keep) {
+    const auto it = h->lens_memo.find(bound);
+    if (it != h->lens_memo.end() && (int)it->second.size() == n) {
+      std::copy(it->second.begin(), it->second.end(), out);
+      return;
+    }
+  }
+  for (int c = 0; c < n; ++c) {
     const auto &ch = h->chain[(size_t)c];
     out[c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)std::min<int64_t>(bound, INT32_MAX)) - ch.begin());
+  }
+  if (keep) {
+    if (h->lens_memo.size() >= 1024) h->lens_memo.clear();
+    h->lens_memo[bound].assign(out, out + n);
   }
 }
 
@@ -861,7 +916,7 @@ int split_prepare(bh_handle *x, const SplitPlan &p, size_t bytes) {
   }
   HIPCHK(x, copy_sync(x->stream, x->xseg, p.tab.data(), p.tab.size() * 4, hipMemcpyHostToDevice));
   if (bytes > x->xcap) {
-    HIPCHK(x, hipStreamSynchronize(x->stream2));
+    HIPCHK(x, wait_stream(x->stream2));
     if (x->xbuf) (void)hipFree(x->xbuf);
     x->xbuf = nullptr;
     x->xcap = 0;
@@ -1009,12 +1064,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   std::vector<int64_t> Ns((size_t)K + 1, base);
   segment_bounds(base, N, K, Ns.data());
   // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
-  auto lens_at = [&](int64_t bound, int32_t *out) {
-    for (int c = 0; c < n; ++c) {
-      const auto &ch = h->chain[(size_t)c];
-      out[c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)std::min<int64_t>(bound, INT32_MAX)) - ch.begin());
-    }
-  };
+  auto lens_at = [&](int64_t bound, int32_t *out) { chain_lens_at(h, bound, out); };
   if (sp) {  // the plan's tables and the receive buffer (every segment's blocks)
     size_t bytes = 0;
     for (int k = 0; k < K; ++k)
@@ -1215,14 +1265,19 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       // left unmatched
       int32_t *ovf = h->pinned_state + bh::ST_COUNT + 4;
       HIPCHK(h, hipMemcpyAsync(ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, sr));
-      HIPCHK(h, hipStreamSynchronize(sr));
+      HIPCHK(h, wait_stream(sr));
       if (*ovf == 2) wd_fired = true;
     }
     if (k + 1 < K) {
       // segment k + 1 reuses the segbuf parity of k - 1, last read by its
-      // resume point on the loop stream
-      HIPCHK(h, hipEventRecord(sr_mark, sr));
-      HIPCHK(h, hipStreamWaitEvent(sc, sr_mark, 0));
+      // loop (async: the loop's own stop event -- no marker packet on the
+      // loop stream) or its resume point
+      if (async && k > 0) {
+        HIPCHK(h, hipStreamWaitEvent(sc, h->loop_evs[(size_t)2 * k - 1], 0));
+      } else {
+        HIPCHK(h, hipEventRecord(sr_mark, sr));
+        HIPCHK(h, hipStreamWaitEvent(sc, sr_mark, 0));
+      }
       if ((rc = coords(k + 1))) { (void)hipEventDestroy(sr_mark); return rc; }
     }
     if (wd_fired) continue;  // (the remaining segments' receives are posted above)
@@ -1231,6 +1286,13 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if (dbg) HIPCHK(h, hipEventRecord(lt0, sr));
     if (k == 0 && base == 0) {
       bh::launch_round_init(rv, sr);
+    } else if (async && k > 0) {
+      // the previous loop's resume point and this segment's first
+      // candidates in one launch (k_seg_resume: k_resume_point +
+      // k_round_resume + k_cand_rows)
+      Dev rs = rv;
+      rs.seg_lo = view(k).seg_lo;  // (the previous prefix's lengths)
+      bh::launch_seg_resume(rs, sr);
     } else {
       if (k == 0) {
         if (h->reset_on) {
@@ -1250,11 +1312,9 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       bh::launch_round_resume(rv, sr);
     }
     if (async) {
-      HIPCHK(h, hipEventRecord(h->loop_evs[(size_t)2 * k], sr));
       ++h->persist_loops;
-      bh::launch_round_persist(rv, sr);
+      bh::launch_round_persist(rv, sr, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]);
       HIPCHK(h, hipGetLastError());
-      HIPCHK(h, hipEventRecord(h->loop_evs[(size_t)2 * k + 1], sr));
     } else if ((rc = run_round_loop(h, rv, &h->seg_graph[k & 1], &h->seg_graph_dev[k & 1], &h->seg_graph_s[k & 1],
                                     &h->seg_graph_dev_s[k & 1], st))) {
       (void)hipEventDestroy(sr_mark);
@@ -1266,10 +1326,11 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * K + k + 1], 0));
       next_len = view(k + 1).chain_len;
     }
-    bh::launch_resume_point(rv, async ? -1 : st[bh::ST_ROUNDS], next_len, sr);
+    // (async: the next segment's k_seg_resume finds it)
+    if (!(async && k + 1 < K)) bh::launch_resume_point(rv, async ? -1 : st[bh::ST_ROUNDS], next_len, sr);
     if (dbg) {
       HIPCHK(h, hipEventRecord(lt1, sr));
-      HIPCHK(h, hipStreamSynchronize(sr));
+      HIPCHK(h, wait_stream(sr));
       float lms = 0, cms = 0, fms = 0;
       (void)hipEventElapsedTime(&lms, lt0, lt1);
       (void)hipEventElapsedTime(&fms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]);
@@ -1284,12 +1345,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   if (lt1) (void)hipEventDestroy(lt1);
   (void)hipEventDestroy(sr_mark);
   if (async) {  // every loop's end: one host synchronisation for the call
-    HIPCHK(h, copy_sync(sr, st, d.state, bh::ST_COUNT * 4, hipMemcpyDeviceToHost));
-    const bool loop_timing = !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
-    float lms = 0;
-    for (int k = 0; loop_timing && k < K; ++k)
-      if (hipEventElapsedTime(&lms, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]) == hipSuccess)
-        h->loop_ms_acc += lms;
+    if ((rc = rd_async(h, sr, st, d.state, bh::ST_COUNT * 4)) || (rc = rd_wait(h, sr))) return rc;
     const int32_t fail = std::max(st[bh::ST_PFAIL], st[bh::ST_ERR]);
     if (fail == 1 || (fail == 0 && st[bh::ST_FLOWOVF] != 2 && !st[bh::ST_DONE]))
       return h->fail(fail == 1 ? BH_ERR_CAPACITY : BH_ERR_STATE,
@@ -1301,7 +1357,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       ++h->persist_fallbacks;
       h->inc_valid = false;
       h->segments_used = 1;
-      HIPCHK(h, hipStreamSynchronize(sc));
+      HIPCHK(h, wait_stream(sc));
       const int32_t keep = d.round_persist;
       d.round_persist = 0;
       if (!(rc = rounds_coords(h))) rc = rounds_loop(h);
@@ -1316,7 +1372,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     // sweep)
     h->inc_valid = false;
     h->segments_used = 1;
-    HIPCHK(h, hipStreamSynchronize(sc));
+    HIPCHK(h, wait_stream(sc));
     if ((rc = rounds_coords(h))) return rc;
     return rounds_loop(h);
   }
@@ -1330,17 +1386,25 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     h->rows_lens = h->lens_h;
     h->rows_built = true;
   }
+  h->sweep_kernel = wide ? bh::floww_kernel(d) : bh::flow_kernel(d);
+  if (h->reset_on && base > 0) h->fiat_max = h->pinned_state[bh::ST_COUNT + 2];
+  if ((rc = rounds_tail(h, st, base))) return rc;
+  // the timings (every event completed before rounds_tail's synchronisation;
+  // read after its launches, so the device does not wait for them)
+  if (async && !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")))) {
+    float lms = 0;
+    for (int k = 0; k < K; ++k)
+      if (hipEventElapsedTime(&lms, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]) == hipSuccess)
+        h->loop_ms_acc += lms;
+  }
   float ms = 0;
   h->sweep_ms = 0;
   for (int k = 0; k < K; ++k)
     if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
-  h->sweep_kernel = wide ? bh::floww_kernel(d) : bh::flow_kernel(d);
   if (sp) {  // the coordinate time is the coordinate shards'; the receive windows are the exchange
     h->xchg_ms = h->sweep_ms;
     h->sweep_ms = 0;
   }
-  if (h->reset_on && base > 0) h->fiat_max = h->pinned_state[bh::ST_COUNT + 2];
-  if ((rc = rounds_tail(h, st, base))) return rc;
   h->n_coord = N;
   h->lens_coord = h->lens_h;
   h->inc_valid = !h->fdt_lost;
@@ -1456,7 +1520,7 @@ int rounds_split_stage(bh_handle *h) {
   for (bh_handle *x : sh) {  // the sends / copies of this call are done
     if (x->rank == 0) continue;
     HIPCHK(x, hipSetDevice(x->device));
-    HIPCHK(x, hipStreamSynchronize(x->stream2));
+    HIPCHK(x, wait_stream(x->stream2));
   }
   (void)hipSetDevice(h->device);
   return rc;
@@ -1530,13 +1594,12 @@ int fame_finish(bh_handle *h) {
   // the decided flags of PendingRounds' rounds [P, R) only (the rest are
   // final) and the error word, behind one synchronisation
   h->decided_h.assign((size_t)h->R, 0);
-  if (h->R > h->P)
-    HIPCHK(h, hipMemcpyAsync(h->decided_h.data() + h->P, h->d.decided + h->P, (size_t)(h->R - h->P),
-                             hipMemcpyDeviceToHost, h->stream));
-  int32_t *err = h->pinned_state + bh::ST_COUNT + 3;  // pinned staging word
-  HIPCHK(h, hipMemcpyAsync(err, h->d.state + bh::ST_ERR, 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (*err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
+  int rc;
+  if (h->R > h->P && (rc = rd_async(h, h->stream, h->decided_h.data() + h->P, h->d.decided + h->P, (size_t)(h->R - h->P))))
+    return rc;
+  int32_t err = 0;
+  if ((rc = rd_async(h, h->stream, &err, h->d.state + bh::ST_ERR, 4)) || (rc = rd_wait(h, h->stream))) return rc;
+  if (err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
   // updatePendingRounds (hashgraph.go:689-695): set, never cleared
   for (int32_t r = h->P; r < h->R; ++r)
     if (h->decided_h[(size_t)r]) h->pend_dec[(size_t)r] = 1;
@@ -1589,8 +1652,8 @@ int stage_rr_local(bh_handle *h) {
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[4], h->stream));
   int64_t und = 0;
-  HIPCHK(h, hipMemcpyAsync(&und, h->d.counters + 3, 8, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int rc;
+  if ((rc = rd_async(h, h->stream, &und, h->d.counters + 3, 8)) || (rc = rd_wait(h, h->stream))) return rc;
   h->nundet = und;
   h->n_rr = h->n_div;
   h->R_rr = h->R;
@@ -1626,9 +1689,10 @@ int order_local(bh_handle *h) {
   HIPCHK(h, hipGetLastError());
   if (pass_world(h) > 1) {  // frame offsets: the order exchange's ranges
     h->fofs_h.resize((size_t)P1 + 1);
-    if (P1 > 0) HIPCHK(h, hipMemcpyAsync(h->fofs_h.data(), d.frame_ofs, (size_t)P1 * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(h->fofs_h.data() + P1, d.state + bh::ST_NCONS, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipStreamSynchronize(s));
+    int rc;
+    if ((rc = rd_async(h, s, h->fofs_h.data(), d.frame_ofs, (size_t)P1 * 4)) ||
+        (rc = rd_async(h, s, h->fofs_h.data() + P1, d.state + bh::ST_NCONS, 4)) || (rc = rd_wait(h, s)))
+      return rc;
   }
   return BH_OK;
 }
@@ -1651,14 +1715,12 @@ int order_finish(bh_handle *h) {
   int32_t st[bh::ST_COUNT];
   std::vector<int32_t> cnt(k), ofs(k), ld(k);
   std::vector<int64_t> ntx(k);
-  HIPCHK(h, hipMemcpyAsync(st, d.state, sizeof st, hipMemcpyDeviceToHost, s));
-  if (k) {
-    HIPCHK(h, hipMemcpyAsync(cnt.data(), d.frame_cnt + P0, k * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(ofs.data(), d.frame_ofs + P0, k * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(ntx.data(), d.frame_ntx + P0, k * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(ld.data(), d.frame_loaded + P0, k * 4, hipMemcpyDeviceToHost, s));
-  }
-  HIPCHK(h, hipStreamSynchronize(s));
+  int rc;
+  if ((rc = rd_async(h, s, st, d.state, sizeof st)) || (rc = rd_async(h, s, cnt.data(), d.frame_cnt + P0, k * 4)) ||
+      (rc = rd_async(h, s, ofs.data(), d.frame_ofs + P0, k * 4)) ||
+      (rc = rd_async(h, s, ntx.data(), d.frame_ntx + P0, k * 8)) ||
+      (rc = rd_async(h, s, ld.data(), d.frame_loaded + P0, k * 4)) || (rc = rd_wait(h, s)))
+    return rc;
   const int64_t ncons0 = h->ncons;
   h->P = P1;
   h->ncons = st[bh::ST_NCONS];
@@ -2170,7 +2232,7 @@ int bh_synchronize(bh_handle *h) {
   if (!h) return BH_ERR_INVALID;
   for (bh_handle *x : local_shards(h)) {
     HIPCHK(h, hipSetDevice(x->device));
-    HIPCHK(h, hipStreamSynchronize(x->stream));
+    HIPCHK(h, wait_stream(x->stream));
   }
   HIPCHK(h, hipSetDevice(h->device));
   return BH_OK;
@@ -2180,8 +2242,10 @@ int bh_reset_consensus(bh_handle *h) {
   if (!h) return BH_ERR_INVALID;
   for (bh_handle *x : local_shards(h)) {
     HIPCHK(h, hipSetDevice(x->device));
-    HIPCHK(h, hipStreamSynchronize(x->stream));
-    HIPCHK(h, hipMemset(x->d.blocked, 0, ((size_t)x->d.R_cap + 1) * 4));
+    HIPCHK(h, wait_stream(x->stream));
+    // (on the handle's stream, ahead of the next pass: no blocking
+    // legacy-stream memset between two bench steps)
+    HIPCHK(h, hipMemsetAsync(x->d.blocked, 0, ((size_t)x->d.R_cap + 1) * 4, x->stream));
     x->stage = 0;
     x->coords_for = -1;
     x->n_div = x->n_rr = 0;
@@ -2517,7 +2581,7 @@ int bh_get_event_meta(bh_handle *h, int64_t first, int64_t count, int32_t *round
   if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (count == 0) return BH_OK;
   (void)hipSetDevice(h->device);
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   const Dev &d = h->d;
   // events [first, first + k) were divided; the rest are not (Go: nil fields)
   const int64_t k = std::max<int64_t>(0, std::min<int64_t>(count, h->n_div - first));
@@ -2548,7 +2612,7 @@ int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *
   if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (first + count > h->ncons) return h->fail(BH_ERR_INVALID, "range beyond consensus");
   (void)hipSetDevice(h->device);
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   if (count) HIPCHK(h, hipMemcpy(ids, h->d.order + first, (size_t)count * 4, hipMemcpyDeviceToHost));
   return BH_OK;
 }
@@ -2586,7 +2650,7 @@ int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap) {
   if (!ids || cap <= 0) return total;
   std::vector<int32_t> rr((size_t)h->n_rr);
   (void)hipSetDevice(h->device);
-  if (hipStreamSynchronize(h->stream) != hipSuccess) return -1;
+  if (wait_stream(h->stream) != hipSuccess) return -1;
   if (h->n_rr && hipMemcpy(rr.data(), h->d.rr, (size_t)h->n_rr * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   int64_t k = 0;
   for (int64_t i = 0; i < h->n_rr && k < cap; ++i)
@@ -2601,7 +2665,7 @@ int bh_get_round_info(bh_handle *h, int32_t r, bh_round_info *info, int32_t *wit
   if (h->no_results()) return h->fail(BH_ERR_STATE, "results live on rank 0 of a split group (this is rank %d)", h->rank);
   if (r < 0 || r >= h->R) return h->fail(BH_ERR_KEY_NOT_FOUND, "GetRound %d: Not Found", r);
   (void)hipSetDevice(h->device);
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   const Dev &d = h->d;
   const int n = d.n;
   memset(info, 0, sizeof *info);
@@ -2698,7 +2762,7 @@ static int ensure_coords(bh_handle *h) {
       bh::launch_floww(full, s);
       int32_t ovf = 0;
       HIPCHK(h, hipMemcpyAsync(&ovf, d.state + bh::ST_FLOWOVF, 4, hipMemcpyDeviceToHost, s));
-      HIPCHK(h, hipStreamSynchronize(s));
+      HIPCHK(h, wait_stream(s));
       if (ovf) {  // the watchdog or the LT clamp: the chunked sweep below
         HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, s));
         wide = false;
@@ -2738,14 +2802,14 @@ static int ensure_coords(bh_handle *h) {
         lens[(size_t)c] = (int32_t)(std::lower_bound(ch.begin(), ch.end(), (int32_t)h->n_div) - ch.begin());
       }
       HIPCHK(h, hipMemcpyAsync(d.chain_len, lens.data(), (size_t)d.n * 4, hipMemcpyHostToDevice, s));
-      HIPCHK(h, hipStreamSynchronize(s));
+      HIPCHK(h, wait_stream(s));
       d.N = h->n_div;
       h->lens_h = lens;
     }
     if (h->layout_changed && h->R > 0)  // the witness tables' LA / FD rows moved with the layout
       bh::launch_witness_tables(d, h->R, s);
   }
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   return BH_OK;
 }
 
@@ -2757,7 +2821,7 @@ int bh_get_coordinates(bh_handle *h, int64_t id, int32_t *last_ancestors, int32_
   if (int rc = ensure_coords(h)) return rc;
   const int32_t c = h->h_creator[(size_t)id];
   const int64_t row = (int64_t)h->cstart_h[(size_t)c] + h->h_index[(size_t)id];  // chain-major layout
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   if (last_ancestors)
     HIPCHK(h, hipMemcpy(last_ancestors, d.la + row * d.npad, (size_t)d.n * 4, hipMemcpyDeviceToHost));
   if (first_descendants && (d.fd_cols || !d.fd_rows)) {  // one column of FDT
@@ -2805,7 +2869,7 @@ int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x,
   bh::launch_query(h->d, kind, count, dx, dy, dout, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipMemcpyAsync(out, dout, (size_t)count * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(h, hipStreamSynchronize(s));
+  HIPCHK(h, wait_stream(s));
   return BH_OK;
 }
 
@@ -2878,7 +2942,7 @@ int bh_hash_bodies(bh_handle *h, const uint8_t *bytes, const int64_t *offsets, i
   bh::launch_sha256(db, doff, dlen, count, dout, h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipMemcpyAsync(digests, dout, (size_t)count * 32, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   return BH_OK;
 }
 
@@ -2911,7 +2975,7 @@ int bh_verify_signatures(bh_handle *h, const uint8_t *hashes, const uint8_t *sig
   bh::launch_ecdsa_verify(dh, dr, ds, dk, dp, count, dok, h->stream);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipMemcpyAsync(ok, dok, (size_t)count, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, wait_stream(h->stream));
   return BH_OK;
 }
 

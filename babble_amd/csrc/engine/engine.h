@@ -351,6 +351,10 @@ void launch_round_resume(const Dev &d, hipStream_t s);
 // null: every chain), so they hold for that prefix; rq[q] = chain q's
 // first r with B[r][q] >= len_q (kernels_rounds.hip)
 void launch_resume_point(const Dev &d, int32_t R, const int32_t *next_len, hipStream_t s);
+// the n <= 128 persistent pipeline's next segment in one launch: the previous
+// loop's resume point (d.seg_lo = the previous prefix's lengths, d.chain_len
+// this one's), k_round_resume's loop state and k_cand_rows' first candidates
+void launch_seg_resume(const Dev &d, hipStream_t s);
 // FD entries of a segment's new rows for chains with no event in the segment
 void launch_fd_idle(const Dev &d, hipStream_t s);
 // the coordinate split's packed blocks (kernels_split.hip): one per
@@ -382,7 +386,7 @@ void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_roun
 bool round_solo_eligible(const Dev &d);
 bool round2_eligible(const Dev &d);
 bool round_persist_eligible(const Dev &d);
-void launch_round_persist(const Dev &d, hipStream_t s);
+void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 bool round_wide_persist_eligible(const Dev &d);
 void launch_round_wide_persist(const Dev &d, hipStream_t s);
 void launch_round_solo(const Dev &d, hipStream_t s);

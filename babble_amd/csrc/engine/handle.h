@@ -67,6 +67,11 @@ struct bh_handle {
     }
   }
   std::vector<std::vector<int32_t>> chain;  // ids by creator, by index
+  // per-chain prefix lengths at an insertion-order bound (chain_lens_at):
+  // chains only grow by appends, so a bound's lengths never change once
+  // every event below it is inserted -- kept, since each is n binary searches
+  // over cold multi-MB id vectors (~250 us at C3 before the first loop)
+  mutable std::unordered_map<int64_t, std::vector<int32_t>> lens_memo;
   std::vector<int32_t> h_creator, h_index, h_sp, h_op, h_ntx;
   std::vector<uint8_t> h_coin;
   std::vector<uint32_t> h_sigw;
@@ -95,6 +100,15 @@ struct bh_handle {
   hipGraphExec_t graph = nullptr, graph_s = nullptr;  // ITER_BATCH / ITER_FIRST iterations
   Dev graph_dev{}, graph_dev_s{};
   int32_t *pinned_state = nullptr;
+  // pinned staging for a pass's device-to-host reads (rd_async / rd_wait):
+  // a pageable destination makes every hipMemcpyAsync a blocking staged copy
+  uint8_t *pin_rd = nullptr;
+  size_t pin_rd_cap = 0, pin_rd_used = 0;
+  struct PinRead {
+    void *dst;
+    size_t off, bytes;
+  };
+  std::vector<PinRead> pin_rd_list;
   uint8_t *sha_buf = nullptr;  // bh_hash_bodies scratch
   uint8_t *q_buf = nullptr;    // bh_query_events scratch
   size_t q_cap = 0;

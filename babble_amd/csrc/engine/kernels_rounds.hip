@@ -28,6 +28,8 @@
 // involvement and every load of an iteration depends only on B[r].
 #include "engine.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 
 namespace bh {
@@ -1290,10 +1292,8 @@ __device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, in
 // candidates' FD rows for the first iteration of a loop (parity 0): round 0
 // (B = 0) or the resume round ST_RESUME (B[r0]), searched in la_col -- one
 // workgroup per candidate chain c, a 16-lane group per chain i
-__global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
-  const int c = blockIdx.x, t = threadIdx.x;
-  const int32_t r = from_resume ? d.state[ST_RESUME] : 0;
-  const int32_t b = from_resume ? d.B[(int64_t)r * d.n + c] : 0;
+__device__ __forceinline__ void cand_row(const Dev &d, int c, int32_t r, int32_t b) {
+  const int t = threadIdx.x;
   if (t == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
   if (d.fd_cols) {  // k_round2p's parity-1 hand-off slots: tag 0, which its iteration 1 does not accept
     for (int i = t; i < d.npad; i += blockDim.x) d.candfd[((int64_t)d.n + c) * d.npad + i] = 0;
@@ -1314,7 +1314,12 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
     const int i = i0 + (t >> 4);
     const bool on = i < d.n;
     const int32_t cs = on ? d.chain_start[i] : 0, len = on ? d.chain_len[i] : 0;
-    const int32_t j = first_ge16(colc + cs, 0, len, b, on && len > 0, false);
+    // FD[(c, b)][i] >= B[r][i]: (c, b = B[r][c]) is in round >= r, and so
+    // is every event that sees it (a round is the maximum of its parents'
+    // or one more) -- the search starts there, and usually ends within the
+    // first 1024 rows (two dependent loads instead of ~5 over the chain)
+    const int32_t lo0 = r > 0 && on ? min(d.B[(int64_t)r * d.n + i], len) : 0;
+    const int32_t j = first_ge16(colc + cs, lo0, len, b, on && len > lo0, r > 0);
     const int32_t f = on && j < len ? j : FD_NONE;
     if ((t & 15) == 0 && i < nrow) {
       if (c16) c16[i] = (uint16_t)min((uint32_t)f + 1u, 0xFFFFu);
@@ -1322,6 +1327,74 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
     }
   }
 }
+
+__global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
+  const int c = blockIdx.x;
+  const int32_t r = from_resume ? d.state[ST_RESUME] : 0;
+  cand_row(d, c, r, from_resume ? d.B[(int64_t)r * d.n + c] : 0);
+}
+
+// A segment's start in one launch (the n <= 128 persistent pipeline, segments
+// after the first): the previous segment's resume point (k_resume_point's
+// search, made by every workgroup -- the view's seg_lo is the previous
+// prefix's lengths, its chain_len this one's), then k_round_resume's and
+// k_cand_rows' work for chain c.  Three launches and their dispatch gaps
+// were ~70 us between two segments' loops at C3 (profiles/r5_gaps_c3_async.txt).
+// The search: 8 lanes per chain, 8-ary over rounds [0, R] (B[R][q] >= len_q)
+__global__ __launch_bounds__(1024) void k_seg_resume(Dev d) {
+  __shared__ int32_t m;
+  const int c = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int n = d.n;
+  const int32_t R = d.state[ST_ROUNDS];
+  if (t == 0) m = R;
+  __syncthreads();
+  for (int q0 = 0; q0 < n; q0 += (int)(blockDim.x >> 3)) {  // (uniform trip count)
+    const int q = q0 + (t >> 3), g = t & 7, gb = lane & 56;
+    const bool on = q < n;
+    const int32_t len = on ? d.seg_lo[q] : 0;
+    int32_t lo = 0, hi = R;  // the first r in [lo, hi] with B[r][q] >= len
+    bool go = on && lo < hi;
+    while (__any(go)) {
+      const int32_t s = (hi - lo + 7) >> 3;
+      const int32_t pr = min(lo + (g + 1) * s, hi) - 1;
+      const bool ge = go && d.B[(int64_t)pr * n + q] >= len;
+      const uint32_t mk = (uint32_t)(__ballot(ge) >> gb) & 0xFFu;
+      if (go) {
+        if (mk) {
+          const int f = __builtin_ctz(mk);
+          hi = min(lo + (f + 1) * s, hi) - 1;
+          lo += f * s;
+        } else {
+          lo = min(lo + 8 * s, hi);
+        }
+        go = lo < hi;
+      }
+    }
+    if (on && g == 0) {
+      if (c == 0 && d.rq) d.rq[q] = lo;
+      if (d.chain_len[q] > len) atomicMin(&m, lo);
+    }
+  }
+  __syncthreads();
+  const int32_t r0 = max(d.r0, m - 1);
+  const int32_t b = d.B[(int64_t)r0 * n + c];
+  if (t == 0) {
+    d.Bp[c] = b;
+    if (c == 0) {
+      // (ST_ROUNDS stays: every workgroup reads it above; the loop sets it)
+      d.state[ST_RESUME] = r0;
+      d.state[ST_PFAIL] = max(d.state[ST_PFAIL], d.state[ST_ERR]);
+      d.state[ST_CUR0] = r0;
+      d.state[ST_CUR0 + 1] = 0;
+      d.state[ST_DONE] = 0;
+      d.state[ST_ERR] = 0;
+      d.state[ST_ITERS] = r0;
+    }
+  }
+  cand_row(d, c, r0, b);
+}
+
+void launch_seg_resume(const Dev &d, hipStream_t s) { k_seg_resume<<<d.n, 1024, 0, s>>>(d); }
 
 // TQ (default): every lane group binary-searches its own T_q (the first
 // window row strongly seeing candidate q) with no barrier between probes; one
@@ -2093,18 +2166,16 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
   }
 }
 
-void launch_round_persist(const Dev &d, hipStream_t s) {
-  const size_t lds = (size_t)HWL * (d.npad / 4 + 1) * 16;
+// e0 / e1: the launch's own start / stop timestamps (hipExtLaunchKernel: no
+// marker packets of their own between the segments' kernels, ~5 us each)
+void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  const uint32_t lds = (uint32_t)(HWL * (d.npad / 4 + 1) * 16);
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
-  if (d.round_f32) {
-    if (d.npad <= 32) k_round2p<1, true><<<d.n, nt, lds, s>>>(d);
-    else if (d.npad <= 64) k_round2p<2, true><<<d.n, nt, lds, s>>>(d);
-    else k_round2p<4, true><<<d.n, nt, lds, s>>>(d);
-  } else {
-    if (d.npad <= 32) k_round2p<1, false><<<d.n, nt, lds, s>>>(d);
-    else if (d.npad <= 64) k_round2p<2, false><<<d.n, nt, lds, s>>>(d);
-    else k_round2p<4, false><<<d.n, nt, lds, s>>>(d);
-  }
+  void (*k)(Dev);
+  if (d.round_f32) k = d.npad <= 32 ? k_round2p<1, true> : d.npad <= 64 ? k_round2p<2, true> : k_round2p<4, true>;
+  else k = d.npad <= 32 ? k_round2p<1, false> : d.npad <= 64 ? k_round2p<2, false> : k_round2p<4, false>;
+  if (e0 || e1) hipExtLaunchKernelGGL(k, dim3((unsigned)d.n), dim3(nt), lds, s, e0, e1, 0, d);
+  else k<<<d.n, nt, lds, s>>>(d);
 }
 
 // k_round2r (BH_ROUND_SRC=rows, A/B): the round-3 iteration, reading its
