@@ -265,12 +265,24 @@ __device__ void bitonic_lds(uint64_t *key, int32_t *id, int32_t p2) {
 // FS_BUCKETS or more take the bitonic network.
 constexpr int FS_BUCKETS = 1024;
 
-__global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
+// Two launches (late round 5), each sorting the frames that fit it and that
+// no earlier pass sorted (frame_loaded still -1): 512 threads and 4,096
+// events of LDS (48 KiB, three workgroups per compute unit: the C3 and C4
+// frames, ~1,600 / ~3,200 events spanning < 100 timestamps), then 1024
+// threads and FRAME_LDS_MAX (96 KiB, one per unit: the rest).  A frame's
+// sort is a few dependent gathers per phase, so frames in flight per unit is
+// what counts: one 96-KiB launch for all of them took 0.43 ms at C3, the two
+// 0.28 (r5_ab_frame_sort2.txt; a third, 256-thread pass for frames up to
+// 2,048 -- six per unit -- measured slower: 0.31).
+__global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0, int32_t cap, int32_t pass) {
+  const bool last = cap >= FRAME_LDS_MAX;  // (the last pass takes whatever is left)
   extern __shared__ __attribute__((aligned(16))) unsigned char osm[];
   __shared__ unsigned long long sh_ntx, sh_loaded;
   __shared__ int32_t bend[FS_BUCKETS + 1], sh_lt[2], wsum[16];
   const int32_t f = f0 + (int32_t)blockIdx.x;
+  if (pass > 0 && d.frame_loaded[f] >= 0) return;  // (sorted by an earlier pass)
   const int32_t cnt = d.frame_cnt[f];
+  if (!last && cnt > cap) return;
   if (cnt == 0) {
     if (threadIdx.x == 0) { d.frame_ntx[f] = 0; d.frame_loaded[f] = 0; }
     return;
@@ -281,7 +293,7 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
   if (t == 0) { sh_ntx = 0; sh_loaded = 0; sh_lt[0] = INT32_MAX; sh_lt[1] = INT32_MIN; }
   // the timestamps' range
   int32_t lmin = INT32_MAX, lmax = INT32_MIN;
-  if (cnt <= FRAME_LDS_MAX) {
+  if (cnt <= cap) {
     for (int32_t i = t; i < cnt; i += nt) {
       const int32_t v = d.lt[ids[i]];
       lmin = min(lmin, v);
@@ -301,7 +313,13 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
     lmin = sh_lt[0];
     lmax = sh_lt[1];
   }
-  if (cnt <= FRAME_LDS_MAX && (int64_t)lmax - lmin < FS_BUCKETS) {
+  int32_t p2 = 64;
+  while (p2 < cnt) p2 <<= 1;
+  // (a frame neither LDS path fits -- a wide span and a network past the
+  // cap -- is left to the next pass, untouched)
+  const bool bucket = cnt <= cap && (int64_t)lmax - lmin < min(FS_BUCKETS, nt);
+  if (!last && !bucket && p2 > cap) return;
+  if (bucket) {
     const int32_t span = lmax - lmin + 1;
     uint32_t *sk = reinterpret_cast<uint32_t *>(osm);  // bucketed: signature word 0, id, bucket
     int32_t *sid = reinterpret_cast<int32_t *>(sk + cnt), *sb = sid + cnt;
@@ -309,8 +327,8 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
     __syncthreads();
     for (int32_t i = t; i < cnt; i += nt) atomicAdd(&bend[d.lt[ids[i]] - lmin], 1);
     __syncthreads();
-    // exclusive prefix of the counts (span <= 1024 = one per thread): DPP
-    // scan per wave, then the waves' totals
+    // exclusive prefix of the counts (span <= the threads: one per thread):
+    // DPP scan per wave, then the waves' totals
     {
       const int32_t v = t < span ? bend[t] : 0;
       int32_t h = v;
@@ -350,9 +368,7 @@ __global__ __launch_bounds__(1024) void k_frame_sort(Dev d, int32_t f0) {
       ids[lo + rank] = ep;
     }
     __syncthreads();
-  } else if (cnt <= FRAME_LDS_MAX) {
-    int32_t p2 = 64;
-    while (p2 < cnt) p2 <<= 1;
+  } else if (p2 <= cap) {
     uint64_t *key = reinterpret_cast<uint64_t *>(osm);
     int32_t *id = reinterpret_cast<int32_t *>(key + p2);
     for (int32_t i = t; i < p2; i += nt) {
@@ -437,7 +453,9 @@ void launch_order_buckets(const Dev &d, int32_t R, int32_t P0, hipStream_t s) {
 
 void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s) {
   if (f1 <= f0) return;
-  k_frame_sort<<<f1 - f0, 1024, FRAME_LDS_MAX * 12, s>>>(d, f0);
+  (void)hipMemsetAsync(d.frame_loaded + f0, 0xFF, (size_t)(f1 - f0) * 4, s);  // (pass 1 sorts what is still -1)
+  k_frame_sort<<<f1 - f0, 512, 4096 * 12, s>>>(d, f0, 4096, 0);
+  k_frame_sort<<<f1 - f0, 1024, FRAME_LDS_MAX * 12, s>>>(d, f0, FRAME_LDS_MAX, 1);
 }
 
 __global__ void k_cons_pos(Dev d, int64_t i0, int64_t i1) {
