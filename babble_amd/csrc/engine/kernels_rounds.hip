@@ -1777,6 +1777,23 @@ __device__ __forceinline__ int4 f32_bits4(int4 v) {
                    __float_as_int((float)v.w));
 }
 
+// the probe's dependent chain, shortened: the window row's offset by the
+// full-rate 24-bit multiply (the compiler turned __mul24 into the
+// quarter-rate v_mul_lo_u32 here), and the lane group's indicator sum in f32
+// straight through DPP (v_add_f32_dpp: no convert before the group sum)
+__device__ __forceinline__ int mul_u24(int a, int b_uniform) {
+  int r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(b_uniform), "v"(a));
+  return r;
+}
+template <int LPC>
+__device__ __forceinline__ float group_total_f(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));  // quad_perm [1,0,3,2]
+  if (LPC >= 4) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));
+  if (LPC >= 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, true));
+  return v;
+}
+
 template <int PPL, bool F32>
 __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   constexpr int LPC = 8;
@@ -1916,6 +1933,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       if (F32) f[u] = f32_bits4(f[u]);
     }
     const bool act = q < n && bq < lq;
+    const float ltmax = (float)(LPC * PPL * 4 - sm);  // the most LA < FD columns a strongly seeing row has
     auto ss_row = [&](const int4 *x4) {
       int4 x[PPL];
 #pragma unroll
@@ -1934,7 +1952,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
         for (int w = 1; w < 2 * PPL; w *= 2)
 #pragma unroll
           for (int u = 0; u + w < 2 * PPL; u += 2 * w) a[u] += a[u + w];
-        lt = (int)(a[0].x + a[0].y);
+        return group_total_f<LPC>(a[0].x + a[0].y) <= ltmax;  // (#{LA >= FD} >= sm)
       } else {
 #pragma unroll
         for (int u = 0; u < PPL; ++u) lt += lt4(x[u], f[u]);
@@ -1961,7 +1979,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       while (__any(lo < hi)) {
         ++nprobe;
         const int mid = (lo + hi) >> 1;
-        const bool sv = ss_row(w0 + __mul24(min(mid, rows - 1), rs4));  // (24-bit multiply: full rate)
+        const bool sv = ss_row(w0 + mul_u24(min(mid, rows - 1), rs4));
         if (lo < hi) {
           hi = sv ? mid : hi;
           lo = sv ? lo : mid + 1;
