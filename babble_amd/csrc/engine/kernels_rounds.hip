@@ -1777,13 +1777,16 @@ __device__ __forceinline__ int4 f32_bits4(int4 v) {
                    __float_as_int((float)v.w));
 }
 
-// the probe's dependent chain, shortened: the window row's offset by the
-// full-rate 24-bit multiply (the compiler turned __mul24 into the
-// quarter-rate v_mul_lo_u32 here), and the lane group's indicator sum in f32
-// straight through DPP (v_add_f32_dpp: no convert before the group sum)
-__device__ __forceinline__ int mul_u24(int a, int b_uniform) {
+// the probe's dependent chain, shortened: window rows of a constant width
+// (the row offset a shift and an add -- the compiler had turned __mul24 by
+// the runtime width into the quarter-rate v_mul_lo_u32 -- and a lane's four
+// pieces at immediate offsets from one address), and the lane group's
+// indicator sum in f32 straight through DPP (v_add_f32_dpp: no convert
+// before the group sum)
+template <int RB>
+__device__ __forceinline__ int row_bytes(int m) {  // m * RB by the full-rate 24-bit multiply (the compiler picks a 64-bit mad)
   int r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "s"(b_uniform), "v"(a));
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "i"(RB), "v"(m));
   return r;
 }
 template <int LPC>
@@ -1817,12 +1820,16 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     return;
   }
   const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
-  const int rs4 = q4 + 1, rs = 4 * rs4;
+  // window rows of LPC * PPL pieces whatever npad (columns past n hold -1):
+  // a lane's four pieces are one LDS base plus immediate offsets
+  constexpr int rs4 = LPC * PPL + 1, rs = 4 * rs4;
   const int64_t stride = la_col_stride(d);
   int4 *win = sm4;
   int32_t *win32 = reinterpret_cast<int32_t *>(sm4);
   const int32_t len = d.chain_len[c], cs = d.chain_start[c];
-  const int q = t / LPC, part = t % LPC, rot = q & (PPL - 1);
+  // (one piece order for every candidate: the four pieces' LDS addresses are
+  // one base plus immediate offsets, three VALU off each probe's chain)
+  const int q = t / LPC, part = t % LPC, rot = 0;
   const int32_t lq = q < n ? d.chain_len[q] : 0;
   const int32_t *colc = d.la_col + (int64_t)c * stride;
   const __amdgpu_buffer_rsrc_t cfr = __builtin_amdgcn_make_buffer_rsrc(d.candfd, (short)0, 0x7fffffff, 0x00020000);
@@ -1845,9 +1852,9 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   };
   own_loads();
   if (t == 0) sh_fail = 0;
-  if (npad > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
-    for (int j = t; j < (npad - n) * HWL; j += nt)
-      win32[(j / (npad - n)) * rs + n + j % (npad - n)] = F32 ? __float_as_int(-1.f) : -1;
+  if (4 * LPC * PPL > n)  // columns past n: LA -1 (never >= an FD); the staging never writes them
+    for (int j = t; j < (4 * LPC * PPL - n) * HWL; j += nt)
+      win32[(j / (4 * LPC * PPL - n)) * rs + n + j % (4 * LPC * PPL - n)] = F32 ? __float_as_int(-1.f) : -1;
   int p = 0;
   // a candidate piece's dwords all carry tag `want` in their top byte
   auto tagged = [](int4 v, uint32_t want) {
@@ -1937,7 +1944,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     auto ss_row = [&](const int4 *x4) {
       int4 x[PPL];
 #pragma unroll
-      for (int u = 0; u < PPL; ++u) x[u] = x4[min(part + LPC * ((u + rot) & (PPL - 1)), q4 - 1)];
+      for (int u = 0; u < PPL; ++u) x[u] = x4[part + LPC * ((u + rot) & (PPL - 1))];
       int lt = 0;
       if constexpr (F32) {
         // every indicator pair first, then a tree of packed adds (no
@@ -1979,7 +1986,8 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
       while (__any(lo < hi)) {
         ++nprobe;
         const int mid = (lo + hi) >> 1;
-        const bool sv = ss_row(w0 + mul_u24(min(mid, rows - 1), rs4));
+        const bool sv = ss_row(reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(w0) +
+                                                               row_bytes<16 * rs4>(min(mid, rows - 1))));
         if (lo < hi) {
           hi = sv ? mid : hi;
           lo = sv ? lo : mid + 1;
@@ -2187,7 +2195,8 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
 // e0 / e1: the launch's own start / stop timestamps (hipExtLaunchKernel: no
 // marker packets of their own between the segments' kernels, ~5 us each)
 void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  const uint32_t lds = (uint32_t)(HWL * (d.npad / 4 + 1) * 16);
+  const int ppl = d.npad <= 32 ? 1 : d.npad <= 64 ? 2 : 4;  // (k_round2p's rows: 8 * PPL + 1 pieces)
+  const uint32_t lds = (uint32_t)(HWL * (8 * ppl + 1) * 16);
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
   void (*k)(Dev);
   if (d.round_f32) k = d.npad <= 32 ? k_round2p<1, true> : d.npad <= 64 ? k_round2p<2, true> : k_round2p<4, true>;
