@@ -797,7 +797,9 @@ static void segment_bounds(int64_t base, int64_t N, int K, int64_t *Ns) {
   // segment k holds a ratio^k share: a short first segment (the loop waits
   // for its coordinates) and segments growing about as fast as the loop
   // outruns the dataflow (BH_SEG_RATIO: A/B)
-  const double ratio = getenv("BH_SEG_RATIO") ? std::max(1.0, atof(getenv("BH_SEG_RATIO"))) : 1.38;
+  // (1.38 until the loop reached ~5.25 us per round; 1.24-1.32 then measured
+  // alike and ahead of 1.38 by ~2 %, profiles/r5_seg_ratio_late.txt)
+  const double ratio = getenv("BH_SEG_RATIO") ? std::max(1.0, atof(getenv("BH_SEG_RATIO"))) : 1.32;
   for (int k = 0; k < K; ++k) tot += (w[k] = std::pow(ratio, k));
   double acc = 0;
   for (int k = 1; k < K; ++k) {
