@@ -77,6 +77,10 @@ void free_all(bh_handle *h) {
   h->xport = nullptr;
   if (h->xbuf) (void)hipFree(h->xbuf);
   if (h->xseg) (void)hipFree(h->xseg);
+  for (auto &e : h->pack_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->xprep) (void)hipEventDestroy(h->xprep);
+  if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->xbase) (void)hipFree(h->xbase);
 }
 
@@ -858,6 +862,12 @@ struct SplitPlan {
   int64_t base = 0;
   std::vector<int64_t> Ns, S, NQ;
   std::vector<int32_t> tab;  // [K][lo, hi][n], then [K][P, Q][n + 1]
+  // block (k, r) at byte offset off[k * world + r] of every shard's xbuf
+  // (segment-major, then coordinate rank): one layout everywhere, so a
+  // block is broadcast in place and peer-copied offset to offset
+  std::vector<size_t> off;
+  size_t total = 0;
+  size_t boff(const bh_handle *h, int k, int32_t rank) const { return off[(size_t)k * h->world + rank]; }
   const int32_t *dview(const bh_handle *h, int k) const { return h->xseg + (size_t)k * 2 * h->d.n; }
   const int32_t *dpq(const bh_handle *h, int k) const {
     return h->xseg + (size_t)K * 2 * h->d.n + (size_t)k * 2 * (h->d.n + 1);
@@ -873,8 +883,13 @@ struct SplitPlan {
     bh::SplitBlock b;
     bh::split_layout((int)(c1 - c0), S[(size_t)k], NQ[(size_t)k], rank == 1, &b, at);
     b.c0 = (int32_t)c0;
-    const char *e = getenv("BH_SPLIT_RANGE");  // (read per block: the tests switch it)
-    b.range = e ? std::clamp(atoi(e), 0, 65535) : 65535;
+    // (test knobs, read per block: the tests switch them) BH_SPLIT_RANGE
+    // lowers the 16-bit range so gossip DAGs fill the overflow slots, from
+    // segment BH_SPLIT_RANGE_SEG on (0: every segment) -- a LATER segment's
+    // overflow while earlier loops run
+    const char *e = getenv("BH_SPLIT_RANGE");
+    const char *es = getenv("BH_SPLIT_RANGE_SEG");
+    b.range = e && k >= (es ? atoi(es) : 0) ? std::clamp(atoi(e), 0, 65535) : 65535;
     return b;
   }
 };
@@ -903,6 +918,12 @@ SplitPlan split_plan(const bh_handle *h, int K, int64_t base) {
     p.S[(size_t)k] = P[n];
     p.NQ[(size_t)k] = Q[n];
   }
+  p.off.assign((size_t)K * h->world, 0);
+  for (int k = 0; k < K; ++k)
+    for (int r = 1; r < h->world; ++r) {
+      p.off[(size_t)k * h->world + r] = p.total;
+      p.total += p.block_bytes(h, k, r);
+    }
   return p;
 }
 
@@ -931,13 +952,25 @@ int split_prepare(bh_handle *x, const SplitPlan &p, size_t bytes) {
     HIPCHK(x, hipEventCreate(&e));
     x->seg_ev.push_back(e);
   }
+  while ((int)x->pack_ev.size() < p.K) {
+    hipEvent_t e;
+    HIPCHK(x, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    x->pack_ev.push_back(e);
+  }
+  if (!x->xprep) HIPCHK(x, hipEventCreateWithFlags(&x->xprep, hipEventDisableTiming));
+  if (!x->stream3) {  // (the coordinate stream's priority: the loop stream keeps the higher one)
+    int lo_pri = 0, hi_pri = 0;
+    HIPCHK(x, hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
+    HIPCHK(x, hipStreamCreateWithPriority(&x->stream3, hipStreamNonBlocking, lo_pri));
+  }
   return BH_OK;
 }
 
 // a coordinate shard's part of the call, enqueued on its stream2: per
-// segment the descriptors, k_flow32 over its columns (+ LT on rank 1), the
-// packed block, then its send (ncclSend to rank 0, or an event rank 0's
-// peer copy waits for)
+// segment the descriptors, k_flow32 over its columns (+ LT on rank 1) and
+// the packed block (pack_ev[k]).  The narrow split all-gathers the blocks
+// from rounds_pipelined (every shard runs the loop); the wide split sends
+// each to rank 0 here (ncclSend, or rank 0's peer copy waits for pack_ev)
 int split_coords(bh_handle *x, const SplitPlan &p) {
   Dev dv = x->d;
   const int n = dv.n;
@@ -947,16 +980,13 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
   dv.ncol = (int32_t)(c1 - c0);
   dv.flow_lt = x->rank == 1;
   const bool wide = !dv.fd_cols;  // 128 < n <= 512: k_floww2
-  size_t bytes = 0;
-  for (int k = 0; k < p.K; ++k) bytes += p.block_bytes(x, k, x->rank);
   int rc;
-  if ((rc = split_prepare(x, p, bytes))) return rc;
+  if ((rc = split_prepare(x, p, p.total))) return rc;
   hipStream_t sc = x->stream2;
   x->segments_used = p.K;
   if (p.base == 0) bh::launch_prep(dv, sc);
   else bh::launch_chain_scatter(dv, p.base, sc);
   HIPCHK(x, hipMemsetAsync(dv.state + bh::ST_FLOWOVF, 0, 4, sc));
-  size_t off = 0;
   for (int k = 0; k < p.K; ++k) {
     Dev v = dv;
     v.seg_lo = const_cast<int32_t *>(p.dview(x, k));
@@ -973,15 +1003,11 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
       bh::launch_flow_desc(v, sc);
       if (dv.ncol > 0 || dv.flow_lt) bh::launch_flow(v, sc);
     }
-    const bh::SplitBlock b = p.block(x, k, x->rank, x->xbuf + off);
+    uint8_t *at = x->xbuf + p.boff(x, k, x->rank);
+    const bh::SplitBlock b = p.block(x, k, x->rank, at);
     bh::launch_split_pack(v, p.dpq(x, k), b, sc);
-    const size_t bb = p.block_bytes(x, k, x->rank);
-    if (x->xport) {
-      if ((rc = x->xport->send(x, x->xbuf + off, bb, 0, sc))) return rc;
-    } else {
-      HIPCHK(x, hipEventRecord(x->seg_ev[(size_t)k], sc));
-    }
-    off += bb;
+    HIPCHK(x, hipEventRecord(x->pack_ev[(size_t)k], sc));
+    if (wide && x->xport && (rc = x->xport->send(x, at, p.block_bytes(x, k, x->rank), 0, sc))) return rc;
   }
   HIPCHK(x, hipGetLastError());
   // bookkeeping alike on every shard (the next call's base is rank 0's anyway)
@@ -996,13 +1022,17 @@ int split_coords(bh_handle *x, const SplitPlan &p) {
 
 // base > 0: an incremental call -- events [0, base) hold coordinates and
 // the round loop left its resume point (ST_RESUME) for that prefix.  sp: the
-// coordinate split -- shard 0's segments arrive from the coordinate shards
-// (grp: the in-process group, else over h->xport) instead of being computed
+// coordinate split -- the segments' columns arrive from the coordinate
+// shards (grp: the in-process group, else over h->xport) instead of being
+// computed here; on a coordinate shard of the narrow split (split_all) its
+// own columns come from its dataflow (split_coords, stream2) and the
+// others' arrive beside it
 int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nullptr,
                      const std::vector<bh_handle *> *grp = nullptr) {
   int rc;
   Dev &d = h->d;  // the whole prefix: every segment's view derives from it
   const int n = d.n;
+  const bool cshard = sp && h->rank > 0;  // (split_all: a coordinate shard that runs the loop too)
   const bool wide = !d.fd_cols;  // k_floww2 + k_round_wide (cand16 from FDT)
   if (wide) d.fd_rows = 0;
   // n <= 128: k_round2 and fame read only the dataflow's column-major LA, so
@@ -1032,6 +1062,12 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     if ((rc = build_rows(h, h->lens_coord, h->stream))) return rc;
   }
   hipStream_t sr = h->stream, sc = h->stream2;
+  if (sp && !cshard) {  // (a coordinate shard's split_coords prepared the plan already)
+    if ((rc = split_prepare(h, *sp, sp->total))) return rc;
+  }
+  // the split's receives and unpacks: a stream of their own, beside a
+  // coordinate shard's dataflow on stream2
+  hipStream_t sx = sp ? h->stream3 : sc;
   h->segments_used = K;
   h->fdt_lost = false;
   if ((int)h->seg_ev.size() < 4 * K) {
@@ -1056,23 +1092,23 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // the coordinate stream starts after everything queued on the main one
   HIPCHK(h, hipEventRecord(h->ev[0], sr));
   HIPCHK(h, hipStreamWaitEvent(sc, h->ev[0], 0));
-  if (base == 0) {
-    bh::launch_prep(d, sc);
-  } else {  // only the new events' chain-table entries; loop state kept
-    bh::launch_chain_scatter(d, base, sc);
+  if (!cshard) {  // (a coordinate shard's split_coords queued them ahead of its dataflow)
+    if (base == 0) {
+      bh::launch_prep(d, sc);
+    } else {  // only the new events' chain-table entries; loop state kept
+      bh::launch_chain_scatter(d, base, sc);
+    }
+    HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, sc));
   }
-  HIPCHK(h, hipMemsetAsync(d.state + bh::ST_FLOWOVF, 0, 4, sc));
+  if (sp && !cshard) {  // the unpacks wait for the chain tables and the cleared flag
+    HIPCHK(h, hipEventRecord(h->xprep, sc));
+    HIPCHK(h, hipStreamWaitEvent(sx, h->xprep, 0));
+  }
   const int64_t N = d.N;
   std::vector<int64_t> Ns((size_t)K + 1, base);
   segment_bounds(base, N, K, Ns.data());
   // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
   auto lens_at = [&](int64_t bound, int32_t *out) { chain_lens_at(h, bound, out); };
-  if (sp) {  // the plan's tables and the receive buffer (every segment's blocks)
-    size_t bytes = 0;
-    for (int k = 0; k < K; ++k)
-      for (int r = 1; r < h->world; ++r) bytes += sp->block_bytes(h, k, r);
-    if ((rc = split_prepare(h, *sp, bytes))) return rc;
-  }
   auto view = [&](int k) {  // segment k: events [Ns[k], Ns[k + 1])
     Dev v = d;
     v.seg_lo = sp ? const_cast<int32_t *>(sp->dview(h, k)) : h->segbuf + (size_t)(k & 1) * 2 * n;
@@ -1086,7 +1122,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   // each chain's run [start + lo, start + hi), in layout order, shared
   // boundary tiles once (eager runs wait for each loop: the staging's two
   // halves cannot be overtaken)
-  auto tiles = [&](int k, const int32_t *lo, const int32_t *hi, Dev &v) -> int {
+  auto tiles = [&](int k, const int32_t *lo, const int32_t *hi, Dev &v, hipStream_t ts) -> int {
     int32_t *tl = h->tlist_stage + (size_t)(k & 1) * h->tlist_cap;
     int64_t nt = 0;
     for (int c = 0; c < n; ++c) {
@@ -1095,58 +1131,63 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       for (int64_t t = (nt && tl[nt - 1] >= a) ? tl[nt - 1] + 1 : a; t <= b; ++t) tl[nt++] = (int32_t)t;
     }
     int32_t *dtl = h->tlist + (size_t)(k & 1) * h->tlist_cap;
-    if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, sc));
+    if (nt) HIPCHK(h, hipMemcpyAsync(dtl, tl, (size_t)nt * 4, hipMemcpyHostToDevice, ts));
     v.tile_list = dtl;
     v.ntiles = nt;
     return BH_OK;
   };
-  size_t xoff = 0;  // the receive buffer's next block
-  auto receive = [&](int k) -> int {  // the split: segment k's columns from the coordinate shards
+  // the split: segment k's columns from the coordinate shards (every other
+  // one: a coordinate shard of the narrow split computed its own), into the
+  // common block layout -- the narrow split all-gathers them (a broadcast
+  // per coordinate rank, in place; in process, peer copies), the wide one
+  // receives them on shard 0 only
+  auto receive = [&](int k) -> int {
     Dev v = view(k);
-    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sc));
-    if (grp) {  // peer copies (xGMI between devices, a device copy on a shared one)
-      for (int r = 1; r < h->world; ++r) HIPCHK(h, hipStreamWaitEvent(sc, (*grp)[(size_t)r]->seg_ev[(size_t)k], 0));
-    }
-    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sc));
-    std::vector<bh::SplitBlock> blk((size_t)h->world);
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sx));
+    if (cshard) HIPCHK(h, hipStreamWaitEvent(sx, h->pack_ev[(size_t)k], 0));  // its own block (its dataflow) done
     if (grp) {
+      for (int r = 1; r < h->world; ++r)
+        if (r != h->rank) HIPCHK(h, hipStreamWaitEvent(sx, (*grp)[(size_t)r]->pack_ev[(size_t)k], 0));
+    }
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 1], sx));
+    std::vector<bh::SplitBlock> blk((size_t)h->world);
+    for (int r = 1; r < h->world; ++r) blk[(size_t)r] = sp->block(h, k, r, h->xbuf + sp->boff(h, k, r));
+    if (grp) {  // peer copies (xGMI between devices, a device copy on a shared one)
       for (int r = 1; r < h->world; ++r) {
+        if (r == h->rank) continue;
         const bh_handle *x = (*grp)[(size_t)r];
-        size_t soff = 0;  // x's block of segment k in its send buffer
-        for (int j = 0; j < k; ++j) soff += sp->block_bytes(h, j, r);
-        const size_t bb = sp->block_bytes(h, k, r);
-        blk[(size_t)r] = sp->block(h, k, r, h->xbuf + xoff);
-        HIPCHK(h, hipMemcpyPeerAsync(h->xbuf + xoff, h->device, x->xbuf + soff, x->device, bb, sc));
-        xoff += bb;
+        const size_t o = sp->boff(h, k, r);
+        HIPCHK(h, hipMemcpyPeerAsync(h->xbuf + o, h->device, x->xbuf + o, x->device, sp->block_bytes(h, k, r), sx));
       }
     } else {
       int rc2;
       if ((rc2 = h->xport->group_start(h))) return rc2;
       for (int r = 1; r < h->world; ++r) {
+        uint8_t *at = h->xbuf + sp->boff(h, k, r);
         const size_t bb = sp->block_bytes(h, k, r);
-        blk[(size_t)r] = sp->block(h, k, r, h->xbuf + xoff);
-        if ((rc2 = h->xport->recv(h, h->xbuf + xoff, bb, r, sc))) {
+        rc2 = h->split_all() ? h->xport->bcast(h, at, bb, r, sx) : h->xport->recv(h, at, bb, r, sx);
+        if (rc2) {
           (void)h->xport->group_end(h);
           return rc2;
         }
-        xoff += bb;
       }
       if ((rc2 = h->xport->group_end(h))) return rc2;
     }
-    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sc));
-    for (int r = 1; r < h->world; ++r) bh::launch_split_unpack(v, sp->dpq(h, k), blk[(size_t)r], sc);
-    bh::launch_lt_rows(v, sc);
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k + 2], sx));
+    for (int r = 1; r < h->world; ++r)
+      if (r != h->rank) bh::launch_split_unpack(v, sp->dpq(h, k), blk[(size_t)r], sx);
+    bh::launch_lt_rows(v, sx);
     if (eager) {
       // the wide loop reads the row-major LA and FDT: the segment's rows
       // transposed here, from the columns just unpacked
       const int32_t *lo = sp->tab.data() + (size_t)k * 2 * n;
-      if ((rc = tiles(k, lo, lo + n, v))) return rc;
-      bh::launch_flow_transpose(v, sc);
-      bh::launch_fd_idle(v, sc);
+      if ((rc = tiles(k, lo, lo + n, v, sx))) return rc;
+      bh::launch_flow_transpose(v, sx);
+      bh::launch_fd_idle(v, sx);
     }
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sc));
-    if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sc));
+    HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * k], sx));
+    if (k == K - 1) HIPCHK(h, hipEventRecord(h->ev[1], sx));
     return BH_OK;
   };
   // where a segment's Lamport timestamps run: k_flow32x2 (the default)
@@ -1177,7 +1218,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     HIPCHK(h, hipMemcpyAsync(v.seg_lo, stg, (size_t)2 * n * 4, hipMemcpyHostToDevice, sc));
     HIPCHK(h, hipEventRecord(h->seg_ev[(size_t)3 * K + k], sc));  // the segment's lengths are on the device
     if (eager) {
-      if ((rc = tiles(k, stg, stg + n, v))) return rc;
+      if ((rc = tiles(k, stg, stg + n, v, sc))) return rc;
     } else {
       v.tile_list = nullptr;
       v.ntiles = 0;
@@ -1270,19 +1311,30 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       HIPCHK(h, wait_stream(sr));
       if (*ovf == 2) wd_fired = true;
     }
-    if (k + 1 < K) {
-      // segment k + 1 reuses the segbuf parity of k - 1, last read by its
-      // loop (async: the loop's own stop event -- no marker packet on the
-      // loop stream) or its resume point
+    // segment k + 1's coordinates (or receive).  A blocking transport (the
+    // host transport's receives and broadcasts wait on the host) takes them
+    // after loop k is enqueued, so loop k runs while the host waits for
+    // segment k + 1; stream-ordered exchanges go first, as the
+    // dataflow's launches do
+    const bool late = sp && h->xport && h->xport->blocking();
+    auto next = [&]() -> int {
+      if (k + 1 >= K) return BH_OK;
+      // segment k + 1 reuses the segbuf parity (and tile-list parity) of k - 1,
+      // last read by its loop (async: the loop's own stop event -- no marker
+      // packet on the loop stream) or its resume point
       if (async && k > 0) {
-        HIPCHK(h, hipStreamWaitEvent(sc, h->loop_evs[(size_t)2 * k - 1], 0));
+        HIPCHK(h, hipStreamWaitEvent(sx, h->loop_evs[(size_t)2 * k - 1], 0));
       } else {
         HIPCHK(h, hipEventRecord(sr_mark, sr));
-        HIPCHK(h, hipStreamWaitEvent(sc, sr_mark, 0));
+        HIPCHK(h, hipStreamWaitEvent(sx, sr_mark, 0));
       }
-      if ((rc = coords(k + 1))) { (void)hipEventDestroy(sr_mark); return rc; }
+      return coords(k + 1);
+    };
+    if (!late && (rc = next())) { (void)hipEventDestroy(sr_mark); return rc; }
+    if (wd_fired) {  // (every segment's receive is still posted)
+      if (late && (rc = next())) { (void)hipEventDestroy(sr_mark); return rc; }
+      continue;
     }
-    if (wd_fired) continue;  // (the remaining segments' receives are posted above)
     Dev rv = d;  // the loop's view: only the prefix lengths differ from d
     rv.chain_len = view(k).chain_len;
     if (dbg) HIPCHK(h, hipEventRecord(lt0, sr));
@@ -1322,6 +1374,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       (void)hipEventDestroy(sr_mark);
       return rc;
     }
+    if (late && (rc = next())) { (void)hipEventDestroy(sr_mark); return rc; }
     // where the next segment -- or the next call's new events -- resume
     const int32_t *next_len = nullptr;
     if (k + 1 < K) {
@@ -1360,6 +1413,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
       h->inc_valid = false;
       h->segments_used = 1;
       HIPCHK(h, wait_stream(sc));
+      HIPCHK(h, wait_stream(sx));
       const int32_t keep = d.round_persist;
       d.round_persist = 0;
       if (!(rc = rounds_coords(h))) rc = rounds_loop(h);
@@ -1375,6 +1429,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     h->inc_valid = false;
     h->segments_used = 1;
     HIPCHK(h, wait_stream(sc));
+    HIPCHK(h, wait_stream(sx));
     if ((rc = rounds_coords(h))) return rc;
     return rounds_loop(h);
   }
@@ -1452,7 +1507,10 @@ int rounds_segmented(bh_handle *h, bool *used) {
 // DivideRounds of a split group: this process's
 // shards -- the whole group in process, or this rank -- each in its role.
 // Rank 0 decides the call's base (its own resume state; broadcast across
-// processes), so every shard cuts the same segments.
+// processes), so every shard cuts the same segments.  The narrow split
+// (split_all): the coordinate shards' dataflow first (stream2), then every
+// shard's pipeline, which all-gathers the blocks and runs the loop; the
+// wide split: the same dataflow and sends, then shard 0's pipeline alone
 int rounds_split_stage(bh_handle *h) {
   int rc;
   std::vector<bh_handle *> sh = local_shards(h);
@@ -1464,6 +1522,7 @@ int rounds_split_stage(bh_handle *h) {
     if ((rc = set_chain_tables(x))) return rc;
   }
   (void)hipSetDevice(h->device);
+  const bool all = h->split_all();
   bh_handle *h0 = sh[0]->rank == 0 ? sh[0] : nullptr;  // the loop shard, if this process drives it
   const int64_t N = sh[0]->d.N;
   int64_t base = 0;
@@ -1477,21 +1536,38 @@ int rounds_split_stage(bh_handle *h) {
     HIPCHK(h, copy_sync(h->stream, pin, h->xbase, 8, hipMemcpyDeviceToHost));
     base = *pin;
   }
+  // the shards that run the loop, fame and order
+  std::vector<bh_handle *> loopers;
+  for (bh_handle *x : sh)
+    if (all || x->rank == 0) loopers.push_back(x);
+  auto on_loopers = [&](auto fn) -> int {  // (one host thread per shard in process: their host waits overlap)
+    if (loopers.empty()) return BH_OK;
+    if (loopers.size() == 1) {
+      HIPCHK(loopers[0], hipSetDevice(loopers[0]->device));
+      const int r = fn(loopers[0]);
+      if (r && loopers[0] != h) h->err = "shard " + std::to_string(loopers[0]->rank) + ": " + loopers[0]->err;
+      (void)hipSetDevice(h->device);
+      return r;
+    }
+    return run_local(h, fn);
+  };
   if (!split_active(sh[0])) {
-    // n > 128, chains beyond k_flow32's limits, or nothing inserted: shard 0
-    // alone takes the unsplit path; the coordinate shards start over when
+    // n > 128 beyond the wide dataflow's limits, chains beyond k_flow32's,
+    // a Reset hashgraph, or nothing inserted: the unsplit path on every
+    // shard that runs the loop (no exchange); the others start over when
     // the split applies again
     for (bh_handle *x : sh)
-      if (x->rank > 0) x->inc_valid = false;
-    if (!h0) return BH_OK;
-    bool used = false;
-    if ((rc = rounds_segmented(h0, &used))) return rc;
-    if (used) return BH_OK;
-    if ((rc = rounds_coords(h0))) return rc;
-    return rounds_loop(h0);
+      if (!all && x->rank > 0) x->inc_valid = false;
+    return on_loopers([](bh_handle *x) {
+      bool used = false;
+      int r;
+      if ((r = rounds_segmented(x, &used)) || used) return r;
+      if ((r = rounds_coords(x))) return r;
+      return rounds_loop(x);
+    });
   }
   if (base == N) {  // nothing new to divide
-    if (h0) h0->stage = std::max(h0->stage, 1);
+    for (bh_handle *x : loopers) x->stage = std::max(x->stage, 1);
     return BH_OK;
   }
   // the wide split pipelines as well: k_floww2 runs on the coordinate
@@ -1501,7 +1577,7 @@ int rounds_split_stage(bh_handle *h) {
   int K = segments_for(sh[0]->d, N - base);
   if (!sh[0]->d.fd_cols && !getenv("BH_SEGMENTS")) K = N - base >= 1000000 ? 4 : 1;
   const SplitPlan plan = split_plan(sh[0], K, base);
-  // the coordinate shards' work first: shard 0's receive waits on it
+  // the coordinate shards' dataflow first: the receives wait on it
   for (bh_handle *x : sh) {
     if (x->rank == 0) continue;
     HIPCHK(x, hipSetDevice(x->device));
@@ -1512,17 +1588,19 @@ int rounds_split_stage(bh_handle *h) {
     }
   }
   (void)hipSetDevice(h->device);
-  if (h0) {
-    h0->d.rows = h0->layout_rows;
-    h0->d.e0 = 0;
-    h0->d.seg_lo = h0->seg_zero;
-    h0->inc_calls += base > 0;
-    rc = rounds_pipelined(h0, plan.K, base, &plan, h->xport ? nullptr : &sh);
-  }
+  const std::vector<bh_handle *> *grp = h->xport ? nullptr : &h->group;
+  rc = on_loopers([&](bh_handle *x) {
+    x->d.rows = x->layout_rows;
+    x->d.e0 = 0;
+    x->d.seg_lo = x->seg_zero;
+    x->inc_calls += base > 0;
+    return rounds_pipelined(x, plan.K, base, &plan, grp);
+  });
   for (bh_handle *x : sh) {  // the sends / copies of this call are done
     if (x->rank == 0) continue;
     HIPCHK(x, hipSetDevice(x->device));
     HIPCHK(x, wait_stream(x->stream2));
+    if (x->stream3) HIPCHK(x, wait_stream(x->stream3));
   }
   (void)hipSetDevice(h->device);
   return rc;
@@ -1567,13 +1645,16 @@ int stage_rounds(bh_handle *h) {
 // ---------------------------------------------------------------------------
 // stage 2: DecideFame -- this shard's rounds, then exchanged
 
-// the shards the passes after DivideRounds split between: every shard, or
-// with the coordinate split shard 0 alone (it holds the rounds)
-inline int32_t pass_world(const bh_handle *h) { return h->split ? 1 : h->world; }
+// the shards the passes after DivideRounds split between: every shard
+// (replicated coordinates, or the narrow split, where every shard ran the
+// loop), or with the wide split shard 0 alone (it holds the rounds)
+inline bool pass_solo(const bh_handle *h) { return h->split && !h->split_all(); }
+inline int32_t pass_world(const bh_handle *h) { return pass_solo(h) ? 1 : h->world; }
+inline int32_t pass_rank(const bh_handle *h) { return pass_solo(h) ? 0 : h->rank; }
 
 template <class F>
 int run_pass(bh_handle *h, F fn) {
-  if (!h->split) return run_local(h, fn);
+  if (!pass_solo(h)) return run_local(h, fn);
   return h->rank == 0 ? fn(h) : BH_OK;  // (in process, h is shard 0)
 }
 
@@ -1582,7 +1663,7 @@ int run_pass(bh_handle *h, F fn) {
 int fame_local(bh_handle *h) {
   if (h->stage < 1) return h->fail(BH_ERR_STATE, "DecideFame before DivideRounds");
   int64_t r0, r1;
-  shard_range(std::max(0, h->R - h->P), pass_world(h), h->split ? 0 : h->rank, &r0, &r1);
+  shard_range(std::max(0, h->R - h->P), pass_world(h), pass_rank(h), &r0, &r1);
   if (r1 > r0) bh::launch_fame(h->d, h->R, (int32_t)(h->P + r0), (int32_t)(h->P + r1), h->stream);
   HIPCHK(h, hipGetLastError());
   return BH_OK;
@@ -1686,7 +1767,7 @@ int order_local(bh_handle *h) {
   // frames [P, P1): rounds this call processes (earlier frames are final)
   bh::launch_order_buckets(d, h->R, h->P, s);
   int64_t f0, f1;
-  shard_range(P1 - h->P, pass_world(h), h->split ? 0 : h->rank, &f0, &f1);
+  shard_range(P1 - h->P, pass_world(h), pass_rank(h), &f0, &f1);
   bh::launch_order_sort(d, (int32_t)(h->P + f0), (int32_t)(h->P + f1), s);
   HIPCHK(h, hipGetLastError());
   if (pass_world(h) > 1) {  // frame offsets: the order exchange's ranges
@@ -1798,18 +1879,24 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out);
 void bh_destroy(bh_handle *h);
 
 // How a group shares the coordinates (BH_SHARD_COORDS):
-//   split (2, the default at n <= 128; BH_SHARD_COORDS=split above it) --
-//     shard 0 runs the round loop, fame and order; the other shards compute
-//     LA columns and ship them to it per segment (kernels_split.hip);
+//   split (2) -- the coordinate shards 1 .. G-1 compute LA column ranges and
+//     ship them per segment (kernels_split.hip).  n <= 128: all-gathered,
+//     every shard runs the round loop, fame rounds and frame sorts split
+//     between all shards.  128 < n <= 512 (the wide split): shard 0 alone
+//     receives them and runs the loop, fame and order.  The default where
+//     the coordinate shards' links carry a step's columns in less than the
+//     step (DESIGN.md section 7's table, 2.06 B per column and event): from
+//     G = 3 at n <= 128 (C3: 2.7 GB per step, 42 ms over G = 2's one link
+//     against a 35-ms step), from G = 4 up to n = 512 (C4: 21 GB);
 //   columns (1) -- every shard computes a range of LA columns, all-gathered;
-//   replicate (0, the default above n = 128) -- every shard computes all of
-//     it; fame rounds and frame sorts are split.
-static int shard_mode(int n) {
+//   replicate (0, the default otherwise) -- every shard computes all of it;
+//     fame rounds and frame sorts are split.
+static int shard_mode(int n, int world) {
   const char *e = getenv("BH_SHARD_COORDS");
   if (e && !strcmp(e, "columns")) return 1;
   if (e && !strcmp(e, "replicate")) return 0;
-  if (e && !strcmp(e, "split")) return 2;  // (n > 128 as well: the wide split)
-  return n <= bh::FL_MAXN ? 2 : 0;
+  if (e && !strcmp(e, "split")) return 2;
+  return (n <= bh::FL_MAXN && world >= 3) || (n <= bh::FW_MAXN && world >= 4) ? 2 : 0;
 }
 
 int bh_create(const bh_config *cfg, bh_handle **out) {
@@ -1828,7 +1915,7 @@ int bh_create(const bh_config *cfg, bh_handle **out) {
       return rc;
     }
   }
-  const int mode = shard_mode(cfg->n_participants);
+  const int mode = shard_mode(cfg->n_participants, G);
   for (int r = 0; r < G; ++r) {
     bh_handle *x = g[(size_t)r];
     x->rank = r;
@@ -2523,7 +2610,7 @@ static int comm_join(bh_handle *h, int32_t rank, int32_t world, bh::Comm *x) {
   h->xport = x;
   h->rank = rank;
   h->world = world;
-  const int mode = world > 1 ? shard_mode(h->d.n) : 0;  // see bh_create
+  const int mode = world > 1 ? shard_mode(h->d.n, world) : 0;  // see bh_create
   h->shard_cols = mode == 1;
   h->split = mode == 2;
   int64_t c0 = 0, c1 = h->d.n;

@@ -54,6 +54,7 @@ struct RcclComm final : Comm {
 };
 
 struct HostComm final : Comm {
+  bool blocking() const override { return true; }
   bh_transport t{};
   int32_t rank = 0;
   uint8_t *stage = nullptr;  // pinned

@@ -47,7 +47,13 @@ enum StateSlot {
   ST_RESUME = 11,   // k_resume_point: the last round whose boundaries B[r][*] a prefix run fixed
   ST_FIATMAX = 12,  // k_fiat: the highest round of an event below the closed form's first round (-1: none)
   ST_FIATDONE = 13, ST_FIATEV = 14, ST_FIATCH = 15,  // k_fiat: chains done, events visited, chunks scanned
-  ST_COUNT = 16
+  // k_round2p's entry gate: ST_FLOWOVF == 2 as the kernel before the loop on
+  // the loop stream saw it (k_cand_rows / k_seg_resume).  ST_FLOWOVF itself
+  // may change while a loop's workgroups are being dispatched (the split's
+  // unpack of a LATER segment runs on the coordinate stream), so every
+  // workgroup of one loop decides on this copy
+  ST_GATE = 16,
+  ST_COUNT = 18  // (even: the pinned staging words after ST_COUNT hold an 8-byte value at ST_COUNT + 6)
 };
 
 // FDT: firstDescendants by column, tiled by 64 chain-major rows --

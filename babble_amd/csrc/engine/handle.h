@@ -36,6 +36,9 @@ struct Comm {
   virtual int recv(bh_handle *h, void *buf, size_t bytes, int32_t peer, hipStream_t s) = 0;
   virtual int group_start(bh_handle *) { return 0; }  // (RCCL: receives from several peers at once)
   virtual int group_end(bh_handle *) { return 0; }
+  // true: the calls wait on the host (the host transport); false: they are
+  // enqueued on s and return (RCCL)
+  virtual bool blocking() const { return false; }
 };
 Comm *make_rccl_comm(bh_handle *h, int32_t rank, int32_t world, const uint8_t *id);  // nullptr on failure (h->err)
 Comm *make_host_comm(const bh_transport &t, int32_t rank);
@@ -160,15 +163,22 @@ struct bh_handle {
   std::vector<bh_handle *> group;  // in-process group: every shard (group[rank] == this); empty otherwise
   bh::Comm *xport = nullptr;       // multi-process group (bh_comm_init / bh_comm_init_transport)
   bool shard_cols = false;         // split the coordinate dataflow's LA columns (else every shard computes all)
-  // the coordinate split (kernels_split.hip): shard 0
-  // runs the round loop, fame and order; shards 1 .. G-1 the dataflow for a
-  // range of LA columns each, shipped to shard 0 per segment
+  // the coordinate split (kernels_split.hip): shards
+  // 1 .. G-1 run the dataflow for a range of LA columns each and ship every
+  // segment's rows of them.  n <= 128 (split_all): the blocks are
+  // all-gathered and EVERY shard runs the round loop on the full columns, so
+  // fame rounds and frame sorts split between all shards as in the
+  // replicated mode; 128 < n <= 512 (the wide split): shard 0 alone receives
+  // them and runs the loop, fame and order
   bool split = false;
-  uint8_t *xbuf = nullptr;        // coordinate shard: packed blocks of every segment; shard 0: received blocks
+  bool split_all() const { return split && d.fd_cols; }
+  uint8_t *xbuf = nullptr;        // every segment's blocks of every coordinate shard, at SplitPlan::boff
   size_t xcap = 0;
   int32_t *xseg = nullptr;        // [K][lo, hi][n] segment views, then [K][P, Q][n + 1] packing tables
   int32_t xseg_k = 0;             // segments xseg has room for
-  hipEvent_t xev[2]{};            // shard 0: around a segment's receive (exchange time)
+  std::vector<hipEvent_t> pack_ev;  // coordinate shard: segment k's own block packed (stream2)
+  hipStream_t stream3 = nullptr;    // the split's receives and unpacks, beside the dataflow (stream2)
+  hipEvent_t xprep = nullptr;       // the call's chain tables prepared (stream2), before any unpack
   int32_t *xbase = nullptr;       // multi-process: rank 0's base for the call (broadcast)
   float xchg_ms = 0;               // exchange time of the last pass sequence (host wall, incl. waits)
   std::vector<int32_t> wofs_h;     // [R + 1] witness offsets (fame exchange ranges; launch size)
@@ -213,9 +223,9 @@ struct bh_handle {
   // it was); -1 otherwise
   int fail_alloc_in = -1;
 
-  // a coordinate rank of a multi-process split group: it ran no consensus
-  // pass, so it holds no results (rank 0 does)
-  bool no_results() const { return split && rank > 0 && xport != nullptr; }
+  // a coordinate rank of a multi-process WIDE split group: it ran no
+  // consensus pass, so it holds no results (rank 0 does)
+  bool no_results() const { return split && !split_all() && rank > 0 && xport != nullptr; }
   int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;

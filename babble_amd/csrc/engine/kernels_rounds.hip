@@ -1331,6 +1331,7 @@ __device__ __forceinline__ void cand_row(const Dev &d, int c, int32_t r, int32_t
 __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
   const int c = blockIdx.x;
   const int32_t r = from_resume ? d.state[ST_RESUME] : 0;
+  if (c == 0 && threadIdx.x == 0) d.state[ST_GATE] = d.state[ST_FLOWOVF] == 2 ? 1 : 0;  // (k_round2p's entry gate)
   cand_row(d, c, r, from_resume ? d.B[(int64_t)r * d.n + c] : 0);
 }
 
@@ -1384,6 +1385,7 @@ __global__ __launch_bounds__(1024) void k_seg_resume(Dev d) {
       // (ST_ROUNDS stays: every workgroup reads it above; the loop sets it)
       d.state[ST_RESUME] = r0;
       d.state[ST_PFAIL] = max(d.state[ST_PFAIL], d.state[ST_ERR]);
+      d.state[ST_GATE] = d.state[ST_FLOWOVF] == 2 ? 1 : 0;  // (k_round2p's entry gate)
       d.state[ST_CUR0] = r0;
       d.state[ST_CUR0 + 1] = 0;
       d.state[ST_DONE] = 0;
@@ -1811,8 +1813,11 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   // trip: after a failed one (ST_PFAIL: capacity, or a barrier that gave up)
   // or unfinished coordinates (ST_FLOWOVF = 2: a split block without room),
   // the later ones leave at once -- every workgroup reads the same words,
-  // written before the launch -- and the host falls back after the last
-  if (d.state[ST_PFAIL] || d.state[ST_FLOWOVF] == 2) {
+  // written before the launch by the kernels ahead of it on the loop stream
+  // (ST_GATE: the copy of ST_FLOWOVF k_cand_rows / k_seg_resume took; the
+  // word itself can change mid-dispatch when a later segment's unpack
+  // overflows) -- and the host falls back after the last
+  if (d.state[ST_PFAIL] || d.state[ST_GATE]) {
     if (c == 0 && t == 0) {
       d.state[ST_DONE] = 1;
       signal_done(d);

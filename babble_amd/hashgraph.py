@@ -243,6 +243,8 @@ class Hashgraph:
     @property
     def pending_rounds(self):
         k = self._L.bh_get_pending_rounds(self._h, None, None, 0)
+        if k < 0:  # a negated BH_ERR_* (a coordinate rank of a split group holds no rounds)
+            self._check(-k)
         idx = np.zeros(max(k, 1), np.int32)
         dec = np.zeros(max(k, 1), np.int8)
         self._L.bh_get_pending_rounds(self._h, _ptr(idx), _ptr(dec), k)
@@ -251,6 +253,8 @@ class Hashgraph:
     @property
     def undetermined_events(self):
         k = self._L.bh_get_undetermined(self._h, None, 0)
+        if k < 0:
+            self._check(-k)
         ids = np.zeros(max(k, 1), np.int32)
         self._L.bh_get_undetermined(self._h, _ptr(ids), k)
         return ids[:k]

@@ -8,19 +8,23 @@ region.  Workload: BASELINE.json's headline config C3 (128 participants,
 10M-event random-gossip DAG).
 
 Multi-GPU (one process per GPU):
-  --mode replicas (the default): every rank orders a DAG of its own (a
-      node's independent hashgraphs; weak scaling) -- value = events ordered
-      by all ranks / the slowest rank's time.  One hashgraph's rounds are a
-      serial chain (the round loop is 90 % of the step), so this is how the
-      path scales;
-  --mode shards: the ranks order ONE DAG together (strong scaling): rank 0
-      runs the round loop, fame and the order, ranks 1..N-1 the coordinate
-      dataflow over LA column ranges, shipping every pipeline segment's
-      columns to rank 0 (ncclSend / ncclRecv over xGMI, 16-bit packed);
-      BH_SHARD_COORDS=replicate / columns select the round-3 splits.  Rank
-      0's step is bounded by the loop alone: 5.81 against 5.94 us per round
-      beside the coordinates on one GPU (profiles/r5_bench_seg1.json), so
-      at most ~2 % faster than one GPU.
+  --mode shards (the default): the ranks order ONE DAG together (strong
+      scaling; value = the DAG's events ordered per step / the slowest
+      rank's time).  At n <= 128 (C3) from 3 ranks, ranks 1..N-1 run the coordinate
+      dataflow over LA column ranges and all-gather every pipeline
+      segment's columns (ncclBroadcast per coordinate rank over xGMI,
+      16-bit packed); every rank runs the round loop on them, and the fame
+      rounds and frame sorts are split between all ranks (bh_shard_range)
+      and exchanged.  At 128 < n <= 512 (C4) from 4 ranks the coordinate
+      ranks send their columns to rank 0, which runs the loop, fame and
+      order.  Below that (C3 at 2 ranks: one link would carry the step's
+      2.7 GB of columns in ~42 ms, longer than the step) every rank computes
+      the coordinates and the loop, and the fame rounds and frame sorts are
+      split.  One hashgraph's rounds
+      are a serial chain (the round loop is ~95 % of a C3 step), so the
+      expected curve is flat (DESIGN.md section 7's table);
+  --mode replicas: every rank orders a DAG of its own (weak scaling, no
+      data-path collective) -- N copies of the 1-GPU number, labelled so.
 
 usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg 3] [--events N] [--mode replicas|shards]
        torchrun ... bench.py --gpus N ...
@@ -85,15 +89,21 @@ def _per_launch(pmc, kernel, launches):
     return v["hbm_bytes_per_step"] / launches if v and launches else None
 
 
-def _shard_mode(n):
+def _shard_mode(n, world):
     """the engine's shard mode (BH_SHARD_COORDS; api.cpp shard_mode)"""
     e = os.environ.get("BH_SHARD_COORDS")
-    return e if e in ("columns", "replicate") else ("split" if n <= 128 else "replicate")
+    if e in ("columns", "replicate", "split"):
+        return e
+    return "split" if (n <= 128 and world >= 3) or (n <= 512 and world >= 4) else "replicate"
 
 
 def _parallelism(world, n, one_dev=False):
-    mode = _shard_mode(n)
+    mode = _shard_mode(n, world)
     xp = "host transport over gloo, all ranks on device 0" if one_dev else None
+    if mode == "split" and n <= 128:
+        return (f"{world} shards ({xp or 'RCCL broadcast over xGMI'}): ranks 1..{world - 1} run the coordinate "
+                f"dataflow over LA column ranges and all-gather every segment's columns (16-bit packed); every "
+                f"rank runs the round loop; fame rounds and frame sorts split over all {world} ranks")
     if mode == "split":
         return (f"{world} shards ({xp or 'RCCL send/recv over xGMI'}): rank 0 runs the round loop, fame and "
                 f"order; ranks 1..{world - 1} run the coordinate dataflow over LA column ranges and ship every "
@@ -135,11 +145,30 @@ def cpu_baseline(cfg, sample_events, log):
     ordered = len(o.consensus_order())
     o.close()
     log(f"cpu baseline: {ordered} events ordered in {dt:.2f}s")
-    return dict(value=ordered / dt, unit="events/s", cores=1, kind="port", cpu_model=_cpu_model(),
-                nproc=os.cpu_count(), threads_used=1,
-                sample=f"first {sample_events} events of the cfg{cfg} DAG (prefix), batch schedule "
-                       f"(coordinates+DivideRounds+DecideFame+DecideRoundReceived+ProcessDecidedRounds), "
-                       f"C restatement of hashgraph.go, 1 thread, {ordered} events ordered in {dt:.2f}s")
+    out = dict(value=ordered / dt, unit="events/s", cores=1, kind="port", cpu_model=_cpu_model(),
+               nproc=os.cpu_count(), threads_used=1, host="this bench box (rank 0's host cores)",
+               sample=f"first {sample_events} events of the cfg{cfg} DAG (prefix), batch schedule "
+                      f"(coordinates+DivideRounds+DecideFame+DecideRoundReceived+ProcessDecidedRounds), "
+                      f"C restatement of hashgraph.go, 1 thread, {ordered} events ordered in {dt:.2f}s")
+    # the same oracle over the WHOLE DAG, from the run that made the committed
+    # digests (tests/golden/make_whole_digests.py) -- not timed here (minutes
+    # to an hour); its per-event cost grows with the DAG, so the prefix rate
+    # above flatters the CPU
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", f"whole_c{cfg}.json")) as f:
+            w = json.load(f)
+        o = w["oracle"]
+        sec = o["insert_s"] + o["consensus_s"]
+        out["whole_dag"] = dict(
+            value=w["n_ordered"] / sec, unit="events/s", threads=o.get("threads", 1), events=w["events"],
+            ordered=w["n_ordered"], seconds=sec,
+            host="the build container (Intel Xeon Processor, 8 vCPU), not the bench box",
+            source=f"tests/golden/whole_c{cfg}.json: oracle ({o['lib']}), insert {o['insert_s']} s + "
+                   f"consensus {o['consensus_s']} s")
+        out["prefix_over_whole"] = out["value"] / out["whole_dag"]["value"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def main():
@@ -152,8 +181,8 @@ def main():
     ap.add_argument("--sig", type=int, default=0, help="1 = deterministic ECDSA signatures")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="events for the CPU baseline (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
-    ap.add_argument("--mode", choices=("shards", "replicas"), default="replicas",
-                    help="N>1: order one DAG per rank (weak, the default) or shard one DAG over the ranks (strong)")
+    ap.add_argument("--mode", choices=("shards", "replicas"), default="shards",
+                    help="N>1: shard one DAG over the ranks (strong, the default) or order one DAG per rank (weak)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -240,8 +269,8 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist)
     persist_per_step = (hg.loop_stats()[0] - persist0) / args.steps  # persistent loop launches (one per segment)
-    if sharded and rank > 0 and _shard_mode(c["n"]) == "split":
-        # a coordinate rank of the split holds no consensus results (the
+    if sharded and rank > 0 and _shard_mode(c["n"], world) == "split" and c["n"] > 128:
+        # a coordinate rank of the wide split holds no consensus results (the
         # engine refuses the query); rank 0 reports the step
         hg.close()
         dist.destroy_process_group()
@@ -290,11 +319,21 @@ def main():
         loop_ms = float(stage_tot[1] / args.steps)
     iter_us = 1000.0 * loop_ms / max(iters, 1)
     loop_launches = persist_per_step if persistent else iters
-    loop_alg = ordered * B  # the loop orders every event once: B(n) per event over its launches
+    # B(n) split between the two kernels, so that their fractions add up to
+    # the whole step's: the coordinate kernel is charged 12n + 12 B per
+    # inserted event (two parent LA rows read, its own row and LT written),
+    # the loop the remainder of the step's B(n) x ordered events -- the
+    # per-event scalars, sort key and value, signature tie-break (84 B per
+    # event at any n), which the loop's rounds decide.  What the loop READS
+    # (window rows, candidates' rows, from L2 / MALL) is not algorithmic: its
+    # PMC traffic is quoted beside it
+    coord_alg = N * (12 * n + 12)
+    loop_alg = max(ordered * B - coord_alg, 0)
     loop_obj = {"kernel": round_kernel, "launches_per_step": loop_launches, "device_ms_per_step": loop_ms,
                 "avg_launch_ms": loop_ms / max(loop_launches, 1e-9),
                 "alg_bytes_per_launch": loop_alg / max(loop_launches, 1e-9),
                 "achieved": loop_alg / (loop_ms * 1e-3) / 1e9, "frac": loop_alg / (loop_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "alg_bytes_per_event": (loop_alg / ordered) if ordered else None,
                 "round_iterations": iters, "us_per_iteration": iter_us,
                 "traffic_per_launch": _per_launch(pmc, round_kernel, loop_launches),
                 "note": "latency-bound: the rounds are a serial chain; one persistent launch per pipeline "
@@ -305,10 +344,10 @@ def main():
     # coordinate stream around each launch
     coord_ms = float(np.mean(sweep_ms))
     coord_launches = segments if hg.profile_kernel() in ("k_flow32x2", "k_flow32", "k_floww2", "k_floww") else 1
-    coord_alg = N * (12 * n + 12)
     coord_obj = {"kernel": hg.profile_kernel(), "launches_per_step": coord_launches, "device_ms_per_step": coord_ms,
                  "avg_launch_ms": coord_ms / max(coord_launches, 1),
                  "alg_bytes_per_launch": coord_alg / max(coord_launches, 1),
+                 "alg_bytes_per_event": 12 * n + 12,
                  # (shards: rank 0 runs no dataflow -- its coordinate time is the exchange)
                  "achieved": coord_alg / (coord_ms * 1e-3) / 1e9 if coord_ms > 0 else None,
                  "frac": coord_alg / (coord_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if coord_ms > 0 else None,
@@ -359,7 +398,10 @@ def main():
     if rank == 0 and world == 1 and cpu_sample > 0:
         out["cpu_baseline"] = cpu_baseline(args.cfg, cpu_sample, log)
         cv = out["cpu_baseline"]["value"]
-        out["speedup_vs_cpu"] = value / cv if cv > 0 else None
+        out["speedup_vs_cpu"] = value / cv if cv > 0 else None  # (against the prefix rate)
+        wd = out["cpu_baseline"].get("whole_dag")
+        if wd:
+            out["speedup_vs_cpu_whole_dag"] = value / wd["value"]
     else:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -196,6 +196,7 @@ class Hashgraph {
 
   std::vector<int32_t> UndeterminedEvents() const {
     const int64_t cnt = bh_get_undetermined(h_, nullptr, 0);
+    if (cnt < 0) check((int)-cnt);  // a negated BH_ERR_* code
     std::vector<int32_t> ids((size_t)std::max<int64_t>(cnt, 0));
     if (cnt > 0) bh_get_undetermined(h_, ids.data(), cnt);
     return ids;
@@ -203,6 +204,7 @@ class Hashgraph {
 
   std::vector<PendingRound> PendingRounds() const {
     const int32_t cnt = bh_get_pending_rounds(h_, nullptr, nullptr, 0);
+    if (cnt < 0) check(-cnt);  // a negated BH_ERR_* code
     std::vector<int32_t> idx((size_t)std::max(cnt, 0));
     std::vector<int8_t> dec((size_t)std::max(cnt, 0));
     if (cnt > 0) bh_get_pending_rounds(h_, idx.data(), dec.data(), cnt);

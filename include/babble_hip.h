@@ -170,10 +170,14 @@ int bh_get_consensus_order(bh_handle *h, int64_t first, int64_t count, int32_t *
  * #events of its Frame, #transactions (concatenated in consensus order). */
 int bh_get_blocks(bh_handle *h, int64_t first, int64_t count, int32_t *round_received,
                   int64_t *first_event, int64_t *n_events, int64_t *n_transactions);
-/* Hashgraph.PendingRounds: returns the count, fills up to cap entries */
+/* Hashgraph.PendingRounds: returns the count, fills up to cap entries.
+ * A negative return is a negated BH_ERR_* code (-BH_ERR_STATE on a shard
+ * that holds no consensus results: a coordinate rank of a wide split) --
+ * check it before using the count. */
 int32_t bh_get_pending_rounds(bh_handle *h, int32_t *index, int8_t *decided, int32_t cap);
 /* Hashgraph.UndeterminedEvents (insertion order): returns the count, fills
- * up to cap ids (ids may be NULL) */
+ * up to cap ids (ids may be NULL).  Negative: a negated BH_ERR_* code, as
+ * for bh_get_pending_rounds. */
 int64_t bh_get_undetermined(bh_handle *h, int32_t *ids, int64_t cap);
 
 /* Store.GetRound(r) / RoundWitnesses(r) (inmem_store.go:185-211) and the

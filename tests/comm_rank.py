@@ -9,8 +9,11 @@ Every rank inserts the same DAG in per-sync batches and calls RunConsensus
 after each (every pass is collective); rank 0 compares its state with the
 oracle's after every call -- the cross-node agreement check of the
 reference (node/core_test.go:361-380: every node's blocks and consensus
-events are the same) with rank 0 as the node -- and a coordinate rank of
-the split must refuse result queries (it ran no consensus pass).
+events are the same) with rank 0 as the node.  Every rank that holds
+results (all of them, except the coordinate ranks of a wide split, which
+must refuse result queries: they ran no consensus pass) reports a digest of
+its whole final state, which the test requires to be the same on every
+such rank: the sharded fame rounds and frame sorts reached every rank.
 """
 import argparse
 import json
@@ -35,6 +38,7 @@ def main():
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank, world_size=a.world)
     from babble_amd import Hashgraph, HashgraphError
     from babble_amd.dag import Dag
+    from digest import engine_digest
 
     def t(buf):
         return torch.frombuffer(buf, dtype=torch.uint8)
@@ -66,16 +70,19 @@ def main():
                 o.insert_dag(*(x[lo:hi] for x in args))
                 o.run_consensus()
                 _compare(o, hg, f"rank 0 of {a.world} after [0, {hi})")
-        if a.rank == 0:
-            res["segments"], res["incremental_calls"] = hg.pipeline()
-            res["exchange_ms"] = hg.stage_ms()[5]
+        res["segments"], res["incremental_calls"] = hg.pipeline()
+        res["exchange_ms"] = hg.stage_ms()[5]
+        try:
             res["consensus_events"] = int(hg.stats().consensus_events)
-        else:
-            try:
-                hg.stats()
-                res["stats_on_coordinate_rank"] = "returned"
-            except HashgraphError as e:
-                res["stats_on_coordinate_rank"] = f"refused ({e.code})"
+            res["digest"] = engine_digest(hg)
+            res["stats"] = "returned"
+        except HashgraphError as e:
+            res["stats"] = f"refused ({e.code})"
+            try:  # the other result getters refuse alike (a negated code, not an empty list)
+                hg.pending_rounds
+                res["pending_rounds"] = "returned"
+            except HashgraphError as e2:
+                res["pending_rounds"] = f"refused ({e2.code})"
         res["calls"] = calls
         res["ok"] = True
         hg.close()

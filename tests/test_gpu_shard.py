@@ -2,13 +2,15 @@
 in-process shard group on ONE device (device_ids = [0, 0] / [0, 0, 0]) runs
 exactly the split kernels and device-to-device exchanges a multi-GPU group
 runs over xGMI, and must match the single-shard engine -- and the oracle --
-bit for bit: the coordinate split (the default at n <= 128: shard 0 runs the
-round loop, fame and order; the other shards compute LA columns and ship
-them per segment), LA columns all-gathered (BH_SHARD_COORDS=columns) or
-replicated coordinates with fame by round ranges and frames sorted by
-range (BH_SHARD_COORDS=replicate).  The split at 128 < n <= 512 (k_floww2 on
-the coordinate shards, shard 0 transposing each received segment) is opt-in
-(BH_SHARD_COORDS=split)."""
+bit for bit: the coordinate split (the default at n <= 128: shards 1 .. G-1
+compute LA column ranges and all-gather them per segment, every shard runs
+the round loop, fame rounds and frame sorts split between all shards), LA
+columns all-gathered unpipelined (BH_SHARD_COORDS=columns) or replicated
+coordinates with fame by round ranges and frames sorted by range
+(BH_SHARD_COORDS=replicate).  The split at 128 < n <= 512 (k_floww2 on the
+coordinate shards, shard 0 transposing each received segment and running
+the loop, fame and order alone) is the default from 4 shards and
+BH_SHARD_COORDS=split below."""
 import numpy as np
 import pytest
 
@@ -184,26 +186,33 @@ def test_group_rerun_after_reset(monkeypatch, coords, devs):
         assert grp.pipeline()[0] == 8
 
 
-@pytest.mark.parametrize("rng", [2, 60, 120, 250])
-def test_split_overflow_chunks(monkeypatch, rng):
+@pytest.mark.parametrize("rng,seg", [(2, 0), (60, 0), (120, 0), (250, 0), (2, 2), (2, 5)])
+def test_split_overflow_chunks(monkeypatch, rng, seg):
     """Chunks whose 64 rows span more than the 16-bit range travel raw in the
     block's overflow slots (BH_SPLIT_RANGE lowers the range so gossip DAGs
     have them); a block that runs out of slots sends the call to the unsplit
-    path on shard 0 -- either way the result is the oracle's."""
+    path -- either way the result is the oracle's.  seg > 0: only the blocks
+    of segment `seg` on overflow (BH_SPLIT_RANGE_SEG), so the flag is raised
+    by a later segment's unpack while earlier segments' persistent loops run
+    (every workgroup of a loop decides on the copy k_seg_resume
+    took, ST_GATE; the call is a split overflow, not a loop that gave up)."""
     from babble_amd import Hashgraph
     from babble_amd.dag import Dag
     monkeypatch.setenv("BH_SHARD_COORDS", "split")
-    monkeypatch.setenv("BH_SEGMENTS", "3")
+    monkeypatch.setenv("BH_SEGMENTS", "3" if seg == 0 else "8")
     monkeypatch.setenv("BH_SPLIT_RANGE", str(rng))
-    n, N = 32, 30_000
+    monkeypatch.setenv("BH_SPLIT_RANGE_SEG", str(seg))
+    n, N = 32, 30_000 if seg == 0 else 60_000
     d = Dag(n, N, 95, lagging=4, sig_mode=0)
     o = Oracle(n, d.participant_ids, capacity=N)
     o.insert_dag(d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
     o.run_consensus()
     grp = Hashgraph(d.participant_ids, N, devices=[0, 0, 0])
     assert not grp.insert_dag(d).any()
+    fb0 = grp.loop_stats()[1]
     grp.run_consensus()
-    _compare(o, grp, f"split, range {rng}")
+    _compare(o, grp, f"split, range {rng} from segment {seg}")
+    assert grp.loop_stats()[1] == fb0  # no persistent loop gave up (no pbar_spin stall)
 
 
 @pytest.mark.parametrize("devs,K", [([0, 0], 3), ([0, 0, 0, 0], 4)])
