@@ -1984,6 +1984,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.flow_lt = 1;
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.round_f32 = getenv("BH_ROUND_F32") ? atoi(getenv("BH_ROUND_F32")) != 0 : 1;
+  d.round_early = getenv("BH_ROUND_EARLY") ? atoi(getenv("BH_ROUND_EARLY")) != 0 : 0;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
   // the XCD-hierarchical barrier above 64 workgroups (with per-workgroup
   // release words in both forms: C3 7.6 -> 7.05 us per iteration; C5's 64

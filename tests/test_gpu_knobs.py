@@ -13,7 +13,13 @@ test_gpu_shard.py, test_gpu_comm.py).
   for every segment's loop;
 * BH_LOOP_TIMING=0 -- no HIP events around the loop (stage 7 reads 0);
 * BH_ROUND_F32=0 -- k_round2p's search counting in int32 (sign bits of
-  LA - FD) instead of packed f32 with the clamp modifier (the default).
+  LA - FD) instead of packed f32 with the clamp modifier (the default);
+* BH_ROUND_EARLY=0 -- k_round2p without the early loads (round 6's
+  default issues the next round's candidate, window and hand-off loads
+  before the workgroup's own hand-off stores);
+* BH_SEG_RATIO -- the segment pipeline's growth ratio (segment k holds a
+  ratio^k share of the events): equal segments (1.0) and steep ones (1.8)
+  cut the DAG at other boundaries than the default 1.32.
 """
 import os
 
@@ -84,3 +90,19 @@ def test_round_int32_search(monkeypatch, n, N, seed, lag, K):
     monkeypatch.setenv("BH_SEGMENTS", str(K))
     loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
     assert loops >= 1 and fallbacks == 0
+
+
+@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xDC, 0, 3), (64, 40_000, 0xDD, 21, 4), (20, 8_000, 0xDE, 2, 2)])
+def test_round_no_early_loads(monkeypatch, n, N, seed, lag, K):
+    monkeypatch.setenv("BH_ROUND_EARLY", "0")
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
+    assert loops >= 1 and fallbacks == 0
+
+
+@pytest.mark.parametrize("ratio,n,N,K", [("1.0", 128, 80_000, 8), ("1.8", 64, 60_000, 6), ("1.32", 32, 50_000, 12)])
+def test_segment_ratio(monkeypatch, ratio, n, N, K):
+    monkeypatch.setenv("BH_SEG_RATIO", ratio)
+    monkeypatch.setenv("BH_SEGMENTS", str(K))
+    hg = _random_parity(n, N, 0xDF + K, 2)
+    assert hg.pipeline()[0] == K

@@ -31,6 +31,13 @@ for step in "$@"; do
         --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus $N --steps 3 --warmup 1 --cfg $cfg --events $ev \
         > $out/${tag}_multi$N.json 2> $out/${tag}_multi$N.log || { tail -30 $out/${tag}_multi$N.log; exit 1; }
       tail -c 600 $out/${tag}_multi$N.json ;;
+    timeline)
+      IFS=: read -r cfg envs <<< "$arg"
+      name=${tag}_tl_c${cfg}${envs:+_$(echo $envs | tr ',=' '__')}
+      echo "== timeline cfg$cfg $envs"
+      env BH_DIAG=1 BH_TIMELINE=$out/$name.bin $(echo $envs | tr ',' ' ') timeout -k 10 600 python -u bench.py --cfg $cfg \
+        --steps 1 --warmup 1 --cpu-sample 0 > $out/$name.json 2> $out/$name.log || { tail -20 $out/$name.log; exit 1; }
+      python3 tools/timeline.py --tagged $out/$name.bin | tee $out/$name.txt ;;
     prof)
       echo "== rocprofv3 cfg$arg"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/${tag}_prof -o run -- python3 -u bench.py --cfg $arg --steps 3 --warmup 1 --cpu-sample 0 \
