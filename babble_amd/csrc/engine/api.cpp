@@ -793,17 +793,28 @@ int segments_for(const Dev &d, int64_t events) {
 // segment's dataflow, 1/49 of the events at K = 8 (round 4: a first segment
 // of 1/(4K) and K - 1 equal ones after it, which at C3 left the loop waiting
 // ~2 ms for the second segment)
-static void segment_bounds(int64_t base, int64_t N, int K, int64_t *Ns) {
+// The growth ratio: segment k + 1's dataflow runs beside segment k's loop,
+// so it can grow by (loop time / dataflow time) per event and still be ready
+// when the loop reaches it.  That ratio depends on n: at C3 (n = 128) the
+// loop outruns the dataflow 1.32x (33 against 25 ms per step; 1.24-1.32
+// measured alike, profiles/r5_seg_ratio_late.txt); at C5 (n = 64) the two
+// take the same time and at C2 (n = 32) the loop is 1.12x the dataflow
+// (profiles/r6_seg_sweep_*), where growing segments only leave a long last
+// loop after the dataflow's end.  BH_SEG_RATIO overrides it (A/B)
+constexpr double SEG_RATIO_MID = 1.32, SEG_RATIO_SMALL = 1.32;  // (n <= 96, n <= 48: the round-6 sweep sets them)
+static double seg_ratio(const Dev &d) {
+  if (const char *e = getenv("BH_SEG_RATIO")) return std::max(1.0, atof(e));
+  return d.n > 96 ? 1.32 : d.n > 48 ? SEG_RATIO_MID : SEG_RATIO_SMALL;
+}
+
+static void segment_bounds(int64_t base, int64_t N, int K, double ratio, int64_t *Ns) {
   Ns[0] = base;
   if (K <= 1) { Ns[1] = N; return; }
   double w[64], tot = 0;
   K = std::min(K, 64);
   // segment k holds a ratio^k share: a short first segment (the loop waits
   // for its coordinates) and segments growing about as fast as the loop
-  // outruns the dataflow (BH_SEG_RATIO: A/B)
-  // (1.38 until the loop reached ~5.25 us per round; 1.24-1.32 then measured
-  // alike and ahead of 1.38 by ~2 %, profiles/r5_seg_ratio_late.txt)
-  const double ratio = getenv("BH_SEG_RATIO") ? std::max(1.0, atof(getenv("BH_SEG_RATIO"))) : 1.32;
+  // outruns the dataflow (seg_ratio)
   for (int k = 0; k < K; ++k) tot += (w[k] = std::pow(ratio, k));
   double acc = 0;
   for (int k = 1; k < K; ++k) {
@@ -901,7 +912,7 @@ SplitPlan split_plan(const bh_handle *h, int K, int64_t base) {
   p.K = K;
   p.base = base;
   p.Ns.assign((size_t)K + 1, base);
-  segment_bounds(base, N, K, p.Ns.data());
+  segment_bounds(base, N, K, seg_ratio(h->d), p.Ns.data());
   p.tab.assign((size_t)K * 2 * n + (size_t)K * 2 * (n + 1), 0);
   p.S.assign((size_t)K, 0);
   p.NQ.assign((size_t)K, 0);
@@ -1106,7 +1117,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   }
   const int64_t N = d.N;
   std::vector<int64_t> Ns((size_t)K + 1, base);
-  segment_bounds(base, N, K, Ns.data());
+  segment_bounds(base, N, K, seg_ratio(d), Ns.data());
   // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
   auto lens_at = [&](int64_t bound, int32_t *out) { chain_lens_at(h, bound, out); };
   auto view = [&](int k) {  // segment k: events [Ns[k], Ns[k + 1])
@@ -1984,7 +1995,6 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
   d.flow_lt = 1;
   d.round_persist = getenv("BH_ROUND_PERSIST") ? atoi(getenv("BH_ROUND_PERSIST")) != 0 : 1;
   d.round_f32 = getenv("BH_ROUND_F32") ? atoi(getenv("BH_ROUND_F32")) != 0 : 1;
-  d.round_early = getenv("BH_ROUND_EARLY") ? atoi(getenv("BH_ROUND_EARLY")) != 0 : 0;
   d.pbar_spin = getenv("BH_PBAR_SPIN") ? std::max(0, atoi(getenv("BH_PBAR_SPIN"))) : (1 << 24);
   // the XCD-hierarchical barrier above 64 workgroups (with per-workgroup
   // release words in both forms: C3 7.6 -> 7.05 us per iteration; C5's 64

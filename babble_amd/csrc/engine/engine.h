@@ -137,7 +137,6 @@ struct Dev {
   int32_t wide_cols;  // the 16-bit wide loop reads la_col (k_round_wide<*, true, true>; no FDT)
   int32_t round_persist;  // k_round2p: the whole n <= 128 loop in one launch (default; BH_ROUND_PERSIST=0: one launch per iteration)
   int32_t round_f32;      // k_round2p's search compares in packed f32 (BH_ROUND_F32=0: the int32 sign-bit count)
-  int32_t round_early;    // k_round2p issues the next round's loads before its own hand-off stores (BH_ROUND_EARLY)
   int32_t *pbar;          // the persistent wide loop's grid barrier (k_round2p hands off through tagged Bp / candfd dwords instead)
   int32_t pbar_spin;      // polls before a persistent loop gives up waiting (barrier or tagged hand-off; BH_PBAR_SPIN lowers it to test the fallback)
   int32_t pbar_mode;      // the wide persistent loop's barrier: 0 one counter, 1 XCD-hierarchical (n > 64; BH_PBAR=xcd|flat)

@@ -1799,27 +1799,7 @@ __device__ __forceinline__ float group_total_f(float v) {
   return v;
 }
 
-// k_round2p<*, *, true> (round 6): a store every lane of every wave issues
-// -- lanes with !on aim past the resource's end, which the buffer unit
-// drops -- so every wave issues the same stores each iteration and the
-// compiler waits for the loads issued before them by count, never behind
-// them (a wave's vector memory counter completes in order: a wait that
-// covered the stores would wait for their acknowledgements, ~1.8 us for
-// write-through stores)
-template <int AUX>
-__device__ __forceinline__ void st_all32(const void *base, uint32_t nbytes, bool on, uint32_t off, int32_t v) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)nbytes, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b32(v, rs, on ? off : 0x7FFFFFF0u, 0, AUX);
-}
-template <int AUX>
-__device__ __forceinline__ void st_all64(const void *base, uint32_t nbytes, bool on, uint32_t off, unsigned long long v) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)nbytes, 0x00020000);
-  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-  const u2 w = {(unsigned)v, (unsigned)(v >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b64(w, rs, on ? off : 0x7FFFFFF0u, 0, AUX);
-}
-
-template <int PPL, bool F32, bool EARLY = false>
+template <int PPL, bool F32>
 __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   constexpr int LPC = 8;
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
@@ -1827,7 +1807,6 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   __shared__ int32_t hist[HW + 1];
   __shared__ int32_t sh_fail;
   __shared__ uint32_t sh_cur;  // (BH_DIAG: the last wave's inputs-current time this round, low 32 bits)
-  __shared__ __attribute__((aligned(16))) int32_t own_fd[4 * LPC * PPL];  // (early) this chain's new candidate row, tagged
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x;
   // the segment pipeline enqueues every segment's loop without a host round
@@ -1870,26 +1849,11 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   const int wi = t >> 3, wr4 = 4 * (t & 7);
   const bool wst = wi < n;
   int4 wv;
-  bool wvon = true;  // (EARLY: wv holds the window piece; else the staging writes -1)
   auto own_loads = [&]() {  // chain c's window from k0 and its hand-off rows from j0
     const int32_t rb = (cs + k0) & ~3;
-    if constexpr (EARLY) {
-      // every lane loads (a valid address where it has nothing to load) and
-      // the value is masked where it is used, next iteration: a select here
-      // would let the compiler put the load behind a branch and wait for it
-      // before the stores
-      wvon = wst && k0 < len;
-      wv = *reinterpret_cast<const int4 *>(wvon ? d.la_col + (int64_t)wi * stride + (rb + wr4) : d.la_col);
-      const int l8 = t & 7;
-      const bool live = hin.j0 != FD_NONE;  // (hand_entry reads fb only when live)
-      const int32_t a = live ? (hin.cs + hin.j0) & ~3 : 0;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) hin.fb[u] = *reinterpret_cast<const int4 *>(colc + (live ? a + 8 * l8 + 4 * u : 0));
-    } else {
-      wv = wst && k0 < len ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
-                           : make_int4(-1, -1, -1, -1);
-      hand_load(colc, hin);
-    }
+    wv = wst && k0 < len ? *reinterpret_cast<const int4 *>(d.la_col + (int64_t)wi * stride + (rb + wr4))
+                         : make_int4(-1, -1, -1, -1);
+    hand_load(colc, hin);
   };
   own_loads();
   if (t == 0) sh_fail = 0;
@@ -1903,48 +1867,6 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     return an == want && o == want;
   };
   constexpr uint32_t VMASK24 = 0xFFFFFFu;  // value bits of a handed-over dword (0xFFFFFF: FD_NONE)
-  // round r's candidates (parity pp): boundary bqr and FD row pieces f.  A
-  // poll's reload is volatile (bit 31: never merged with an earlier load);
-  // the early load (vol = false) is issued once, before this workgroup's own
-  // hand-off stores, so that waiting for it never waits for their
-  // acknowledgements (a wave's vector memory counter completes in order)
-  constexpr bool early = EARLY;
-  uint32_t bqr = 0;
-  int4 f[PPL];
-  auto load_early = [&](int pp) {  // (EARLY: every lane loads, the value masked)
-    const int qq = min(q, n - 1);
-    const int32_t row0 = (int32_t)(((int64_t)pp * n + qq) * npad * 4);
-    // (raw values: q >= n lanes' boundary is never read, pieces past npad
-    // are masked to FD_NONE after the check)
-    bqr = (uint32_t)__hip_atomic_load(d.Bp + (int64_t)pp * n + qq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int u = 0; u < PPL; ++u) {
-      const int pc = part + LPC * ((u + rot) & (PPL - 1));
-      f[u] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * (pc < q4 ? pc : 0), 0,
-                                                                             (int)0x80000010u));
-    }
-  };
-  auto load_in = [&](int pp, bool vol) {
-    const int32_t row0 = (int32_t)(((int64_t)pp * n + min(q, n - 1)) * npad * 4);
-    bqr = q < n ? (uint32_t)__hip_atomic_load(d.Bp + (int64_t)pp * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-    for (int u = 0; u < PPL; ++u) {
-      const int pc = part + LPC * ((u + rot) & (PPL - 1));
-      if (pc >= q4)
-        f[u] = make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
-      else if (vol)
-        f[u] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * pc, 0, (int)0x80000010u));
-      else
-        f[u] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * pc, 0, 0x10));
-    }
-  };
-  if constexpr (EARLY) {
-    // iteration 0's inputs (written before the launch), and nothing left
-    // pending at the loop's entry: the loop header then merges no state in
-    // which a load is the most recent memory operation
-    load_in(p, true);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  }
   for (int it = 0;; ++it) {
     // BH_DIAG timeline (tools/timeline.py): iteration start (inputs current),
     // window staged, search done, hand-off stored -- rounds TL_R0 .. + TL_NR
@@ -1962,19 +1884,30 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // values, top byte 0 or 0x7F: the same decode), and k_cand_rows zeroed
     // parity 1 (tag 0), which iteration 1 must not take for its own
     const uint32_t want = (uint32_t)it & 0xFFu;
+    uint32_t bqr = 0;
+    int4 f[PPL];
+    const int32_t row0 = (int32_t)(((int64_t)p * n + min(q, n - 1)) * npad * 4);
+    auto load_in = [&]() {
+      bqr = q < n ? (uint32_t)__hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) {
+        const int pc = part + LPC * ((u + rot) & (PPL - 1));
+        // (sc1, and volatile -- bit 31 -- so the poll below reloads)
+        f[u] = pc < q4 ? __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cfr, row0 + 16 * pc, 0,
+                                                                                         (int)0x80000010u))
+                       : make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
+      }
+    };
     const unsigned long long rtp = dgt ? __builtin_amdgcn_s_memrealtime() : 0;  // waiting starts
     int32_t polls = 0;
-    // (EARLY: iteration it's loads were issued at the end of iteration it - 1,
-    // before that iteration's own hand-off stores; iteration 0's before the loop)
-    if constexpr (!EARLY) load_in(p, true);
+    load_in();
     // the window first (its rows were loaded at the end of the last
     // iteration): staged while the candidates' rows are in flight, so each
     // wave starts its search as soon as ITS candidates' rows are current
     const int off = (cs + k0) & 3;
     const int rows = min(HWL - off, max(0, len - k0));
     if (wst) {
-      const int4 wm = wvon ? wv : make_int4(-1, -1, -1, -1);
-      const int4 sv = F32 ? f32_bits4(wm) : wm;
+      const int4 sv = F32 ? f32_bits4(wv) : wv;
       win32[(wr4 + 0) * rs + wi] = sv.x;
       win32[(wr4 + 1) * rs + wi] = sv.y;
       win32[(wr4 + 2) * rs + wi] = sv.z;
@@ -1985,43 +1918,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     if (t == 0) sh_cur = 0;
     __syncthreads();
     const unsigned long long rt1 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (early && it > 0 && q == c) {
-      // this chain's own candidate: its row from the LDS (the early load was
-      // issued before this workgroup stored it)
-      bqr = ((uint32_t)it & 0xFFu) << 24 | (uint32_t)k0;
-#pragma unroll
-      for (int u = 0; u < PPL; ++u) {
-        const int pc = part + LPC * ((u + rot) & (PPL - 1));
-        if (pc < q4) f[u] = *reinterpret_cast<const int4 *>(own_fd + 4 * pc);
-      }
-    }
-    if (EARLY && it > 0) {
-      // the first check on the early loads; reloads (after the stores) only
-      // for what was not current yet
-      auto check = [&]() {
-        bool ok = q >= n || (bqr >> 24) == want;
-        if (ok && q < n && (int32_t)(bqr & VMASK24) < lq) {
-#pragma unroll
-          for (int u = 0; u < PPL; ++u)
-            ok &= part + LPC * ((u + rot) & (PPL - 1)) >= q4 || tagged(f[u], want);
-        }
-        return ok;
-      };
-      bool ok = check();
-      if (!__all(ok)) {
-        for (int32_t spin = 0;; ++spin) {
-          ++polls;
-          if (spin >= d.pbar_spin) {  // a workgroup never published: the host falls back
-            sh_fail = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          if (!ok) load_in(p, true);
-          ok = check();
-          if (__all(ok)) break;
-        }
-      }
-    } else if (it > 0) {
+    if (it > 0) {
       for (int32_t spin = 0;; ++spin, ++polls) {
         bool ok = q >= n || (bqr >> 24) == want;
         if (ok && q < n && (int32_t)(bqr & VMASK24) < lq) {  // a live candidate: its row as well
@@ -2035,7 +1932,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        if (!ok) load_in(p, true);
+        if (!ok) load_in();
       }
     }
     const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -2045,7 +1942,6 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
 #pragma unroll
     for (int u = 0; u < PPL; ++u) {
       f[u] = make_int4(f[u].x & VMASK24, f[u].y & VMASK24, f[u].z & VMASK24, f[u].w & VMASK24);
-      if (EARLY && part + LPC * ((u + rot) & (PPL - 1)) >= q4) f[u] = make_int4(FD_NONE, FD_NONE, FD_NONE, FD_NONE);
       if (F32) f[u] = f32_bits4(f[u]);
     }
     const bool act = q < n && bq < lq;
@@ -2204,32 +2100,15 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     // ---- hand-off: FD[(c, result)][i] and B[r + 1][c], tagged it + 1 ----
     const uint32_t tagw = (uint32_t)((it + 1) & 0xFF) << 24;
     int32_t fdv = FD_NONE;
-    if (result < len) fdv = hand_entry(colc, hin, t >> 3, c, result);
-    if constexpr (EARLY) {
-      // Every load the next iteration waits for is issued HERE, ahead of the
-      // hand-off stores below: the other chains' candidate rows (for the
-      // round's last producer they are all published already -- it starts
-      // the next round one load latency from now instead of after its own
-      // stores' acknowledgements, ~1.8 us, plus a load) and this chain's
-      // window and hand-off rows.  Its own row goes through the LDS.  The
-      // stores are issued by every lane (st_all32: a fixed count per wave)
-      if ((t & 7) == 0 && (t >> 3) < npad) own_fd[t >> 3] = (int32_t)(tagw | ((uint32_t)fdv & VMASK24));
-      load_early(p ^ 1);
-      k0 = result;
-      hin.j0 = result < len ? fdv : FD_NONE;
-      own_loads();
-      st_all32<0x10>(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad, (uint32_t)npad * 4,
-                     result < len && (t & 7) == 0 && (t >> 3) < npad, (uint32_t)(t >> 3) * 4,
-                     (int32_t)(tagw | ((uint32_t)fdv & VMASK24)));
-      st_all32<0x10>(d.Bp + (int64_t)(p ^ 1) * n + c, 4, t == 0, 0, (int32_t)(tagw | (uint32_t)result));
-    } else {
-      if (result < len && (t & 7) == 0 && (t >> 3) < npad)
+    if (result < len) {
+      fdv = hand_entry(colc, hin, t >> 3, c, result);
+      if ((t & 7) == 0 && (t >> 3) < npad)
         __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + (t >> 3),
                            (int32_t)(tagw | ((uint32_t)fdv & VMASK24)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == 0)
-        __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (t == 0)
+      __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     if (dgt && c < 128) {
       unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
       tl[0] = rt0;
@@ -2253,28 +2132,18 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
     }
     // what no workgroup reads inside the loop -- fame's inputs (the new
     // candidate's LA row and its ballots) and the round table
-    if constexpr (EARLY) {
-      const int tc = t < npad ? t : 0;
-      st_all32<0>(d.cla + cla_row(d, c, r + 1) * npad, (uint32_t)npad * 4, result < len && t < npad, (uint32_t)t * 4,
-                  F32 ? (int32_t)__int_as_float(win32[lrow * rs + tc]) : win32[lrow * rs + tc]);
-      st_all64<0>(d.ssm + ballot_row(d, c, r + 1) * 16, 16 * 8, result < len && lane == 0, (uint32_t)wave * 8, ssb);
-      st_all32<0>(d.B + (int64_t)(r + 1) * n + c, 4, t == 0, 0, result);
-    } else {
-      if (result < len) {
-        if (t < npad)
-          d.cla[cla_row(d, c, r + 1) * npad + t] = F32 ? (int32_t)__int_as_float(win32[lrow * rs + t]) : win32[lrow * rs + t];
-        if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
-      }
-      if (t == 0) d.B[(int64_t)(r + 1) * n + c] = result;
+    if (result < len) {
+      if (t < npad)
+        d.cla[cla_row(d, c, r + 1) * npad + t] = F32 ? (int32_t)__int_as_float(win32[lrow * rs + t]) : win32[lrow * rs + t];
+      if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
     }
+    if (t == 0) d.B[(int64_t)(r + 1) * n + c] = result;
     ++r;
     p ^= 1;
-    if (!early) {
-      k0 = result;
-      hin.j0 = result < len ? fdv : FD_NONE;
-      own_loads();  // the next window and hand-off rows: they land while the candidates are awaited
-    }
-    __syncthreads();  // (the window, cntk and hist are rewritten next; own_fd is read next)
+    k0 = result;
+    hin.j0 = result < len ? fdv : FD_NONE;
+    own_loads();  // the next window and hand-off rows: they land while the candidates are awaited
+    __syncthreads();  // (the window, cntk and hist are rewritten next)
   }
 }
 
@@ -2335,9 +2204,7 @@ void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0, hipEvent_t
   const uint32_t lds = (uint32_t)(HWL * (8 * ppl + 1) * 16);
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
   void (*k)(Dev);
-  if (d.round_f32 && d.round_early)
-    k = d.npad <= 32 ? k_round2p<1, true, true> : d.npad <= 64 ? k_round2p<2, true, true> : k_round2p<4, true, true>;
-  else if (d.round_f32) k = d.npad <= 32 ? k_round2p<1, true> : d.npad <= 64 ? k_round2p<2, true> : k_round2p<4, true>;
+  if (d.round_f32) k = d.npad <= 32 ? k_round2p<1, true> : d.npad <= 64 ? k_round2p<2, true> : k_round2p<4, true>;
   else k = d.npad <= 32 ? k_round2p<1, false> : d.npad <= 64 ? k_round2p<2, false> : k_round2p<4, false>;
   if (e0 || e1) hipExtLaunchKernelGGL(k, dim3((unsigned)d.n), dim3(nt), lds, s, e0, e1, 0, d);
   else k<<<d.n, nt, lds, s>>>(d);
@@ -2896,7 +2763,6 @@ void configure_round_kernels() {
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
   CFG((k_round2p<1, true>)); CFG((k_round2p<2, true>)); CFG((k_round2p<4, true>));
   CFG((k_round2p<1, false>)); CFG((k_round2p<2, false>)); CFG((k_round2p<4, false>));
-  CFG((k_round2p<1, true, true>)); CFG((k_round2p<2, true, true>)); CFG((k_round2p<4, true, true>));
   CFG(k_round_solo);
 #undef CFG
 }

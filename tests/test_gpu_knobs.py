@@ -14,12 +14,9 @@ test_gpu_shard.py, test_gpu_comm.py).
 * BH_LOOP_TIMING=0 -- no HIP events around the loop (stage 7 reads 0);
 * BH_ROUND_F32=0 -- k_round2p's search counting in int32 (sign bits of
   LA - FD) instead of packed f32 with the clamp modifier (the default);
-* BH_ROUND_EARLY=0 -- k_round2p without the early loads (round 6's
-  default issues the next round's candidate, window and hand-off loads
-  before the workgroup's own hand-off stores);
 * BH_SEG_RATIO -- the segment pipeline's growth ratio (segment k holds a
   ratio^k share of the events): equal segments (1.0) and steep ones (1.8)
-  cut the DAG at other boundaries than the default 1.32.
+  cut the DAG at other boundaries than the defaults (1.32 above n = 96).
 """
 import os
 
@@ -87,14 +84,6 @@ def test_loop_timing_off(monkeypatch):
 @pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xD9, 0, 3), (100, 40_000, 0xDA, 4, 1), (7, 6_000, 0xDB, 2, 2)])
 def test_round_int32_search(monkeypatch, n, N, seed, lag, K):
     monkeypatch.setenv("BH_ROUND_F32", "0")
-    monkeypatch.setenv("BH_SEGMENTS", str(K))
-    loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
-    assert loops >= 1 and fallbacks == 0
-
-
-@pytest.mark.parametrize("n,N,seed,lag,K", [(128, 60_000, 0xDC, 0, 3), (64, 40_000, 0xDD, 21, 4), (20, 8_000, 0xDE, 2, 2)])
-def test_round_no_early_loads(monkeypatch, n, N, seed, lag, K):
-    monkeypatch.setenv("BH_ROUND_EARLY", "0")
     monkeypatch.setenv("BH_SEGMENTS", str(K))
     loops, fallbacks = _random_parity(n, N, seed, lag).loop_stats()
     assert loops >= 1 and fallbacks == 0

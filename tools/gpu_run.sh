@@ -17,11 +17,12 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $arg \
         > $out/${tag}_tests.log 2>&1 || { tail -40 $out/${tag}_tests.log; exit 1; }
       tail -3 $out/${tag}_tests.log ;;
-    bench)
+    bench|benchq)
       IFS=: read -r cfg steps envs <<< "$arg"
       name=${tag}_bench_c${cfg}${envs:+_$(echo $envs | tr ',=' '__')}
       echo "== bench cfg$cfg $envs"
-      env $(echo $envs | tr ',' ' ') timeout -k 10 600 python -u bench.py --cfg $cfg --steps $steps --warmup 1 \
+      cpu=""; [ $kind = benchq ] && cpu="--cpu-sample 0"
+      env $(echo $envs | tr ',' ' ') timeout -k 10 600 python -u bench.py --cfg $cfg --steps $steps --warmup 1 $cpu \
         > $out/$name.json 2> $out/$name.log || { tail -20 $out/$name.log; exit 1; }
       python3 -c "import json,sys; d=json.load(open('$out/$name.json')); print('$name', round(d['value']/1e6,2), 'M ev/s', round(d['ms_per_step'],2), 'ms', d['stages_ms'])" ;;
     multi)
