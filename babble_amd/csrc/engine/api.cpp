@@ -769,7 +769,11 @@ int segments_for(const Dev &d, int64_t events) {
   // one's columns, 8 segments 188.8M events/s, 16 187.6M, 24 184.1M)
   // (round 5, C3 10M events, segment k holding a 1.38^k share: 38.1-38.4 ms
   // per step at 10-14 segments against 40.1 at 8 segments of 1.5^k)
-  int K = !d.fd_cols ? 1 : events >= 4000000 ? 12 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1;
+  // (round 6: at n <= 96 the dataflow and the loop take about as long, so
+  // more, flatter segments shorten the loop left after the dataflow's end)
+  int K = !d.fd_cols ? 1
+          : d.n <= 96 ? (events >= 1500000 ? 12 : events >= 1000000 ? 8 : 1)
+                      : (events >= 4000000 ? 12 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1);
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>({K, events / 4096 + 1, 64}));
 }
@@ -801,7 +805,9 @@ int segments_for(const Dev &d, int64_t events) {
 // take the same time and at C2 (n = 32) the loop is 1.12x the dataflow
 // (profiles/r6_seg_sweep_*), where growing segments only leave a long last
 // loop after the dataflow's end.  BH_SEG_RATIO overrides it (A/B)
-constexpr double SEG_RATIO_MID = 1.32, SEG_RATIO_SMALL = 1.32;  // (n <= 96, n <= 48: the round-6 sweep sets them)
+// (round 6, profiles/r6_seg_sweep.txt: C5 16.89 -> 15.00 ms with 12 equal
+// segments, C2 11.63 -> 10.31 ms with 8 segments of 1.12x)
+constexpr double SEG_RATIO_MID = 1.0, SEG_RATIO_SMALL = 1.12;
 static double seg_ratio(const Dev &d) {
   if (const char *e = getenv("BH_SEG_RATIO")) return std::max(1.0, atof(e));
   return d.n > 96 ? 1.32 : d.n > 48 ? SEG_RATIO_MID : SEG_RATIO_SMALL;
