@@ -392,6 +392,7 @@ void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_roun
 bool round_solo_eligible(const Dev &d);
 bool round2_eligible(const Dev &d);
 bool round_persist_eligible(const Dev &d);
+bool round_lean_eligible(const Dev &d);  // k_round_lean (biased f32, chains < 2^23 - 2) over k_round2p
 void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 bool round_wide_persist_eligible(const Dev &d);
 void launch_round_wide_persist(const Dev &d, hipStream_t s);

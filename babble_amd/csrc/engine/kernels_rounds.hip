@@ -2147,6 +2147,426 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_round_lean<PPL, FULL, DIAG>: k_round2p's loop -- the same search, the
+// same tagged hand-off, the same results -- cut down for VALU issue (round
+// 6).  What bounds k_round2p's work (profiles/pmc_sq.json, n128_N10000000):
+// ~396 VALU instructions per wave per round; 16 waves on 4 SIMDs issue one
+// wave-instruction per cycle per CU, so ~6,300 cycles = 2.6 us at 2.4 GHz,
+// which is the round's measured work (profiles/r6_timeline_c3_base.txt).
+// The loop is VALU-issue-bound on its CU, not LDS- or latency-bound.  Here:
+//  * biased f32 values: an entry x in [-1, 2^23 - 2] is the f32 with bits
+//    x + 0x4B800000, i.e. 2^24 + 2x (x = -1 gives 2^24 - 1), so one integer
+//    add stages an LA entry, one add strips a received FD entry's (checked)
+//    tag and biases it, and clamp(FD - LA) (v_pk_add_f32 ... clamp) is still
+//    the 0/1 indicator [LA < FD] (FD - LA is 2(fd - la) >= 2, or <= 0, or
+//    2 fd + 1 >= 1 for la = -1);
+//  * the per-candidate search is five fixed probes with no loop control: the
+//    probed row is an LDS immediate offset from the lane's address, one add
+//    and one select move it; rows past the window's valid ones read +inf (a
+//    sentinel that strongly sees everything), so the search is over
+//    [0, min(rows, 31)] and 31 or the sentinel row means "not in the window";
+//  * window rows at a power-of-two stride with their first 128 B repeated
+//    after them: candidates 2 and 3 of every four read their pieces 128 B
+//    further on (the repeat covers the wrap), so the 16 lanes of each LDS
+//    cycle group of a ds_read_b128 touch 16 different bank quads whichever
+//    rows their candidates probe;
+//  * the hand-off counts the lane's 8 loaded rows without per-row bounds:
+//    rows before the previous entry are below the new boundary (LA is
+//    monotone on a chain), so the entry is the block's first row + the
+//    group's count; a wave that has a chain within 64 rows of its end takes
+//    hand_entry's bounded count;
+//  * two windows and histograms by parity.
+// Needs chains < 2^23 - 1 (else k_round2p's int32 search).
+template <int PPL, bool FULL, bool DIAG>
+__global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
+  constexpr int LPC = 8, RS4 = LPC * PPL, COLS = 4 * RS4, RB = 16 * RS4;
+  constexpr int RST = RB + 128 <= 256 ? 256 : RB + 128 <= 512 ? 512 : 1024;  // window row stride, bytes
+  constexpr int RSH = RST == 256 ? 8 : RST == 512 ? 9 : 10;
+  constexpr int WR = HWL + 2;  // + two sentinel rows (a probe reaches row off + 30 <= 33)
+  constexpr uint32_t WBYTES = (uint32_t)WR * RST;
+  constexpr uint32_t BIAS = 0x4B800000u, INF = 0x7F800000u;
+  constexpr uint32_t VMASK24 = 0xFFFFFFu;
+  extern __shared__ __attribute__((aligned(16))) int4 sm4[];
+  char *const wb = reinterpret_cast<char *>(sm4);
+  uint32_t *const wb32 = reinterpret_cast<uint32_t *>(sm4);
+  __shared__ int32_t cntk[2][16];
+  __shared__ int32_t hist[2][HW + 1];
+  __shared__ int32_t sh_fail;
+  __shared__ uint32_t sh_cur, sh_pend;  // (DIAG: the last wave's inputs current, probes done)
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
+  const int c = blockIdx.x;
+  if (d.state[ST_PFAIL] || d.state[ST_GATE]) {  // (k_round2p's entry gate)
+    if (c == 0 && t == 0) {
+      d.state[ST_DONE] = 1;
+      signal_done(d);
+    }
+    return;
+  }
+  const int n = d.n, npad = d.npad, sm = d.sm, q4 = npad / 4;
+  const int64_t stride = la_col_stride(d);
+  const int32_t len = d.chain_len[c], cs = d.chain_start[c];
+  const int q = t / LPC, part = t % LPC, rot = (q >> 1) & 1;
+  const int qc = min(q, n - 1);
+  const int32_t lq = q < n ? d.chain_len[q] : 0;
+  const int32_t *colc = d.la_col + (int64_t)c * stride;
+  const __amdgpu_buffer_rsrc_t cfr = __builtin_amdgcn_make_buffer_rsrc(d.candfd, (short)0, 0x7fffffff, 0x00020000);
+  int32_t r = d.state[ST_CUR0];  // the first iteration has parity 0
+  int32_t k0 = d.Bp[c];
+  const int hc = t >> 3;  // the hand-off's chain
+  HandIn hin{FD_NONE, 0, 0, {}};
+  if (hc < n) {
+    hin.cs = d.chain_start[hc];
+    hin.len = d.chain_len[hc];
+    if (k0 < len) hin.j0 = d.candfd[(int64_t)c * npad + hc];
+  }
+  // the window's staging: thread t holds rows 4 sg .. 4 sg + 3 of column swi
+  // (8 lanes per column: a wave's loads touch 8 cache lines, not 64 -- with
+  // one column per lane, 1,024 line requests per round per workgroup slowed
+  // the hand-off's loads: hop 1.5 -> 3.0 us.  The LDS writes of a column's
+  // 8 lanes then share a bank: 8-way, off the critical path)
+  const int swi = t >> 3, sg = t & 7;
+  const bool sst = sg < 8 && swi < n;
+  const int32_t *scol = d.la_col + (int64_t)(sst ? swi : 0) * stride;
+  int4 wv;
+  f32x2 hfb[4];  // hin.fb biased (the fast hand-off count)
+  bool hslow = false;  // the lane's 64-row block is not wholly inside chain hc (hand_entry's bounded count)
+  auto own_loads = [&]() {  // chain c's window from k0 and the hand-off rows from j0
+    const int32_t rb = (cs + k0) & ~3;
+    wv = sst && k0 < len ? *reinterpret_cast<const int4 *>(scol + (rb + 4 * sg)) : make_int4(-1, -1, -1, -1);
+    hand_load(colc, hin);
+    const int32_t ab = (hin.cs + hin.j0) & ~3;
+    hslow = hin.j0 != FD_NONE && (ab < hin.cs || ab + FDB > hin.cs + hin.len);
+  };
+  own_loads();
+  // what no staging writes: columns n .. COLS (and their repeats) LA -1, the
+  // two rows after the window +inf, in both parity windows
+  for (int j = t; j < (int)(2 * WBYTES / 4); j += nt) {
+    const int row = (j / (RST / 4)) % WR, col = j % (RST / 4);
+    const int lc = col < COLS ? col : col < COLS + 32 ? col - COLS : COLS;
+    if (row >= HWL) wb32[j] = INF;
+    else if (lc >= n) wb32[j] = BIAS - 1u;
+  }
+  if (t == 0) sh_fail = 0;
+  const uint32_t lane_off = 16u * part + 128u * rot;  // the lane's first piece (rotated by 128 B for odd pairs)
+  const int32_t rowq0 = (int32_t)((int64_t)qc * npad * 4), rowq1 = (int32_t)(((int64_t)n + qc) * npad * 4);
+  const float ltmax = (float)(COLS - sm);  // the most LA < FD columns a strongly seeing row has
+  // a candidate piece's global index for register u (the LDS read of u is at
+  // lane_off + 128 u: piece part + 8 (u + rot), the last one in the repeat)
+  auto gpiece = [&](int u) { return part + LPC * ((u + rot) & (PPL - 1)); };
+  int p = 0;
+  for (int it = 0;; ++it) {
+    const bool dgt = DIAG && d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
+    const uint32_t want = (uint32_t)it & 0xFFu;
+    uint32_t bqr = 0;
+    int4 f[PPL];
+    const int32_t row0 = p ? rowq1 : rowq0;
+    auto load_in = [&]() {
+      bqr = q < n ? (uint32_t)__hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const int32_t none = (int32_t)((want << 24) | VMASK24);  // (a padding column: FD_NONE, tagged)
+#pragma unroll
+      for (int u = 0; u < PPL; ++u)
+        f[u] = FULL || gpiece(u) < q4 ? __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                    cfr, row0 + 16 * gpiece(u), 0, (int)0x80000010u))
+                                      : make_int4(none, none, none, none);
+    };
+    const unsigned long long rtp = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    int32_t polls = 0;
+    // the candidates' loads leave only once this wave's own hand-off stores
+    // are acknowledged (~1.8 us after them): issued earlier they reach the
+    // rows while the other workgroups are still writing them, and every
+    // consumer's polls slow those writes down (k_round2p got this wait from
+    // its loop latch; MEASUREMENTS.md round 6: polls 0 -> 2, hop 1.2 -> 4 us
+    // without it)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    load_in();
+    // this iteration's window (parity p), staged while the candidates' rows
+    // are in flight; rows at or past the chain's end read +inf
+    const uint32_t wbase = (uint32_t)p * WBYTES;
+    const int32_t rb = (cs + k0) & ~3;
+    const int off = cs + k0 - rb;
+    const int rows = min(HWL - off, max(0, len - k0));
+    const int R = min(rows, HWL - 1);  // searched rows [0, R); R: not in the window
+    if (sst) {
+      uint32_t v[4] = {(uint32_t)wv.x + BIAS, (uint32_t)wv.y + BIAS, (uint32_t)wv.z + BIAS, (uint32_t)wv.w + BIAS};
+      const int32_t lim = cs + len - rb - 4 * sg;  // (uniform test: the window reaches the chain's end)
+      if (cs + len < rb + HWL) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = j >= lim ? INF : v[j];
+      }
+      uint32_t *w = wb32 + (wbase + (uint32_t)(4 * sg) * RST) / 4 + swi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j * (RST / 4)] = v[j];
+      if (swi < 32) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j * (RST / 4) + COLS] = v[j];
+      }
+    }
+    // the hand-off rows in the biased f32 domain (the fast count below)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      hfb[2 * u] = f32x2{__uint_as_float((uint32_t)hin.fb[u].x + BIAS), __uint_as_float((uint32_t)hin.fb[u].y + BIAS)};
+      hfb[2 * u + 1] = f32x2{__uint_as_float((uint32_t)hin.fb[u].z + BIAS), __uint_as_float((uint32_t)hin.fb[u].w + BIAS)};
+    }
+    if (t < 16) cntk[p][t] = 0;
+    if (t <= HW) hist[p][t] = 0;
+    if (DIAG && t == 0) sh_cur = sh_pend = 0;
+    __syncthreads();
+    const unsigned long long rt1 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    // round r's candidates, stored by the other workgroups at the end of
+    // round r - 1 as dwords tagged with the iteration (k_round2p): reload
+    // until every dword this lane needs carries tag `want`
+    if (it > 0) {
+      for (int32_t spin = 0;; ++spin) {
+        bool ok = q >= n || (bqr >> 24) == want;
+        if (ok && q < n && (int32_t)(bqr & VMASK24) < lq) {  // a live candidate: its row as well
+          uint32_t an = 0xFFFFFFFFu, o = 0;
+#pragma unroll
+          for (int u = 0; u < PPL; ++u) {
+            an &= (uint32_t)(f[u].x & f[u].y & f[u].z & f[u].w);
+            o |= (uint32_t)(f[u].x | f[u].y | f[u].z | f[u].w);
+          }
+          ok = (an >> 24) == want && (o >> 24) == want;
+        }
+        if (__all(ok)) break;
+        if (spin >= d.pbar_spin) {  // a workgroup never published: the host falls back
+          sh_fail = 1;  // (read after the search's barrier)
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        ++polls;
+        load_in();  // (the whole wave: no per-lane merge of old and new rows; the
+                    // buffer is not rewritten before this workgroup publishes)
+      }
+    }
+    const unsigned long long rt0 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (DIAG && d.diag != nullptr && lane == 0) atomicMax(&sh_cur, (uint32_t)__builtin_amdgcn_s_memrealtime());
+    const int32_t bq = (int32_t)(bqr & VMASK24);
+    const bool act = q < n && bq < lq;
+    // strip the tag and bias in one add: every dword a live candidate's
+    // lanes use carries tag `want` (checked above), so x - (want << 24) is
+    // its value (FD_NONE's 0xFFFFFF lands above every entry); iteration 0's
+    // rows are untagged (top byte 0, or 0x7F for FD_NONE): masked
+    const uint32_t kb = BIAS - (want << 24);
+    f32x2 fd[2 * PPL];
+    if (it == 0) {
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) {
+        fd[2 * u] = f32x2{__uint_as_float(((uint32_t)f[u].x & VMASK24) + BIAS), __uint_as_float(((uint32_t)f[u].y & VMASK24) + BIAS)};
+        fd[2 * u + 1] = f32x2{__uint_as_float(((uint32_t)f[u].z & VMASK24) + BIAS), __uint_as_float(((uint32_t)f[u].w & VMASK24) + BIAS)};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) {
+        fd[2 * u] = f32x2{__uint_as_float((uint32_t)f[u].x + kb), __uint_as_float((uint32_t)f[u].y + kb)};
+        fd[2 * u + 1] = f32x2{__uint_as_float((uint32_t)f[u].z + kb), __uint_as_float((uint32_t)f[u].w + kb)};
+      }
+    }
+    // one window row (LDS byte address of the lane's first piece) strongly
+    // sees candidate q: #{LA < FD} over its COLS columns <= COLS - SM
+    auto ss_row = [&](uint32_t a) {
+      f32x2 s[2 * PPL];
+#pragma unroll
+      for (int u = 0; u < PPL; ++u) {
+        const int4 x = *reinterpret_cast<const int4 *>(wb + a + 128u * u);
+        s[2 * u] = lt_ind2(fd[2 * u], f32x2{__int_as_float(x.x), __int_as_float(x.y)});
+        s[2 * u + 1] = lt_ind2(fd[2 * u + 1], f32x2{__int_as_float(x.z), __int_as_float(x.w)});
+      }
+#pragma unroll
+      for (int w = 1; w < 2 * PPL; w *= 2)
+#pragma unroll
+        for (int u = 0; u + w < 2 * PPL; u += 2 * w) s[u] += s[u + w];
+      return group_total_f<LPC>(s[0].x + s[0].y) <= ltmax;
+    };
+    {
+      const unsigned long long m = __ballot(act && part == 0);
+      if (lane == 0 && m) atomicAdd(&cntk[p][0], __popcll(m));
+    }
+    // T_q: the first row in [0, 31] that strongly sees q (31: none in rows
+    // 0 .. 30; rows >= R read +inf), five probes
+    const uint32_t a0 = wbase + (uint32_t)off * RST + lane_off;
+    uint32_t a = a0;
+#pragma unroll
+    for (int s = 4; s >= 0; --s) {
+      const bool sv = ss_row(a + (uint32_t)((1 << s) - 1) * RST);
+      a = sv ? a : a + (uint32_t)(1 << s) * RST;
+    }
+    const int pos = (int)((a - a0) >> RSH);
+    const unsigned long long rs1 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (DIAG && d.diag != nullptr && lane == 0) atomicMax(&sh_pend, (uint32_t)__builtin_amdgcn_s_memrealtime());
+    if (act && part == 0 && pos < R) atomicAdd(&hist[p][pos], 1);
+    __syncthreads();
+    const unsigned long long rs2 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (sh_fail) {  // a workgroup never published: ST_ERR = 3, the host falls back
+      if (t == 0) {
+        d.state[ST_ERR] = 3;
+        d.state[ST_ROUNDS] = r;
+        d.state[ST_DONE] = 1;
+        if (c == 0) signal_done(d);
+      }
+      break;
+    }
+    // B[r+1][c]: the first row whose prefix count of T_q reaches SM (an
+    // inclusive DPP scan of the bins -- lanes < 32 -- in every wave, no
+    // second barrier)
+    int res;
+    {
+      int h = lane < R ? hist[p][lane] : 0;
+      h += __builtin_amdgcn_update_dpp(0, h, 0x111, 0xF, 0xF, true);  // row_shr:1
+      h += __builtin_amdgcn_update_dpp(0, h, 0x112, 0xF, 0xF, true);  // row_shr:2
+      h += __builtin_amdgcn_update_dpp(0, h, 0x114, 0xF, 0xF, true);  // row_shr:4
+      h += __builtin_amdgcn_update_dpp(0, h, 0x118, 0xF, 0xF, true);  // row_shr:8
+      h += __builtin_amdgcn_update_dpp(0, h, 0x142, 0xA, 0xF, false);  // row_bcast:15 into rows 1, 3
+            const unsigned long long hit = __ballot(lane < R && h >= sm);
+      res = hit ? (int)__builtin_ctzll(hit) : -1;
+    }
+    unsigned long long ssb = __ballot(act && part == 0 && res >= 0 && pos <= res);
+    const int nc = cntk[p][0];
+    const unsigned long long rt2 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
+    int32_t result = len;
+    int lrow = 0;
+    if (res >= 0) {
+      result = k0 + res;
+      lrow = off + res;
+    } else if (nc > 0) {
+      // SM not reached in the window (rare): the rows after it, window by
+      // window, a row probe per step (every candidate on one row, cntk)
+      auto probe = [&](uint32_t ra, int slot) {
+        const bool sv = ss_row(ra + lane_off);
+        const unsigned long long m = __ballot(act && part == 0 && sv);
+        if (lane == 0 && m) atomicAdd(&cntk[p][slot], __popcll(m));
+        return m;
+      };
+      for (int32_t wk = k0 + R, wr = 0; wk < len && result == len; wk += wr) {
+        const int32_t rb2 = (cs + wk) & ~3;
+        const int off2 = cs + wk - rb2;
+        wr = min(HWL - off2, len - wk);
+        __syncthreads();
+        if (sst) {
+          const int4 x = *reinterpret_cast<const int4 *>(scol + (rb2 + 4 * sg));
+          uint32_t *w = wb32 + (wbase + (uint32_t)(4 * sg) * RST) / 4 + swi;
+          w[0] = (uint32_t)x.x + BIAS;
+          w[RST / 4] = (uint32_t)x.y + BIAS;
+          w[2 * (RST / 4)] = (uint32_t)x.z + BIAS;
+          w[3 * (RST / 4)] = (uint32_t)x.w + BIAS;
+          if (swi < 32) {
+            w[COLS] = (uint32_t)x.x + BIAS;
+            w[RST / 4 + COLS] = (uint32_t)x.y + BIAS;
+            w[2 * (RST / 4) + COLS] = (uint32_t)x.z + BIAS;
+            w[3 * (RST / 4) + COLS] = (uint32_t)x.w + BIAS;
+          }
+        }
+        if (t < 16) cntk[p][t] = 0;
+        __syncthreads();
+        const uint32_t x0 = wbase + (uint32_t)off2 * RST;
+        const unsigned long long ml = probe(x0 + (uint32_t)(wr - 1) * RST, 1);
+        __syncthreads();
+        if (cntk[p][1] < sm) continue;
+        int lo = 0, hi = wr - 1, sl = 1;
+        ssb = ml;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          ++sl;
+          const unsigned long long m = probe(x0 + (uint32_t)mid * RST, sl);
+          __syncthreads();
+          if (cntk[p][sl] >= sm) {
+            hi = mid;
+            ssb = m;
+          } else {
+            lo = mid + 1;
+          }
+        }
+        result = wk + lo;
+        lrow = off2 + lo;
+      }
+      __syncthreads();
+    }
+    // the loop's end, the same in every workgroup: no candidates (R = r), or
+    // the round table's capacity
+    if (nc == 0 || r + 1 >= d.R_cap) {
+      if (c == 0 && t == 0) {
+        if (nc > 0) d.state[ST_ERR] = 1;
+        d.state[ST_ROUNDS] = r;
+        d.state[ST_ITERS] = r;
+        d.state[ST_DONE] = 1;
+        signal_done(d);
+      }
+      break;
+    }
+    // ---- hand-off: FD[(c, result)][i] and B[r + 1][c], tagged it + 1 ----
+    const uint32_t tagw = (uint32_t)((it + 1) & 0xFF) << 24;
+    int32_t fdv = FD_NONE;
+    if (result < len) {
+      if (__any(hslow)) {
+        fdv = hand_entry(colc, hin, hc, c, result);
+      } else if (hin.j0 != FD_NONE) {  // rows [ab, cs + j0) are below the boundary: counted
+        // #{rows < result}: clamp(result - LA) in the biased f32 domain, the
+        // rows converted while the candidates were awaited
+        const float rf = __uint_as_float((uint32_t)result + BIAS);
+        const f32x2 r2{rf, rf};
+        f32x2 e0 = lt_ind2(r2, hfb[0]) + lt_ind2(r2, hfb[1]), e1 = lt_ind2(r2, hfb[2]) + lt_ind2(r2, hfb[3]);
+        e0 += e1;
+        const int cnt = (int)group_total_f<8>(e0.x + e0.y);
+        const int32_t ab = (hin.cs + hin.j0) & ~3, jn = ab + cnt;
+        fdv = hc == c ? result : jn < ab + FDB ? jn - hin.cs : FD_NONE;
+        // (jn reaching the block's end: the entry lies further on -- searched
+        // by hand_entry's wave search, as there)
+        const bool miss = hc != c && jn >= ab + FDB;
+        if (__any(miss)) {
+          const int32_t j = first_ge_group<8>(colc, ab + FDB, hin.cs + hin.len, result, miss, true);
+          if (miss) fdv = j < hin.cs + hin.len ? j - hin.cs : FD_NONE;
+        }
+      }
+      if ((t & 7) == 0 && hc < npad)
+        __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + hc,
+                           (int32_t)(tagw | ((uint32_t)fdv & VMASK24)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 0)
+      __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    if (dgt && c < 128) {
+      unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
+      tl[0] = rt0;
+      tl[1] = rt2;
+      tl[2] = rt1;
+      tl[3] = __builtin_amdgcn_s_memrealtime();
+      unsigned long long *tb = d.diag + DG_TLB + ((int64_t)(r - TL_R0) * 512 + c) * 4;
+      tb[0] = rtp;
+      tb[1] = rt0;
+      tb[2] = (unsigned long long)polls;
+      tb[3] = tl[3];
+      unsigned long long *ts = d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4;
+      ts[0] = rs1;
+      ts[1] = rs2;
+      // (bit 31: the low word is the last wave's probes-done time, not a probe count)
+      ts[2] = (unsigned long long)(0x80000000u | (sh_pend - (uint32_t)rt0)) | (unsigned long long)(sh_cur - (uint32_t)rt0) << 32;
+      ts[3] = rt2;
+    }
+    // fame's inputs (the new candidate's LA row and its ballots) and the
+    // round table: nothing inside the loop reads them
+    if (result < len) {
+      if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = (int32_t)(wb32[(wbase + (uint32_t)lrow * RST) / 4 + t] - BIAS);
+      if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
+    }
+    if (t == 0) d.B[(int64_t)(r + 1) * n + c] = result;
+    ++r;
+    p ^= 1;
+    k0 = result;
+    hin.j0 = result < len ? fdv : FD_NONE;
+    own_loads();  // the next window and hand-off rows: they land while the candidates are awaited
+    // the next iteration stages the other parity's window and histogram, but
+    // this barrier stays: without it a wave's first candidate loads leave
+    // while the other workgroups' rows are still being written (polls 0 -> 1,
+    // hop 1.2 -> 4.2 us, MEASUREMENTS.md round 6)
+    __syncthreads();
+  }
+}
+
+bool round_lean_eligible(const Dev &d) {
+  // biased f32 entries: chain rows <= 2^23 - 3 (FD_NONE's bias stays above them)
+  return d.round_f32 && d.max_chain_len < (1 << 23) - 2;
+}
+
 bool round_persist_eligible(const Dev &d) {
   // (the tagged hand-off carries chain rows in 24 bits: 0xFFFFFF is FD_NONE)
   return d.round_persist && round2_eligible(d) && !d.round_src_rows && d.n <= 256 && d.max_chain_len < 0xFFFFFF;
@@ -2201,11 +2621,23 @@ void launch_round_wide_persist(const Dev &d, hipStream_t s) {
 // marker packets of their own between the segments' kernels, ~5 us each)
 void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   const int ppl = d.npad <= 32 ? 1 : d.npad <= 64 ? 2 : 4;  // (k_round2p's rows: 8 * PPL + 1 pieces)
-  const uint32_t lds = (uint32_t)(HWL * (8 * ppl + 1) * 16);
+  uint32_t lds = (uint32_t)(HWL * (8 * ppl + 1) * 16);
   const unsigned nt = (unsigned)((8 * d.npad + 63) / 64 * 64);
   void (*k)(Dev);
-  if (d.round_f32) k = d.npad <= 32 ? k_round2p<1, true> : d.npad <= 64 ? k_round2p<2, true> : k_round2p<4, true>;
-  else k = d.npad <= 32 ? k_round2p<1, false> : d.npad <= 64 ? k_round2p<2, false> : k_round2p<4, false>;
+  if (round_lean_eligible(d)) {
+    // two parity windows of HWL + 2 rows at k_round_lean's stride
+    const int rst = ppl == 1 ? 256 : ppl == 2 ? 512 : 1024;
+    // (at least 148 KiB: no other kernel's workgroup shares the loop's
+    // compute unit -- at 88 VGPRs a k_flow32x2 workgroup otherwise fits
+    // beside the loop's 16 waves and takes their VALU issue slots)
+    lds = (uint32_t)std::max(2 * (HWL + 2) * rst, 148 * 1024);
+    const bool full = d.npad == 32 * ppl, diag = d.diag != nullptr && full;
+    if (diag) k = ppl == 1 ? k_round_lean<1, true, true> : ppl == 2 ? k_round_lean<2, true, true> : k_round_lean<4, true, true>;
+    else if (full) k = ppl == 1 ? k_round_lean<1, true, false> : ppl == 2 ? k_round_lean<2, true, false> : k_round_lean<4, true, false>;
+    else k = ppl == 1 ? k_round_lean<1, false, false> : ppl == 2 ? k_round_lean<2, false, false> : k_round_lean<4, false, false>;
+  } else {
+    k = d.npad <= 32 ? k_round2p<1, false> : d.npad <= 64 ? k_round2p<2, false> : k_round2p<4, false>;
+  }
   if (e0 || e1) hipExtLaunchKernelGGL(k, dim3((unsigned)d.n), dim3(nt), lds, s, e0, e1, 0, d);
   else k<<<d.n, nt, lds, s>>>(d);
 }
@@ -2761,7 +3193,9 @@ void configure_round_kernels() {
   CFG((k_round2<1, true>)); CFG((k_round2<2, true>)); CFG((k_round2<4, true>));
   CFG((k_round2<1, false>)); CFG((k_round2<2, false>)); CFG((k_round2<4, false>));
   CFG((k_round2r<1, true>)); CFG((k_round2r<2, true>)); CFG((k_round2r<4, true>));
-  CFG((k_round2p<1, true>)); CFG((k_round2p<2, true>)); CFG((k_round2p<4, true>));
+  CFG((k_round_lean<1, true, false>)); CFG((k_round_lean<2, true, false>)); CFG((k_round_lean<4, true, false>));
+  CFG((k_round_lean<1, false, false>)); CFG((k_round_lean<2, false, false>)); CFG((k_round_lean<4, false, false>));
+  CFG((k_round_lean<1, true, true>)); CFG((k_round_lean<2, true, true>)); CFG((k_round_lean<4, true, true>));
   CFG((k_round2p<1, false>)); CFG((k_round2p<2, false>)); CFG((k_round2p<4, false>));
   CFG(k_round_solo);
 #undef CFG

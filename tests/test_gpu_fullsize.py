@@ -8,8 +8,8 @@ longer run: the pipelined coordinates of segment s + 1, the round loop's
 resume at the last round segment s fixed and the incremental layout are all
 on the path these checks cover:
 
-  * C2 (32 peers, 1M events: 4 segments) and C5 (64 peers with 21 lagging,
-    2M events: 8 segments), whole;
+  * C2 (32 peers, 1M events: 8 segments) and C5 (64 peers with 21 lagging,
+    2M events: 12 segments), whole;
   * C3's DAG (128 peers, the bench's 10M-event DAG) on its first 2.5M
     events with 5 segments of 500k events -- every chain resumes 4 times at
     real chain lengths (the oracle needs about 25 s for them);
@@ -48,13 +48,13 @@ def _whole(cfg, N=None, segments=None, monkeypatch=None, ordered=0.9):
 @pytest.mark.timeout(600)
 def test_c2_whole_dag():
     hg = _whole(2)
-    assert hg.pipeline()[0] == 4  # the default for >= 1M events
+    assert hg.pipeline()[0] == 8  # the default for >= 1M events at n <= 96
 
 
 @pytest.mark.timeout(600)
 def test_c5_whole_dag():
     hg = _whole(5)
-    assert hg.pipeline()[0] == 8  # the default from 1.5M events
+    assert hg.pipeline()[0] == 12  # the default from 1.5M events at n <= 96
 
 
 @pytest.mark.timeout(900)

@@ -41,7 +41,7 @@ for step in "$@"; do
       python3 tools/timeline.py --tagged $out/$name.bin | tee $out/$name.txt ;;
     prof)
       echo "== rocprofv3 cfg$arg"
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/${tag}_prof -o run -- python3 -u bench.py --cfg $arg --steps 3 --warmup 1 --cpu-sample 0 \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_prof -o run -- python3 -u bench.py --cfg $arg --steps 3 --warmup 1 --cpu-sample 0 \
         > $out/${tag}_prof.json 2> $out/${tag}_prof.log || { tail -20 $out/${tag}_prof.log; exit 1; }
       f=$(find $out/${tag}_prof -name '*kernel_stats.csv' | head -1); cp "$f" $out/${tag}_kernel_stats.csv; head -8 $out/${tag}_kernel_stats.csv ;;
   esac

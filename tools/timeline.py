@@ -99,7 +99,11 @@ def tagged(path):
                 print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
             pc = g[:, :, 2][m] & 0xFFFFFFFF
             spread = (g[:, :, 2][m] >> 32).astype(np.int64)
-            print(f"{'probe count':14s} median {np.median(pc):6.1f}     p90 {np.percentile(pc, 90):6.1f}")
+            if (pc & 0x80000000).all():  # k_round_lean: the last wave's probes done (from wave 0's inputs current)
+                v = pc & 0x7FFFFFFF
+                print(f"{'last probes':14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us  (last wave's probes done - wave 0's inputs current)")
+            else:
+                print(f"{'probe count':14s} median {np.median(pc):6.1f}     p90 {np.percentile(pc, 90):6.1f}")
             if spread.any():
                 print(f"{'waves current':14s} median {np.median(spread) * ns / 1000:6.2f} us  p90 {np.percentile(spread, 90) * ns / 1000:6.2f} us  (last wave's inputs current - wave 0's)")
 
