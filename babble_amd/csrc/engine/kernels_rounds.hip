@@ -2193,7 +2193,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   __shared__ int32_t cntk[2][16];
   __shared__ int32_t hist[2][HW + 1];
   __shared__ int32_t sh_fail;
-  __shared__ uint32_t sh_cur, sh_pend;  // (DIAG: the last wave's inputs current, probes done)
+  __shared__ uint32_t sh_cur, sh_pend, sh_st, sh_flags, sh_hs;  // (DIAG: the last wave's inputs current, probes done, hand-off start, store)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nt = blockDim.x;
   const int c = blockIdx.x;
   if (d.state[ST_PFAIL] || d.state[ST_GATE]) {  // (k_round2p's entry gate)
@@ -2247,13 +2247,22 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     if (row >= HWL) wb32[j] = INF;
     else if (lc >= n) wb32[j] = BIAS - 1u;
   }
-  if (t == 0) sh_fail = 0;
+  if (t == 0) sh_fail = 0, sh_st = sh_flags = sh_hs = 0;
   const uint32_t lane_off = 16u * part + 128u * rot;  // the lane's first piece (rotated by 128 B for odd pairs)
   const int32_t rowq0 = (int32_t)((int64_t)qc * npad * 4), rowq1 = (int32_t)(((int64_t)n + qc) * npad * 4);
   const float ltmax = (float)(COLS - sm);  // the most LA < FD columns a strongly seeing row has
   // a candidate piece's global index for register u (the LDS read of u is at
   // lane_off + 128 u: piece part + 8 (u + rot), the last one in the repeat)
   auto gpiece = [&](int u) { return part + LPC * ((u + rot) & (PPL - 1)); };
+  // the per-iteration stores' addresses, kept as running pointers (no 64-bit
+  // multiplies or cla's ring modulo per round in the hand-off's scalar path)
+  int32_t *const cfs0 = d.candfd + ((int64_t)n + c) * npad, *const cfs1 = d.candfd + (int64_t)c * npad;
+  int32_t *const bps0 = d.Bp + n + c, *const bps1 = d.Bp + c;
+  int32_t cla_pos = (r + 1 - d.rbase) % d.cla_span;
+  const int32_t cla_span = d.cla_span;
+  int32_t *const cla_c = d.cla + (int64_t)c * cla_span * npad;
+  auto *ssm_p = d.ssm + ballot_row(d, c, r + 1) * 16 + wave;
+  int32_t *b_p = d.B + (int64_t)(r + 1) * n + c;
   int p = 0;
   for (int it = 0;; ++it) {
     const bool dgt = DIAG && d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
@@ -2279,6 +2288,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     // its loop latch; MEASUREMENTS.md round 6: polls 0 -> 2, hop 1.2 -> 4 us
     // without it)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long rta = dgt ? __builtin_amdgcn_s_memrealtime() : 0;  // (own stores acknowledged)
     load_in();
     // this iteration's window (parity p), staged while the candidates' rows
     // are in flight; rows at or past the chain's end read +inf
@@ -2302,7 +2312,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
         for (int j = 0; j < 4; ++j) w[j * (RST / 4) + COLS] = v[j];
       }
     }
-    // the hand-off rows in the biased f32 domain (the fast count below)
+    // the hand-off rows in the biased f32 domain (the fast count at the end)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       hfb[2 * u] = f32x2{__uint_as_float((uint32_t)hin.fb[u].x + BIAS), __uint_as_float((uint32_t)hin.fb[u].y + BIAS)};
@@ -2494,6 +2504,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
       break;
     }
     // ---- hand-off: FD[(c, result)][i] and B[r + 1][c], tagged it + 1 ----
+    if (DIAG && d.diag != nullptr && lane == 0) atomicMax(&sh_hs, (uint32_t)__builtin_amdgcn_s_memrealtime());
     const uint32_t tagw = (uint32_t)((it + 1) & 0xFF) << 24;
     int32_t fdv = FD_NONE;
     if (result < len) {
@@ -2513,52 +2524,72 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
         // by hand_entry's wave search, as there)
         const bool miss = hc != c && jn >= ab + FDB;
         if (__any(miss)) {
+          if (DIAG && d.diag != nullptr && lane == 0) atomicOr(&sh_flags, 2u);
           const int32_t j = first_ge_group<8>(colc, ab + FDB, hin.cs + hin.len, result, miss, true);
           if (miss) fdv = j < hin.cs + hin.len ? j - hin.cs : FD_NONE;
         }
       }
       if ((t & 7) == 0 && hc < npad)
-        __hip_atomic_store(d.candfd + ((int64_t)(p ^ 1) * n + c) * npad + hc,
-                           (int32_t)(tagw | ((uint32_t)fdv & VMASK24)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((p ? cfs1 : cfs0) + hc, (int32_t)(tagw | ((uint32_t)fdv & VMASK24)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t == 0)
-      __hip_atomic_store(d.Bp + (int64_t)(p ^ 1) * n + c, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    if (dgt && c < 128) {
-      unsigned long long *tl = d.diag + DG_TL + ((r - TL_R0) * 128 + c) * 4;
-      tl[0] = rt0;
-      tl[1] = rt2;
-      tl[2] = rt1;
-      tl[3] = __builtin_amdgcn_s_memrealtime();
-      unsigned long long *tb = d.diag + DG_TLB + ((int64_t)(r - TL_R0) * 512 + c) * 4;
-      tb[0] = rtp;
-      tb[1] = rt0;
-      tb[2] = (unsigned long long)polls;
-      tb[3] = tl[3];
-      unsigned long long *ts = d.diag + DG_TLS + ((int64_t)(r - TL_R0) * 512 + c) * 4;
-      ts[0] = rs1;
-      ts[1] = rs2;
-      // (bit 31: the low word is the last wave's probes-done time, not a probe count)
-      ts[2] = (unsigned long long)(0x80000000u | (sh_pend - (uint32_t)rt0)) | (unsigned long long)(sh_cur - (uint32_t)rt0) << 32;
-      ts[3] = rt2;
+      __hip_atomic_store(p ? bps1 : bps0, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (DIAG: the row's last store -- every wave's -- and whether a wave took
+    // the bounded count; recorded after the iteration's last barrier)
+    if (DIAG && d.diag != nullptr && lane == 0) {
+      atomicMax(&sh_st, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      if (__any(hslow)) atomicOr(&sh_flags, 1u);
     }
+    const int32_t rd = r;
+    const unsigned long long rt3 = dgt ? __builtin_amdgcn_s_memrealtime() : 0;
     // fame's inputs (the new candidate's LA row and its ballots) and the
     // round table: nothing inside the loop reads them
     if (result < len) {
-      if (t < npad) d.cla[cla_row(d, c, r + 1) * npad + t] = (int32_t)(wb32[(wbase + (uint32_t)lrow * RST) / 4 + t] - BIAS);
-      if (lane == 0) d.ssm[ballot_row(d, c, r + 1) * 16 + wave] = ssb;
+      if (t < npad) cla_c[(int64_t)cla_pos * npad + t] = (int32_t)(wb32[(wbase + (uint32_t)lrow * RST) / 4 + t] - BIAS);
+      if (lane == 0) *ssm_p = ssb;
     }
-    if (t == 0) d.B[(int64_t)(r + 1) * n + c] = result;
+    if (t == 0) *b_p = result;
+    cla_pos = cla_pos + 1 == cla_span ? 0 : cla_pos + 1;
+    ssm_p += 16;
+    b_p += n;
     ++r;
     p ^= 1;
     k0 = result;
     hin.j0 = result < len ? fdv : FD_NONE;
-    own_loads();  // the next window and hand-off rows: they land while the candidates are awaited
-    // the next iteration stages the other parity's window and histogram, but
-    // this barrier stays: without it a wave's first candidate loads leave
-    // while the other workgroups' rows are still being written (polls 0 -> 1,
-    // hop 1.2 -> 4.2 us, MEASUREMENTS.md round 6)
+    // every wave's hand-off stores leave before any wave's next loads: the
+    // compute unit's vector memory unit takes instructions in order, and a
+    // late wave's row store queued behind the other waves' window and
+    // hand-off loads (3 per wave) -- the row completed ~0.9 us after the last
+    // wave began its hand-off (loading the hand-off rows after the next
+    // candidates instead measured slower: C3 34.4 -> 35.8 ms).  (The next
+    // iteration stages the other parity's
+    // window and histogram; the barrier also keeps a wave's first candidate
+    // loads from leaving while the other workgroups' rows are still being
+    // written: polls 0 -> 1, hop 1.2 -> 4.2 us without it, MEASUREMENTS.md)
     __syncthreads();
+    own_loads();  // the next window and hand-off rows: they land while this wave's stores are acknowledged
+    if (dgt && c < 128) {
+      // tl / tb [3]: the row complete (every wave's store); the flags in tb[0] bits 60+
+      const unsigned long long st = (rt3 & ~0xFFFFFFFFull) | sh_st;
+      unsigned long long *tl = d.diag + DG_TL + ((rd - TL_R0) * 128 + c) * 4;
+      tl[0] = rt0;
+      tl[1] = rt2;
+      tl[2] = rt1;
+      tl[3] = st;
+      unsigned long long *tb = d.diag + DG_TLB + ((int64_t)(rd - TL_R0) * 512 + c) * 4;
+      tb[0] = rtp | (unsigned long long)sh_flags << 60;
+      tb[1] = rt0;
+      tb[2] = (unsigned long long)polls | (unsigned long long)(rta - rtp) << 32;  // (high: the own-store wait)
+      tb[3] = st;
+      unsigned long long *ts = d.diag + DG_TLS + ((int64_t)(rd - TL_R0) * 512 + c) * 4;
+      ts[0] = rs1;
+      ts[1] = rs2;
+      // (bit 31: the low word is the last wave's probes-done time, not a probe count)
+      ts[2] = (unsigned long long)(0x80000000u | (sh_pend - (uint32_t)rt0)) | (unsigned long long)(sh_cur - (uint32_t)rt0) << 32;
+      ts[3] = (rt3 & ~0xFFFFFFFFull) | sh_hs;  // (the last wave's hand-off start)
+      sh_st = sh_flags = sh_hs = 0;  // (wave 0 only: the other waves' next atomics come after the next barrier)
+    }
   }
 }
 

@@ -304,13 +304,15 @@ def main():
                       if pmc else "none: profiles/pmc_traffic.json holds no table of this build's kernels for "
                                   "this config")
     # the round loop, timed live by HIP events around each launch on the
-    # loop's stream (stage 7).  Persistent (the default): n <= 128 k_round2p,
-    # one launch per pipeline segment running all of that segment's rounds;
-    # n <= 512 k_round_wide<..., true>, one launch per call.  Otherwise one
-    # k_round2 / k_round_wide launch per round
+    # loop's stream (stage 7).  Persistent (the default): n <= 128
+    # k_round_lean (k_round2p with BH_ROUND_F32=0), one launch per pipeline
+    # segment running all of that segment's rounds; n <= 512
+    # k_round_wide<..., true>, one launch per call.  Otherwise one k_round2 /
+    # k_round_wide launch per round
     persistent = persist_per_step > 0
     if npad <= 128:
-        round_kernel = "k_round2p" if persistent else "k_round2"
+        lean = os.environ.get("BH_ROUND_F32", "1") != "0"
+        round_kernel = ("k_round_lean" if lean else "k_round2p") if persistent else "k_round2"
     else:
         round_kernel = "k_round_wide"
     segments = hg.pipeline()[0]
@@ -337,7 +339,7 @@ def main():
                 "round_iterations": iters, "us_per_iteration": iter_us,
                 "traffic_per_launch": _per_launch(pmc, round_kernel, loop_launches),
                 "note": "latency-bound: the rounds are a serial chain; one persistent launch per pipeline "
-                        "segment (k_round2p: workgroups hand each other the candidates' rows as data-tagged "
+                        "segment (k_round_lean: workgroups hand each other the candidates' rows as data-tagged "
                         "dwords) or per call (k_round_wide: a grid barrier per round)"}
     # the coordinate kernel: the sum of its launches per step (one per
     # segment; k_flow32x2 carries LT inside them), HIP events on the

@@ -30,7 +30,7 @@ def load(d):
     return ops
 
 
-def main(d, loopk="k_round2p"):
+def main(d, loopk="k_round_lean"):
     ops = load(d)
     fame = [o for o in ops if "k_fame_masks" in o[2]]
     loops = [o for o in ops if loopk in o[2]]

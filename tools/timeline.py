@@ -58,8 +58,10 @@ def tagged(path):
     b = np.fromfile(path, dtype=np.uint64)
     off = TL_NR * NC * 4
     b = b[off: off + TL_NR * 512 * 4].reshape(TL_NR, 512, 4).astype(np.int64)[:, :NC]
+    flags = (b[:, :, 0] >> 60) & 0xF  # (k_round_lean: a wave took the bounded hand-off count)
+    b[:, :, 0] &= (1 << 60) - 1
     live = (b[:, :, 1] > 0) & (b[:, :, 3] > 0)
-    rows = []
+    rows, lastc = [], []
     for r in range(1, TL_NR):
         m, mp = live[r], live[r - 1]
         if m.sum() < 2 or mp.sum() < 2:
@@ -68,7 +70,15 @@ def tagged(path):
         cur = b[r, m, 1]
         rows.append((cur.min() - last_store, np.median(cur - last_store), cur.max() - last_store,
                      np.median(b[r, m, 1] - b[r, m, 0]), np.median(b[r, m, 3] - b[r, m, 1]),
-                     b[r, m, 3].max() - b[r, m, 3].min(), np.median(b[r, m, 2]), cur.min() - b[r - 1, mp, 1].min()))
+                     b[r, m, 3].max() - b[r, m, 3].min(), np.median(b[r, m, 2] & 0xFFFFFFFF),
+                     cur.min() - b[r - 1, mp, 1].min()))
+        # k_round_lean: the last consumer's own path -- its store of round r - 1
+        # -> its iteration start -> own stores acknowledged -> inputs current
+        ack = b[r, :, 2] >> 32
+        w = int(np.flatnonzero(m)[np.argmax(cur)])
+        if ack[w] > 0 and mp[w]:
+            lastc.append((b[r, w, 0] - b[r - 1, w, 3], ack[w], b[r, w, 1] - b[r, w, 0] - ack[w],
+                          int(w == int(np.flatnonzero(mp)[np.argmax(b[r - 1, mp, 3])]))))
     if not rows:
         print("no tagged stamps")
         return
@@ -79,6 +89,19 @@ def tagged(path):
         scale = 1.0 if name == "polls" else ns / 1000
         unit = "" if name == "polls" else " us"
         print(f"{name:14s} median {np.median(v) * scale:6.2f}{unit}  p90 {np.percentile(v, 90) * scale:6.2f}{unit}")
+    if lastc:
+        for i, name in enumerate(["last: store->it", "last: own ack", "last: ack->cur"]):
+            v = [x[i] for x in lastc]
+            print(f"{name:14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us")
+        print(f"{'last = last st':14s} {np.mean([x[3] for x in lastc]):6.2f}  (share of rounds whose last consumer stored last)")
+    if flags.any():
+        print(f"{'bounded count':14s} {np.mean(flags[live] & 1):6.3f}  (share of workgroup-rounds)")
+        print(f"{'hand-off miss':14s} {np.mean((flags[live] >> 1) & 1):6.3f}  (share of workgroup-rounds: an entry past the 64 loaded rows)")
+        for r in range(1, TL_NR):
+            pass
+        # rounds whose latest row had a miss / bounded count
+        lat = [(flags[r, live[r]][np.argmax(b[r, live[r], 3])]) for r in range(TL_NR) if live[r].sum() > 1]
+        print(f"{'latest row flg':14s} miss {np.mean([(x >> 1) & 1 for x in lat]):6.3f}  bounded {np.mean([x & 1 for x in lat]):6.3f}  (the round's last-completed row)")
     # the work's two phases from the first block (k_round2p: inputs current,
     # search done, window staged, rows stored): search, then the hand-off
     # (the new candidate's FD entries counted, its rows stored)
@@ -102,6 +125,11 @@ def tagged(path):
             if (pc & 0x80000000).all():  # k_round_lean: the last wave's probes done (from wave 0's inputs current)
                 v = pc & 0x7FFFFFFF
                 print(f"{'last probes':14s} median {np.median(v) * ns / 1000:6.2f} us  p90 {np.percentile(v, 90) * ns / 1000:6.2f} us  (last wave's probes done - wave 0's inputs current)")
+                # (ts[3]: the last wave's hand-off start; tl[3]: every wave stored)
+                hs = (g[:, :, 3] - a[:, :, 0])[m]
+                hst = (a[:, :, 3] - g[:, :, 3])[m]
+                print(f"{'last hand st':14s} median {np.median(hs) * ns / 1000:6.2f} us  p90 {np.percentile(hs, 90) * ns / 1000:6.2f} us  (last wave's hand-off start - wave 0's inputs current)")
+                print(f"{'hand st->row':14s} median {np.median(hst) * ns / 1000:6.2f} us  p90 {np.percentile(hst, 90) * ns / 1000:6.2f} us  (-> every wave stored)")
             else:
                 print(f"{'probe count':14s} median {np.median(pc):6.1f}     p90 {np.percentile(pc, 90):6.1f}")
             if spread.any():
