@@ -770,10 +770,11 @@ int segments_for(const Dev &d, int64_t events) {
   // (round 5, C3 10M events, segment k holding a 1.38^k share: 38.1-38.4 ms
   // per step at 10-14 segments against 40.1 at 8 segments of 1.5^k)
   // (round 6: at n <= 96 the dataflow and the loop take about as long, so
-  // more, flatter segments shorten the loop left after the dataflow's end)
+  // more, flatter segments shorten the loop left after the dataflow's end;
+  // at n = 128 the lean loop is only ~1.14x the dataflow: 16 of 1.15x)
   int K = !d.fd_cols ? 1
-          : d.n <= 96 ? (events >= 1500000 ? 12 : events >= 1000000 ? 8 : 1)
-                      : (events >= 4000000 ? 12 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1);
+          : d.n <= 96 ? (events >= 1000000 ? 12 : 1)
+                      : (events >= 4000000 ? 16 : events >= 1500000 ? 8 : events >= 1000000 ? 4 : 1);
   if (const char *e = getenv("BH_SEGMENTS")) K = atoi(e);
   return (int)std::max<int64_t>(1, std::min<int64_t>({K, events / 4096 + 1, 64}));
 }
@@ -799,18 +800,20 @@ int segments_for(const Dev &d, int64_t events) {
 // ~2 ms for the second segment)
 // The growth ratio: segment k + 1's dataflow runs beside segment k's loop,
 // so it can grow by (loop time / dataflow time) per event and still be ready
-// when the loop reaches it.  That ratio depends on n: at C3 (n = 128) the
-// loop outruns the dataflow 1.32x (33 against 25 ms per step; 1.24-1.32
-// measured alike, profiles/r5_seg_ratio_late.txt); at C5 (n = 64) the two
-// take the same time and at C2 (n = 32) the loop is 1.12x the dataflow
-// (profiles/r6_seg_sweep_*), where growing segments only leave a long last
-// loop after the dataflow's end.  BH_SEG_RATIO overrides it (A/B)
-// (round 6, profiles/r6_seg_sweep.txt: C5 16.89 -> 15.00 ms with 12 equal
-// segments, C2 11.63 -> 10.31 ms with 8 segments of 1.12x)
-constexpr double SEG_RATIO_MID = 1.0, SEG_RATIO_SMALL = 1.12;
+// when the loop reaches it; grown faster, the loop waits for it between
+// segments.  That ratio depends on n: at C3 (n = 128) the loop is ~1.14x
+// the dataflow (29.4 against 25.9 ms per step with k_round_lean; 1.32 with
+// k_round2p left 3.35 ms of waits between the loop's launches,
+// profiles/r6_seg_sweep_lean.txt: 34.5 -> 32.0 ms at 1.15 x 16 segments);
+// at C5 (n = 64) and C2 (n = 32) the two take about the same time, where
+// growing segments only leave a long last loop after the dataflow's end:
+// equal segments.  BH_SEG_RATIO overrides it (A/B)
+// (round 6, profiles/r6_seg_sweep.txt, r6_seg_sweep_lean.txt: C5 16.89 ->
+// 14.3 ms with 12 equal segments, C2 11.63 -> 9.6 ms with 12 equal segments)
+constexpr double SEG_RATIO_WIDE = 1.15, SEG_RATIO_NARROW = 1.0;
 static double seg_ratio(const Dev &d) {
   if (const char *e = getenv("BH_SEG_RATIO")) return std::max(1.0, atof(e));
-  return d.n > 96 ? 1.32 : d.n > 48 ? SEG_RATIO_MID : SEG_RATIO_SMALL;
+  return d.n > 96 ? SEG_RATIO_WIDE : SEG_RATIO_NARROW;
 }
 
 static void segment_bounds(int64_t base, int64_t N, int K, double ratio, int64_t *Ns) {

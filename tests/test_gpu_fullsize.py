@@ -8,7 +8,7 @@ longer run: the pipelined coordinates of segment s + 1, the round loop's
 resume at the last round segment s fixed and the incremental layout are all
 on the path these checks cover:
 
-  * C2 (32 peers, 1M events: 8 segments) and C5 (64 peers with 21 lagging,
+  * C2 (32 peers, 1M events: 12 segments) and C5 (64 peers with 21 lagging,
     2M events: 12 segments), whole;
   * C3's DAG (128 peers, the bench's 10M-event DAG) on its first 2.5M
     events with 5 segments of 500k events -- every chain resumes 4 times at
@@ -48,7 +48,7 @@ def _whole(cfg, N=None, segments=None, monkeypatch=None, ordered=0.9):
 @pytest.mark.timeout(600)
 def test_c2_whole_dag():
     hg = _whole(2)
-    assert hg.pipeline()[0] == 8  # the default for >= 1M events at n <= 96
+    assert hg.pipeline()[0] == 12  # the default for >= 1M events at n <= 96
 
 
 @pytest.mark.timeout(600)

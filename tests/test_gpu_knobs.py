@@ -16,7 +16,7 @@ test_gpu_shard.py, test_gpu_comm.py).
   LA - FD) instead of packed f32 with the clamp modifier (the default);
 * BH_SEG_RATIO -- the segment pipeline's growth ratio (segment k holds a
   ratio^k share of the events): equal segments (1.0) and steep ones (1.8)
-  cut the DAG at other boundaries than the defaults (1.32 above n = 96).
+  cut the DAG at other boundaries than the defaults (1.15 above n = 96).
 """
 import os
 

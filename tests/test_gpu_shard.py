@@ -183,7 +183,12 @@ def test_group_rerun_after_reset(monkeypatch, coords, devs):
             grp.reset_consensus()
         grp.run_consensus()
         _compare(o, grp, f"{coords} {len(devs)} shards, run {run}")
-        assert grp.pipeline()[0] == 8
+        # (four split shards on ONE device each run the 128-workgroup
+        # persistent loop: more workgroups than one MI355X holds at once, so
+        # a loop may give up waiting for an unplaced workgroup and the call
+        # falls back to the unpipelined passes -- exact, as _compare checked;
+        # with one rank per GPU no two loops share a device)
+        assert grp.pipeline()[0] == 8 or (len(devs) > 2 and grp.loop_stats()[1] > 0)
 
 
 @pytest.mark.parametrize("rng,seg", [(2, 0), (60, 0), (120, 0), (250, 0), (2, 2), (2, 5)])

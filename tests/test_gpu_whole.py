@@ -66,11 +66,11 @@ def _whole_digest(name, monkeypatch=None, segments=None, reruns=2):
 @pytest.mark.timeout(900)
 def test_c3_whole_dag():
     """The bench's headline DAG, all 10M events, through the default pipeline
-    (12 segments from 4M events, the persistent loop), on a fresh handle and
+    (16 segments from 4M events, the persistent loop), on a fresh handle and
     on two reruns after bh_reset_consensus (the bench's timed step)."""
     d, hg = _whole_digest("c3")
-    assert hg.pipeline()[0] == 12 and hg.profile_kernel() == "k_flow32x2"
-    assert hg.loop_stats() == (12 * 3, 0)  # one persistent loop per segment and run, no fallback
+    assert hg.pipeline()[0] == 16 and hg.profile_kernel() == "k_flow32x2"
+    assert hg.loop_stats() == (16 * 3, 0)  # one persistent loop per segment and run, no fallback
     invariants(d, hg)
 
 
