@@ -1442,33 +1442,38 @@ void launch_cand_rows(const Dev &d, int from_resume, hipStream_t s) {
 // the previous candidate's entry j0 = FD[(c, B[r][c])][i], and the lane's
 // 8 rows of LA[.][c] on chain i: 2 aligned 16-B pieces at ab + 8 (t % 8)
 // (ab = chain i's row of j0 rounded down to 4; FDB = 64 rows per chain).
-struct HandIn {
+template <int NP = 2>
+struct HandInT {
   int32_t j0, cs, len;
-  int4 fb[2];
+  int4 fb[NP];
 };
+using HandIn = HandInT<2>;
 
-__device__ __forceinline__ void hand_load(const int32_t *colc, HandIn &h) {
+template <int NP>
+__device__ __forceinline__ void hand_load(const int32_t *colc, HandInT<NP> &h) {
   const int l8 = threadIdx.x & 7;
   const bool live = h.j0 != FD_NONE;
   const int32_t a = live ? (h.cs + h.j0) & ~3 : 0;
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-    h.fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 8 * l8 + 4 * u)) : make_int4(0, 0, 0, 0);
+  for (int u = 0; u < NP; ++u)
+    h.fb[u] = live ? *reinterpret_cast<const int4 *>(colc + (a + 4 * NP * l8 + 4 * u)) : make_int4(0, 0, 0, 0);
 }
 
 // FD[(c, row)][i] for the lane's chain i: j0 + #{rows from j0 below `row`}
-// among the 64 loaded (a count and a group sum); an entry beyond them (rare)
-// is searched by the wave, chain by chain (first_ge_wave).  Every lane of
-// the chain's group returns it; FD_NONE if no row of the view sees (c, row)
-__device__ __forceinline__ int32_t hand_entry(const int32_t *colc, const HandIn &h, int i, int c, int32_t row) {
+// among the 32 NP loaded (a count and a group sum); an entry beyond them
+// (rare) is searched by the wave, chain by chain (first_ge_wave).  Every lane
+// of the chain's group returns it; FD_NONE if no row of the view sees (c, row)
+template <int NP>
+__device__ __forceinline__ int32_t hand_entry(const int32_t *colc, const HandInT<NP> &h, int i, int c, int32_t row) {
+  constexpr int FB = 32 * NP;
   const int lane = threadIdx.x & 63, l8 = lane & 7;
   const bool live = h.j0 != FD_NONE;
   const int32_t a = h.cs + h.j0, ab = a & ~3, end = h.cs + h.len;
-  const int32_t x0 = ab + 8 * l8, elo = a - x0, ehi = end - x0;  // rows a .. end - 1 of the lane's 8
+  const int32_t x0 = ab + 4 * NP * l8, elo = a - x0, ehi = end - x0;  // rows a .. end - 1 of the lane's 4 NP
   int cnt = 0;
   if (live) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NP; ++u) {
       cnt += (4 * u + 0 >= elo) & (4 * u + 0 < ehi) & (h.fb[u].x < row);
       cnt += (4 * u + 1 >= elo) & (4 * u + 1 < ehi) & (h.fb[u].y < row);
       cnt += (4 * u + 2 >= elo) & (4 * u + 2 < ehi) & (h.fb[u].z < row);
@@ -1476,7 +1481,7 @@ __device__ __forceinline__ int32_t hand_entry(const int32_t *colc, const HandIn 
     }
   }
   cnt = group_total<8>(cnt);
-  const int32_t jn = a + cnt, bend = min(ab + FDB, end);
+  const int32_t jn = a + cnt, bend = min(ab + FB, end);
   int32_t fd = FD_NONE;
   bool miss = false;
   if (live) {
@@ -1484,9 +1489,9 @@ __device__ __forceinline__ int32_t hand_entry(const int32_t *colc, const HandIn 
     else if (jn < bend) fd = jn - h.cs;
     else miss = bend < end;  // (else: no row of chain i in this view sees the candidate)
   }
-  // the entry lies beyond the 64 rows loaded (a lagging chain's candidate
-  // jumps far): every such chain's 8 lanes search on at once, the first pass
-  // over the 512 rows after them
+  // the entry lies beyond the rows loaded (a lagging chain's candidate jumps
+  // far): every such chain's 8 lanes search on at once, the first pass over
+  // the 512 rows after them
   if (__any(miss)) {
     const int32_t j = first_ge_group<8>(colc, bend, end, row, miss, true);
     if (miss) fd = j < end ? j - h.cs : FD_NONE;
@@ -2187,6 +2192,9 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   constexpr uint32_t WBYTES = (uint32_t)WR * RST;
   constexpr uint32_t BIAS = 0x4B800000u, INF = 0x7F800000u;
   constexpr uint32_t VMASK24 = 0xFFFFFFu;
+  // the hand-off's rows per chain: 8 lanes x 4 HNP (32 rows: an entry past them in 6 % of
+  // workgroup-rounds, 77 % of rounds, C3 32.0 -> 32.9 ms)
+  constexpr int HNP = 2, FBL = 32 * HNP;
   extern __shared__ __attribute__((aligned(16))) int4 sm4[];
   char *const wb = reinterpret_cast<char *>(sm4);
   uint32_t *const wb32 = reinterpret_cast<uint32_t *>(sm4);
@@ -2214,7 +2222,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   int32_t r = d.state[ST_CUR0];  // the first iteration has parity 0
   int32_t k0 = d.Bp[c];
   const int hc = t >> 3;  // the hand-off's chain
-  HandIn hin{FD_NONE, 0, 0, {}};
+  HandInT<HNP> hin{FD_NONE, 0, 0, {}};
   if (hc < n) {
     hin.cs = d.chain_start[hc];
     hin.len = d.chain_len[hc];
@@ -2229,14 +2237,14 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   const bool sst = sg < 8 && swi < n;
   const int32_t *scol = d.la_col + (int64_t)(sst ? swi : 0) * stride;
   int4 wv;
-  f32x2 hfb[4];  // hin.fb biased (the fast hand-off count)
+  f32x2 hfb[2 * HNP];  // hin.fb biased (the fast hand-off count)
   bool hslow = false;  // the lane's 64-row block is not wholly inside chain hc (hand_entry's bounded count)
   auto own_loads = [&]() {  // chain c's window from k0 and the hand-off rows from j0
     const int32_t rb = (cs + k0) & ~3;
     wv = sst && k0 < len ? *reinterpret_cast<const int4 *>(scol + (rb + 4 * sg)) : make_int4(-1, -1, -1, -1);
     hand_load(colc, hin);
     const int32_t ab = (hin.cs + hin.j0) & ~3;
-    hslow = hin.j0 != FD_NONE && (ab < hin.cs || ab + FDB > hin.cs + hin.len);
+    hslow = hin.j0 != FD_NONE && (ab < hin.cs || ab + FBL > hin.cs + hin.len);
   };
   own_loads();
   // what no staging writes: columns n .. COLS (and their repeats) LA -1, the
@@ -2286,6 +2294,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     // rows while the other workgroups are still writing them, and every
     // consumer's polls slow those writes down (k_round2p got this wait from
     // its loop latch; MEASUREMENTS.md round 6: polls 0 -> 2, hop 1.2 -> 4 us
+    // without it; with the stores-before-loads barrier, C3 32.1 -> 35.5 ms
     // without it)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned long long rta = dgt ? __builtin_amdgcn_s_memrealtime() : 0;  // (own stores acknowledged)
@@ -2314,7 +2323,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     }
     // the hand-off rows in the biased f32 domain (the fast count at the end)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < HNP; ++u) {
       hfb[2 * u] = f32x2{__uint_as_float((uint32_t)hin.fb[u].x + BIAS), __uint_as_float((uint32_t)hin.fb[u].y + BIAS)};
       hfb[2 * u + 1] = f32x2{__uint_as_float((uint32_t)hin.fb[u].z + BIAS), __uint_as_float((uint32_t)hin.fb[u].w + BIAS)};
     }
@@ -2515,17 +2524,18 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
         // rows converted while the candidates were awaited
         const float rf = __uint_as_float((uint32_t)result + BIAS);
         const f32x2 r2{rf, rf};
-        f32x2 e0 = lt_ind2(r2, hfb[0]) + lt_ind2(r2, hfb[1]), e1 = lt_ind2(r2, hfb[2]) + lt_ind2(r2, hfb[3]);
-        e0 += e1;
+        f32x2 e0 = lt_ind2(r2, hfb[0]) + lt_ind2(r2, hfb[1]);
+#pragma unroll
+        for (int u = 1; u < HNP; ++u) e0 += lt_ind2(r2, hfb[2 * u]) + lt_ind2(r2, hfb[2 * u + 1]);
         const int cnt = (int)group_total_f<8>(e0.x + e0.y);
         const int32_t ab = (hin.cs + hin.j0) & ~3, jn = ab + cnt;
-        fdv = hc == c ? result : jn < ab + FDB ? jn - hin.cs : FD_NONE;
+        fdv = hc == c ? result : jn < ab + FBL ? jn - hin.cs : FD_NONE;
         // (jn reaching the block's end: the entry lies further on -- searched
         // by hand_entry's wave search, as there)
-        const bool miss = hc != c && jn >= ab + FDB;
+        const bool miss = hc != c && jn >= ab + FBL;
         if (__any(miss)) {
           if (DIAG && d.diag != nullptr && lane == 0) atomicOr(&sh_flags, 2u);
-          const int32_t j = first_ge_group<8>(colc, ab + FDB, hin.cs + hin.len, result, miss, true);
+          const int32_t j = first_ge_group<8>(colc, ab + FBL, hin.cs + hin.len, result, miss, true);
           if (miss) fdv = j < hin.cs + hin.len ? j - hin.cs : FD_NONE;
         }
       }
