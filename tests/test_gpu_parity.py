@@ -344,6 +344,68 @@ def _wild_parity(n, N, seed, back):
     _compare(o, hg, f"wild n={n} N={N} back={back}")
 
 
+def _burst_dag(n, N, seed, burst):
+    """Gossip with bursts: now and then one creator emits `burst` events in a
+    row (other-parents: recent events of others), so its chain advances
+    far more than 31 rows within a round -- the n <= 128 loop's window
+    continuation (SM not reached in the staged window) and the hand-off's
+    entries past the 64 loaded rows (its wave search)."""
+    rng = np.random.default_rng(seed)
+    creator = np.empty(N, np.int32)
+    index = np.empty(N, np.int32)
+    sp = np.empty(N, np.int32)
+    op = np.empty(N, np.int32)
+    last = np.full(n, -1, np.int64)
+    cnt = np.zeros(n, np.int32)
+    run_c, run_left = -1, 0
+    for e in range(N):
+        if e < n:
+            c = e
+        elif run_left > 0:
+            c, run_left = run_c, run_left - 1
+        else:
+            c = int(rng.integers(n))
+            if rng.random() < 0.002:
+                run_c, run_left = c, burst
+        creator[e], index[e], sp[e] = c, cnt[c], last[c]
+        o = -1
+        if e >= n:
+            for _ in range(8):
+                cand = int(rng.integers(max(0, e - 4 * n), e))
+                if creator[cand] != c:
+                    o = cand
+                    break
+        op[e] = o
+        last[c] = e
+        cnt[c] += 1
+    hashes = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    sig = rng.integers(0, 256, (N, 32), dtype=np.uint8)
+    ntx = (rng.random(N) < 0.5).astype(np.int32)
+    return creator, index, sp, op, hashes, sig, ntx
+
+
+@pytest.mark.parametrize("n,N,seed,burst", [(32, 40_000, 41, 120), (128, 60_000, 42, 200), (100, 50_000, 43, 90)])
+def test_burst_dag_parity(n, N, seed, burst):
+    from babble_amd import Hashgraph
+    creator, index, sp, op, hashes, sig, ntx = _burst_dag(n, N, seed, burst)
+    pid = np.sort(np.random.default_rng(seed + 1).choice(2**31 - 1, n, replace=False)).astype(np.int64)
+    o = Oracle(n, pid, capacity=N)
+    o.insert_dag(creator, index, sp, op, hashes, sig, ntx)
+    o.run_consensus()
+    hg = Hashgraph(pid, N)
+    spi = np.where(sp >= 0, index - 1, -1)
+    opc = np.where(op >= 0, pid[creator[np.maximum(op, 0)]], -1)
+    opi = np.where(op >= 0, index[np.maximum(op, 0)], -1)
+    assert not hg.insert_events(pid[creator], index, spi, opc, opi, hashes, sig, ntx).any()
+    hg.run_consensus()
+    _compare(o, hg, f"burst n={n} N={N} burst={burst}")
+    # the DAG does what it is for: some chain holds more than 31 events of
+    # one round (its boundary jumps past the staged window)
+    rd = o.results()["round"]
+    per = np.bincount(creator.astype(np.int64) * (int(rd.max()) + 2) + (rd.astype(np.int64) + 1))
+    assert per.max() > 31
+
+
 @pytest.mark.parametrize("n,N,seed,back", [
     (8, 30_000, 21, 20_000),     # parents far behind the LDS rings (flow: 64/chain, sweep: 16K)
     (24, 40_000, 22, 3_000),
