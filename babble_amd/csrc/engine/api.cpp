@@ -289,6 +289,7 @@ int run_round_loop(bh_handle *h, const Dev &v, hipGraphExec_t *graph, Dev *graph
     // take the per-iteration launches (counted in stats.persist_fallbacks)
     ++h->persist_fallbacks;
     if ((rc = snapshot(true))) return rc;
+    if (pers && bh::cand_fe(v)) bh::launch_cand_defe(v, s);  // (k_round2 reads plain entries)
   }
   if (!no_graph && (rc = build_graph(h, v, graph, graph_dev, ITER_BATCH))) return rc;
   if (!no_graph && (rc = build_graph(h, v, graph_s, graph_dev_s, ITER_FIRST))) return rc;

@@ -25,6 +25,20 @@ namespace bh {
 
 constexpr int32_t UNSET = INT32_MIN;    // Go nil
 constexpr int32_t FD_NONE = INT32_MAX;  // math.MaxInt32 (hashgraph.go:447)
+// k_round_lean's hand-off encoding of a firstDescendants entry x (a chain
+// row < 2^22 - 1, or FD_NONE as 2^22 - 1) with the 1-bit tag b: the f32
+// 2^22 + x + b / 2, bits 0x4A800000 + 2x + b (the binade [2^22, 2^23) has
+// spacing 1/2), so a received entry is used as it arrives
+constexpr uint32_t FE_BASE = 0x4A800000u;
+constexpr int32_t FE_NONE_X = (1 << 22) - 1;
+__host__ __device__ inline uint32_t fe_encode(int32_t x, uint32_t b) {
+  const uint32_t v = x == FD_NONE || x >= FE_NONE_X ? (uint32_t)FE_NONE_X : (uint32_t)x;
+  return FE_BASE + 2u * v + b;
+}
+__host__ __device__ inline int32_t fe_decode(uint32_t bits) {
+  const int32_t x = (int32_t)((bits - FE_BASE) >> 1);
+  return x >= FE_NONE_X ? FD_NONE : x;
+}
 constexpr int32_t P16_MAXLEN = 65000;  // longest chain the 16-bit round loop takes
 constexpr int P8G_DELTA = 20;  // k_round_wide's shared 8-bit base: B[r-1][i] - 20
 constexpr int P8_XMAX = 126;  // largest window-relative LA of k_round_wide's 8-bit rows (bit 7 is the compare's)
@@ -137,6 +151,7 @@ struct Dev {
   int32_t wide_cols;  // the 16-bit wide loop reads la_col (k_round_wide<*, true, true>; no FDT)
   int32_t round_persist;  // k_round2p: the whole n <= 128 loop in one launch (default; BH_ROUND_PERSIST=0: one launch per iteration)
   int32_t round_f32;      // k_round2p's search compares in packed f32 (BH_ROUND_F32=0: the int32 sign-bit count)
+  int32_t cand_fe;        // candfd rows in k_round_lean's float encoding (set by the launchers, cand_fe())
   int32_t *pbar;          // the persistent wide loop's grid barrier (k_round2p hands off through tagged Bp / candfd dwords instead)
   int32_t pbar_spin;      // polls before a persistent loop gives up waiting (barrier or tagged hand-off; BH_PBAR_SPIN lowers it to test the fallback)
   int32_t pbar_mode;      // the wide persistent loop's barrier: 0 one counter, 1 XCD-hierarchical (n > 64; BH_PBAR=xcd|flat)
@@ -392,7 +407,11 @@ void launch_round_iteration(const Dev &d, int parity, hipStream_t s);  // k_roun
 bool round_solo_eligible(const Dev &d);
 bool round2_eligible(const Dev &d);
 bool round_persist_eligible(const Dev &d);
-bool round_lean_eligible(const Dev &d);  // k_round_lean (biased f32, chains < 2^23 - 2) over k_round2p
+bool round_lean_eligible(const Dev &d);  // k_round_lean (float-encoded hand-off, chains < 2^22 - 2) over k_round2p
+// the loop that runs on this Dev is k_round_lean: candfd rows in its float
+// encoding (fe_encode; the launchers of k_cand_rows / k_seg_resume set it)
+bool cand_fe(const Dev &d);
+void launch_cand_defe(const Dev &d, hipStream_t s);  // parity-0 candfd rows: fe_encode -> plain
 void launch_round_persist(const Dev &d, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 bool round_wide_persist_eligible(const Dev &d);
 void launch_round_wide_persist(const Dev &d, hipStream_t s);

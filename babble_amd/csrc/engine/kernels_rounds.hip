@@ -1295,8 +1295,11 @@ __device__ __forceinline__ int32_t first_ge16(const int32_t *col, int32_t lo, in
 __device__ __forceinline__ void cand_row(const Dev &d, int c, int32_t r, int32_t b) {
   const int t = threadIdx.x;
   if (t == 0 && d.c8tag) d.c8tag[c] = d.c8tag[d.n + c] = -1;
-  if (d.fd_cols) {  // k_round2p's parity-1 hand-off slots: tag 0, which its iteration 1 does not accept
-    for (int i = t; i < d.npad; i += blockDim.x) d.candfd[((int64_t)d.n + c) * d.npad + i] = 0;
+  if (d.fd_cols) {
+    // the parity-1 hand-off slots, which the loop's iteration 1 must not take
+    // for its own: top byte 0 (k_round2p's tag 1 differs) and bit 0 set
+    // (k_round_lean's tag bit for iteration 1 is 0)
+    for (int i = t; i < d.npad; i += blockDim.x) d.candfd[((int64_t)d.n + c) * d.npad + i] = 1;
     if (t == 0) d.Bp[d.n + c] = 0;
   }
   if (b >= d.chain_len[c]) return;  // no candidate on chain c
@@ -1323,7 +1326,7 @@ __device__ __forceinline__ void cand_row(const Dev &d, int c, int32_t r, int32_t
     const int32_t f = on && j < len ? j : FD_NONE;
     if ((t & 15) == 0 && i < nrow) {
       if (c16) c16[i] = (uint16_t)min((uint32_t)f + 1u, 0xFFFFu);
-      else cf[i] = f;
+      else cf[i] = d.cand_fe ? (int32_t)fe_encode(f, 0) : f;  // (k_round_lean: iteration 0's tag bit is 0)
     }
   }
 }
@@ -1396,7 +1399,11 @@ __global__ __launch_bounds__(1024) void k_seg_resume(Dev d) {
   cand_row(d, c, r0, b);
 }
 
-void launch_seg_resume(const Dev &d, hipStream_t s) { k_seg_resume<<<d.n, 1024, 0, s>>>(d); }
+void launch_seg_resume(const Dev &d, hipStream_t s) {
+  Dev dd = d;
+  dd.cand_fe = cand_fe(d);
+  k_seg_resume<<<d.n, 1024, 0, s>>>(dd);
+}
 
 // TQ (default): every lane group binary-searches its own T_q (the first
 // window row strongly seeing candidate q) with no barrier between probes; one
@@ -1434,7 +1441,9 @@ constexpr int FDB = 64;      // LA rows per chain loaded for the hand-off
 
 // the first iteration's candidate rows (round 0, or the resume round)
 void launch_cand_rows(const Dev &d, int from_resume, hipStream_t s) {
-  k_cand_rows<<<d.n, 1024, 0, s>>>(d, from_resume);
+  Dev dd = d;
+  dd.cand_fe = cand_fe(d);
+  k_cand_rows<<<d.n, 1024, 0, s>>>(dd, from_resume);
 }
 
 // The hand-off's per-lane inputs (k_round2 / k_round2p): chain i = t / 8
@@ -2160,12 +2169,12 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
 // wave-instruction per cycle per CU, so ~6,300 cycles = 2.6 us at 2.4 GHz,
 // which is the round's measured work (profiles/r6_timeline_c3_base.txt).
 // The loop is VALU-issue-bound on its CU, not LDS- or latency-bound.  Here:
-//  * biased f32 values: an entry x in [-1, 2^23 - 2] is the f32 with bits
-//    x + 0x4B800000, i.e. 2^24 + 2x (x = -1 gives 2^24 - 1), so one integer
-//    add stages an LA entry, one add strips a received FD entry's (checked)
-//    tag and biases it, and clamp(FD - LA) (v_pk_add_f32 ... clamp) is still
-//    the 0/1 indicator [LA < FD] (FD - LA is 2(fd - la) >= 2, or <= 0, or
-//    2 fd + 1 >= 1 for la = -1);
+//  * float entries: the producers store each FD entry x as fe_encode's f32
+//    2^22 + x + b / 2 (b: a 1-bit tag, iteration it's (it >> 1) & 1, which
+//    tells it from the parity buffer's last use, it - 2), and the window
+//    stages LA as la + 2^22 + b / 2 (a convert and an add), so a received
+//    row is used as it arrives and clamp(FD - LA) (v_pk_add_f32 ... clamp)
+//    is the 0/1 indicator [LA < FD] (FD - LA = fd - la, an integer);
 //  * the per-candidate search is five fixed probes with no loop control: the
 //    probed row is an LDS immediate offset from the lane's address, one add
 //    and one select move it; rows past the window's valid ones read +inf (a
@@ -2182,7 +2191,7 @@ __global__ __launch_bounds__(1024) void k_round2p(Dev d) {
 //    group's count; a wave that has a chain within 64 rows of its end takes
 //    hand_entry's bounded count;
 //  * two windows and histograms by parity.
-// Needs chains < 2^23 - 1 (else k_round2p's int32 search).
+// Needs chains < 2^22 - 2 (else k_round2p's int32 search).
 template <int PPL, bool FULL, bool DIAG>
 __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   constexpr int LPC = 8, RS4 = LPC * PPL, COLS = 4 * RS4, RB = 16 * RS4;
@@ -2190,7 +2199,8 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   constexpr int RSH = RST == 256 ? 8 : RST == 512 ? 9 : 10;
   constexpr int WR = HWL + 2;  // + two sentinel rows (a probe reaches row off + 30 <= 33)
   constexpr uint32_t WBYTES = (uint32_t)WR * RST;
-  constexpr uint32_t BIAS = 0x4B800000u, INF = 0x7F800000u;
+  constexpr uint32_t BIAS = 0x4B800000u, INF = 0x7F800000u;  // (BIAS: the hand-off count's own domain)
+  constexpr float FE_LA0 = 4194304.0f;  // 2^22: a window entry la is la + 2^22 + b / 2 (fe_encode's domain)
   constexpr uint32_t VMASK24 = 0xFFFFFFu;
   // the hand-off's rows per chain: 8 lanes x 4 HNP (32 rows: an entry past them in 6 % of
   // workgroup-rounds, 77 % of rounds, C3 32.0 -> 32.9 ms)
@@ -2226,7 +2236,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   if (hc < n) {
     hin.cs = d.chain_start[hc];
     hin.len = d.chain_len[hc];
-    if (k0 < len) hin.j0 = d.candfd[(int64_t)c * npad + hc];
+    if (k0 < len) hin.j0 = fe_decode((uint32_t)d.candfd[(int64_t)c * npad + hc]);  // (k_cand_rows: float-encoded)
   }
   // the window's staging: thread t holds rows 4 sg .. 4 sg + 3 of column swi
   // (8 lanes per column: a wave's loads touch 8 cache lines, not 64 -- with
@@ -2253,7 +2263,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     const int row = (j / (RST / 4)) % WR, col = j % (RST / 4);
     const int lc = col < COLS ? col : col < COLS + 32 ? col - COLS : COLS;
     if (row >= HWL) wb32[j] = INF;
-    else if (lc >= n) wb32[j] = BIAS - 1u;
+    else if (lc >= n) wb32[j] = __float_as_uint(FE_LA0 - 1.0f);
   }
   if (t == 0) sh_fail = 0, sh_st = sh_flags = sh_hs = 0;
   const uint32_t lane_off = 16u * part + 128u * rot;  // the lane's first piece (rotated by 128 B for odd pairs)
@@ -2274,13 +2284,15 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
   int p = 0;
   for (int it = 0;; ++it) {
     const bool dgt = DIAG && d.diag != nullptr && t == 0 && r >= TL_R0 && r < TL_R0 + TL_NR;
-    const uint32_t want = (uint32_t)it & 0xFFu;
+    const uint32_t want = (uint32_t)it & 0xFFu;  // (Bp's tag)
+    const uint32_t tb = ((uint32_t)it >> 1) & 1u;  // (candfd's tag bit: iterations it and it - 2 differ)
+    const float la_off = FE_LA0 + 0.5f * (float)tb;  // a window entry la stages as la + la_off
     uint32_t bqr = 0;
     int4 f[PPL];
     const int32_t row0 = p ? rowq1 : rowq0;
     auto load_in = [&]() {
       bqr = q < n ? (uint32_t)__hip_atomic_load(d.Bp + (int64_t)p * n + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      const int32_t none = (int32_t)((want << 24) | VMASK24);  // (a padding column: FD_NONE, tagged)
+      const int32_t none = (int32_t)fe_encode(FD_NONE, tb);  // (a padding column: FD_NONE, tagged)
 #pragma unroll
       for (int u = 0; u < PPL; ++u)
         f[u] = FULL || gpiece(u) < q4 ? __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -2307,7 +2319,8 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     const int rows = min(HWL - off, max(0, len - k0));
     const int R = min(rows, HWL - 1);  // searched rows [0, R); R: not in the window
     if (sst) {
-      uint32_t v[4] = {(uint32_t)wv.x + BIAS, (uint32_t)wv.y + BIAS, (uint32_t)wv.z + BIAS, (uint32_t)wv.w + BIAS};
+      uint32_t v[4] = {__float_as_uint((float)wv.x + la_off), __float_as_uint((float)wv.y + la_off),
+                       __float_as_uint((float)wv.z + la_off), __float_as_uint((float)wv.w + la_off)};
       const int32_t lim = cs + len - rb - 4 * sg;  // (uniform test: the window reaches the chain's end)
       if (cs + len < rb + HWL) {
 #pragma unroll
@@ -2345,7 +2358,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
             an &= (uint32_t)(f[u].x & f[u].y & f[u].z & f[u].w);
             o |= (uint32_t)(f[u].x | f[u].y | f[u].z | f[u].w);
           }
-          ok = (an >> 24) == want && (o >> 24) == want;
+          ok = (an & 1u) == tb && (o & 1u) == tb;
         }
         if (__all(ok)) break;
         if (spin >= d.pbar_spin) {  // a workgroup never published: the host falls back
@@ -2362,24 +2375,13 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     if (DIAG && d.diag != nullptr && lane == 0) atomicMax(&sh_cur, (uint32_t)__builtin_amdgcn_s_memrealtime());
     const int32_t bq = (int32_t)(bqr & VMASK24);
     const bool act = q < n && bq < lq;
-    // strip the tag and bias in one add: every dword a live candidate's
-    // lanes use carries tag `want` (checked above), so x - (want << 24) is
-    // its value (FD_NONE's 0xFFFFFF lands above every entry); iteration 0's
-    // rows are untagged (top byte 0, or 0x7F for FD_NONE): masked
-    const uint32_t kb = BIAS - (want << 24);
+    // the candidates' entries are used as they arrive: fe_encode's f32 (the
+    // tag bit is the window's half; FD - LA is then an integer)
     f32x2 fd[2 * PPL];
-    if (it == 0) {
 #pragma unroll
-      for (int u = 0; u < PPL; ++u) {
-        fd[2 * u] = f32x2{__uint_as_float(((uint32_t)f[u].x & VMASK24) + BIAS), __uint_as_float(((uint32_t)f[u].y & VMASK24) + BIAS)};
-        fd[2 * u + 1] = f32x2{__uint_as_float(((uint32_t)f[u].z & VMASK24) + BIAS), __uint_as_float(((uint32_t)f[u].w & VMASK24) + BIAS)};
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < PPL; ++u) {
-        fd[2 * u] = f32x2{__uint_as_float((uint32_t)f[u].x + kb), __uint_as_float((uint32_t)f[u].y + kb)};
-        fd[2 * u + 1] = f32x2{__uint_as_float((uint32_t)f[u].z + kb), __uint_as_float((uint32_t)f[u].w + kb)};
-      }
+    for (int u = 0; u < PPL; ++u) {
+      fd[2 * u] = f32x2{__uint_as_float((uint32_t)f[u].x), __uint_as_float((uint32_t)f[u].y)};
+      fd[2 * u + 1] = f32x2{__uint_as_float((uint32_t)f[u].z), __uint_as_float((uint32_t)f[u].w)};
     }
     // one window row (LDS byte address of the lane's first piece) strongly
     // sees candidate q: #{LA < FD} over its COLS columns <= COLS - SM
@@ -2464,15 +2466,17 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
         if (sst) {
           const int4 x = *reinterpret_cast<const int4 *>(scol + (rb2 + 4 * sg));
           uint32_t *w = wb32 + (wbase + (uint32_t)(4 * sg) * RST) / 4 + swi;
-          w[0] = (uint32_t)x.x + BIAS;
-          w[RST / 4] = (uint32_t)x.y + BIAS;
-          w[2 * (RST / 4)] = (uint32_t)x.z + BIAS;
-          w[3 * (RST / 4)] = (uint32_t)x.w + BIAS;
+          const uint32_t v0 = __float_as_uint((float)x.x + la_off), v1 = __float_as_uint((float)x.y + la_off),
+                         v2 = __float_as_uint((float)x.z + la_off), v3 = __float_as_uint((float)x.w + la_off);
+          w[0] = v0;
+          w[RST / 4] = v1;
+          w[2 * (RST / 4)] = v2;
+          w[3 * (RST / 4)] = v3;
           if (swi < 32) {
-            w[COLS] = (uint32_t)x.x + BIAS;
-            w[RST / 4 + COLS] = (uint32_t)x.y + BIAS;
-            w[2 * (RST / 4) + COLS] = (uint32_t)x.z + BIAS;
-            w[3 * (RST / 4) + COLS] = (uint32_t)x.w + BIAS;
+            w[COLS] = v0;
+            w[RST / 4 + COLS] = v1;
+            w[2 * (RST / 4) + COLS] = v2;
+            w[3 * (RST / 4) + COLS] = v3;
           }
         }
         if (t < 16) cntk[p][t] = 0;
@@ -2514,7 +2518,8 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     }
     // ---- hand-off: FD[(c, result)][i] and B[r + 1][c], tagged it + 1 ----
     if (DIAG && d.diag != nullptr && lane == 0) atomicMax(&sh_hs, (uint32_t)__builtin_amdgcn_s_memrealtime());
-    const uint32_t tagw = (uint32_t)((it + 1) & 0xFF) << 24;
+    const uint32_t tagw = (uint32_t)((it + 1) & 0xFF) << 24;  // (Bp's)
+    const uint32_t fe_base_n = FE_BASE + (((uint32_t)(it + 1) >> 1) & 1u);  // (candfd's: iteration it + 1's tag bit)
     int32_t fdv = FD_NONE;
     if (result < len) {
       if (__any(hslow)) {
@@ -2540,8 +2545,8 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
         }
       }
       if ((t & 7) == 0 && hc < npad)
-        __hip_atomic_store((p ? cfs1 : cfs0) + hc, (int32_t)(tagw | ((uint32_t)fdv & VMASK24)), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((p ? cfs1 : cfs0) + hc, (int32_t)(fe_base_n + 2u * min((uint32_t)fdv, (uint32_t)FE_NONE_X)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t == 0)
       __hip_atomic_store(p ? bps1 : bps0, (int32_t)(tagw | (uint32_t)result), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2556,7 +2561,7 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
     // fame's inputs (the new candidate's LA row and its ballots) and the
     // round table: nothing inside the loop reads them
     if (result < len) {
-      if (t < npad) cla_c[(int64_t)cla_pos * npad + t] = (int32_t)(wb32[(wbase + (uint32_t)lrow * RST) / 4 + t] - BIAS);
+      if (t < npad) cla_c[(int64_t)cla_pos * npad + t] = (int32_t)(__uint_as_float(wb32[(wbase + (uint32_t)lrow * RST) / 4 + t]) - la_off);
       if (lane == 0) *ssm_p = ssb;
     }
     if (t == 0) *b_p = result;
@@ -2604,8 +2609,22 @@ __global__ __launch_bounds__(1024) void k_round_lean(Dev d) {
 }
 
 bool round_lean_eligible(const Dev &d) {
-  // biased f32 entries: chain rows <= 2^23 - 3 (FD_NONE's bias stays above them)
-  return d.round_f32 && d.max_chain_len < (1 << 23) - 2;
+  // float-encoded entries: chain rows <= 2^22 - 3 (fe_encode; FD_NONE is 2^22 - 1)
+  return d.round_f32 && d.max_chain_len < (1 << 22) - 2;
+}
+
+bool cand_fe(const Dev &d) { return round_persist_eligible(d) && round_lean_eligible(d) && !round_solo_eligible(d); }
+
+// parity 0's candidate rows back to plain entries (run_round_loop: a
+// persistent k_round_lean that gave up hands its restored inputs to the
+// per-iteration k_round2)
+__global__ void k_cand_defe(Dev d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int64_t)d.n * d.npad) d.candfd[i] = fe_decode((uint32_t)d.candfd[i]);
+}
+
+void launch_cand_defe(const Dev &d, hipStream_t s) {
+  k_cand_defe<<<(unsigned)(((int64_t)d.n * d.npad + 255) / 256), 256, 0, s>>>(d);
 }
 
 bool round_persist_eligible(const Dev &d) {
