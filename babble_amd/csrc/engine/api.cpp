@@ -1130,9 +1130,16 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   segment_bounds(base, N, K, seg_ratio(d), Ns.data());
   // per-chain prefix lengths at a boundary: ids of a chain ascend with its index
   auto lens_at = [&](int64_t bound, int32_t *out) { chain_lens_at(h, bound, out); };
+  // segment lengths on the device: three buffers round robin, so that
+  // segment k + 1's dataflow waits only for loop k - 2 (long finished) and
+  // runs beside loop k - 1 -- with two, its launches (the lengths' copy,
+  // k_flow_desc32x2) waited for loop k - 1 and landed on the compute units
+  // in the gap between two loops, beside k_seg_resume (15 -> 35 us, C3).
+  // The eager rows' tile lists keep two
+  const int npar = sp || eager ? 2 : 3;
   auto view = [&](int k) {  // segment k: events [Ns[k], Ns[k + 1])
     Dev v = d;
-    v.seg_lo = sp ? const_cast<int32_t *>(sp->dview(h, k)) : h->segbuf + (size_t)(k & 1) * 2 * n;
+    v.seg_lo = sp ? const_cast<int32_t *>(sp->dview(h, k)) : h->segbuf + (size_t)(k % npar) * 2 * n;
     v.chain_len = v.seg_lo + n;
     v.N = Ns[(size_t)k + 1];
     v.e0 = Ns[(size_t)k];
@@ -1340,10 +1347,12 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     const bool late = sp && h->xport && h->xport->blocking();
     auto next = [&]() -> int {
       if (k + 1 >= K) return BH_OK;
-      // segment k + 1 reuses the segbuf parity (and tile-list parity) of k - 1,
+      // segment k + 1 reuses the segbuf (and tile-list) slot of k + 1 - npar,
       // last read by its loop (async: the loop's own stop event -- no marker
       // packet on the loop stream) or its resume point
-      if (async && k > 0) {
+      if (async && npar == 3) {
+        if (k >= 2) HIPCHK(h, hipStreamWaitEvent(sx, h->loop_evs[(size_t)2 * (k - 2) + 1], 0));
+      } else if (async && k > 0) {
         HIPCHK(h, hipStreamWaitEvent(sx, h->loop_evs[(size_t)2 * k - 1], 0));
       } else {
         HIPCHK(h, hipEventRecord(sr_mark, sr));
@@ -1399,7 +1408,10 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
     // where the next segment -- or the next call's new events -- resume
     const int32_t *next_len = nullptr;
     if (k + 1 < K) {
-      HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * K + k + 1], 0));
+      // (async: the next iteration's wait for segment k + 1's columns, recorded
+      // after its lengths on the same stream, covers k_seg_resume -- one
+      // barrier packet less between two loops)
+      if (!async) HIPCHK(h, hipStreamWaitEvent(sr, h->seg_ev[(size_t)3 * K + k + 1], 0));
       next_len = view(k + 1).chain_len;
     }
     // (async: the next segment's k_seg_resume finds it)
@@ -2117,7 +2129,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
     if (rc == BH_OK && hipGetDeviceProperties(&prop, device) == hipSuccess) h->ncu = prop.multiProcessorCount;
   }
   if (rc == BH_OK) rc = dalloc(h, &h->seg_zero, (size_t)n);
-  if (rc == BH_OK) rc = dalloc(h, &h->segbuf, (size_t)4 * n);
+  if (rc == BH_OK) rc = dalloc(h, &h->segbuf, (size_t)6 * n);  // (three segments' [lo | len], rounds_pipelined)
   if (rc == BH_OK && hipMemset(h->seg_zero, 0, (size_t)n * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipHostMalloc((void **)&h->seg_stage, (size_t)2 * 64 * n * 4, hipHostMallocDefault) != hipSuccess)
     rc = BH_ERR_DEVICE;

@@ -599,6 +599,13 @@ __host__ __device__ constexpr uint32_t x2_desc(int32_t dch, int32_t j) {
 __host__ __device__ constexpr uint32_t x2_noop(int n) { return (X2_GNOOP << 21) | (uint32_t)((n * X2_RS + X2_R - 1) * 8); }
 __host__ __device__ constexpr uint32_t x2_wait(int n) { return (X2_GWAIT << 21) | (uint32_t)((n * X2_RS + X2_R - 2) * 8); }
 
+// Dynamic LDS the segments' small kernels ask for and never touch: more than
+// the 12 KiB a persistent round-loop workgroup (>= 148 KiB) leaves on its
+// compute unit, so their workgroups run on the others instead of taking the
+// loop's issue slots (C3: k_flow_desc32x2 beside the loop cost 10-30 us per
+// segment).  Ten such workgroups still fit a free compute unit
+constexpr size_t GUARD_LDS = 16 * 1024;
+
 __global__ void k_flow_desc32x2(Dev d) {
   const int64_t e = d.e0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.N) return;
@@ -1043,7 +1050,8 @@ const char *flow_kernel(const Dev &d) {
 
 void launch_flow_desc(const Dev &d, hipStream_t s) {
   if (d.N <= d.e0) return;
-  if (flow32x2_eligible(d)) k_flow_desc32x2<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+  // (GUARD_LDS: its workgroups stay off the compute units the round loop holds)
+  if (flow32x2_eligible(d)) k_flow_desc32x2<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, GUARD_LDS, s>>>(d);
   else if (flow32_eligible(d)) k_flow_desc32<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
   else k_flow_desc<<<(unsigned)((d.N + 255) / 256), 256, 0, s>>>(d);
 }
@@ -1101,7 +1109,7 @@ __global__ __launch_bounds__(256) void k_lt_rows(Dev d) {
 
 void launch_lt_rows(const Dev &d, hipStream_t s) {
   if (d.N <= d.e0) return;
-  k_lt_rows<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, 0, s>>>(d);
+  k_lt_rows<<<(unsigned)((d.N - d.e0 + 255) / 256), 256, GUARD_LDS, s>>>(d);
 }
 
 void launch_flow_coordinates(const Dev &d, hipStream_t s) {

@@ -1344,7 +1344,8 @@ __global__ __launch_bounds__(1024) void k_cand_rows(Dev d, int from_resume) {
 // prefix's lengths, its chain_len this one's), then k_round_resume's and
 // k_cand_rows' work for chain c.  Three launches and their dispatch gaps
 // were ~70 us between two segments' loops at C3 (profiles/r5_gaps_c3_async.txt).
-// The search: 8 lanes per chain, 8-ary over rounds [0, R] (B[R][q] >= len_q)
+// The search: 8 lanes per chain, a pass over the last 64 rounds, then 8-ary
+// over what is left of [0, R] (B[R][q] >= len_q)
 __global__ __launch_bounds__(1024) void k_seg_resume(Dev d) {
   __shared__ int32_t m;
   const int c = blockIdx.x, t = threadIdx.x, lane = t & 63;
@@ -1357,6 +1358,21 @@ __global__ __launch_bounds__(1024) void k_seg_resume(Dev d) {
     const bool on = q < n;
     const int32_t len = on ? d.seg_lo[q] : 0;
     int32_t lo = 0, hi = R;  // the first r in [lo, hi] with B[r][q] >= len
+    if (R >= 64) {
+      // a first pass over the last 64 rounds (where a segment's boundary
+      // usually lies: two dependent loads instead of ~5), rows R - 64 + 8 g
+      const bool ge = on && d.B[(int64_t)(R - 64 + 8 * g) * n + q] >= len;
+      const uint32_t mk = (uint32_t)(__ballot(ge) >> gb) & 0xFFu;
+      if (mk & 1u) {
+        hi = R - 64;  // at or before row R - 64: the whole range below
+      } else if (mk) {
+        const int f = __builtin_ctz(mk);
+        lo = R - 64 + 8 * (f - 1) + 1;
+        hi = R - 64 + 8 * f;
+      } else {
+        lo = R - 7;
+      }
+    }
     bool go = on && lo < hi;
     while (__any(go)) {
       const int32_t s = (hi - lo + 7) >> 3;
