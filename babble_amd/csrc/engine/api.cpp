@@ -161,6 +161,40 @@ int rd_async(bh_handle *h, hipStream_t s, void *dst, const void *src, size_t byt
   return BH_OK;
 }
 
+// The last run's device timings, read from its events when asked (stage
+// table, profile) rather than where the device would wait for the host's
+// queries: the segment pipeline's coordinate windows and loop launches
+// (rounds_pipelined), then the stage events (order_finish)
+void settle_timings(bh_handle *h) {
+  if (h->tm_seg) {
+    h->tm_seg = false;
+    const int K = h->tm_seg_K;
+    float ms = 0;
+    if (h->tm_seg_loops)
+      for (int k = 0; k < K; ++k)
+        if (hipEventElapsedTime(&ms, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]) == hipSuccess)
+          h->loop_ms_acc += ms;
+    h->sweep_ms = 0;
+    for (int k = 0; k < K; ++k)
+      if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess)
+        h->sweep_ms += ms;
+    if (h->tm_seg_sp) {  // the coordinate time is the coordinate shards'; the receive windows are the exchange
+      h->xchg_ms = h->sweep_ms;
+      h->sweep_ms = 0;
+    }
+  }
+  if (h->tm_stages) {
+    h->tm_stages = false;
+    for (int i = 0; i < NSTAGE; ++i) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]) == hipSuccess) h->stage_ms[i] = ms;
+    }
+    float sms = 0;
+    if (hipEventElapsedTime(&sms, h->ev_sweep[0], h->ev_sweep[1]) == hipSuccess) h->sweep_ms = sms;
+  }
+  (void)hipGetLastError();  // (an unrecorded event must not stay sticky)
+}
+
 // Chain-major layout: chain c's events occupy rows [chain_start[c],
 // chain_start[c] + len_c) of a region of cap_c rows.  The regions are kept
 // while every chain fits (appended events extend a region in place, so the
@@ -168,7 +202,7 @@ int rd_async(bh_handle *h, hipStream_t s, void *dst, const void *src, size_t byt
 // laid out again with fresh slack (max(BH_LAYOUT_SLACK or 1024, len / 8)
 // rows each, if the allocation has room; none otherwise) and layout_changed
 // is set.  Rows past a chain's events are gaps (chain_ids -1).
-int set_chain_tables(bh_handle *h) {
+int set_chain_tables(bh_handle *h, bool wait = true) {
   const int n = h->d.n;
   std::vector<int32_t> len((size_t)n);
   int32_t mx = 0;
@@ -203,7 +237,11 @@ int set_chain_tables(bh_handle *h) {
   h->d.max_chain_len = mx;
   h->lens_h = len;
   HIPCHK(h, hipMemcpyAsync(h->d.chain_len, h->lens_h.data(), n * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, wait_stream(h->stream));
+  // (!wait: the caller orders every later reader after h->stream -- the
+  // segment pipeline's coordinate stream waits for an event recorded on it
+  // -- and lens_h / cstart_h change only in the next call, after its
+  // stages' synchronisations)
+  if (wait) HIPCHK(h, wait_stream(h->stream));
   return BH_OK;
 }
 
@@ -1479,22 +1517,14 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   h->sweep_kernel = wide ? bh::floww_kernel(d) : bh::flow_kernel(d);
   if (h->reset_on && base > 0) h->fiat_max = h->pinned_state[bh::ST_COUNT + 2];
   if ((rc = rounds_tail(h, st, base))) return rc;
-  // the timings (every event completed before rounds_tail's synchronisation;
-  // read after its launches, so the device does not wait for them)
-  if (async && !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")))) {
-    float lms = 0;
-    for (int k = 0; k < K; ++k)
-      if (hipEventElapsedTime(&lms, h->loop_evs[(size_t)2 * k], h->loop_evs[(size_t)2 * k + 1]) == hipSuccess)
-        h->loop_ms_acc += lms;
-  }
-  float ms = 0;
-  h->sweep_ms = 0;
-  for (int k = 0; k < K; ++k)
-    if (hipEventElapsedTime(&ms, h->seg_ev[(size_t)3 * k + 1], h->seg_ev[(size_t)3 * k + 2]) == hipSuccess) h->sweep_ms += ms;
-  if (sp) {  // the coordinate time is the coordinate shards'; the receive windows are the exchange
-    h->xchg_ms = h->sweep_ms;
-    h->sweep_ms = 0;
-  }
+  // the timings: every event completed before rounds_tail's synchronisation.
+  // Read when asked (settle_timings): ~2K event queries here would hold the
+  // device idle between DivideRounds and DecideFame
+  h->tm_seg_K = K;
+  h->tm_seg_loops = async && !(getenv("BH_LOOP_TIMING") && !atoi(getenv("BH_LOOP_TIMING")));
+  h->tm_seg_sp = sp != nullptr;
+  h->tm_seg = true;
+  if (sp) settle_timings(h);  // (the exchange time feeds the split's stage table now)
   h->n_coord = N;
   h->lens_coord = h->lens_h;
   h->inc_valid = !h->fdt_lost;
@@ -1512,7 +1542,7 @@ int rounds_segmented(bh_handle *h, bool *used) {
   d.N = (int64_t)h->h_creator.size();
   if (d.N == 0) return BH_OK;
   if ((rc = upload(h))) return rc;
-  if ((rc = set_chain_tables(h))) return rc;
+  if ((rc = set_chain_tables(h, false))) return rc;
   const bool eligible = segments_eligible(h);
   const int64_t base = (!h->layout_changed && h->inc_valid && d.N >= h->n_coord) ? h->n_coord : 0;
   if (getenv("BH_SEG_DEBUG") && atoi(getenv("BH_SEG_DEBUG")))
@@ -1642,7 +1672,10 @@ int rounds_split_stage(bh_handle *h) {
 int stage_rounds(bh_handle *h) {
   int rc;
   h->xchg_ms = 0;
-  for (bh_handle *x : local_shards(h)) x->loop_ms_acc = 0;
+  for (bh_handle *x : local_shards(h)) {
+    x->loop_ms_acc = 0;
+    x->tm_seg = x->tm_stages = false;  // (the last run's events are about to be reused: unread timings go)
+  }
   if (h->split) return rounds_split_stage(h);
   if (!h->shard_cols) {
     // every shard holds the whole DAG and computes the same coordinates and
@@ -1852,12 +1885,7 @@ int order_finish(bh_handle *h) {
     if (rc != BH_OK) return rc;
   }
   h->stage = 4;
-  for (int i = 0; i < NSTAGE; ++i) {
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, h->ev[i], h->ev[i + 1]) == hipSuccess) h->stage_ms[i] = ms;
-  }
-  float sms = 0;
-  if (hipEventElapsedTime(&sms, h->ev_sweep[0], h->ev_sweep[1]) == hipSuccess) h->sweep_ms = sms;
+  h->tm_stages = true;  // (the stage events are read when asked: settle_timings)
   if (d.diag) {  // diagnostic run only: phase counters to stderr, then reset
     std::vector<unsigned long long> gv(bh::DG_COUNT);
     unsigned long long *g = gv.data();
@@ -2997,6 +3025,7 @@ int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x,
 
 int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap) {
   if (!h) return 0;
+  settle_timings(h);
   for (int i = 0; i < NSTAGE && i < cap; ++i) ms[i] = h->stage_ms[i];
   if (cap > NSTAGE) ms[NSTAGE] = h->xchg_ms;
   if (cap > NSTAGE + 1) ms[NSTAGE + 1] = h->frames_ms;
@@ -3006,6 +3035,7 @@ int32_t bh_get_stage_ms(bh_handle *h, float *ms, int32_t cap) {
 
 int bh_get_profile(bh_handle *h, int64_t *rounds_iterated, float *sweep_ms) {
   if (!h) return BH_ERR_INVALID;
+  settle_timings(h);
   if (rounds_iterated) *rounds_iterated = h->iters;
   if (sweep_ms) *sweep_ms = h->sweep_ms;
   return BH_OK;

@@ -123,6 +123,9 @@ struct bh_handle {
   float sweep_ms = 0;
   const char *sweep_kernel = "";
   float stage_ms[NSTAGE]{};
+  // timings of the last run not yet read from its events (settle_timings)
+  bool tm_seg = false, tm_stages = false, tm_seg_loops = false, tm_seg_sp = false;
+  int tm_seg_K = 0;
   int64_t iters = 0;
   int64_t *d_counters_host = nullptr;
   // segment pipeline: coordinates of prefix s + 1 on

@@ -254,7 +254,6 @@ def main():
         hg.reset_consensus()
         hg.run_consensus()
         log(f"warmup {w}: stages_ms={['%.2f' % x for x in hg.stage_ms()]}")
-    sweep_ms, stage_tot = [], np.zeros(8)
     persist0 = hg.loop_stats()[0]
     barrier()
     sync()
@@ -262,8 +261,6 @@ def main():
     for _ in range(args.steps):
         hg.reset_consensus()
         hg.run_consensus()
-        sweep_ms.append(hg.profile()[1])
-        stage_tot += np.array(hg.stage_ms())
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -275,6 +272,11 @@ def main():
         hg.close()
         dist.destroy_process_group()
         return
+    # the device timings of the last step's stages and kernels (HIP events
+    # recorded inside the timed region, read after it: reading them between
+    # steps would hold the device idle)
+    stage_last = np.array(hg.stage_ms())
+    coord_ms = float(hg.profile()[1])
     stats = hg.stats()
     ordered = stats.consensus_events
     # whole-job events ordered: one DAG per step when sharded, one per rank per step as replicas
@@ -286,7 +288,7 @@ def main():
     n = c["n"]
     npad = (n + 3) & ~3
     stages = dict(zip(["coordinates", "rounds", "fame", "round_received", "order", "exchange"],
-                      (stage_tot / args.steps).round(3).tolist()))
+                      stage_last.round(3).tolist()))
     pmc, pmc_meta = _pmc_table(n, N)
     # the table holds THIS build's kernels only if it names the coordinate
     # kernel this run timed (a table of an older build reads as no table)
@@ -316,9 +318,9 @@ def main():
     else:
         round_kernel = "k_round_wide"
     segments = hg.pipeline()[0]
-    loop_ms = float(stage_tot[7] / args.steps) if len(stage_tot) > 7 else 0.0
+    loop_ms = float(stage_last[7]) if len(stage_last) > 7 else 0.0
     if loop_ms <= 0:  # (BH_LOOP_TIMING=0: the rounds stage instead)
-        loop_ms = float(stage_tot[1] / args.steps)
+        loop_ms = float(stage_last[1])
     iter_us = 1000.0 * loop_ms / max(iters, 1)
     loop_launches = persist_per_step if persistent else iters
     # B(n) split between the two kernels, so that their fractions add up to
@@ -344,7 +346,6 @@ def main():
     # the coordinate kernel: the sum of its launches per step (one per
     # segment; k_flow32x2 carries LT inside them), HIP events on the
     # coordinate stream around each launch
-    coord_ms = float(np.mean(sweep_ms))
     coord_launches = segments if hg.profile_kernel() in ("k_flow32x2", "k_flow32", "k_floww2", "k_floww") else 1
     coord_obj = {"kernel": hg.profile_kernel(), "launches_per_step": coord_launches, "device_ms_per_step": coord_ms,
                  "avg_launch_ms": coord_ms / max(coord_launches, 1),
