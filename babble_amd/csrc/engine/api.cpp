@@ -50,6 +50,7 @@ void free_all(bh_handle *h) {
   if (h->pin_rd) (void)hipHostFree(h->pin_rd);
   if (h->sha_buf) (void)hipFree(h->sha_buf);
   if (h->q_buf) (void)hipFree(h->q_buf);
+  if (h->pack_buf) (void)hipFree(h->pack_buf);
   if (h->graph) (void)hipGraphExecDestroy(h->graph);
   if (h->graph_s) (void)hipGraphExecDestroy(h->graph_s);
   for (auto &e : h->ev)
@@ -58,6 +59,7 @@ void free_all(bh_handle *h) {
     if (e) (void)hipEventDestroy(e);
   for (auto &e : h->ev_loop)
     if (e) (void)hipEventDestroy(e);
+  if (h->ev_st) (void)hipEventDestroy(h->ev_st);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   for (auto &e : h->loop_evs)
@@ -135,6 +137,16 @@ hipError_t copy_sync(hipStream_t s, void *dst, const void *src, size_t bytes, hi
 // staged copy of its own)
 int rd_wait(bh_handle *h, hipStream_t s) {
   HIPCHK(h, wait_stream(s));
+  for (const auto &r : h->pin_rd_list) memcpy(r.dst, h->pin_rd + r.off, r.bytes);
+  h->pin_rd_list.clear();
+  h->pin_rd_used = 0;
+  return BH_OK;
+}
+
+// rd_wait up to an event recorded after the reads (work queued behind it
+// keeps running)
+int rd_wait_event(bh_handle *h, hipEvent_t e) {
+  HIPCHK(h, hipEventSynchronize(e));
   for (const auto &r : h->pin_rd_list) memcpy(r.dst, h->pin_rd + r.off, r.bytes);
   h->pin_rd_list.clear();
   h->pin_rd_used = 0;
@@ -643,7 +655,7 @@ int rounds_coords(bh_handle *h) {
 }
 
 // the rest: LA rows + firstDescendants, the round loop, witness tables
-int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin);
+int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin, bool tables_done = false);
 
 int rounds_loop(bh_handle *h) {
   int rc;
@@ -742,7 +754,7 @@ int rounds_loop(bh_handle *h) {
 // after the loop: witness tables, per-event rounds, PendingRounds.  Rounds
 // and witness flags of events [0, e_begin) are unchanged (an incremental
 // call appended events only)
-int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
+int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin, bool tables_done) {
   Dev &d = h->d;
   hipStream_t s = h->stream;
   h->R = st[bh::ST_ROUNDS];
@@ -765,13 +777,20 @@ int rounds_tail(bh_handle *h, const int32_t *st, int64_t e_begin) {
       bh::launch_flow_lt_fallback(d, s);
     }
   }
-  bh::launch_witness_tables(d, h->R, s);
+  // (tables_done: rounds_pipelined launched them from the device's round
+  // count, ahead of its synchronisation)
+  if (!tables_done) bh::launch_witness_tables(d, h->R, s);
   bh::launch_assign_rounds(d, e_begin, h->n_div, h->P, s);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[2], s));
-  h->wofs_h.resize((size_t)h->R + 1);
-  int rc;
-  if ((rc = rd_async(h, s, h->wofs_h.data(), d.wofs, ((size_t)h->R + 1) * 4)) || (rc = rd_wait(h, s))) return rc;
+  if (!(h->fuse_fame && h->world == 1)) {
+    // the witness offsets (the split's fame exchange reads them), behind the
+    // stage's synchronisation.  bh_run_consensus on one shard goes on to
+    // DecideFame at once instead: its scatter reads the bounds on the device
+    h->wofs_h.resize((size_t)h->R + 1);
+    int rc;
+    if ((rc = rd_async(h, s, h->wofs_h.data(), d.wofs, ((size_t)h->R + 1) * 4)) || (rc = rd_wait(h, s))) return rc;
+  }
   h->n_div = d.N;
   // rounds new to this call join PendingRounds undecided (hashgraph.go:809-815;
   // every round >= LastConsensusRound is queued when it first appears)
@@ -1470,8 +1489,20 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   if (lt0) (void)hipEventDestroy(lt0);
   if (lt1) (void)hipEventDestroy(lt1);
   (void)hipEventDestroy(sr_mark);
+  // the witness tables from the device's round count, launched behind the
+  // state's read-back so that they run while the host wakes up (the host
+  // checks the state before anything reads them: a failed loop's fallback
+  // builds them again)
+  const bool tables_early = async && !h->reset_on;
   if (async) {  // every loop's end: one host synchronisation for the call
-    if ((rc = rd_async(h, sr, st, d.state, bh::ST_COUNT * 4)) || (rc = rd_wait(h, sr))) return rc;
+    if ((rc = rd_async(h, sr, st, d.state, bh::ST_COUNT * 4))) return rc;
+    if (tables_early) {
+      HIPCHK(h, hipEventRecord(h->ev_st, sr));
+      bh::launch_witness_tables(d, -1, sr);
+      if ((rc = rd_wait_event(h, h->ev_st))) return rc;
+    } else if ((rc = rd_wait(h, sr))) {
+      return rc;
+    }
     const int32_t fail = std::max(st[bh::ST_PFAIL], st[bh::ST_ERR]);
     if (fail == 1 || (fail == 0 && st[bh::ST_FLOWOVF] != 2 && !st[bh::ST_DONE]))
       return h->fail(fail == 1 ? BH_ERR_CAPACITY : BH_ERR_STATE,
@@ -1516,7 +1547,7 @@ int rounds_pipelined(bh_handle *h, int K, int64_t base, const SplitPlan *sp = nu
   }
   h->sweep_kernel = wide ? bh::floww_kernel(d) : bh::flow_kernel(d);
   if (h->reset_on && base > 0) h->fiat_max = h->pinned_state[bh::ST_COUNT + 2];
-  if ((rc = rounds_tail(h, st, base))) return rc;
+  if ((rc = rounds_tail(h, st, base, tables_early))) return rc;
   // the timings: every event completed before rounds_tail's synchronisation.
   // Read when asked (settle_timings): ~2K event queries here would hold the
   // device idle between DivideRounds and DecideFame
@@ -1736,8 +1767,10 @@ int fame_local(bh_handle *h) {
 }
 
 int fame_finish(bh_handle *h) {
-  if (h->R > h->P)  // (a Reset hashgraph starts with P = LastConsensusRound, possibly above R)
-    bh::launch_fame_scatter_range(h->d, h->wofs_h[(size_t)h->P], h->wofs_h[(size_t)h->R], h->stream);
+  if (h->R > h->P) {  // (a Reset hashgraph starts with P = LastConsensusRound, possibly above R)
+    if (h->world == 1) bh::launch_fame_scatter_rounds(h->d, h->P, h->R, h->stream);  // (bounds on the device)
+    else bh::launch_fame_scatter_range(h->d, h->wofs_h[(size_t)h->P], h->wofs_h[(size_t)h->R], h->stream);
+  }
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev[3], h->stream));
   // the decided flags of PendingRounds' rounds [P, R) only (the rest are
@@ -1865,11 +1898,26 @@ int order_finish(bh_handle *h) {
   std::vector<int32_t> cnt(k), ofs(k), ld(k);
   std::vector<int64_t> ntx(k);
   int rc;
-  if ((rc = rd_async(h, s, st, d.state, sizeof st)) || (rc = rd_async(h, s, cnt.data(), d.frame_cnt + P0, k * 4)) ||
-      (rc = rd_async(h, s, ofs.data(), d.frame_ofs + P0, k * 4)) ||
-      (rc = rd_async(h, s, ntx.data(), d.frame_ntx + P0, k * 8)) ||
-      (rc = rd_async(h, s, ld.data(), d.frame_loaded + P0, k * 4)) || (rc = rd_wait(h, s)))
-    return rc;
+  // packed on the device first: one copy (k_pack_frames)
+  const size_t words = bh::pack_words((int32_t)k);
+  if (words > h->pack_cap) {
+    if (h->pack_buf) (void)hipFree(h->pack_buf);
+    h->pack_buf = nullptr;
+    h->pack_cap = 0;
+    if ((rc = dalloc(h, &h->pack_buf, words + words / 2))) return rc;
+    h->pack_cap = words + words / 2;
+  }
+  bh::launch_pack_frames(d, P0, (int32_t)k, h->pack_buf, s);
+  HIPCHK(h, hipGetLastError());
+  std::vector<int32_t> pk(words);
+  if ((rc = rd_async(h, s, pk.data(), h->pack_buf, words * 4)) || (rc = rd_wait(h, s))) return rc;
+  memcpy(st, pk.data(), sizeof st);
+  if (k) {
+    memcpy(cnt.data(), pk.data() + bh::ST_COUNT, k * 4);
+    memcpy(ofs.data(), pk.data() + bh::ST_COUNT + k, k * 4);
+    memcpy(ld.data(), pk.data() + bh::ST_COUNT + 2 * k, k * 4);
+    memcpy(ntx.data(), pk.data() + bh::pack_ntx_at((int32_t)k), k * 8);
+  }
   const int64_t ncons0 = h->ncons;
   h->P = P1;
   h->ncons = st[bh::ST_NCONS];
@@ -2180,6 +2228,7 @@ static int create_one(const bh_config *cfg, int device, bh_handle **out) {
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
   for (auto &e : h->ev_loop)
     if (rc == BH_OK && hipEventCreate(&e) != hipSuccess) rc = BH_ERR_DEVICE;
+  if (rc == BH_OK && hipEventCreateWithFlags(&h->ev_st, hipEventDisableTiming) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.state, 0, bh::ST_COUNT * 4) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.counters, 0, 4 * 8) != hipSuccess) rc = BH_ERR_DEVICE;
   if (rc == BH_OK && hipMemset(d.blocked, 0, R1 * 4) != hipSuccess) rc = BH_ERR_DEVICE;
@@ -2373,7 +2422,10 @@ int bh_run_consensus(bh_handle *h) {
   int rc;
   if (!h) return BH_ERR_INVALID;
   (void)hipSetDevice(h->device);
-  if ((rc = stage_rounds(h))) return rc;
+  h->fuse_fame = true;  // (rounds_tail: DecideFame follows at once, no read-back of the witness offsets)
+  rc = stage_rounds(h);
+  h->fuse_fame = false;
+  if (rc) return rc;
   if ((rc = stage_fame(h))) return rc;
   if ((rc = stage_rr(h))) return rc;
   return stage_order(h);
@@ -3006,6 +3058,7 @@ int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x,
   const size_t need = (size_t)count * 20;
   if (need > h->q_cap) {
     if (h->q_buf) (void)hipFree(h->q_buf);
+  if (h->pack_buf) (void)hipFree(h->pack_buf);
     h->q_buf = nullptr;
     h->q_cap = 0;
     HIPCHK(h, hipMalloc((void **)&h->q_buf, need));

@@ -432,6 +432,7 @@ void launch_fame(const Dev &d, int32_t R, int32_t r0, int32_t r1, hipStream_t s)
 void launch_fame_scatter(const Dev &d, int32_t W, hipStream_t s);
 // DecideFame of the rounds [r0, r1): wfame entries [wofs[r0], wofs[r1]) to fame
 void launch_fame_scatter_range(const Dev &d, int32_t w0, int32_t w1, hipStream_t s);
+void launch_fame_scatter_rounds(const Dev &d, int32_t P, int32_t R, hipStream_t s);  // bounds from wofs on the device
 // rr of events still undetermined (rr already set is kept); rounds < P are
 // live-decided iff no trapped witness; counters[3] = undetermined after it;
 // frame_cnt[r] = events received in r (every r < R)
@@ -448,6 +449,10 @@ void launch_order_sort(const Dev &d, int32_t f0, int32_t f1, hipStream_t s);
 void launch_cons_pos(const Dev &d, int64_t i0, int64_t i1, hipStream_t s);
 // witnesses of rounds [P0, P1) still Undefined when those rounds were processed
 void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s);
+// k_pack_frames' layout: int32 words, the int64 transaction counts from word pack_ntx_at(k)
+__host__ __device__ inline int32_t pack_ntx_at(int32_t k) { return (ST_COUNT + 3 * k + 1) & ~1; }
+inline size_t pack_words(int32_t k) { return (size_t)pack_ntx_at(k) + 2 * (size_t)k; }
+void launch_pack_frames(const Dev &d, int32_t P0, int32_t k, int32_t *out, hipStream_t s);
 // pair predicates for bh_query_events (kernels_query.hip): kind 0 ancestor,
 // 1 selfAncestor, 2 see, 3 stronglySee, 4 roundDiff
 void launch_query(const Dev &d, int32_t kind, int64_t count, const int64_t *x, const int64_t *y, int32_t *out,

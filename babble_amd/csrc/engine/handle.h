@@ -114,11 +114,15 @@ struct bh_handle {
   std::vector<PinRead> pin_rd_list;
   uint8_t *sha_buf = nullptr;  // bh_hash_bodies scratch
   uint8_t *q_buf = nullptr;    // bh_query_events scratch
+  int32_t *pack_buf = nullptr;  // order_finish's read-back (k_pack_frames)
+  size_t pack_cap = 0;          // (int32 words)
   size_t q_cap = 0;
   size_t sha_cap = 0;
   hipEvent_t ev[NSTAGE + 1]{};
   hipEvent_t ev_sweep[2]{};  // around k_la_sweep alone (roofline timing)
-  hipEvent_t ev_loop[2]{};   // around each round loop (run_round_loop): its device time, summed per run
+  hipEvent_t ev_loop[2]{};
+  hipEvent_t ev_st = nullptr;  // behind the loop state's read-back (rounds_pipelined: the witness tables run after it)
+  bool fuse_fame = false;      // bh_run_consensus: DecideFame follows DivideRounds at once (rounds_tail)   // around each round loop (run_round_loop): its device time, summed per run
   float loop_ms = 0, loop_ms_acc = 0;
   float sweep_ms = 0;
   const char *sweep_kernel = "";

@@ -474,4 +474,20 @@ void launch_fame_scatter_range(const Dev &d, int32_t w0, int32_t w1, hipStream_t
   k_fame_scatter<<<(unsigned)((w1 - w0 + 255) / 256), 256, 0, s>>>(d, w0, w1);
 }
 
+// the witnesses of rounds [P, R), bounded on the device (wofs[P], wofs[R]):
+// the host launches it without having read wofs back (fame_finish, one shard)
+__global__ void k_fame_scatter_rounds(Dev d, int32_t P, int32_t R) {
+  const int32_t w0 = d.wofs[P], w1 = d.wofs[R];
+  for (int32_t i = w0 + (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); i < w1; i += (int32_t)(gridDim.x * blockDim.x)) {
+    const int32_t e = d.wids[i];
+    d.fame[e] = d.trapped[e] ? 0 : d.wfame[i];
+  }
+}
+
+void launch_fame_scatter_rounds(const Dev &d, int32_t P, int32_t R, hipStream_t s) {
+  if (R <= P) return;
+  const int64_t most = (int64_t)(R - P) * d.n;  // (at most one witness per chain and round)
+  k_fame_scatter_rounds<<<(unsigned)std::min<int64_t>((most + 255) / 256, 4096), 256, 0, s>>>(d, P, R);
+}
+
 }  // namespace bh

@@ -3334,8 +3334,8 @@ void launch_round_iteration(const Dev &d, int p, hipStream_t s) {
 // witness tables for DecideFame, once after the loop: W(r) = the candidates
 // of round r whose round is exactly r (B[r+1][q] > B[r][q]), in chain order;
 // wrow = the row of their firstDescendants in fd (chain_start[q] + B[r][q]).
-__global__ __launch_bounds__(64) void k_wcount(Dev d) {
-  const int r = blockIdx.x, lane = threadIdx.x, n = d.n;
+__device__ __forceinline__ void k_wcount_round(const Dev &d, int r) {
+  const int lane = threadIdx.x, n = d.n;
   int cnt = 0;
   for (int q = lane; q < n; q += 64) {
     if (r < d.r0) {  // k_fiat's witnesses (Reset)
@@ -3349,9 +3349,20 @@ __global__ __launch_bounds__(64) void k_wcount(Dev d) {
   if (lane == 0) d.wcnt[r] = cnt;
 }
 
+// R < 0: the loop's round count from the device (ST_ROUNDS, at most R_cap),
+// read before the host has it (rounds_pipelined launches the tables ahead of
+// its synchronisation); the workgroups stride over the rounds
+__device__ __forceinline__ int wt_rounds(const Dev &d, int R) { return R >= 0 ? R : min(d.state[ST_ROUNDS], d.R_cap); }
+
+__global__ __launch_bounds__(64) void k_wcount(Dev d, int R) {
+  const int RR = wt_rounds(d, R);
+  for (int r = blockIdx.x; r < RR; r += gridDim.x) k_wcount_round(d, r);
+}
+
 __global__ __launch_bounds__(1024) void k_wscan(Dev d, int R) {
   __shared__ int32_t part[1024];
   const int t = threadIdx.x;
+  R = wt_rounds(d, R);
   const int per = (R + 1023) / 1024;
   const int lo = min(R, t * per), hi = min(R, lo + per);
   int32_t s = 0;
@@ -3372,8 +3383,8 @@ __global__ __launch_bounds__(1024) void k_wscan(Dev d, int R) {
   if (t == 1023) d.wofs[R] = part[1023];
 }
 
-__global__ __launch_bounds__(64) void k_wfill(Dev d) {
-  const int r = blockIdx.x, lane = threadIdx.x, n = d.n;
+__device__ __forceinline__ void k_wfill_round(const Dev &d, int r) {
+  const int lane = threadIdx.x, n = d.n;
   int32_t j = d.wofs[r];
   for (int c0 = 0; c0 < n; c0 += 64) {
     const int q = c0 + lane;
@@ -3388,8 +3399,8 @@ __global__ __launch_bounds__(64) void k_wfill(Dev d) {
       w = b0 < d.chain_len[q] && d.B[(int64_t)(r + 1) * n + q] > b0;
     }
     const unsigned long long m = __ballot(w);
-    if (w) {
-      const int32_t k = j + popc64(m & ((1ull << lane) - 1ull));
+    const int32_t k = j + popc64(m & ((1ull << lane) - 1ull));
+    if (w && k < d.W_cap) {  // (W_cap: tables of a loop that failed are never read, but stay in bounds)
       d.wids[k] = d.chain_ids[d.chain_start[q] + b0];
       d.wrow[k] = d.chain_start[q] + b0;  // the witness's LA / FD row
     }
@@ -3397,11 +3408,18 @@ __global__ __launch_bounds__(64) void k_wfill(Dev d) {
   }
 }
 
+__global__ __launch_bounds__(64) void k_wfill(Dev d, int R) {
+  const int RR = wt_rounds(d, R);
+  for (int r = blockIdx.x; r < RR; r += gridDim.x) k_wfill_round(d, r);
+}
+
 void launch_witness_tables(const Dev &d, int R, hipStream_t s) {
-  if (R <= 0) return;
-  k_wcount<<<R, 64, 0, s>>>(d);
+  if (R == 0) return;
+  // (R < 0: the device's round count, 2048 workgroups striding over it)
+  const unsigned g = R > 0 ? (unsigned)R : (unsigned)std::min(d.R_cap + 1, 2048);
+  k_wcount<<<g, 64, 0, s>>>(d, R);
   k_wscan<<<1, 1024, 0, s>>>(d, R);
-  k_wfill<<<R, 64, 0, s>>>(d);
+  k_wfill<<<g, 64, 0, s>>>(d, R);
 }
 
 // ---------------------------------------------------------------------------
@@ -3465,6 +3483,24 @@ __global__ __launch_bounds__(64) void k_trap_processed(Dev d, int32_t P0) {
       atomicAdd(&d.blocked[r], 1);
     }
   }
+}
+
+// ProcessDecidedRounds' read-back in one buffer (one device-to-host copy
+// instead of five): the state words, then frames [P0, P0 + k)'s counts,
+// offsets and loaded counts, then their transaction counts (8-byte aligned)
+__global__ void k_pack_frames(Dev d, int32_t P0, int32_t k, int32_t *out) {
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < ST_COUNT) out[i] = d.state[i];
+  if (i >= k) return;
+  out[ST_COUNT + i] = d.frame_cnt[P0 + i];
+  out[ST_COUNT + k + i] = d.frame_ofs[P0 + i];
+  out[ST_COUNT + 2 * k + i] = d.frame_loaded[P0 + i];
+  reinterpret_cast<int64_t *>(out + pack_ntx_at(k))[i] = d.frame_ntx[P0 + i];
+}
+
+void launch_pack_frames(const Dev &d, int32_t P0, int32_t k, int32_t *out, hipStream_t s) {
+  const int32_t m = k > ST_COUNT ? k : ST_COUNT;
+  k_pack_frames<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(d, P0, k, out);
 }
 
 void launch_trap_processed(const Dev &d, int32_t P0, int32_t P1, hipStream_t s) {
