@@ -1755,6 +1755,23 @@ int run_pass(bh_handle *h, F fn) {
   return h->rank == 0 ? fn(h) : BH_OK;  // (in process, h is shard 0)
 }
 
+// DecideRoundReceived's launch and its undetermined-count read-back (done
+// by the caller's rd_wait), then the host state once that has landed
+int32_t last_consensus_round(const bh_handle *h);
+int rr_launch(bh_handle *h, int64_t *und) {
+  bh::launch_round_received(h->d, h->R, h->P, last_consensus_round(h), h->stream);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipEventRecord(h->ev[4], h->stream));
+  return rd_async(h, h->stream, und, h->d.counters + 3, 8);
+}
+
+void rr_done(bh_handle *h, int64_t und) {
+  h->nundet = und;
+  h->n_rr = h->n_div;
+  h->R_rr = h->R;
+  h->stage = 3;
+}
+
 // only PendingRounds' rounds [P, R): a processed round's witnesses are
 // decided for good (or trapped), DecideFame never visits it again
 int fame_local(bh_handle *h) {
@@ -1780,12 +1797,20 @@ int fame_finish(bh_handle *h) {
   if (h->R > h->P && (rc = rd_async(h, h->stream, h->decided_h.data() + h->P, h->d.decided + h->P, (size_t)(h->R - h->P))))
     return rc;
   int32_t err = 0;
-  if ((rc = rd_async(h, h->stream, &err, h->d.state + bh::ST_ERR, 4)) || (rc = rd_wait(h, h->stream))) return rc;
+  if ((rc = rd_async(h, h->stream, &err, h->d.state + bh::ST_ERR, 4))) return rc;
+  // bh_run_consensus on one shard: DecideRoundReceived, which reads nothing
+  // the host learns here, is queued behind fame before the synchronisation
+  // (one host round trip less; its stage completes below, after fame's)
+  const bool with_rr = h->fuse_fame && h->world == 1;
+  int64_t und = 0;
+  if (with_rr && (rc = rr_launch(h, &und))) return rc;
+  if ((rc = rd_wait(h, h->stream))) return rc;
   if (err) return h->fail(BH_ERR_STATE, "inconsistent fame decision (forked DAG?)");
   // updatePendingRounds (hashgraph.go:689-695): set, never cleared
   for (int32_t r = h->P; r < h->R; ++r)
     if (h->decided_h[(size_t)r]) h->pend_dec[(size_t)r] = 1;
   h->stage = 2;
+  if (with_rr) rr_done(h, und);
   return BH_OK;
 }
 
@@ -1830,16 +1855,10 @@ int32_t stale_head(const bh_handle *h) { return h->reset_on && h->P > h->reset_l
 
 int stage_rr_local(bh_handle *h) {
   if (h->stage < 2) return h->fail(BH_ERR_STATE, "DecideRoundReceived before DecideFame");
-  bh::launch_round_received(h->d, h->R, h->P, last_consensus_round(h), h->stream);
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipEventRecord(h->ev[4], h->stream));
   int64_t und = 0;
   int rc;
-  if ((rc = rd_async(h, h->stream, &und, h->d.counters + 3, 8)) || (rc = rd_wait(h, h->stream))) return rc;
-  h->nundet = und;
-  h->n_rr = h->n_div;
-  h->R_rr = h->R;
-  h->stage = 3;
+  if ((rc = rr_launch(h, &und)) || (rc = rd_wait(h, h->stream))) return rc;
+  rr_done(h, und);
   return BH_OK;
 }
 
@@ -2422,12 +2441,15 @@ int bh_run_consensus(bh_handle *h) {
   int rc;
   if (!h) return BH_ERR_INVALID;
   (void)hipSetDevice(h->device);
-  h->fuse_fame = true;  // (rounds_tail: DecideFame follows at once, no read-back of the witness offsets)
+  // fuse_fame: DecideFame follows DivideRounds at once (rounds_tail reads no
+  // witness offsets back) and, on one shard, DecideRoundReceived rides on
+  // DecideFame's synchronisation (fame_finish)
+  h->fuse_fame = true;
   rc = stage_rounds(h);
+  if (!rc) rc = stage_fame(h);
   h->fuse_fame = false;
   if (rc) return rc;
-  if ((rc = stage_fame(h))) return rc;
-  if ((rc = stage_rr(h))) return rc;
+  if (h->stage < 3 && (rc = stage_rr(h))) return rc;
   return stage_order(h);
 }
 int bh_synchronize(bh_handle *h) {
