@@ -3080,7 +3080,6 @@ int bh_query_events(bh_handle *h, int32_t kind, int64_t count, const int64_t *x,
   const size_t need = (size_t)count * 20;
   if (need > h->q_cap) {
     if (h->q_buf) (void)hipFree(h->q_buf);
-  if (h->pack_buf) (void)hipFree(h->pack_buf);
     h->q_buf = nullptr;
     h->q_cap = 0;
     HIPCHK(h, hipMalloc((void **)&h->q_buf, need));
