@@ -1313,18 +1313,23 @@ __device__ __forceinline__ void cand_row(const Dev &d, int c, int32_t r, int32_t
   const int w16 = (d.npad + 7) / 8 * 4;
   uint16_t *c16 = d.wide_cols ? reinterpret_cast<uint16_t *>(d.cand16 + (int64_t)c * w16) : nullptr;
   const int nrow = c16 ? 2 * w16 : d.npad;
-  for (int i0 = 0; i0 < nrow; i0 += blockDim.x >> 4) {  // (uniform trip count)
-    const int i = i0 + (t >> 4);
+  // 8-lane groups when that covers every row in one pass (1024 threads,
+  // npad <= 128: the segment start's dependent loads once, not twice)
+  const bool g8 = !c16 && nrow * 8 <= (int)blockDim.x;
+  const int gsh = g8 ? 3 : 4;
+  for (int i0 = 0; i0 < nrow; i0 += blockDim.x >> gsh) {  // (uniform trip count)
+    const int i = i0 + (t >> gsh);
     const bool on = i < d.n;
     const int32_t cs = on ? d.chain_start[i] : 0, len = on ? d.chain_len[i] : 0;
     // FD[(c, b)][i] >= B[r][i]: (c, b = B[r][c]) is in round >= r, and so
     // is every event that sees it (a round is the maximum of its parents'
     // or one more) -- the search starts there, and usually ends within the
-    // first 1024 rows (two dependent loads instead of ~5 over the chain)
+    // first rows after it (two dependent loads instead of ~5 over the chain)
     const int32_t lo0 = r > 0 && on ? min(d.B[(int64_t)r * d.n + i], len) : 0;
-    const int32_t j = first_ge16(colc + cs, lo0, len, b, on && len > lo0, r > 0);
+    const int32_t j = g8 ? first_ge_group<8>(colc + cs, lo0, len, b, on && len > lo0, r > 0)
+                         : first_ge16(colc + cs, lo0, len, b, on && len > lo0, r > 0);
     const int32_t f = on && j < len ? j : FD_NONE;
-    if ((t & 15) == 0 && i < nrow) {
+    if ((t & ((1 << gsh) - 1)) == 0 && i < nrow) {
       if (c16) c16[i] = (uint16_t)min((uint32_t)f + 1u, 0xFFFFu);
       else cf[i] = d.cand_fe ? (int32_t)fe_encode(f, 0) : f;  // (k_round_lean: iteration 0's tag bit is 0)
     }
