@@ -133,6 +133,37 @@ def test_stepwise_passes_across_calls():
             _compare(o, hg, f"[0, {hi}) after {go}")
 
 
+def test_stepwise_passes_pipelined(monkeypatch):
+    """The passes one at a time through the n <= 128 segment pipeline (the
+    persistent loop, witness tables launched from the device's round count,
+    DecideFame's device-bounded scatter, no fused DecideRoundReceived): the
+    state after each pass equals the oracle's, and the same DAG through
+    RunConsensus ends in the same state."""
+    from babble_amd import Hashgraph
+    from babble_amd.dag import Dag
+    monkeypatch.setenv("BH_SEGMENTS", "3")
+    n, N, step = 128, 30000, 10000
+    d = Dag(n, N, 606, lagging=20, sig_mode=0)
+    args = (d.creator, d.index, d.self_parent, d.other_parent, d.hash, d.sig_r, d.ntx)
+    o = Oracle(n, d.participant_ids, capacity=N)
+    hg = Hashgraph(d.participant_ids, N)
+    whole = Hashgraph(d.participant_ids, N)
+    batch = _wire_batches(d)
+    passes = ("divide_rounds", "decide_fame", "decide_round_received", "process_decided_rounds")
+    for lo in range(0, N, step):
+        hi = min(N, lo + step)
+        o.insert_dag(*(a[lo:hi] for a in args))
+        hg.insert_events(*batch(lo, hi))
+        whole.insert_events(*batch(lo, hi))
+        for p in passes:
+            getattr(o, p)()
+            getattr(hg, p)()
+            _compare(o, hg, f"[0, {hi}) after {p}")
+        whole.run_consensus()
+        _compare(o, whole, f"[0, {hi}) RunConsensus")
+    assert hg.pipeline()[0] == 3 and whole.pipeline()[0] == 3
+
+
 def test_round_info_kat():
     """TestDivideRounds' per-round witness sets (hashgraph_test.go:746-828) and
     TestDecideFame's fame (:1267-1343) through Store.GetRound / RoundInfo;
